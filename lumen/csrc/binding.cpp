@@ -1,0 +1,262 @@
+// Python binding for lumen's native ops (built into lumen/_C*.so by lumen/csrc/build.py).
+//
+// Every function here only checks arguments, picks the dtype code and the current HIP stream,
+// and calls an `extern "C"` launcher from kernels/*.hip.  Allocation and shape logic live in
+// lumen/ops/*.py so this translation unit (the only one that includes the heavy torch headers)
+// rarely changes.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+extern "C" {
+hipError_t lumen_rmsnorm_fwd(int, const void*, const void*, const void*, void*, void*, float*, int,
+                             int, float, hipStream_t);
+hipError_t lumen_rmsnorm_bwd(int, const void*, const void*, const void*, const float*, const void*,
+                             void*, float*, int, int, hipStream_t);
+hipError_t lumen_qkv_rope(int, int, void*, void*, void*, void*, const int*, const float*,
+                          const float*, int, int, int, int, int, hipStream_t);
+hipError_t lumen_rope_inplace(int, void*, const int*, const float*, const float*, int, int, int,
+                              int, hipStream_t);
+hipError_t lumen_swiglu(int, int, const void*, const void*, void*, int, int, hipStream_t);
+hipError_t lumen_cross_entropy(int, void*, const int64_t*, float*, float*, int, int, int, float,
+                               int, hipStream_t);
+hipError_t lumen_grad_norm_sq(int, const void*, long long, float*, hipStream_t);
+hipError_t lumen_adamw(float*, int, const void*, float*, float*, int, void*, long long, float, float,
+                       float, float, float, float, float, float, const float*, float, hipStream_t);
+hipError_t lumen_lora_gemm(int, int, int, const void*, const void*, void*, long long, long long,
+                           long long, long long, float, int, unsigned long long, unsigned int, float,
+                           long long, int, const long long*, const long long*, const long long*,
+                           const int*, const int*, const int*, hipStream_t);
+hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
+                                        const int*, const int*, int, int, int, int, int, int, int,
+                                        float, float*, float*, void*, int, hipStream_t);
+hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, const long long*,
+                                   int, int, int, int, long long, long long, int, hipStream_t);
+hipError_t lumen_sample(int, const void*, const float*, const float*, const int*,
+                        unsigned long long, long long, long long*, float*, int, int, hipStream_t);
+void lumen_cpu_adamw(float*, const float*, float*, float*, long long, float, float, float, float,
+                     float, float, float, float);
+int lumen_cpu_has_avx512();
+}
+
+namespace {
+
+int dcode(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kHalf: return 1;
+    case at::kBFloat16: return 2;
+    default: throw std::invalid_argument("lumen: unsupported dtype " + std::string(toString(t.scalar_type())));
+  }
+}
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("lumen native op ") + what + " failed: " + hipGetErrorString(e));
+}
+
+void need_cuda(const at::Tensor& t, const char* name) {
+  if (!t.is_cuda()) throw std::invalid_argument(std::string("lumen: ") + name + " must be a GPU tensor");
+  if (!t.is_contiguous()) throw std::invalid_argument(std::string("lumen: ") + name + " must be contiguous");
+}
+
+template <typename T = void>
+T* ptr(const std::optional<at::Tensor>& t) {
+  return t.has_value() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void rmsnorm_fwd(const at::Tensor& x, const std::optional<at::Tensor>& residual, const at::Tensor& w,
+                 at::Tensor& y, const std::optional<at::Tensor>& s_out, at::Tensor& rstd, double eps) {
+  need_cuda(x, "x"); need_cuda(w, "w"); need_cuda(y, "y");
+  const int H = static_cast<int>(x.size(-1));
+  const int rows = static_cast<int>(x.numel() / H);
+  check(lumen_rmsnorm_fwd(dcode(x), x.data_ptr(), ptr(residual), w.data_ptr(), y.data_ptr(),
+                          ptr(s_out), rstd.data_ptr<float>(), rows, H, static_cast<float>(eps),
+                          cur_stream()),
+        "rmsnorm_fwd");
+}
+
+void rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Tensor& w, const at::Tensor& rstd,
+                 const std::optional<at::Tensor>& ds_res, at::Tensor& dx,
+                 const std::optional<at::Tensor>& dw) {
+  need_cuda(dy, "dy"); need_cuda(s, "s");
+  const int H = static_cast<int>(dy.size(-1));
+  const int rows = static_cast<int>(dy.numel() / H);
+  check(lumen_rmsnorm_bwd(dcode(dy), dy.data_ptr(), s.data_ptr(), w.data_ptr(),
+                          rstd.data_ptr<float>(), ptr(ds_res), dx.data_ptr(), ptr<float>(dw), rows,
+                          H, cur_stream()),
+        "rmsnorm_bwd");
+}
+
+void qkv_rope(bool bwd, at::Tensor& qkv, at::Tensor& q, at::Tensor& k, at::Tensor& v,
+              const std::optional<at::Tensor>& pos, const at::Tensor& cos_t, const at::Tensor& sin_t,
+              int64_t S, int64_t nh, int64_t nkv, int64_t D) {
+  need_cuda(qkv, "qkv"); need_cuda(q, "q"); need_cuda(k, "k"); need_cuda(v, "v");
+  const int T = static_cast<int>(qkv.numel() / ((nh + 2 * nkv) * D));
+  check(lumen_qkv_rope(dcode(qkv), bwd ? 1 : 0, qkv.data_ptr(), q.data_ptr(), k.data_ptr(),
+                       v.data_ptr(), ptr<const int>(pos), cos_t.data_ptr<float>(),
+                       sin_t.data_ptr<float>(), T, static_cast<int>(S), static_cast<int>(nh),
+                       static_cast<int>(nkv), static_cast<int>(D), cur_stream()),
+        "qkv_rope");
+}
+
+void rope_inplace(at::Tensor& x, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t,
+                  int64_t ntok, int64_t row_stride, int64_t nheads, int64_t D) {
+  check(lumen_rope_inplace(dcode(x), x.data_ptr(), pos.data_ptr<int>(), cos_t.data_ptr<float>(),
+                           sin_t.data_ptr<float>(), static_cast<int>(ntok),
+                           static_cast<int>(row_stride), static_cast<int>(nheads),
+                           static_cast<int>(D), cur_stream()),
+        "rope_inplace");
+}
+
+void swiglu(bool bwd, const at::Tensor& gu, const std::optional<at::Tensor>& dact, at::Tensor& out) {
+  need_cuda(gu, "gate_up"); need_cuda(out, "out");
+  const int F = static_cast<int>(gu.size(-1) / 2);
+  const int rows = static_cast<int>(gu.numel() / (2 * F));
+  check(lumen_swiglu(dcode(gu), bwd ? 1 : 0, gu.data_ptr(), ptr(dact), out.data_ptr(), rows, F,
+                     cur_stream()),
+        "swiglu");
+}
+
+void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
+                   const std::optional<at::Tensor>& row_loss, int64_t ignore_index, double scale,
+                   bool write_grad) {
+  need_cuda(logits, "logits"); need_cuda(labels, "labels");
+  if (labels.scalar_type() != at::kLong) throw std::invalid_argument("lumen: labels must be int64");
+  const int V = static_cast<int>(logits.size(-1));
+  const int rows = static_cast<int>(logits.numel() / V);
+  check(lumen_cross_entropy(dcode(logits), logits.data_ptr(), labels.data_ptr<int64_t>(),
+                            ptr<float>(loss_sum), ptr<float>(row_loss), rows, V,
+                            static_cast<int>(ignore_index), static_cast<float>(scale),
+                            write_grad ? 1 : 0, cur_stream()),
+        "cross_entropy");
+}
+
+void grad_norm_sq(const at::Tensor& g, at::Tensor& out) {
+  need_cuda(g, "grad");
+  check(lumen_grad_norm_sq(dcode(g), g.data_ptr(), g.numel(), out.data_ptr<float>(), cur_stream()),
+        "grad_norm_sq");
+}
+
+void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
+           const std::optional<at::Tensor>& out_copy, double lr, double b1, double b2, double eps,
+           double wd, double bc1, double bc2, double inv_scale,
+           const std::optional<at::Tensor>& norm_sq, double max_norm) {
+  need_cuda(p, "param"); need_cuda(g, "grad"); need_cuda(m, "exp_avg"); need_cuda(v, "exp_avg_sq");
+  if (p.scalar_type() != at::kFloat) throw std::invalid_argument("lumen: adamw master must be f32");
+  const int od = out_copy.has_value() ? dcode(*out_copy) : 0;
+  check(lumen_adamw(p.data_ptr<float>(), dcode(g), g.data_ptr(), m.data_ptr<float>(),
+                    v.data_ptr<float>(), od, ptr(out_copy), p.numel(), static_cast<float>(lr),
+                    static_cast<float>(b1), static_cast<float>(b2), static_cast<float>(eps),
+                    static_cast<float>(wd), static_cast<float>(bc1), static_cast<float>(bc2),
+                    static_cast<float>(inv_scale), ptr<const float>(norm_sq),
+                    static_cast<float>(max_norm), cur_stream()),
+        "adamw");
+}
+
+void lora_gemm(int64_t act_dtype, int64_t mode, int64_t bn, const at::Tensor& X, const at::Tensor& W,
+               at::Tensor& C, int64_t ldx, int64_t ldw, int64_t cs_m, int64_t cs_n, double alpha,
+               int64_t ksplit, int64_t seed, int64_t drop_thresh, double drop_scale, int64_t drop_ld,
+               const std::vector<std::vector<int64_t>>& segs) {
+  if (!X.is_cuda() || !W.is_cuda() || !C.is_cuda()) throw std::invalid_argument("lumen: lora_gemm needs GPU tensors");
+  const int nseg = static_cast<int>(segs.size());
+  if (nseg < 1 || nseg > 4) throw std::invalid_argument("lumen: lora_gemm needs 1..4 segments");
+  long long xo[4] = {0}, wo[4] = {0}, co[4] = {0};
+  int Ms[4] = {0}, Ns[4] = {0}, Ks[4] = {0};
+  for (int i = 0; i < nseg; ++i) {
+    if (segs[i].size() != 6) throw std::invalid_argument("lumen: segment = (x_off, w_off, c_off, M, N, K)");
+    xo[i] = segs[i][0]; wo[i] = segs[i][1]; co[i] = segs[i][2];
+    Ms[i] = static_cast<int>(segs[i][3]); Ns[i] = static_cast<int>(segs[i][4]);
+    Ks[i] = static_cast<int>(segs[i][5]);
+  }
+  check(lumen_lora_gemm(static_cast<int>(act_dtype), static_cast<int>(mode), static_cast<int>(bn),
+                        X.data_ptr(), W.data_ptr(), C.data_ptr(), ldx, ldw, cs_m, cs_n,
+                        static_cast<float>(alpha), static_cast<int>(ksplit),
+                        static_cast<unsigned long long>(seed), static_cast<unsigned int>(drop_thresh),
+                        static_cast<float>(drop_scale), drop_ld, nseg, xo, wo, co, Ms, Ns, Ks,
+                        cur_stream()),
+        "lora_gemm");
+}
+
+void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
+                            const at::Tensor& v_cache, const at::Tensor& block_tables,
+                            const at::Tensor& context_lens, int64_t num_kv_heads, int64_t block_size,
+                            int64_t max_blocks_per_seq, double scale, at::Tensor& tmp_m,
+                            at::Tensor& tmp_l, at::Tensor& tmp_o, int64_t partition_size) {
+  need_cuda(q, "q"); need_cuda(out, "out");
+  const int num_seqs = static_cast<int>(q.size(0));
+  const int nh = static_cast<int>(q.size(1));
+  const int D = static_cast<int>(q.size(2));
+  check(lumen_paged_attention_decode(dcode(q), out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
+                                     v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                     context_lens.data_ptr<int>(), num_seqs, nh,
+                                     static_cast<int>(num_kv_heads), D, static_cast<int>(block_size),
+                                     static_cast<int>(max_blocks_per_seq),
+                                     static_cast<int>(tmp_m.size(-1)), static_cast<float>(scale),
+                                     tmp_m.data_ptr<float>(), tmp_l.data_ptr<float>(),
+                                     tmp_o.data_ptr(), static_cast<int>(partition_size), cur_stream()),
+        "paged_attention_decode");
+}
+
+void reshape_and_cache(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at::Tensor& v_cache,
+                       const at::Tensor& slot_mapping, int64_t num_kv_heads, int64_t D,
+                       int64_t block_size, int64_t k_stride, int64_t v_stride) {
+  const int ntok = static_cast<int>(slot_mapping.numel());
+  check(lumen_reshape_and_cache(dcode(k), k.data_ptr(), v.data_ptr(), k_cache.data_ptr(),
+                                v_cache.data_ptr(), reinterpret_cast<const long long*>(slot_mapping.data_ptr<int64_t>()), ntok,
+                                static_cast<int>(num_kv_heads), static_cast<int>(D),
+                                static_cast<int>(block_size), k_stride, v_stride, 0, cur_stream()),
+        "reshape_and_cache");
+}
+
+void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& top_p,
+            const at::Tensor& top_k, int64_t seed, int64_t offset, at::Tensor& out_tokens,
+            const std::optional<at::Tensor>& out_logprob) {
+  need_cuda(logits, "logits");
+  const int V = static_cast<int>(logits.size(-1));
+  const int rows = static_cast<int>(logits.numel() / V);
+  check(lumen_sample(dcode(logits), logits.data_ptr(), temperature.data_ptr<float>(),
+                     top_p.data_ptr<float>(), top_k.data_ptr<int>(),
+                     static_cast<unsigned long long>(seed), offset,
+                     reinterpret_cast<long long*>(out_tokens.data_ptr<int64_t>()),
+                     ptr<float>(out_logprob), rows, V, cur_stream()),
+        "sample");
+}
+
+void cpu_adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, double lr, double b1,
+               double b2, double eps, double wd, double bc1, double bc2, double grad_scale) {
+  if (p.is_cuda() || g.is_cuda()) throw std::invalid_argument("lumen: cpu_adamw takes host tensors");
+  if (p.scalar_type() != at::kFloat || g.scalar_type() != at::kFloat)
+    throw std::invalid_argument("lumen: cpu_adamw needs f32");
+  lumen_cpu_adamw(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                  p.numel(), static_cast<float>(lr), static_cast<float>(b1), static_cast<float>(b2),
+                  static_cast<float>(eps), static_cast<float>(wd), static_cast<float>(bc1),
+                  static_cast<float>(bc2), static_cast<float>(grad_scale));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "lumen native ops for MI355X (gfx950)";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("qkv_rope", &qkv_rope);
+  m.def("rope_inplace", &rope_inplace);
+  m.def("swiglu", &swiglu);
+  m.def("cross_entropy", &cross_entropy);
+  m.def("grad_norm_sq", &grad_norm_sq);
+  m.def("adamw", &adamw);
+  m.def("lora_gemm", &lora_gemm);
+  m.def("paged_attention_decode", &paged_attention_decode);
+  m.def("reshape_and_cache", &reshape_and_cache);
+  m.def("sample", &sample);
+  m.def("cpu_adamw", &cpu_adamw);
+  m.def("cpu_has_avx512", &lumen_cpu_has_avx512);
+}

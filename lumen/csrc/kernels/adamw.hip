@@ -1,0 +1,151 @@
+// Optimizer kernels: grad L2-norm / overflow check and fused AdamW.
+//
+// Reference behaviour: DeepSpeed FusedAdam / torch AdamW with betas (0.9, 0.999), eps 1e-8,
+// weight_decay 0 (configs/ds_config_zero1.json:6-14), gradient_clipping 1.0
+// (configs/ds_config_zero1.json:44) and fp16 dynamic loss scaling
+// (configs/ds_config_zero1.json:25-32) -- i.e. unscale, has_inf_or_nan, global-norm clip and the
+// Adam update as separate multi-tensor passes plus a host sync per step.
+//
+// Here the trainable state lives in ONE flat f32 buffer per rank (the ZeRO partition), so
+//  * `grad_norm_sq` is a single grid-stride reduction -> one f32 on device (RCCL all-reduces it
+//    across ranks when sharded); a non-finite sum doubles as the overflow flag;
+//  * `adamw_step` reads that device scalar and folds unscale (1/loss_scale), clip coefficient
+//    min(1, max_norm/||g||) and the skip-on-overflow decision into the update itself, so a bf16
+//    step needs no device->host synchronisation at all; optionally it writes a 16-bit copy of the
+//    updated parameters in the same pass (the "fp32 master -> bf16 model" copy-out).
+#include "common.h"
+
+namespace lumen {
+
+template <typename G>
+__global__ void __launch_bounds__(256) norm_sq_kernel(const G* __restrict__ g, long long n,
+                                                      float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const long long stride = static_cast<long long>(gridDim.x) * 256 * 8;
+  for (long long i = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 8; i < n;
+       i += stride) {
+    if (i + 8 <= n) {
+      float x[8];
+      load8(g + i, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[j] * x[j];
+    } else {
+      for (long long j = i; j < n; ++j) {
+        const float x = to_f32(g[j]);
+        acc += x * x;
+      }
+    }
+  }
+  acc = block_sum<256>(acc, red);
+  if (threadIdx.x == 0) atomicAdd(out, acc);
+}
+
+template <typename G, typename O>
+__global__ void __launch_bounds__(256) adamw_kernel(
+    float* __restrict__ p, const G* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    O* __restrict__ out_copy, long long n, float lr, float beta1, float beta2, float eps, float wd,
+    float bc1, float bc2, float inv_scale, const float* __restrict__ norm_sq, float max_norm) {
+  float coef = inv_scale;
+  if (norm_sq) {
+    const float nsq = *norm_sq;
+    if (!isfinite(nsq)) return;  // overflow: skip the step (loss scaler backs off on the host)
+    if (max_norm > 0.f) {
+      const float gn = sqrtf(nsq) * inv_scale;
+      if (gn > max_norm) coef *= max_norm / (gn + 1e-6f);
+    }
+  }
+  const float step_size = lr / bc1;
+  const float bc2_sqrt = sqrtf(bc2);
+  const long long stride = static_cast<long long>(gridDim.x) * 256 * 8;
+  for (long long i = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 8; i < n;
+       i += stride) {
+    if (i + 8 <= n) {
+      float pv[8], gv[8], mv[8], vv[8];
+      load8(p + i, pv);
+      load8(g + i, gv);
+      load8(m + i, mv);
+      load8(v + i, vv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gg = gv[j] * coef;
+        mv[j] = beta1 * mv[j] + (1.f - beta1) * gg;
+        vv[j] = beta2 * vv[j] + (1.f - beta2) * gg * gg;
+        pv[j] -= lr * wd * pv[j];
+        const float denom = sqrtf(vv[j]) / bc2_sqrt + eps;
+        pv[j] -= step_size * mv[j] / denom;
+      }
+      store8(p + i, pv);
+      store8(m + i, mv);
+      store8(v + i, vv);
+      if (out_copy) store8(out_copy + i, pv);
+    } else {
+      for (long long j = i; j < n; ++j) {
+        const float gg = to_f32(g[j]) * coef;
+        m[j] = beta1 * m[j] + (1.f - beta1) * gg;
+        v[j] = beta2 * v[j] + (1.f - beta2) * gg * gg;
+        float pp = p[j] - lr * wd * p[j];
+        pp -= step_size * m[j] / (sqrtf(v[j]) / bc2_sqrt + eps);
+        p[j] = pp;
+        if (out_copy) out_copy[j] = from_f32<O>(pp);
+      }
+    }
+  }
+}
+
+static inline unsigned grid_for(long long n) {
+  long long blocks = (n + 256 * 8 - 1) / (256 * 8);
+  if (blocks > 2048) blocks = 2048;  // grid-stride the rest
+  if (blocks < 1) blocks = 1;
+  return static_cast<unsigned>(blocks);
+}
+
+}  // namespace lumen
+
+// out must be zeroed by the caller (it accumulates, so several buffers can share one scalar).
+extern "C" hipError_t lumen_grad_norm_sq(int gdtype, const void* g, long long n, float* out,
+                                         hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  dim3 grid(lumen::grid_for(n)), block(256);
+  if (gdtype == lumen::kF32)
+    hipLaunchKernelGGL(lumen::norm_sq_kernel<float>, grid, block, 0, st, (const float*)g, n, out);
+  else if (gdtype == lumen::kBF16)
+    hipLaunchKernelGGL(lumen::norm_sq_kernel<lumen::bf16>, grid, block, 0, st,
+                       (const lumen::bf16*)g, n, out);
+  else if (gdtype == lumen::kF16)
+    hipLaunchKernelGGL(lumen::norm_sq_kernel<lumen::fp16>, grid, block, 0, st,
+                       (const lumen::fp16*)g, n, out);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m, float* v,
+                                  int out_dtype, void* out_copy, long long n, float lr,
+                                  float beta1, float beta2, float eps, float wd, float bc1,
+                                  float bc2, float inv_scale, const float* norm_sq, float max_norm,
+                                  hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  dim3 grid(lumen::grid_for(n)), block(256);
+#define LUMEN_ADAMW(G, O)                                                                    \
+  hipLaunchKernelGGL((lumen::adamw_kernel<G, O>), grid, block, 0, st, p, (const G*)g, m, v, \
+                     (O*)out_copy, n, lr, beta1, beta2, eps, wd, bc1, bc2, inv_scale, norm_sq,  \
+                     max_norm)
+  if (gdtype == lumen::kF32) {
+    if (out_copy == nullptr || out_dtype == lumen::kF32) LUMEN_ADAMW(float, float);
+    else if (out_dtype == lumen::kBF16) LUMEN_ADAMW(float, lumen::bf16);
+    else LUMEN_ADAMW(float, lumen::fp16);
+  } else if (gdtype == lumen::kBF16) {
+    if (out_copy == nullptr || out_dtype == lumen::kF32) LUMEN_ADAMW(lumen::bf16, float);
+    else if (out_dtype == lumen::kBF16) LUMEN_ADAMW(lumen::bf16, lumen::bf16);
+    else LUMEN_ADAMW(lumen::bf16, lumen::fp16);
+  } else if (gdtype == lumen::kF16) {
+    if (out_copy == nullptr || out_dtype == lumen::kF32) LUMEN_ADAMW(lumen::fp16, float);
+    else if (out_dtype == lumen::kBF16) LUMEN_ADAMW(lumen::fp16, lumen::bf16);
+    else LUMEN_ADAMW(lumen::fp16, lumen::fp16);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef LUMEN_ADAMW
+  return hipGetLastError();
+}

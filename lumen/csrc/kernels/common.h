@@ -1,0 +1,128 @@
+// Common helpers for lumen's gfx950 (CDNA4) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave64: every lane-count constant is 64, block sizes are multiples of 64.
+//  * 16-bit activations (bf16 / fp16) are moved as 16-byte vectors (8 elements per lane),
+//    converted to f32 in registers and accumulated in f32.
+//  * launchers are `extern "C"` functions that take raw pointers + a hipStream_t and never
+//    allocate or synchronise (safe under hipGraph capture).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+namespace lumen {
+
+constexpr int kWave = 64;
+
+using bf16 = __hip_bfloat16;
+using fp16 = __half;
+
+// dtype codes shared with the Python binding
+enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2 };
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return __bfloat162float(x); }
+__device__ __forceinline__ float to_f32(fp16 x) { return __half2float(x); }
+
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return __float2bfloat16(x); }
+template <> __device__ __forceinline__ fp16 from_f32<fp16>(float x) { return __float2half(x); }
+
+// 16-byte vector of 8 half-precision elements.
+template <typename T> struct alignas(16) Vec8 { T v[8]; };
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* __restrict__ p, float (&out)[8]) {
+  const uint4 raw = *reinterpret_cast<const uint4*>(p);
+  const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = to_f32(e[j]);
+}
+
+template <>
+__device__ __forceinline__ void load8<float>(const float* __restrict__ p, float (&out)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+  out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+}
+
+template <typename T>
+__device__ __forceinline__ void store8(T* __restrict__ p, const float (&in)[8]) {
+  Vec8<T> o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o.v[j] = from_f32<T>(in[j]);
+  *reinterpret_cast<Vec8<T>*>(p) = o;
+}
+
+template <>
+__device__ __forceinline__ void store8<float>(float* __restrict__ p, const float (&in)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(in[0], in[1], in[2], in[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(in[4], in[5], in[6], in[7]);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Block-wide sum for blockDim.x = NT (multiple of 64). `scratch` holds NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += scratch[i];
+  __syncthreads();
+  return r;
+}
+
+template <int NT>
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r = fmaxf(r, scratch[i]);
+  __syncthreads();
+  return r;
+}
+
+// Counter-based RNG (a 32-bit avalanche hash of (seed, index)).  Used for LoRA dropout so that
+// the backward pass regenerates the forward's mask from (seed, index) instead of storing it.
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU;
+  x ^= x >> 15; x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t idx) {
+  uint32_t lo = static_cast<uint32_t>(idx), hi = static_cast<uint32_t>(idx >> 32);
+  uint32_t s0 = static_cast<uint32_t>(seed), s1 = static_cast<uint32_t>(seed >> 32);
+  return hash_u32(lo ^ hash_u32(hi ^ hash_u32(s0 ^ hash_u32(s1 + 0x9e3779b9U))));
+}
+
+// keep-probability test: returns true when the element survives dropout with prob (1-p).
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return rng_u32(seed, idx) >= thresh;
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+}  // namespace lumen

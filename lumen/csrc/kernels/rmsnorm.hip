@@ -1,0 +1,186 @@
+// Fused residual-add + RMSNorm, forward and backward.
+//
+// Reference behaviour: transformers' LlamaRMSNorm (upcast to f32, x * rsqrt(mean(x^2) + eps),
+// cast back, multiply by weight), invoked 65x per forward of Llama-2-7B
+// (reference training/train_baseline.py:122 loads the model that runs it).  Eager PyTorch runs it
+// as ~7 launches; here it is one memory-bound pass.
+//
+// Layout: one wave64 per row, each lane owns VPL 16-byte vectors (8 elements each) so a row of
+// up to VPL*512 elements stays in registers between the reduction and the write-back.  The block
+// holds 4 waves = 4 rows (256 threads), so a 1024-token micro-batch launches 256 blocks and larger
+// batches scale past the 256 CUs.
+//
+// fwd:  s = x (+ residual)           -> written to `s_out` when residual is fused
+//       y = s * rsqrt(mean(s^2)+eps) * w
+//       rstd[row] saved (f32) for backward
+// bwd:  g = dy * w;  ds = rstd * (g - s*rstd * mean(g * s*rstd)) (+ ds_residual)
+//       dw (optional) += sum_rows(dy * s * rstd)  (f32, per-block partials then atomics)
+#include "common.h"
+
+namespace lumen {
+
+template <typename T, int VPL>
+__global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
+    const T* __restrict__ x, const T* __restrict__ residual, const T* __restrict__ w,
+    T* __restrict__ y, T* __restrict__ s_out, float* __restrict__ rstd_out, int rows, int H,
+    float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = static_cast<size_t>(row) * H;
+  float v[VPL][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * 8;
+    if (c < H) {
+      load8(x + base + c, v[i]);
+      if (residual) {
+        float r[8];
+        load8(residual + base + c, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += r[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = wave_sum(ss);
+  const float rs = rsqrtf(ss / static_cast<float>(H) + eps);
+  if (lane == 0 && rstd_out) rstd_out[row] = rs;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * 8;
+    if (c < H) {
+      if (s_out) {
+        // round the residual stream to the activation dtype first: the normalisation below
+        // must see exactly the value the next layer reads back.
+        float sr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sr[j] = to_f32(from_f32<T>(v[i][j]));
+        store8(s_out + base + c, sr);
+      }
+      float wv[8], o[8];
+      load8(w + c, wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[j];
+      store8(y + base + c, o);
+    }
+  }
+}
+
+template <typename T, int VPL>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
+    const T* __restrict__ dy, const T* __restrict__ s, const T* __restrict__ w,
+    const float* __restrict__ rstd, const T* __restrict__ ds_res, T* __restrict__ dx,
+    float* __restrict__ dw, int rows, int H) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = static_cast<size_t>(row) * H;
+  const float rs = rstd[row];
+  float g[VPL][8], xh[VPL][8];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * 8;
+    if (c < H) {
+      float dyv[8], sv[8], wv[8];
+      load8(dy + base + c, dyv);
+      load8(s + base + c, sv);
+      load8(w + c, wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh[i][j] = sv[j] * rs;
+        g[i][j] = dyv[j] * wv[j];
+        dot += g[i][j] * xh[i][j];
+      }
+      if (dw) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(dw + c + j, dyv[j] * xh[i][j]);
+      }
+    }
+  }
+  dot = wave_sum(dot) / static_cast<float>(H);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * 8;
+    if (c < H) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - xh[i][j] * dot);
+      if (ds_res) {
+        float r[8];
+        load8(ds_res + base + c, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += r[j];
+      }
+      store8(dx + base + c, o);
+    }
+  }
+}
+
+template <typename T>
+static hipError_t launch_fwd(const void* x, const void* res, const void* w, void* y, void* s_out,
+                             float* rstd, int rows, int H, float eps, hipStream_t st) {
+  dim3 grid((rows + 3) / 4), block(256);
+  const int vpl = (H + 511) / 512;
+#define LUMEN_RMS_FWD(V)                                                                          \
+  hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, V>), grid, block, 0, st, (const T*)x, (const T*)res, \
+                     (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps)
+  if (vpl <= 1) LUMEN_RMS_FWD(1);
+  else if (vpl <= 2) LUMEN_RMS_FWD(2);
+  else if (vpl <= 4) LUMEN_RMS_FWD(4);
+  else if (vpl <= 8) LUMEN_RMS_FWD(8);
+  else if (vpl <= 16) LUMEN_RMS_FWD(16);
+  else return hipErrorInvalidValue;
+#undef LUMEN_RMS_FWD
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const float* rstd,
+                             const void* ds_res, void* dx, float* dw, int rows, int H,
+                             hipStream_t st) {
+  dim3 grid((rows + 3) / 4), block(256);
+  const int vpl = (H + 511) / 512;
+#define LUMEN_RMS_BWD(V)                                                                        \
+  hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, V>), grid, block, 0, st, (const T*)dy, (const T*)s, \
+                     (const T*)w, rstd, (const T*)ds_res, (T*)dx, dw, rows, H)
+  if (vpl <= 1) LUMEN_RMS_BWD(1);
+  else if (vpl <= 2) LUMEN_RMS_BWD(2);
+  else if (vpl <= 4) LUMEN_RMS_BWD(4);
+  else if (vpl <= 8) LUMEN_RMS_BWD(8);
+  else if (vpl <= 16) LUMEN_RMS_BWD(16);
+  else return hipErrorInvalidValue;
+#undef LUMEN_RMS_BWD
+  return hipGetLastError();
+}
+
+}  // namespace lumen
+
+extern "C" hipError_t lumen_rmsnorm_fwd(int dtype, const void* x, const void* residual,
+                                        const void* w, void* y, void* s_out, float* rstd, int rows,
+                                        int H, float eps, hipStream_t st) {
+  if (H % 8 != 0) return hipErrorInvalidValue;
+  if (dtype == lumen::kBF16)
+    return lumen::launch_fwd<lumen::bf16>(x, residual, w, y, s_out, rstd, rows, H, eps, st);
+  if (dtype == lumen::kF16)
+    return lumen::launch_fwd<lumen::fp16>(x, residual, w, y, s_out, rstd, rows, H, eps, st);
+  if (dtype == lumen::kF32)
+    return lumen::launch_fwd<float>(x, residual, w, y, s_out, rstd, rows, H, eps, st);
+  return hipErrorInvalidValue;
+}
+
+extern "C" hipError_t lumen_rmsnorm_bwd(int dtype, const void* dy, const void* s, const void* w,
+                                        const float* rstd, const void* ds_res, void* dx, float* dw,
+                                        int rows, int H, hipStream_t st) {
+  if (H % 8 != 0) return hipErrorInvalidValue;
+  if (dtype == lumen::kBF16)
+    return lumen::launch_bwd<lumen::bf16>(dy, s, w, rstd, ds_res, dx, dw, rows, H, st);
+  if (dtype == lumen::kF16)
+    return lumen::launch_bwd<lumen::fp16>(dy, s, w, rstd, ds_res, dx, dw, rows, H, st);
+  if (dtype == lumen::kF32)
+    return lumen::launch_bwd<float>(dy, s, w, rstd, ds_res, dx, dw, rows, H, st);
+  return hipErrorInvalidValue;
+}

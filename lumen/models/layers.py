@@ -1,0 +1,123 @@
+"""Building blocks shared by the model families: (LoRA-capable) fused linear layers, norms.
+
+``Linear`` owns a (usually frozen) base weight [out, in] and an optional LoRA adapter covering
+one or more output segments (q|k|v fused, gate|up fused).  The weight is always read through
+``self.weight_fn`` at forward AND backward time, so ZeRO-3's parameter coordinator can release a
+gathered weight after the forward and re-gather it before the backward without autograd pinning
+the full tensor.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops.lora import lora_linear, linear
+from ..ops.norm import rms_norm
+
+
+class LoRAAdapter(nn.Module):
+    """Stacked adapter for the adapted output segments of a (fused) linear layer.
+
+    lora_A: [n_seg * r, in]   rows r_off..r_off+r = segment's PEFT ``lora_A.weight`` [r, in]
+    lora_B: [sum(out_i), r]   rows b_off..b_off+out_i = segment's PEFT ``lora_B.weight`` [out_i, r]
+    ``segs`` = (n_off, n_len, r_off, b_off) with n_off the absolute output column of the segment.
+    """
+
+    def __init__(self, in_features: int, seg_offsets: Sequence[int], seg_sizes: Sequence[int],
+                 names: Sequence[str], r: int, alpha: float, dropout: float, device=None):
+        super().__init__()
+        self.r, self.alpha, self.dropout = r, alpha, dropout
+        self.scale = alpha / r
+        self.names = list(names)
+        self.seg_sizes = list(seg_sizes)
+        self.in_features = in_features
+        n = len(seg_sizes)
+        self.lora_A = nn.Parameter(torch.empty(n * r, in_features, dtype=torch.float32, device=device))
+        self.lora_B = nn.Parameter(torch.zeros(sum(seg_sizes), r, dtype=torch.float32, device=device))
+        self.segs: List[Tuple[int, int, int, int]] = []
+        b = 0
+        for i, (o, sz) in enumerate(zip(seg_offsets, seg_sizes)):
+            self.segs.append((o, sz, i * r, b))
+            b += sz
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        # PEFT: kaiming_uniform_(A, a=sqrt(5)) -> U(-1/sqrt(in), 1/sqrt(in)); B = 0
+        bound = 1.0 / math.sqrt(self.in_features)
+        with torch.no_grad():
+            self.lora_A.uniform_(-bound, bound)
+            self.lora_B.zero_()
+
+    def segment(self, name: str):
+        """(A_i, B_i) views for PEFT save/load."""
+        i = self.names.index(name)
+        n_off, n_len, r_off, b_off = self.segs[i]
+        return self.lora_A[r_off:r_off + self.r], self.lora_B[b_off:b_off + n_len]
+
+
+class Linear(nn.Module):
+    def __init__(self, in_features: int, out_features: int, bias: bool = False, dtype=None,
+                 device=None, seg_sizes: Optional[Sequence[int]] = None,
+                 seg_names: Optional[Sequence[str]] = None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features, dtype=dtype, device=device),
+                                   requires_grad=False)
+        self.bias = (nn.Parameter(torch.zeros(out_features, dtype=dtype, device=device),
+                                  requires_grad=False) if bias else None)
+        self.seg_sizes = list(seg_sizes) if seg_sizes else [out_features]
+        self.seg_names = list(seg_names) if seg_names else ["proj"]
+        self.lora: Optional[LoRAAdapter] = None
+        self.lora_enabled = True
+
+    def weight_fn(self) -> torch.Tensor:
+        return self.weight
+
+    def seg_offset(self, name: str) -> Tuple[int, int]:
+        i = self.seg_names.index(name)
+        return sum(self.seg_sizes[:i]), self.seg_sizes[i]
+
+    def add_lora(self, names: Sequence[str], r: int, alpha: float, dropout: float):
+        names = sorted(names, key=self.seg_names.index)
+        offs = [self.seg_offset(n)[0] for n in names]
+        sizes = [self.seg_offset(n)[1] for n in names]
+        self.lora = LoRAAdapter(self.in_features, offs, sizes, names, r, alpha, dropout,
+                                device=self.weight.device)
+        return self.lora
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        lo = self.lora
+        if lo is not None and self.lora_enabled:
+            p = lo.dropout if self.training else 0.0
+            # seed drawn from torch's global CPU RNG: activation checkpointing restores that state
+            # before recomputing, so the recomputed forward regenerates the same dropout mask
+            seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+            return lora_linear(x, self.weight_fn, self.bias, lo.lora_A, lo.lora_B, lo.segs, lo.r,
+                               lo.scale, p, seed, self.weight)
+        return linear(x, self.weight_fn, self.bias, self.weight)
+
+    @torch.no_grad()
+    def merge_lora(self):
+        """W += scale * B A for every adapted segment (serving: merge-on-load)."""
+        lo = self.lora
+        if lo is None:
+            return
+        W = self.weight
+        for (n_off, n_len, r_off, b_off) in lo.segs:
+            A = lo.lora_A[r_off:r_off + lo.r].float()
+            B = lo.lora_B[b_off:b_off + n_len].float()
+            W[n_off:n_off + n_len] = (W[n_off:n_off + n_len].float() + lo.scale * (B @ A)).to(W.dtype)
+        self.lora = None
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, hidden: int, eps: float, dtype=None, device=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(hidden, dtype=dtype, device=device), requires_grad=False)
+
+    def forward(self, x, residual=None):
+        return rms_norm(x, self.weight, self.eps, residual)

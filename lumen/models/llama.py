@@ -1,0 +1,164 @@
+"""Llama / Llama-2 decoder (the model the reference fine-tunes).
+
+Reference: ``AutoModelForCausalLM.from_pretrained("meta-llama/Llama-2-7b-hf", fp16)``
+(training/train_baseline.py:122-126) -> transformers LlamaForCausalLM: 32 layers, hidden 4096,
+32 heads x 128, SwiGLU FFN 11008, RMSNorm eps 1e-5, RoPE theta 1e4, vocab 32000, untied head.
+
+MI355X-first layout: q|k|v and gate|up are fused into one GEMM each (one weight, one launch, one
+LoRA "A" product for the shared input), RoPE is fused with the head-major split, residual adds
+are fused into the RMSNorms, the loss is fused with the LM head.  The decoder-layer loop calls
+an optional ZeRO-3 parameter coordinator (``self.coordinator``) around each unit (embedding,
+each layer, final norm + head) so partitioned weights are gathered / prefetched / released.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.utils.checkpoint as cp
+
+from ..ops.activation import swiglu
+from ..ops.attention import causal_attention
+from ..ops.loss import lm_head_cross_entropy
+from ..ops.rope import qkv_rope_split, rope_tables
+from .config import ModelConfig
+from .layers import Linear, RMSNorm
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype=None, device=None):
+        super().__init__()
+        self.cfg = cfg
+        D, nh, nkv, H = cfg.head_dim, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.hidden_size
+        self.qkv_proj = Linear(H, (nh + 2 * nkv) * D, dtype=dtype, device=device,
+                               seg_sizes=[nh * D, nkv * D, nkv * D],
+                               seg_names=["q_proj", "k_proj", "v_proj"])
+        self.o_proj = Linear(nh * D, H, dtype=dtype, device=device, seg_names=["o_proj"])
+
+    def forward(self, x2d: torch.Tensor, B: int, S: int, pos: Optional[torch.Tensor] = None):
+        c = self.cfg
+        qkv = self.qkv_proj(x2d)
+        cos, sin = rope_tables(c.head_dim, c.max_position_embeddings, c.rope_theta, x2d.device)
+        q, k, v = qkv_rope_split(qkv, B, S, c.num_attention_heads, c.num_key_value_heads,
+                                 c.head_dim, cos, sin, pos)
+        o = causal_attention(q, k, v)
+        return self.o_proj(o)
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype=None, device=None):
+        super().__init__()
+        H, Fd = cfg.hidden_size, cfg.intermediate_size
+        self.gate_up_proj = Linear(H, 2 * Fd, dtype=dtype, device=device, seg_sizes=[Fd, Fd],
+                                   seg_names=["gate_proj", "up_proj"])
+        self.down_proj = Linear(Fd, H, dtype=dtype, device=device, seg_names=["down_proj"])
+
+    def forward(self, x2d):
+        return self.down_proj(swiglu(self.gate_up_proj(x2d)))
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype=None, device=None):
+        super().__init__()
+        self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device)
+        self.self_attn = LlamaAttention(cfg, dtype, device)
+        self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device)
+        self.mlp = LlamaMLP(cfg, dtype, device)
+
+    def forward(self, h, res, B: int, S: int, pos=None):
+        y, s = self.input_layernorm(h, res)
+        a = self.self_attn(y, B, S, pos)
+        y2, s2 = self.post_attention_layernorm(a, s)
+        return self.mlp(y2), s2
+
+
+class LlamaForCausalLM(nn.Module):
+    """forward(input_ids [B,S], labels [B,S] already shifted (-100 = ignore), n_valid) -> loss."""
+
+    def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.config = cfg
+        self.dtype = dtype
+        H, V = cfg.hidden_size, cfg.vocab_size
+        self.embed_tokens = nn.Embedding(V, H, dtype=dtype, device=device)
+        self.embed_tokens.weight.requires_grad_(False)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, dtype, device)
+                                     for _ in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(H, cfg.rms_norm_eps, dtype, device)
+        self.lm_head = Linear(H, V, dtype=dtype, device=device, seg_names=["lm_head"])
+        self.gradient_checkpointing = False
+        self.coordinator = None  # ZeRO-3 parameter coordinator (lumen.parallel.zero)
+
+    # --- ZeRO-3 units, in execution order ------------------------------------------------------
+    def zero_units(self) -> List[List[nn.Module]]:
+        return ([[self.embed_tokens]] + [[l] for l in self.layers] + [[self.norm, self.lm_head]])
+
+    def lora_modules(self):
+        for name, m in self.named_modules():
+            if isinstance(m, Linear) and m.lora is not None:
+                yield name, m
+
+    def init_weights(self, std: float = 0.02, seed: int = 0):
+        """Random init (synthetic benches: no checkpoint download): Normal(0, std) like HF,
+        norms = 1.  Generated on the parameters' device (fast on GPU), identical on every rank
+        for the same seed."""
+        init_normal_(self, std, seed)
+
+    def _run_unit(self, idx, fn, *args):
+        c = self.coordinator
+        if c is None:
+            return fn(*args)
+        c.pre_forward(idx)
+        out = fn(*args)
+        return c.post_forward(idx, out)
+
+    def hidden_states(self, input_ids: torch.Tensor, pos: Optional[torch.Tensor] = None):
+        B, S = input_ids.shape
+        h = self._run_unit(0, lambda ids: F.embedding(ids, self.embed_tokens.weight),
+                           input_ids.reshape(-1))
+        res = None
+        for i, layer in enumerate(self.layers):
+            if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
+                fn = lambda h_, r_, L=layer: cp.checkpoint(L, h_, r_, B, S, pos, use_reentrant=False)  # noqa: E731
+            else:
+                fn = lambda h_, r_, L=layer: L(h_, r_, B, S, pos)  # noqa: E731
+            h, res = self._run_unit(i + 1, fn, h, res)
+        return h, res
+
+    def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
+                n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None):
+        h, res = self.hidden_states(input_ids, pos)
+        last = len(self.layers) + 1
+
+        def head(h_, r_):
+            y, _ = self.norm(h_, r_)
+            if labels is None:
+                return torch.matmul(y, self.lm_head.weight.t())
+            nv = int(n_valid) if n_valid is not None else int((labels != -100).sum())
+            return lm_head_cross_entropy(y, labels.reshape(-1), self.lm_head.weight_fn, nv,
+                                         self.lm_head.weight)
+
+        return self._run_unit(last, head, h, res)
+
+
+def init_normal_(model: nn.Module, std: float = 0.02, seed: int = 0):
+    gens = {}
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if "lora_" in name or p.numel() == 0:
+                continue
+            if p.dim() == 1:
+                if name.endswith("bias"):
+                    p.zero_()
+                else:
+                    p.fill_(1.0)
+                continue
+            dev = p.device
+            g = gens.get(str(dev))
+            if g is None:
+                g = torch.Generator(device=dev)
+                g.manual_seed(seed)
+                gens[str(dev)] = g
+            p.normal_(0.0, std, generator=g)

@@ -1,0 +1,117 @@
+"""OPT decoder (facebook/opt-125m), the model of BASELINE.json config 1
+("OPT-125m LoRA ZeRO-1 on CPU/gloo world_size=2").
+
+Architecture per transformers' OPTForCausalLM (pre-LN variant used by opt-125m): learned
+positions with offset 2, q/k/v/out_proj with bias (q|k|v fused here), LayerNorm, ReLU FFN
+fc1/fc2, final LayerNorm, LM head tied to the token embedding.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.utils.checkpoint as cp
+
+from ..ops.attention import causal_attention
+from ..ops.loss import lm_head_cross_entropy
+from .config import ModelConfig
+from .layers import Linear
+from .llama import init_normal_
+
+
+class OPTDecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype=None, device=None):
+        super().__init__()
+        H, Fd = cfg.hidden_size, cfg.ffn_dim or cfg.intermediate_size
+        self.cfg = cfg
+        self.self_attn_layer_norm = nn.LayerNorm(H, dtype=dtype, device=device)
+        self.qkv_proj = Linear(H, 3 * H, bias=True, dtype=dtype, device=device,
+                               seg_sizes=[H, H, H], seg_names=["q_proj", "k_proj", "v_proj"])
+        self.out_proj = Linear(H, H, bias=True, dtype=dtype, device=device,
+                               seg_names=["out_proj"])
+        self.final_layer_norm = nn.LayerNorm(H, dtype=dtype, device=device)
+        self.fc1 = Linear(H, Fd, bias=True, dtype=dtype, device=device, seg_names=["fc1"])
+        self.fc2 = Linear(Fd, H, bias=True, dtype=dtype, device=device, seg_names=["fc2"])
+        for p in self.parameters():
+            p.requires_grad_(False)
+
+    def forward(self, h, B: int, S: int):
+        c = self.cfg
+        nh, D = c.num_attention_heads, c.head_dim
+        x = self.self_attn_layer_norm(h)
+        qkv = self.qkv_proj(x).view(B, S, 3, nh, D)
+        q = qkv[:, :, 0].transpose(1, 2)
+        k = qkv[:, :, 1].transpose(1, 2)
+        v = qkv[:, :, 2].transpose(1, 2)
+        h = h + self.out_proj(causal_attention(q, k, v))
+        x = self.final_layer_norm(h)
+        return h + self.fc2(F.relu(self.fc1(x)))
+
+
+class OPTForCausalLM(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype=torch.float32, device=None):
+        super().__init__()
+        self.config = cfg
+        self.dtype = dtype
+        H, V = cfg.hidden_size, cfg.vocab_size
+        self.embed_tokens = nn.Embedding(V, H, dtype=dtype, device=device)
+        self.embed_positions = nn.Embedding(cfg.max_position_embeddings + 2, H, dtype=dtype,
+                                           device=device)
+        self.layers = nn.ModuleList([OPTDecoderLayer(cfg, dtype, device)
+                                     for _ in range(cfg.num_hidden_layers)])
+        self.final_layer_norm = nn.LayerNorm(H, dtype=dtype, device=device)
+        for p in self.parameters():
+            p.requires_grad_(False)
+        self.gradient_checkpointing = False
+        self.coordinator = None
+
+    def zero_units(self) -> List[List[nn.Module]]:
+        return ([[self.embed_tokens, self.embed_positions]] + [[l] for l in self.layers]
+                + [[self.final_layer_norm]])
+
+    def lora_modules(self):
+        for name, m in self.named_modules():
+            if isinstance(m, Linear) and m.lora is not None:
+                yield name, m
+
+    def init_weights(self, std: float = 0.02, seed: int = 0):
+        init_normal_(self, std, seed)
+
+    def _run_unit(self, idx, fn, *args):
+        c = self.coordinator
+        if c is None:
+            return fn(*args)
+        c.pre_forward(idx)
+        out = fn(*args)
+        return c.post_forward(idx, out)
+
+    def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
+                n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None):
+        B, S = input_ids.shape
+        if pos is None:
+            pos = torch.arange(S, device=input_ids.device).expand(B, S)
+
+        def embed(ids, p):
+            return (F.embedding(ids, self.embed_tokens.weight)
+                    + F.embedding(p + 2, self.embed_positions.weight)).reshape(B * S, -1)
+
+        h = self._run_unit(0, embed, input_ids, pos)
+        for i, layer in enumerate(self.layers):
+            if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
+                fn = lambda h_, L=layer: cp.checkpoint(L, h_, B, S, use_reentrant=False)  # noqa: E731
+            else:
+                fn = lambda h_, L=layer: L(h_, B, S)  # noqa: E731
+            h = self._run_unit(i + 1, fn, h)
+        last = len(self.layers) + 1
+
+        def head(h_):
+            y = self.final_layer_norm(h_)
+            wfn = lambda: self.embed_tokens.weight  # noqa: E731  (tied head)
+            if labels is None:
+                return torch.matmul(y, wfn().t())
+            nv = int(n_valid) if n_valid is not None else int((labels != -100).sum())
+            return lm_head_cross_entropy(y, labels.reshape(-1), wfn, nv, None)
+
+        return self._run_unit(last, head, h)

@@ -1,0 +1,101 @@
+"""Causal self-attention for training / prefill.
+
+Training uses PyTorch-ROCm's fused scaled-dot-product attention (flash kernels on gfx950) over
+head-major q/k/v produced by ``qkv_rope_split``; GQA is handled natively (no K/V repeat).  The
+output is returned token-major [B*S, nh*D] ready for the o_proj GEMM.
+
+Serving decode uses the paged-KV HIP kernel (``kernels/paged_attention.hip``): see
+``paged_decode`` below; prefill reuses the SDPA path per sequence then writes K/V to the cache.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from ._native import native, use_native
+
+
+def causal_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
+                     scale: Optional[float] = None) -> torch.Tensor:
+    """q [B,nh,S,D], k/v [B,nkv,S,D] -> [B*S, nh*D] (token-major)."""
+    B, nh, S, D = q.shape
+    nkv = k.shape[1]
+    if nkv != nh:
+        if q.is_cuda:
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale,
+                                               enable_gqa=True)
+        else:
+            rep = nh // nkv
+            o = F.scaled_dot_product_attention(q, k.repeat_interleave(rep, 1),
+                                               v.repeat_interleave(rep, 1), is_causal=True,
+                                               scale=scale)
+    else:
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale)
+    return o.transpose(1, 2).reshape(B * S, nh * D)
+
+
+def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                 block_tables: torch.Tensor, context_lens: torch.Tensor, max_context: int,
+                 scale: float, partition_size: int = 512) -> torch.Tensor:
+    """Single-token attention over a paged KV cache.
+
+    q [num_seqs, nh, D]; caches [num_blocks, nkv, block_size, D]; block_tables [num_seqs,
+    max_blocks] int32; context_lens [num_seqs] int32 (number of cached tokens incl. current).
+    """
+    num_seqs, nh, D = q.shape
+    nb, nkv, bs, _ = k_cache.shape
+    if use_native(q):
+        max_parts = max(1, math.ceil(max_context / partition_size))
+        out = torch.empty_like(q)
+        if max_parts > 1:
+            tm = torch.empty(num_seqs, nh, max_parts, device=q.device, dtype=torch.float32)
+            tl = torch.empty_like(tm)
+            to = torch.empty(num_seqs, nh, max_parts, D, device=q.device, dtype=torch.float32)
+        else:
+            tm = torch.empty(1, 1, 1, device=q.device, dtype=torch.float32)
+            tl, to = tm, tm
+        native().paged_attention_decode(out, q.contiguous(), k_cache, v_cache, block_tables,
+                                        context_lens, nkv, bs, block_tables.shape[1], scale, tm,
+                                        tl, to, partition_size)
+        return out
+    return paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale)
+
+
+def paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale):
+    num_seqs, nh, D = q.shape
+    nkv, bs = k_cache.shape[1], k_cache.shape[2]
+    g = nh // nkv
+    out = torch.empty_like(q)
+    for i in range(num_seqs):
+        L = int(context_lens[i])
+        nblk = (L + bs - 1) // bs
+        blks = block_tables[i, :nblk].long()
+        kk = k_cache[blks].permute(1, 0, 2, 3).reshape(nkv, nblk * bs, D)[:, :L].float()
+        vv = v_cache[blks].permute(1, 0, 2, 3).reshape(nkv, nblk * bs, D)[:, :L].float()
+        qq = q[i].float().view(nkv, g, D)
+        s = torch.einsum("hgd,hld->hgl", qq, kk) * scale
+        p = torch.softmax(s, -1)
+        out[i] = torch.einsum("hgl,hld->hgd", p, vv).reshape(nh, D).to(q.dtype)
+    return out
+
+
+def write_kv_cache(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor,
+                   v_cache: torch.Tensor, slot_mapping: torch.Tensor) -> None:
+    """k, v: [T, nkv, D] views (row stride may exceed nkv*D); slot_mapping [T] int64."""
+    T = slot_mapping.numel()
+    if T == 0:
+        return
+    nb, nkv, bs, D = k_cache.shape
+    if use_native(k_cache):
+        native().reshape_and_cache(k, v, k_cache, v_cache, slot_mapping, nkv, D, bs,
+                                   k.stride(0), v.stride(0))
+        return
+    sm = slot_mapping.long()
+    valid = sm >= 0
+    sm = sm[valid]
+    blk, off = sm // bs, sm % bs
+    k_cache[blk, :, off] = k[valid].to(k_cache.dtype)
+    v_cache[blk, :, off] = v[valid].to(v_cache.dtype)

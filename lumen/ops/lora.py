@@ -1,0 +1,242 @@
+"""LoRA linear: frozen base GEMM (hipBLASLt) + adapter GEMMs (HIP MFMA kernel ``kernels/lora.hip``).
+
+Reference behaviour: PEFT LoraLayer (reference training/train_baseline.py:131-141): for each
+adapted projection  y = x W^T + b + (alpha / r) * B(A(dropout(x))).  Here several projections
+that share the input (q|k|v, or gate|up) are ONE base GEMM over a fused weight and ONE adapter
+"A" GEMM over the stacked A matrices; each output segment then gets its own B product added in
+place.  Adapter weights are f32 (PEFT keeps adapters in f32); the adapter math is f32-exact.
+
+Segments: list of ``(n_off, n_len, r_off, b_off)``: output columns [n_off, n_off+n_len) use
+adapter rows A[r_off:r_off+r] and B[b_off:b_off+n_len, :] (B stores only adapted segments).
+
+Dropout uses a counter-based hash of (seed, token*K + feature) so the backward regenerates the
+forward's mask instead of storing a [T, K] tensor; ``dropout_mask_ref`` is the same hash in
+torch (bit-identical), used by the CPU path and the tests.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ._native import DTYPE_CODE, native, use_native
+
+Seg = Tuple[int, int, int, int]
+
+_M32 = 0xFFFFFFFF
+
+
+def _hash_u32(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    x = x ^ (x >> 16)
+    return x
+
+
+def _hash_scalar(x: int) -> int:
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & _M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & _M32
+    x ^= x >> 16
+    return x
+
+
+def rng_u32_ref(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    s0, s1 = seed & _M32, (seed >> 32) & _M32
+    inner = _hash_scalar(s0 ^ _hash_scalar((s1 + 0x9E3779B9) & _M32))
+    lo, hi = idx & _M32, idx >> 32
+    return _hash_u32(lo ^ _hash_u32(hi ^ inner))
+
+
+def drop_threshold(p: float) -> int:
+    return min(int(p * 4294967296.0), 0xFFFFFFFF) if p > 0 else 0
+
+
+def dropout_mask_ref(seed: int, T: int, K: int, p: float, device=None) -> torch.Tensor:
+    """Keep-mask [T, K] (bool) identical to the kernel's."""
+    idx = torch.arange(T * K, dtype=torch.int64, device=device).view(T, K)
+    return rng_u32_ref(seed, idx) >= drop_threshold(p)
+
+
+def _apply_dropout_ref(x, p, seed):
+    if p <= 0:
+        return x
+    keep = dropout_mask_ref(seed, x.shape[0], x.shape[1], p, x.device)
+    return torch.where(keep, x.float() / (1.0 - p), torch.zeros((), device=x.device)).to(x.dtype)
+
+
+# ----------------------------------------------------------------------------------------------
+# native launches
+# ----------------------------------------------------------------------------------------------
+
+def _ksplit(M, N, K, bn, nseg=1, target_blocks=1024, max_atomic=2_000_000, min_k=128):
+    tiles = math.ceil(M / 64) * math.ceil(N / bn) * nseg
+    ks = max(1, math.ceil(target_blocks / max(tiles, 1)))
+    ks = min(ks, max(1, math.ceil(K / min_k)), max(1, max_atomic // max(M * N * nseg, 1)))
+    return int(ks)
+
+
+def _bn(N):
+    return 16 if N <= 16 else 64
+
+
+def _lora_gemm(act, mode, X, W, Cm, ldx, ldw, cs_m, cs_n, alpha, segs6, ksplit, seed=0,
+               p=0.0, drop_ld=0):
+    bn = _bn(max(s[4] for s in segs6))
+    thresh = drop_threshold(p)
+    dscale = 1.0 / (1.0 - p) if p > 0 else 1.0
+    native().lora_gemm(act, mode, bn, X, W, Cm, ldx, ldw, cs_m, cs_n, float(alpha), int(ksplit),
+                       int(seed) & 0x7FFFFFFFFFFFFFFF, thresh, dscale, drop_ld,
+                       [list(map(int, s)) for s in segs6])
+
+
+def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed):
+    """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place)."""
+    T, K = x2d.shape
+    R = A.shape[0]
+    Ntot = y.shape[1]
+    act = DTYPE_CODE[x2d.dtype]
+    Z = torch.zeros(T, R, device=x2d.device, dtype=torch.float32)
+    bn = _bn(R)
+    _lora_gemm(act, 1, x2d, A, Z, K, K, R, 1, 1.0, [(0, 0, 0, T, R, K)],
+               _ksplit(T, R, K, bn), seed, p, K)
+    segs6 = [(r_off, b_off * r, n_off, T, n_len, r) for (n_off, n_len, r_off, b_off) in segs]
+    for i in range(0, len(segs6), 4):
+        _lora_gemm(act, 6, Z, B, y, R, r, Ntot, 1, scale, segs6[i:i + 4], 1)
+    return Z
+
+
+def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed,
+                    need_dA=True, need_dB=True):
+    """Returns (dA, dB); adds dZ A into dx in place."""
+    T, K = x2d.shape
+    R = A.shape[0]
+    Ntot = dy.shape[1]
+    act = DTYPE_CODE[dy.dtype]
+    dev = dy.device
+    dZ = torch.zeros(T, R, device=dev, dtype=torch.float32)
+    s2 = [(n_off, b_off * r, r_off, T, r, n_len) for (n_off, n_len, r_off, b_off) in segs]
+    for i in range(0, len(s2), 4):
+        chunk = s2[i:i + 4]
+        _lora_gemm(act, 2, dy, B, dZ, Ntot, r, R, 1, scale, chunk,
+                   _ksplit(T, r, max(s[5] for s in chunk), 16, len(chunk)))
+    dA = dB = None
+    if need_dA:
+        dA = torch.zeros(R, K, device=dev, dtype=torch.float32)
+        _lora_gemm(act, 3, dZ, x2d, dA, R, K, K, 1, 1.0, [(0, 0, 0, R, K, T)],
+                   _ksplit(R, K, T, 64), seed, p, K)
+    if need_dB:
+        dB = torch.zeros(B.shape[0], r, device=dev, dtype=torch.float32)
+        s4 = [(n_off, r_off, b_off * r, n_len, r, T) for (n_off, n_len, r_off, b_off) in segs]
+        for i in range(0, len(s4), 4):
+            chunk = s4[i:i + 4]
+            _lora_gemm(act, 4, dy, Z, dB, Ntot, R, r, 1, scale, chunk,
+                       _ksplit(max(s[3] for s in chunk), r, T, 16, len(chunk)))
+    if dx is not None:
+        _lora_gemm(act, 5, dZ, A, dx, R, K, K, 1, 1.0, [(0, 0, 0, T, K, R)], 1, seed, p, K)
+    return dA, dB
+
+
+# ----------------------------------------------------------------------------------------------
+# autograd
+# ----------------------------------------------------------------------------------------------
+
+class _LoraLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param):
+        W = weight_fn()
+        y = torch.matmul(x2d, W.t())
+        if bias is not None:
+            y.add_(bias)
+        Z = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed)
+        ctx.weight_fn = weight_fn
+        ctx.meta = (segs, r, scale, p, seed)
+        ctx.w_grad = w_param is not None and w_param.requires_grad
+        ctx.b_grad = bias is not None and bias.requires_grad
+        ctx.save_for_backward(x2d, A, B, Z)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, A, B, Z = ctx.saved_tensors
+        segs, r, scale, p, seed = ctx.meta
+        dy = dy.contiguous()
+        W = ctx.weight_fn()
+        dx = torch.matmul(dy, W) if ctx.needs_input_grad[0] else None
+        dA, dB = lora_bwd_native(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed,
+                                 ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+        dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
+        db = dy.sum(0) if ctx.b_grad else None
+        return dx, None, db, dA, dB, None, None, None, None, None, dw
+
+
+class _Linear(torch.autograd.Function):
+    """Plain (frozen or trainable) linear whose weight is re-fetched at backward."""
+
+    @staticmethod
+    def forward(ctx, x2d, weight_fn, bias, w_param):
+        W = weight_fn()
+        y = torch.matmul(x2d, W.t())
+        if bias is not None:
+            y.add_(bias)
+        ctx.weight_fn = weight_fn
+        ctx.w_grad = w_param is not None and w_param.requires_grad
+        ctx.b_grad = bias is not None and bias.requires_grad
+        ctx.save_for_backward(x2d if ctx.w_grad else torch.empty(0))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x2d,) = ctx.saved_tensors
+        W = ctx.weight_fn()
+        dy = dy.contiguous()
+        dx = torch.matmul(dy, W) if ctx.needs_input_grad[0] else None
+        dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
+        db = dy.sum(0) if ctx.b_grad else None
+        return dx, None, db, dw
+
+
+def linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor] = None,
+           w_param: Optional[torch.Tensor] = None) -> torch.Tensor:
+    shp = x.shape
+    x2d = x.reshape(-1, shp[-1])
+    if use_native(x2d):
+        y = _Linear.apply(x2d.contiguous(), weight_fn, bias, w_param)
+    else:
+        y = F.linear(x2d, weight_fn(), bias)
+    return y.view(*shp[:-1], y.shape[-1])
+
+
+def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: torch.Tensor,
+                B: torch.Tensor, segs: List[Seg], r: int, scale: float, p: float, seed: int,
+                w_param: Optional[torch.Tensor] = None) -> torch.Tensor:
+    shp = x.shape
+    x2d = x.reshape(-1, shp[-1])
+    if use_native(x2d):
+        y = _LoraLinear.apply(x2d.contiguous(), weight_fn, bias, A, B, segs, r, scale, p, seed,
+                              w_param)
+    else:
+        y = lora_linear_ref(x2d, weight_fn(), bias, A, B, segs, r, scale, p, seed)
+    return y.view(*shp[:-1], y.shape[-1])
+
+
+def lora_linear_ref(x2d, W, bias, A, B, segs, r, scale, p, seed):
+    y = F.linear(x2d, W, bias)
+    xd = _apply_dropout_ref(x2d, p, seed)
+    Z = xd.float() @ A.float().t()
+    parts = []
+    cur = 0
+    for (n_off, n_len, r_off, b_off) in sorted(segs):
+        if n_off > cur:
+            parts.append(torch.zeros(x2d.shape[0], n_off - cur, device=x2d.device))
+        parts.append(scale * (Z[:, r_off:r_off + r] @ B[b_off:b_off + n_len].float().t()))
+        cur = n_off + n_len
+    if cur < y.shape[1]:
+        parts.append(torch.zeros(x2d.shape[0], y.shape[1] - cur, device=x2d.device))
+    delta = torch.cat(parts, 1)
+    return (y.float() + delta).to(y.dtype)

@@ -1,0 +1,67 @@
+"""LM head + causal-LM cross-entropy (HIP kernel ``kernels/cross_entropy.hip``).
+
+Reference behaviour (transformers Llama, reference training/train_baseline.py:122): logits =
+lm_head(h) upcast to f32, CrossEntropyLoss(ignore_index=-100) averaged over non-ignored shifted
+labels.  Here the logits stay 16-bit, the CE kernel turns them into d(loss)/d(logits) in place
+during the forward (scaled by 1/num_valid), and the backward is a single GEMM dH = dlogits @ W
+times the upstream scalar.  ``weight_fn`` returns the (possibly ZeRO-3-gathered) weight when
+called, so the backward re-reads it through the parameter coordinator instead of pinning it.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+import torch.nn.functional as F
+
+from ._native import native, use_native
+
+IGNORE_INDEX = -100
+
+
+class _LMHeadCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, labels, weight_fn, n_valid, dummy_w):
+        W = weight_fn()
+        logits = torch.matmul(h, W.t())
+        loss_sum = torch.zeros(1, dtype=torch.float32, device=h.device)
+        native().cross_entropy(logits, labels, loss_sum, None, IGNORE_INDEX,
+                               1.0 / max(n_valid, 1), True)
+        ctx.weight_fn = weight_fn
+        ctx.w_grad = dummy_w is not None and dummy_w.requires_grad
+        ctx.save_for_backward(logits, h if ctx.w_grad else torch.empty(0))
+        return (loss_sum / max(n_valid, 1)).squeeze(0)
+
+    @staticmethod
+    def backward(ctx, g):
+        dlogits, h = ctx.saved_tensors
+        W = ctx.weight_fn()
+        dh = torch.matmul(dlogits, W)
+        dh.mul_(g.to(dh.dtype))
+        dw = None
+        if ctx.w_grad:
+            dw = torch.matmul(dlogits.t(), h) * g.to(h.dtype)
+        return dh, None, None, None, dw
+
+
+def lm_head_cross_entropy(h: torch.Tensor, labels: torch.Tensor,
+                          weight_fn: Callable[[], torch.Tensor], n_valid: int,
+                          weight_param: torch.Tensor = None) -> torch.Tensor:
+    """Mean CE over labels != -100.  h [T, H], labels [T] (already shifted)."""
+    if use_native(h):
+        return _LMHeadCE.apply(h.contiguous(), labels.contiguous(), weight_fn, int(n_valid),
+                               weight_param)
+    W = weight_fn()
+    logits = torch.matmul(h, W.t()).float()
+    loss = F.cross_entropy(logits, labels, ignore_index=IGNORE_INDEX, reduction="sum")
+    return loss / max(int(n_valid), 1)
+
+
+def cross_entropy_rows(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Per-row CE (no grad) -- used by evaluation / serving logprob checks."""
+    if use_native(logits):
+        out = torch.empty(logits.shape[0], dtype=torch.float32, device=logits.device)
+        native().cross_entropy(logits.contiguous(), labels.contiguous(), None, out, IGNORE_INDEX,
+                               1.0, False)
+        return out
+    return F.cross_entropy(logits.float(), labels, ignore_index=IGNORE_INDEX, reduction="none")

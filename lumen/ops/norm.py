@@ -1,0 +1,68 @@
+"""Fused residual-add + RMSNorm (HIP kernel ``kernels/rmsnorm.hip``; torch reference on CPU).
+
+``rms_norm(x, w, eps, residual)`` returns ``(y, s)`` with ``s = x + residual`` (the new residual
+stream, ``x`` itself when no residual is given) and ``y = s * rsqrt(mean(s^2) + eps) * w``.
+Mirrors transformers' LlamaRMSNorm (used by the model loaded at
+reference training/train_baseline.py:122) with the residual add of the decoder layer fused in.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._native import native, use_native
+
+
+def rms_norm_ref(x, w, eps, residual=None):
+    s = x if residual is None else (x.float() + residual.float()).to(x.dtype)
+    sf = s.float()
+    rstd = torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps)
+    y = (sf * rstd * w.float()).to(x.dtype)
+    return y, s
+
+
+class _FusedAddRMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, w, eps):
+        C = native()
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        rows = x.numel() // x.shape[-1]
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        if residual is not None:
+            s = torch.empty_like(x)
+            C.rmsnorm_fwd(x, residual.contiguous(), w, y, s, rstd, eps)
+        else:
+            s = x
+            C.rmsnorm_fwd(x, None, w, y, None, rstd, eps)
+        ctx.save_for_backward(s, w, rstd)
+        ctx.has_res = residual is not None
+        ctx.w_grad = w.requires_grad
+        if residual is not None:
+            return y, s
+        # no residual: s is x itself; hand back a view so autograd tracks it as an output
+        return y, s.view_as(s)
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        C = native()
+        s, w, rstd = ctx.saved_tensors
+        dx = torch.empty_like(s)
+        dw = torch.zeros(w.shape, dtype=torch.float32, device=w.device) if ctx.w_grad else None
+        C.rmsnorm_bwd(dy.contiguous(), s, w, rstd,
+                      ds.contiguous() if ds is not None else None, dx, dw)
+        dres = dx if ctx.has_res else None
+        return dx, dres, (dw.to(w.dtype) if dw is not None else None), None
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
+             residual: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    if use_native(x):
+        return _FusedAddRMSNorm.apply(x, residual, w, eps)
+    return rms_norm_ref(x, w, eps, residual)
+
+
+def layer_norm(x, w, b, eps):
+    """OPT LayerNorm (torch: small model / CPU path)."""
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), w, b, eps)

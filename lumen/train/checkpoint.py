@@ -1,0 +1,101 @@
+"""Checkpoint / resume.
+
+Reference behaviour: HF Trainer + DeepSpeed periodic checkpoints ``{output_dir}/checkpoint-{N}``
+every ``save_steps`` (100) with ``save_total_limit`` rotation (training/train_deepspeed_zero1.py:
+242-245), discovery of the newest ``checkpoint-<N>`` for ``--resume_from_checkpoint``
+(training/train_deepspeed_zero1.py:266-279) and a final PEFT export (train_baseline.py:226-228).
+The HF/DeepSpeed layout holds the adapter, ``trainer_state.json``, per-rank RNG state and a
+``global_step{N}/`` dir of ZeRO shards + ``latest``.
+
+lumen writes the same directory shape with its own shard format:
+    checkpoint-N/adapter_config.json, adapter_model.safetensors     (rank 0, PEFT format)
+    checkpoint-N/trainer_state.json                                 (rank 0)
+    checkpoint-N/rng_state_{rank}.pth                               (every rank)
+    checkpoint-N/global_stepN/zero_pp_rank_{r}_mp_rank_00_optim_states.pt  (every rank: f32
+        master / exp_avg / exp_avg_sq shard + step + loss-scaler state; tensors and plain
+        Python values only, so it loads with ``torch.load(weights_only=True)``)
+    checkpoint-N/latest                                             ("global_stepN")
+Resume is resolved on EVERY rank (fixes reference quirk 7: rank-0-only discovery).
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import shutil
+from typing import Dict, Optional
+
+import torch
+
+from ..lora import load_adapter, save_adapter
+from ..parallel.dist import barrier
+
+_CKPT_RE = re.compile(r"^checkpoint-(\d+)$")
+
+
+def list_checkpoints(output_dir: str):
+    if not os.path.isdir(output_dir):
+        return []
+    out = []
+    for d in os.listdir(output_dir):
+        m = _CKPT_RE.match(d)
+        if m and os.path.isdir(os.path.join(output_dir, d)):
+            out.append((int(m.group(1)), os.path.join(output_dir, d)))
+    return sorted(out)
+
+
+def latest_checkpoint(output_dir: str) -> Optional[str]:
+    """Newest *complete* checkpoint-<N> (trainer_state.json present)."""
+    for step, path in reversed(list_checkpoints(output_dir)):
+        if os.path.exists(os.path.join(path, "trainer_state.json")):
+            return path
+    return None
+
+
+def _rng_state():
+    st = {"cpu": torch.get_rng_state()}
+    if torch.cuda.is_available():
+        st["cuda"] = torch.cuda.get_rng_state()
+    return st
+
+
+def save_checkpoint(output_dir: str, engine, model, trainer_state: Dict, env,
+                    save_total_limit: Optional[int] = None, base_model_name: str = "") -> str:
+    step = engine.global_step
+    path = os.path.join(output_dir, f"checkpoint-{step}")
+    os.makedirs(path, exist_ok=True)
+    gs = os.path.join(path, f"global_step{step}")
+    os.makedirs(gs, exist_ok=True)
+    sd = engine.state_dict()
+    torch.save(sd, os.path.join(gs, f"zero_pp_rank_{env.rank}_mp_rank_00_optim_states.pt"))
+    torch.save(_rng_state(), os.path.join(path, f"rng_state_{env.rank}.pth"))
+    barrier()
+    if env.rank == 0:
+        save_adapter(model, path, base_model_name)
+        with open(os.path.join(path, "latest"), "w") as f:
+            f.write(f"global_step{step}")
+        with open(os.path.join(path, "trainer_state.json"), "w") as f:
+            json.dump(trainer_state, f, indent=2)
+        if save_total_limit:
+            ckpts = list_checkpoints(output_dir)
+            for _, old in ckpts[:-save_total_limit]:
+                shutil.rmtree(old, ignore_errors=True)
+    barrier()
+    return path
+
+
+def load_checkpoint(path: str, engine, model, env) -> Dict:
+    with open(os.path.join(path, "latest")) as f:
+        tag = f.read().strip()
+    load_adapter(model, path, apply=False)
+    shard = os.path.join(path, tag, f"zero_pp_rank_{env.rank}_mp_rank_00_optim_states.pt")
+    sd = torch.load(shard, map_location="cpu", weights_only=True)
+    engine.load_state_dict(sd)
+    rng = os.path.join(path, f"rng_state_{env.rank}.pth")
+    if os.path.exists(rng):
+        st = torch.load(rng, map_location="cpu", weights_only=True)
+        torch.set_rng_state(st["cpu"])
+        if "cuda" in st and torch.cuda.is_available():
+            torch.cuda.set_rng_state(st["cuda"])
+    with open(os.path.join(path, "trainer_state.json")) as f:
+        return json.load(f)

@@ -1,0 +1,218 @@
+"""Training loop (replaces the reference's HF Trainer usage).
+
+Reference behaviour kept: per-rank sharded data, micro-batch x grad-accum, logging every
+``logging_steps`` (10) optimizer steps with keys {loss, grad_norm, learning_rate, epoch}
+(training/train.ipynb:339), periodic ``checkpoint-N`` saves with rotation, resume, final PEFT
+export to ``{output_dir}/final`` and a metrics row (training/train_baseline.py:236-255).
+Added: tokens/s and TFLOP/s, ``max_steps``, synthetic data, random init (offline).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from ..data import CausalLMCollator, ShardedSampler, build_dataset, load_tokenizer
+from ..lora import LoraConfig, apply_lora, print_trainable_parameters, save_adapter
+from ..models import build_model, get_config
+from ..parallel.dist import DistEnv, all_reduce_scalar, barrier
+from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+from .config import DSConfig
+from .engine import ZeroEngine
+
+
+@dataclass
+class TrainArgs:
+    model_name: str = "meta-llama/Llama-2-7b-hf"
+    dataset_path: Optional[str] = "./data/glaive_code_full"
+    output_dir: str = "./checkpoints/run"
+    num_train_epochs: int = 3
+    per_device_train_batch_size: int = 1
+    gradient_accumulation_steps: int = 1
+    learning_rate: float = 2e-4
+    lora_r: int = 16
+    lora_alpha: Optional[float] = None
+    lora_dropout: float = 0.05
+    lora_targets: List[str] = field(default_factory=lambda: ["q_proj", "k_proj", "v_proj", "o_proj"])
+    max_length: int = 512
+    seed: int = 42
+    logging_steps: int = 10
+    save_strategy: str = "steps"   # steps | epoch | no
+    save_steps: int = 100
+    save_total_limit: Optional[int] = 3
+    gradient_checkpointing: bool = False
+    resume_from_checkpoint: bool = False
+    max_steps: int = -1
+    warmup_steps: int = 0
+    synthetic: bool = False
+    synthetic_samples: int = 1024
+    init: str = "auto"
+    experiment: str = "run"
+    strategy: str = ""
+    save_final: bool = True
+    log_file: Optional[str] = None
+
+
+def model_flops_per_token(cfg, seq_len: int, lora: bool = True) -> float:
+    """Approximate training FLOPs/token: fwd 2N + bwd-dX 2N (+ dW 2N when training the base),
+    attention 4*L*S*H fwd (x2 for bwd).  Frozen-base LoRA has no weight-gradient GEMMs."""
+    n = cfg.num_params() - cfg.vocab_size * cfg.hidden_size  # embedding gather is not a GEMM
+    gemm = (4.0 if lora else 6.0) * n
+    attn = 4.0 * cfg.num_hidden_layers * seq_len * cfg.hidden_size * 0.5 * 3  # causal, fwd+bwd
+    return gemm + attn
+
+
+class Trainer:
+    def __init__(self, args: TrainArgs, ds: DSConfig, env: DistEnv, printer=None):
+        self.args, self.ds, self.env = args, ds, env
+        self.print = printer or (lambda *a, **k: print(*a, **k, flush=True) if env.is_main else None)
+        torch.manual_seed(args.seed)
+        dt = ds.torch_dtype
+        cfg = get_config(args.model_name)
+        self.model_cfg = cfg
+        t0 = time.time()
+        self.model = build_model(args.model_name, dtype=dt, device=env.device, init=args.init,
+                                 seed=args.seed)
+        self.print(f"[lumen] model {cfg.name}: {cfg.num_params():,} params, dtype {dt}, "
+                   f"built in {time.time() - t0:.1f}s")
+        lcfg = LoraConfig(r=args.lora_r, lora_alpha=args.lora_alpha, lora_dropout=args.lora_dropout,
+                          target_modules=args.lora_targets)
+        apply_lora(self.model, lcfg)
+        self.model.gradient_checkpointing = args.gradient_checkpointing
+        self.model.train()
+        trainable, total = print_trainable_parameters(self.model, self.print)
+        self.n_trainable, self.n_total = trainable, total
+        self.engine = ZeroEngine(self.model, ds, env)
+        self.tokenizer = load_tokenizer(args.model_name, cfg.vocab_size)
+        pad = getattr(self.tokenizer, "pad_token_id", cfg.eos_token_id)
+        self.dataset = build_dataset(args.dataset_path, self.tokenizer, args.max_length,
+                                     args.synthetic, args.synthetic_samples, cfg.vocab_size,
+                                     seed=args.seed)
+        self.collator = CausalLMCollator(pad_id=pad, max_length=args.max_length)
+        self.sampler = ShardedSampler(len(self.dataset), env.rank, env.world_size, seed=args.seed)
+        self.log_history: List[Dict] = []
+        self.flops_per_token = model_flops_per_token(cfg, args.max_length)
+
+    # ---------------------------------------------------------------------------------------
+    def _batches(self, epoch: int, skip_samples: int):
+        mb = self.ds.micro_batch
+        idx = self.sampler.indices(epoch)[skip_samples:]
+        for i in range(0, len(idx) - mb + 1, mb):
+            yield [self.dataset[j] for j in idx[i:i + mb]]
+
+    def _to_device(self, b):
+        d = self.env.device
+        return {"input_ids": b["input_ids"].to(d, non_blocking=True),
+                "labels": b["labels"].to(d, non_blocking=True),
+                "n_valid": b["n_valid"], "n_tokens": b["n_tokens"]}
+
+    def steps_per_epoch(self) -> int:
+        return len(self.sampler) // (self.ds.micro_batch * self.ds.grad_accum)
+
+    def train(self) -> Dict:
+        a, ds, env, eng = self.args, self.ds, self.env, self.engine
+        start_epoch, skip = 0, 0
+        if a.resume_from_checkpoint:
+            ck = latest_checkpoint(a.output_dir)
+            if ck:
+                st = load_checkpoint(ck, eng, self.model, env)
+                self.log_history = st.get("log_history", [])
+                start_epoch = int(st.get("epoch_int", 0))
+                skip = int(st.get("samples_in_epoch", 0))
+                self.print(f"[lumen] resumed from {ck} (step {eng.global_step})")
+            else:
+                self.print("[lumen] no checkpoint found; starting fresh")
+        spe = max(self.steps_per_epoch(), 1)
+        total_steps = a.max_steps if a.max_steps > 0 else spe * a.num_train_epochs
+        self.print(f"[lumen] ZeRO-{ds.stage} world={env.world_size} micro={ds.micro_batch} "
+                   f"accum={ds.grad_accum} effective batch={ds.train_batch_size} "
+                   f"steps={total_steps}")
+        t_start = time.time()
+        tokens = 0
+        samples = 0
+        loss_acc = torch.zeros((), device=env.device)
+        loss_n = 0
+        last_loss = float("nan")
+        done = eng.global_step >= total_steps
+        epoch = start_epoch
+        while not done:
+            if a.max_steps <= 0 and epoch >= a.num_train_epochs:
+                break
+            samples_in_epoch = skip
+            produced = 0
+            for raw in self._batches(epoch, skip):
+                produced += 1
+                b = self._to_device(self.collator(raw))
+                loss = eng.forward(b)
+                eng.backward(loss)
+                loss_acc += loss.detach().float()
+                loss_n += 1
+                tokens += b["n_tokens"]
+                samples += len(raw)
+                samples_in_epoch += len(raw)
+                if eng.step():
+                    if eng.global_step % a.logging_steps == 0 or eng.global_step == total_steps:
+                        l = all_reduce_scalar(float(loss_acc.item()) / max(loss_n, 1)) / env.world_size
+                        gn = float(eng.last_grad_norm.item()) if eng.last_grad_norm is not None else 0.0
+                        rec = {"loss": round(l, 4), "grad_norm": gn, "learning_rate": eng.last_lr,
+                               "epoch": round(epoch + samples_in_epoch / max(len(self.sampler), 1), 4),
+                               "step": eng.global_step}
+                        el = time.time() - t_start
+                        rec["tokens_per_second"] = round(tokens * env.world_size / max(el, 1e-9), 1)
+                        self.log_history.append(rec)
+                        self.print(json.dumps(rec))
+                        last_loss = l
+                        loss_acc.zero_()
+                        loss_n = 0
+                    if (a.save_strategy == "steps" and a.save_steps > 0
+                            and eng.global_step % a.save_steps == 0):
+                        self._save(epoch, samples_in_epoch)
+                    if eng.global_step >= total_steps:
+                        done = True
+                        break
+            skip = 0
+            if produced == 0:
+                break
+            if not done and a.save_strategy == "epoch":
+                self._save(epoch + 1, 0)
+            epoch += 1
+        if env.device.type == "cuda":
+            torch.cuda.synchronize()
+        elapsed = time.time() - t_start
+        if loss_n:
+            last_loss = all_reduce_scalar(float(loss_acc.item()) / loss_n) / env.world_size
+        if a.save_final:
+            self.save_final()
+        tps = all_reduce_scalar(tokens) / max(elapsed, 1e-9)
+        sps = all_reduce_scalar(samples) / max(elapsed, 1e-9)
+        peak = (torch.cuda.max_memory_allocated(env.device) / 1e9
+                if env.device.type == "cuda" else 0.0)
+        return {"training_time_hours": elapsed / 3600.0, "samples_per_second": sps,
+                "tokens_per_second": tps, "peak_memory_gb": peak, "final_loss": last_loss,
+                "global_step": eng.global_step, "skipped_steps": eng.skipped_steps,
+                "tflops_per_gpu": tps * self.flops_per_token / env.world_size / 1e12}
+
+    def _trainer_state(self, epoch: int, samples_in_epoch: int) -> Dict:
+        return {"global_step": self.engine.global_step, "epoch_int": epoch,
+                "samples_in_epoch": samples_in_epoch, "log_history": self.log_history,
+                "world_size": self.env.world_size, "zero_stage": self.ds.stage,
+                "train_batch_size": self.ds.train_batch_size, "args": asdict(self.args)}
+
+    def _save(self, epoch: int, samples_in_epoch: int):
+        p = save_checkpoint(self.args.output_dir, self.engine, self.model,
+                            self._trainer_state(epoch, samples_in_epoch), self.env,
+                            self.args.save_total_limit, self.args.model_name)
+        self.print(f"[lumen] saved {p}")
+
+    def save_final(self):
+        final = os.path.join(self.args.output_dir, "final")
+        if self.env.is_main:
+            save_adapter(self.model, final, self.args.model_name)
+            self.tokenizer.save_pretrained(final)
+        barrier()
+        self.print(f"[lumen] final adapter saved to {final}")

@@ -1,0 +1,259 @@
+"""Numerics of every HIP kernel against a plain PyTorch f32 reference of the same op (GPU)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from lumen.ops._native import native, native_error
+
+    assert native() is not None, f"native extension must load on the GPU box: {native_error()!r}"
+    torch.manual_seed(0)
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H", [768, 4096, 8192])
+def test_rmsnorm_fwd_bwd(dtype, H):
+    from lumen.ops.norm import rms_norm, rms_norm_ref
+
+    T = 300
+    x = torch.randn(T, H, device=DEV, dtype=dtype, requires_grad=True)
+    r = torch.randn(T, H, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(dtype)
+    y, s = rms_norm(x, w, 1e-5, r)
+    x2 = x.detach().float().requires_grad_(True)
+    r2 = r.detach().float().requires_grad_(True)
+    y2, s2 = rms_norm_ref(x2, w.float(), 1e-5, r2)
+    assert rel(s, s2) < 1e-2 and rel(y, y2) < 1e-2
+    dy = torch.randn_like(y)
+    ds = torch.randn_like(s)
+    torch.autograd.backward([y, s], [dy, ds])
+    torch.autograd.backward([y2, s2], [dy.float(), ds.float()])
+    assert rel(x.grad, x2.grad) < 2e-2
+    assert rel(r.grad, r2.grad) < 2e-2
+    # no-residual variant
+    x3 = x.detach().clone().requires_grad_(True)
+    y3, s3 = rms_norm(x3, w, 1e-5)
+    x4 = x.detach().float().requires_grad_(True)
+    y4, _ = rms_norm_ref(x4, w.float(), 1e-5)
+    assert rel(y3, y4) < 1e-2
+    y3.backward(dy)
+    y4.backward(dy.float())
+    assert rel(x3.grad, x4.grad) < 2e-2
+
+
+@pytest.mark.parametrize("nh,nkv", [(32, 32), (8, 2)])
+def test_qkv_rope_split(nh, nkv):
+    from lumen.ops.rope import qkv_rope_split, qkv_rope_split_ref, rope_tables
+
+    B, S, D = 2, 64, 128
+    cos, sin = rope_tables(D, 4096, 10000.0, DEV)
+    qkv = torch.randn(B * S, (nh + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16,
+                      requires_grad=True)
+    q, k, v = qkv_rope_split(qkv, B, S, nh, nkv, D, cos, sin)
+    qkv2 = qkv.detach().float().requires_grad_(True)
+    q2, k2, v2 = qkv_rope_split_ref(qkv2, B, S, nh, nkv, D, cos, sin)
+    for a, b in ((q, q2), (k, k2), (v, v2)):
+        assert a.shape == b.shape and rel(a, b) < 1e-2
+    g = [torch.randn_like(t) for t in (q, k, v)]
+    torch.autograd.backward([q, k, v], g)
+    torch.autograd.backward([q2, k2, v2], [t.float() for t in g])
+    assert rel(qkv.grad, qkv2.grad) < 1e-2
+    # explicit positions
+    pos = torch.randint(0, 4000, (B * S,), device=DEV)
+    qp, kp, _ = qkv_rope_split(qkv.detach(), B, S, nh, nkv, D, cos, sin, pos)
+    qr, kr, _ = qkv_rope_split_ref(qkv.detach().float(), B, S, nh, nkv, D, cos, sin, pos)
+    assert rel(qp, qr) < 1e-2 and rel(kp, kr) < 1e-2
+
+
+def test_rope_inplace():
+    from lumen.ops.rope import rope_inplace, rope_tables, _rotate_ref
+
+    T, nh, D = 37, 4, 128
+    cos, sin = rope_tables(D, 4096, 10000.0, DEV)
+    x = torch.randn(T, 3 * nh * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 2000, (T,), device=DEV)
+    ref = x.clone().float()
+    view = ref[:, nh * D: 2 * nh * D].view(T, nh, D)
+    view.copy_(_rotate_ref(view, cos[pos][:, None], sin[pos][:, None]))
+    rope_inplace(x, pos, nh, D, cos, sin, col_offset=nh * D)
+    assert rel(x, ref) < 1e-2
+
+
+def test_swiglu():
+    from lumen.ops.activation import swiglu, swiglu_ref
+
+    gu = torch.randn(333, 2 * 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = swiglu(gu)
+    gu2 = gu.detach().float().requires_grad_(True)
+    y2 = swiglu_ref(gu2)
+    assert rel(y, y2) < 1e-2
+    d = torch.randn_like(y)
+    y.backward(d)
+    y2.backward(d.float())
+    assert rel(gu.grad, gu2.grad) < 1e-2
+
+
+@pytest.mark.parametrize("V", [32000, 50272])
+def test_lm_head_cross_entropy(V):
+    from lumen.ops.loss import lm_head_cross_entropy
+
+    T, H = 257, 256
+    h = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    W = (torch.randn(V, H, device=DEV) * 0.05).to(torch.bfloat16)
+    labels = torch.randint(0, V, (T,), device=DEV)
+    labels[::7] = -100
+    n_valid = int((labels != -100).sum())
+    loss = lm_head_cross_entropy(h, labels, lambda: W, n_valid)
+    h2 = h.detach().float().requires_grad_(True)
+    logits = h2 @ W.float().t()
+    loss2 = torch.nn.functional.cross_entropy(logits, labels, ignore_index=-100)
+    assert abs(loss.item() - loss2.item()) < 2e-2 * max(1, abs(loss2.item()))
+    (loss * 3).backward()
+    (loss2 * 3).backward()
+    assert rel(h.grad, h2.grad) < 3e-2
+
+
+def test_grad_norm_and_adamw():
+    from lumen.ops._native import native
+    from lumen.parallel.zero import _adamw_torch
+
+    C = native()
+    n = 1_000_003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV) * 3
+    m = torch.randn(n, device=DEV).abs() * 0.1
+    v = torch.rand(n, device=DEV) * 0.1
+    ns = torch.zeros(1, device=DEV)
+    C.grad_norm_sq(g, ns)
+    assert abs(ns.item() - g.double().pow(2).sum().item()) / g.double().pow(2).sum().item() < 1e-5
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    lr, b1, b2, eps, wd, inv = 1e-3, 0.9, 0.999, 1e-8, 0.01, 0.5
+    maxn = 1.0
+    copy = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    C.adamw(p, g, m, v, copy, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, inv, ns, maxn)
+    gn = math.sqrt(ns.item()) * inv
+    coef = inv * (maxn / (gn + 1e-6) if gn > maxn else 1.0)
+    _adamw_torch(p2, g, m2, v2, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, coef)
+    assert (p - p2).abs().max().item() < 1e-5
+    assert (m - m2).abs().max().item() < 1e-6
+    assert rel(copy, p2) < 1e-2
+    # overflow -> no update
+    p3 = p.clone()
+    bad = torch.tensor([float("inf")], device=DEV)
+    C.adamw(p, g, m, v, None, lr, b1, b2, eps, wd, 0.1, 0.1, 1.0, bad, 1.0)
+    assert torch.equal(p, p3)
+
+
+@pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_lora_linear_fwd_bwd(segs_kind, p_drop):
+    from lumen.ops.lora import lora_linear, lora_linear_ref
+
+    T, K, r = 512 + 64, 1024, 16
+    if segs_kind == "qkv":
+        sizes = [1024, 1024, 1024]
+        segs = [(0, 1024, 0, 0), (1024, 1024, 16, 1024), (2048, 1024, 32, 2048)]
+    elif segs_kind == "o":
+        sizes = [1024]
+        segs = [(0, 1024, 0, 0)]
+    else:  # GQA q|k|v with adapters on q and v only
+        sizes = [1024, 256, 256]
+        segs = [(0, 1024, 0, 0), (1280, 256, 16, 1024)]
+    N = sum(sizes)
+    R = r * len(segs)
+    nb = sum(s[1] for s in segs)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    A = (torch.randn(R, K, device=DEV) / math.sqrt(K)).requires_grad_(True)
+    B = (torch.randn(nb, r, device=DEV) * 0.1).requires_grad_(True)
+    seed = 1234567
+    y = lora_linear(x, lambda: W, None, A, B, segs, r, 2.0, p_drop, seed)
+    x2 = x.detach().float().requires_grad_(True)
+    A2 = A.detach().clone().requires_grad_(True)
+    B2 = B.detach().clone().requires_grad_(True)
+    y2 = lora_linear_ref(x2.to(torch.bfloat16).float(), W.float(), None, A2, B2, segs, r, 2.0,
+                         p_drop, seed)
+    assert rel(y, y2) < 1e-2
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    y2.backward(dy.float())
+    assert rel(x.grad, x2.grad) < 2e-2
+    assert rel(A.grad, A2.grad) < 1e-2
+    assert rel(B.grad, B2.grad) < 1e-2
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (64, 8, 128), (12, 12, 64)])
+@pytest.mark.parametrize("ctx_max", [37, 700, 2100])
+def test_paged_decode(nh, nkv, D, ctx_max):
+    from lumen.ops.attention import paged_decode, paged_decode_ref, write_kv_cache
+
+    bs, nseq = 16, 5
+    lens = torch.randint(1, ctx_max + 1, (nseq,))
+    lens[0] = ctx_max
+    max_blocks = (ctx_max + bs - 1) // bs
+    nblocks = nseq * max_blocks + 3
+    kc = torch.zeros(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    perm = torch.randperm(nblocks)[: nseq * max_blocks].view(nseq, max_blocks).int()
+    # fill caches through the cache-write kernel
+    for i in range(nseq):
+        L = int(lens[i])
+        k = torch.randn(L, nkv, D, device=DEV, dtype=torch.bfloat16)
+        v = torch.randn(L, nkv, D, device=DEV, dtype=torch.bfloat16)
+        t = torch.arange(L)
+        slots = (perm[i, t // bs].long() * bs + t % bs).to(DEV)
+        write_kv_cache(k, v, kc, vc, slots)
+    q = torch.randn(nseq, nh, D, device=DEV, dtype=torch.bfloat16)
+    bt = perm.to(DEV)
+    cl = lens.int().to(DEV)
+    scale = 1 / math.sqrt(D)
+    o = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale)
+    o2 = paged_decode_ref(q, kc, vc, bt, cl, scale)
+    assert rel(o, o2) < 1e-2
+
+
+def test_sampling_greedy_and_topk():
+    from lumen.ops._native import native
+
+    C = native()
+    R, V = 6, 32000
+    logits = torch.randn(R, V, device=DEV)
+    temp = torch.zeros(R, device=DEV)
+    top_p = torch.ones(R, device=DEV)
+    top_k = torch.zeros(R, device=DEV, dtype=torch.int32)
+    out = torch.empty(R, device=DEV, dtype=torch.int64)
+    C.sample(logits, temp, top_p, top_k, 1, 0, out, None)
+    assert torch.equal(out, logits.argmax(-1))
+    # top-k = 1 with temperature must also be the argmax
+    temp.fill_(0.7)
+    top_k.fill_(1)
+    C.sample(logits, temp, top_p, top_k, 7, 3, out, None)
+    assert torch.equal(out, logits.argmax(-1))
+    # top-p tiny -> argmax
+    top_k.zero_()
+    top_p.fill_(1e-6)
+    C.sample(logits, temp, top_p, top_k, 7, 4, out, None)
+    assert torch.equal(out, logits.argmax(-1))
+    # distribution check: 2-token vocab-like logits
+    V2 = 1024
+    lg = torch.full((4096, V2), -30.0, device=DEV)
+    lg[:, 0] = 0.0
+    lg[:, 1] = math.log(3.0)
+    t2 = torch.ones(4096, device=DEV)
+    o2 = torch.empty(4096, device=DEV, dtype=torch.int64)
+    C.sample(lg, t2, torch.ones(4096, device=DEV), torch.zeros(4096, device=DEV, dtype=torch.int32),
+             11, 0, o2, None)
+    frac1 = (o2 == 1).float().mean().item()
+    assert 0.70 < frac1 < 0.80
