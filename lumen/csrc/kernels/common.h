@@ -103,24 +103,22 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
   return r;
 }
 
-// Counter-based RNG (a 32-bit avalanche hash of (seed, index)).  Used for LoRA dropout so that
-// the backward pass regenerates the forward's mask from (seed, index) instead of storing it.
-__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
-  x ^= x >> 16; x *= 0x7feb352dU;
-  x ^= x >> 15; x *= 0x846ca68bU;
-  x ^= x >> 16;
-  return x;
-}
-
-__device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t idx) {
-  uint32_t lo = static_cast<uint32_t>(idx), hi = static_cast<uint32_t>(idx >> 32);
-  uint32_t s0 = static_cast<uint32_t>(seed), s1 = static_cast<uint32_t>(seed >> 32);
-  return hash_u32(lo ^ hash_u32(hi ^ hash_u32(s0 ^ hash_u32(s1 + 0x9e3779b9U))));
+// Counter-based RNG for LoRA dropout: the backward regenerates the forward's keep-mask from
+// (seed, element index) instead of storing it.  One multiply-mix of the 64-bit index with the
+// host-premixed 32-bit seed, then the "lowbias32" finaliser (2 multiplies): ~10 VALU ops per
+// element, so mask regeneration stays cheap inside memory-bound staging loops.
+__device__ __forceinline__ uint32_t rng_u32(uint32_t seed32, uint64_t idx) {
+  uint32_t h = static_cast<uint32_t>(idx) * 0x9E3779B1u +
+               static_cast<uint32_t>(idx >> 32) * 0x85EBCA77u + seed32;
+  h ^= h >> 16; h *= 0x7feb352dU;
+  h ^= h >> 15; h *= 0x846ca68bU;
+  h ^= h >> 16;
+  return h;
 }
 
 // keep-probability test: returns true when the element survives dropout with prob (1-p).
-__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
-  return rng_u32(seed, idx) >= thresh;
+__device__ __forceinline__ bool dropout_keep(uint32_t seed32, uint64_t idx, uint32_t thresh) {
+  return rng_u32(seed32, idx) >= thresh;
 }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }

@@ -47,7 +47,7 @@ struct LoraGemmArgs {
   float alpha;
   int ksplit;
   // dropout on the x operand (mode 1: X, mode 3: W); logical element (t, f) -> t * drop_ld + f
-  unsigned long long seed;
+  unsigned int seed;          // host-premixed 32-bit seed
   unsigned int drop_thresh;  // 0 = no dropout
   float drop_scale;
   long long drop_ld;
@@ -164,24 +164,50 @@ __global__ void __launch_bounds__(256) lora_gemm_kernel(LoraGemmArgs a) {
   }
 
   // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg
+  if constexpr (EPI == 0) {
 #pragma unroll
-  for (int n = 0; n < BN / 16; ++n) {
-    const int col = n0 + n * 16 + lr;
-    if (col >= N) continue;
+    for (int n = 0; n < BN / 16; ++n) {
+      const int col = n0 + n * 16 + lr;
+      if (col >= N) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wid * 16 + lk * 4 + r;
-      if (row >= M) continue;
-      const long long off = a.seg.c_off[seg] + row * a.cs_m + col * a.cs_n;
-      float val = a.alpha * acc[n][r];
-      if (DROP == 3)  // dropout mask on the output (mode 5: d/dx through drop(x)), token = row
-        val = dropout_keep(a.seed, static_cast<long long>(row) * a.drop_ld + col, a.drop_thresh)
-                  ? val * a.drop_scale : 0.f;
-      if (EPI == 0) {
-        atomicAdd(reinterpret_cast<float*>(a.C) + off, val);
-      } else {
-        TC* c = reinterpret_cast<TC*>(a.C) + off;
-        *c = from_f32<TC>(to_f32(*c) + val);
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wid * 16 + lk * 4 + r;
+        if (row >= M) continue;
+        const long long off = a.seg.c_off[seg] + row * a.cs_m + col * a.cs_n;
+        atomicAdd(reinterpret_cast<float*>(a.C) + off, a.alpha * acc[n][r]);
+      }
+    }
+  } else {
+    // 16-bit read-modify-write: stage the f32 tile through LDS, then each thread updates 8
+    // consecutive columns of a row with one 16-byte load + one 16-byte store (requires
+    // cs_n == 1, N % 8 == 0 and 16-byte aligned rows; checked on the host).
+    constexpr int CST = BN + 4;
+    __shared__ float cs[kBM * CST];
+#pragma unroll
+    for (int n = 0; n < BN / 16; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[(wid * 16 + lk * 4 + r) * CST + n * 16 + lr] = acc[n][r];
+    __syncthreads();
+    constexpr int TPR = BN / 8;              // threads per row
+    constexpr int RPP = 256 / TPR;           // rows per pass
+    const int tr = threadIdx.x / TPR, tc = (threadIdx.x % TPR) * 8;
+#pragma unroll
+    for (int pass = 0; pass < kBM / RPP; ++pass) {
+      const int lrow = pass * RPP + tr;
+      const int row = m0 + lrow, col = n0 + tc;
+      if (row < M && col < N) {
+        TC* c = reinterpret_cast<TC*>(a.C) + a.seg.c_off[seg] + row * a.cs_m + col;
+        float v[8];
+        load8(c, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float add = a.alpha * cs[lrow * CST + tc + j];
+          if (DROP == 3)  // mode 5: d/dx through drop(x); token = row, feature = col
+            add = dropout_keep(a.seed, static_cast<long long>(row) * a.drop_ld + col + j,
+                               a.drop_thresh) ? add * a.drop_scale : 0.f;
+          v[j] += add;
+        }
+        store8(c, v);
       }
     }
   }
@@ -239,10 +265,12 @@ extern "C" hipError_t lumen_lora_gemm(int act_dtype, int mode, int bn, const voi
                                       const long long* c_off, const int* Ms, const int* Ns,
                                       const int* Ks, hipStream_t st) {
   if (nseg < 1 || nseg > 4 || ksplit < 1) return hipErrorInvalidValue;
-  if ((mode == 5 || mode == 6) && ksplit != 1) return hipErrorInvalidValue;
+  if ((mode == 5 || mode == 6) && (ksplit != 1 || cs_n != 1)) return hipErrorInvalidValue;
   lumen::LoraGemmArgs a;
   a.X = X; a.W = W; a.C = C; a.ldx = ldx; a.ldw = ldw; a.cs_m = cs_m; a.cs_n = cs_n;
-  a.alpha = alpha; a.ksplit = ksplit; a.seed = seed; a.drop_thresh = drop_thresh;
+  a.alpha = alpha; a.ksplit = ksplit;
+  a.seed = static_cast<unsigned int>(seed) ^ static_cast<unsigned int>(seed >> 32);
+  a.drop_thresh = drop_thresh;
   a.drop_scale = drop_scale; a.drop_ld = drop_ld;
   a.seg.nseg = nseg;
   int maxM = 0, maxN = 0;

@@ -79,8 +79,9 @@ __global__ void __launch_bounds__(kSampNT) sample_kernel(
     if (z < tau) continue;
     float key = z;
     if (!greedy) {
-      const uint32_t r = rng_u32(seed + static_cast<unsigned long long>(offset) * 0x9e3779b97f4a7c15ULL,
-                                 static_cast<uint64_t>(row) * static_cast<uint64_t>(V) + j);
+      const uint32_t sd = static_cast<uint32_t>(seed) ^
+                          (static_cast<uint32_t>(offset) * 0x9E3779B9u + 0x7F4A7C15u);
+      const uint32_t r = rng_u32(sd, static_cast<uint64_t>(row) * static_cast<uint64_t>(V) + j);
       const float u = (static_cast<float>(r >> 8) + 0.5f) * (1.f / 16777216.f);
       key = z - __logf(-__logf(u));
     }

@@ -86,6 +86,8 @@ def print_trainable_parameters(model: nn.Module, printer=print):
 def _peft_key(model, module_name: str, seg_name: str, which: str) -> str:
     parts = module_name.split(".")
     parts[-1] = seg_name
+    if model.config.arch == "opt" and seg_name in ("q_proj", "k_proj", "v_proj", "out_proj"):
+        parts.insert(-1, "self_attn")  # HF OPTAttention lives under .self_attn
     return f"base_model.model.{_hf_prefix(model)}{'.'.join(parts)}.lora_{which}.weight"
 
 

@@ -147,7 +147,7 @@ def init_normal_(model: nn.Module, std: float = 0.02, seed: int = 0):
     gens = {}
     with torch.no_grad():
         for name, p in model.named_parameters():
-            if "lora_" in name or p.numel() == 0:
+            if "lora_" in name or p.numel() == 0 or p.is_meta:
                 continue
             if p.dim() == 1:
                 if name.endswith("bias"):

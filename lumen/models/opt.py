@@ -16,6 +16,7 @@ import torch.utils.checkpoint as cp
 
 from ..ops.attention import causal_attention
 from ..ops.loss import lm_head_cross_entropy
+from ..ops.norm import layer_norm
 from .config import ModelConfig
 from .layers import Linear
 from .llama import init_normal_
@@ -40,13 +41,14 @@ class OPTDecoderLayer(nn.Module):
     def forward(self, h, B: int, S: int):
         c = self.cfg
         nh, D = c.num_attention_heads, c.head_dim
-        x = self.self_attn_layer_norm(h)
+        ln1, ln2 = self.self_attn_layer_norm, self.final_layer_norm
+        x = layer_norm(h, ln1.weight, ln1.bias, ln1.eps)
         qkv = self.qkv_proj(x).view(B, S, 3, nh, D)
         q = qkv[:, :, 0].transpose(1, 2)
         k = qkv[:, :, 1].transpose(1, 2)
         v = qkv[:, :, 2].transpose(1, 2)
         h = h + self.out_proj(causal_attention(q, k, v))
-        x = self.final_layer_norm(h)
+        x = layer_norm(h, ln2.weight, ln2.bias, ln2.eps)
         return h + self.fc2(F.relu(self.fc1(x)))
 
 
@@ -69,7 +71,7 @@ class OPTForCausalLM(nn.Module):
 
     def zero_units(self) -> List[List[nn.Module]]:
         return ([[self.embed_tokens, self.embed_positions]] + [[l] for l in self.layers]
-                + [[self.final_layer_norm]])
+                + [[self.final_layer_norm, self.embed_tokens]])  # tied head: depends on unit 0
 
     def lora_modules(self):
         for name, m in self.named_modules():
@@ -107,7 +109,8 @@ class OPTForCausalLM(nn.Module):
         last = len(self.layers) + 1
 
         def head(h_):
-            y = self.final_layer_norm(h_)
+            fl = self.final_layer_norm
+            y = layer_norm(h_, fl.weight, fl.bias, fl.eps)
             wfn = lambda: self.embed_tokens.weight  # noqa: E731  (tied head)
             if labels is None:
                 return torch.matmul(y, wfn().t())

@@ -28,7 +28,7 @@ Seg = Tuple[int, int, int, int]
 _M32 = 0xFFFFFFFF
 
 
-def _hash_u32(x: torch.Tensor) -> torch.Tensor:
+def _lowbias32(x):
     x = x ^ (x >> 16)
     x = (x * 0x7FEB352D) & _M32
     x = x ^ (x >> 15)
@@ -37,20 +37,16 @@ def _hash_u32(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
-def _hash_scalar(x: int) -> int:
-    x ^= x >> 16
-    x = (x * 0x7FEB352D) & _M32
-    x ^= x >> 15
-    x = (x * 0x846CA68B) & _M32
-    x ^= x >> 16
-    return x
+def seed32(seed: int) -> int:
+    """The 32-bit seed the kernels use (same folding as the native launcher)."""
+    seed &= 0x7FFFFFFFFFFFFFFF
+    return (seed ^ (seed >> 32)) & _M32
 
 
 def rng_u32_ref(seed: int, idx: torch.Tensor) -> torch.Tensor:
-    s0, s1 = seed & _M32, (seed >> 32) & _M32
-    inner = _hash_scalar(s0 ^ _hash_scalar((s1 + 0x9E3779B9) & _M32))
-    lo, hi = idx & _M32, idx >> 32
-    return _hash_u32(lo ^ _hash_u32(hi ^ inner))
+    s = seed32(seed)
+    h = ((idx & _M32) * 0x9E3779B1 + (idx >> 32) * 0x85EBCA77 + s) & _M32
+    return _lowbias32(h)
 
 
 def drop_threshold(p: float) -> int:
@@ -208,8 +204,14 @@ def linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor] = None,
     if use_native(x2d):
         y = _Linear.apply(x2d.contiguous(), weight_fn, bias, w_param)
     else:
-        y = F.linear(x2d, weight_fn(), bias)
+        y = F.linear(x2d, _frozen(weight_fn()), bias)
     return y.view(*shp[:-1], y.shape[-1])
+
+
+def _frozen(W: torch.Tensor) -> torch.Tensor:
+    # autograd must not save the Parameter object itself: ZeRO-3 swaps param.data when it
+    # releases a gathered unit; a detached alias keeps the gathered storage alive instead
+    return W if W.requires_grad else W.detach()
 
 
 def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: torch.Tensor,
@@ -221,7 +223,7 @@ def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: tor
         y = _LoraLinear.apply(x2d.contiguous(), weight_fn, bias, A, B, segs, r, scale, p, seed,
                               w_param)
     else:
-        y = lora_linear_ref(x2d, weight_fn(), bias, A, B, segs, r, scale, p, seed)
+        y = lora_linear_ref(x2d, _frozen(weight_fn()), bias, A, B, segs, r, scale, p, seed)
     return y.view(*shp[:-1], y.shape[-1])
 
 

@@ -52,6 +52,8 @@ def lm_head_cross_entropy(h: torch.Tensor, labels: torch.Tensor,
         return _LMHeadCE.apply(h.contiguous(), labels.contiguous(), weight_fn, int(n_valid),
                                weight_param)
     W = weight_fn()
+    if not W.requires_grad:
+        W = W.detach()  # see ops.lora._frozen
     logits = torch.matmul(h, W.t()).float()
     loss = F.cross_entropy(logits, labels, ignore_index=IGNORE_INDEX, reduction="sum")
     return loss / max(int(n_valid), 1)

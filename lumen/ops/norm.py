@@ -18,7 +18,8 @@ def rms_norm_ref(x, w, eps, residual=None):
     s = x if residual is None else (x.float() + residual.float()).to(x.dtype)
     sf = s.float()
     rstd = torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps)
-    y = (sf * rstd * w.float()).to(x.dtype)
+    wf = (w if w.requires_grad else w.detach()).float()  # never save a ZeRO-3 param object
+    y = (sf * rstd * wf).to(x.dtype)
     return y, s
 
 
@@ -64,5 +65,6 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
 
 
 def layer_norm(x, w, b, eps):
-    """OPT LayerNorm (torch: small model / CPU path)."""
-    return torch.nn.functional.layer_norm(x, (x.shape[-1],), w, b, eps)
+    """OPT LayerNorm (torch op); frozen params enter autograd as detached aliases."""
+    fz = lambda t: t if (t is None or t.requires_grad) else t.detach()  # noqa: E731
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), fz(w), fz(b), eps)
