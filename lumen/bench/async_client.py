@@ -1,0 +1,145 @@
+"""Async load generator for the OpenAI-compatible server (aiohttp, installed).
+
+The reference declares "Locust/AsyncIO load testing" (README.md:11,17; requirements.txt:34-36:
+locust 2.29, aiohttp 3.10).  This client keeps ``concurrency`` streaming requests in flight
+(closed loop, like a Locust user pool with zero think time) or fires them at a Poisson
+``request_rate``, and measures at the client: output tokens/s, request/s, TTFT (first SSE chunk
+carrying text) and inter-token latency percentiles.  Prompts can be token-id lists so the bench
+needs no tokenizer files (the boxes are offline).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import random
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+
+@dataclass
+class ReqResult:
+    ok: bool
+    ttft: float = 0.0
+    latency: float = 0.0
+    itl: List[float] = field(default_factory=list)
+    out_tokens: int = 0
+    prompt_tokens: int = 0
+    error: str = ""
+
+
+def _pct(xs, q):
+    if not xs:
+        return 0.0
+    s = sorted(xs)
+    return s[min(len(s) - 1, int(q * len(s)))]
+
+
+def summarize(results: List[ReqResult], wall: float) -> dict:
+    ok = [r for r in results if r.ok]
+    toks = sum(r.out_tokens for r in ok)
+    ttft = [r.ttft for r in ok]
+    itl = [x for r in ok for x in r.itl]
+    lat = [r.latency for r in ok]
+    return {
+        "requests": len(results), "ok": len(ok), "errors": len(results) - len(ok),
+        "wall_s": round(wall, 3),
+        "output_tokens": toks,
+        "output_tok_s": round(toks / wall, 1) if wall > 0 else 0.0,
+        "total_tok_s": round((toks + sum(r.prompt_tokens for r in ok)) / wall, 1) if wall else 0.0,
+        "req_s": round(len(ok) / wall, 3) if wall > 0 else 0.0,
+        "ttft_p50_ms": round(1000 * _pct(ttft, 0.5), 2),
+        "ttft_p90_ms": round(1000 * _pct(ttft, 0.9), 2),
+        "ttft_p99_ms": round(1000 * _pct(ttft, 0.99), 2),
+        "itl_p50_ms": round(1000 * _pct(itl, 0.5), 3),
+        "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
+        "latency_p50_s": round(_pct(lat, 0.5), 3),
+    }
+
+
+async def one_request(session, url: str, prompt, max_tokens: int, model: str) -> ReqResult:
+    body = {"model": model, "prompt": prompt, "max_tokens": max_tokens, "temperature": 0.0,
+            "stream": True, "ignore_eos": True}
+    t0 = time.perf_counter()
+    first = None
+    last = t0
+    itl = []
+    n = 0
+    try:
+        async with session.post(url + "/v1/completions", json=body) as resp:
+            if resp.status != 200:
+                return ReqResult(False, error=f"HTTP {resp.status}")
+            async for raw in resp.content:
+                line = raw.decode().strip()
+                if not line.startswith("data: "):
+                    continue
+                data = line[6:]
+                if data == "[DONE]":
+                    break
+                j = json.loads(data)
+                if "error" in j:
+                    return ReqResult(False, error=j["error"]["message"])
+                ch = j["choices"][0]
+                now = time.perf_counter()
+                if ch.get("text") or ch.get("finish_reason"):
+                    if first is None:
+                        first = now
+                    else:
+                        itl.append(now - last)
+                    last = now
+                    n += 1
+    except Exception as e:  # network error -> failed request
+        return ReqResult(False, error=repr(e))
+    plen = len(prompt) if isinstance(prompt, list) else 0
+    return ReqResult(True, (first or last) - t0, last - t0, itl, max_tokens, plen)
+
+
+async def run_load(url: str, num_requests: int, concurrency: int, prompt_len: int,
+                   max_tokens: int, vocab: int = 32000, request_rate: Optional[float] = None,
+                   model: str = "lumen", seed: int = 0) -> dict:
+    import aiohttp
+
+    rng = random.Random(seed)
+    prompts = [[rng.randrange(3, vocab) for _ in range(prompt_len)] for _ in range(num_requests)]
+    results: List[ReqResult] = []
+    timeout = aiohttp.ClientTimeout(total=3600)
+    conn = aiohttp.TCPConnector(limit=max(concurrency, 1) + 8)
+    async with aiohttp.ClientSession(timeout=timeout, connector=conn) as session:
+        t0 = time.perf_counter()
+        if request_rate:
+            tasks = []
+            for p in prompts:
+                tasks.append(asyncio.create_task(one_request(session, url, p, max_tokens, model)))
+                await asyncio.sleep(rng.expovariate(request_rate))
+            results = list(await asyncio.gather(*tasks))
+        else:
+            it = iter(prompts)
+
+            async def user():
+                for p in it:
+                    results.append(await one_request(session, url, p, max_tokens, model))
+
+            await asyncio.gather(*[user() for _ in range(concurrency)])
+        wall = time.perf_counter() - t0
+    return summarize(results, wall)
+
+
+def main():
+    ap = argparse.ArgumentParser(description="lumen async OpenAI-API load generator")
+    ap.add_argument("--url", default="http://127.0.0.1:8000")
+    ap.add_argument("--num-requests", type=int, default=256)
+    ap.add_argument("--concurrency", type=int, default=64)
+    ap.add_argument("--request-rate", type=float, default=None)
+    ap.add_argument("--prompt-len", type=int, default=512)
+    ap.add_argument("--max-tokens", type=int, default=128)
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--model", default="lumen")
+    a = ap.parse_args()
+    res = asyncio.run(run_load(a.url, a.num_requests, a.concurrency, a.prompt_len, a.max_tokens,
+                               a.vocab, a.request_rate, a.model))
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,72 @@
+"""``python -m lumen.cli.serve`` / ``scripts/serve.py``: OpenAI-compatible server.
+
+    python scripts/serve.py --model meta-llama/Llama-2-7b-hf --adapter checkpoints/x/final
+    torchrun --nproc-per-node 2 --master-addr 127.0.0.1 scripts/serve.py --tp 2 ...
+
+Rank 0 runs the scheduler + HTTP server; under TP the other ranks run the worker loop.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(description="lumen OpenAI-compatible server (MI355X)")
+    ap.add_argument("--model", default="meta-llama/Llama-2-7b-hf",
+                    help="preset / hub id (random init offline) or local HF checkpoint dir")
+    ap.add_argument("--adapter", default=None, help="PEFT LoRA adapter dir to merge")
+    ap.add_argument("--served-model-name", default=None)
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (= world size)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
+    ap.add_argument("--block-size", type=int, default=16)
+    ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap
+
+
+def main(argv=None):
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, root)
+    a = build_parser().parse_args(argv)
+    import torch
+
+    from lumen.parallel.dist import init
+    from lumen.serve.engine import AsyncEngine, EngineConfig, LLMEngine
+
+    env = init()
+    if env.world_size != a.tp:
+        raise SystemExit(f"--tp {a.tp} but WORLD_SIZE={env.world_size}")
+    cfg = EngineConfig(model=a.model, adapter=a.adapter, dtype=a.dtype,
+                       max_model_len=a.max_model_len, block_size=a.block_size,
+                       gpu_memory_utilization=a.gpu_memory_utilization,
+                       max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_num_batched_tokens,
+                       tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs)
+    eng = LLMEngine(cfg)
+    if env.rank != 0:
+        from lumen.serve.tp import worker_loop
+
+        worker_loop(eng.runner)
+        return
+    import uvicorn
+
+    from lumen.serve.api_server import create_app
+
+    app = create_app(AsyncEngine(eng), a.served_model_name)
+    print(f"[lumen.serve] {cfg.model} tp={a.tp} kv_blocks={eng.blocks.num_blocks} "
+          f"on http://{a.host}:{a.port}", flush=True)
+    try:
+        uvicorn.run(app, host=a.host, port=a.port, log_level="warning")
+    finally:
+        eng.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -208,16 +208,16 @@ static hipError_t launch_pa(void* out, const void* q, const void* kc, const void
   dim3 grid(nseq, nkv, max_parts), block(256);
   const size_t smem = (kMaxGroup * D + kMaxGroup * PART + 2 * kMaxGroup +
                        static_cast<size_t>(4) * (nh / nkv) * D) * sizeof(float);
-  if (D == 128)
-    hipLaunchKernelGGL((pa_decode_kernel<T, 128>), grid, block, smem, st, (T*)out, (const T*)q,
-                       (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, max_parts,
-                       scale, tm, tl, (float*)to, PART);
-  else if (D == 64)
-    hipLaunchKernelGGL((pa_decode_kernel<T, 64>), grid, block, smem, st, (T*)out, (const T*)q,
-                       (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, max_parts,
-                       scale, tm, tl, (float*)to, PART);
-  else
-    return hipErrorInvalidValue;
+#define LUMEN_PA(DD)                                                                           \
+  hipLaunchKernelGGL((pa_decode_kernel<T, DD>), grid, block, smem, st, (T*)out, (const T*)q,     \
+                     (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, \
+                     tm, tl, (float*)to, PART)
+  if (D == 128) LUMEN_PA(128);
+  else if (D == 64) LUMEN_PA(64);
+  else if (D == 256) LUMEN_PA(256);
+  else if (D == 32) LUMEN_PA(32);
+  else return hipErrorInvalidValue;
+#undef LUMEN_PA
   if (max_parts > 1) {
     dim3 g2(nseq, nh), b2(128);
     hipLaunchKernelGGL(pa_reduce_kernel<T>, g2, b2, 0, st, (T*)out, cl, tm, tl,

@@ -124,11 +124,11 @@ PRESETS = {
                      word_embed_proj_dim=768, tie_word_embeddings=True, pad_token_id=1,
                      bos_token_id=2, eos_token_id=2, name="facebook/opt-125m"),
     # small test models (CPU unit tests, smoke)
-    "tiny-llama": dict(arch="llama", vocab_size=512, hidden_size=128, intermediate_size=352,
+    "tiny-llama": dict(arch="llama", vocab_size=512, hidden_size=256, intermediate_size=688,
                        num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=4,
                        max_position_embeddings=512, name="tiny-llama"),
-    "tiny-llama-gqa": dict(arch="llama", vocab_size=512, hidden_size=128, intermediate_size=352,
-                           num_hidden_layers=2, num_attention_heads=8, num_key_value_heads=2,
+    "tiny-llama-gqa": dict(arch="llama", vocab_size=512, hidden_size=256, intermediate_size=688,
+                           num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
                            max_position_embeddings=512, name="tiny-llama-gqa"),
     "tiny-opt": dict(arch="opt", vocab_size=512, hidden_size=64, intermediate_size=256,
                      ffn_dim=256, num_hidden_layers=2, num_attention_heads=4,

@@ -1,0 +1,219 @@
+"""OpenAI-compatible HTTP API (FastAPI + uvicorn, both installed) over ``AsyncEngine``.
+
+The reference declares "vLLM ... OpenAI-compatible API" (README.md:10,16): this serves the same
+surface -- ``GET /v1/models``, ``POST /v1/completions``, ``POST /v1/chat/completions`` (both with
+``stream: true`` Server-Sent Events ending in ``data: [DONE]``), ``GET /health`` and a
+Prometheus-format ``GET /metrics`` (requests, tokens, TTFT / inter-token latency summaries,
+KV-cache usage).  Chat requests use the Llama-2 chat template the reference trains with
+(``<s>[INST] {user} [/INST]``, scripts/prepare_dataset.py:12-25).
+"""
+from __future__ import annotations
+
+import json
+import time
+import uuid
+from typing import Any, Dict, List, Optional, Union
+
+from fastapi import FastAPI, HTTPException, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+
+from .engine import AsyncEngine
+from .sequence import SamplingParams
+
+
+def llama2_chat_prompt(messages: List[Dict[str, str]]) -> str:
+    """Llama-2 chat format; system prompt folded into the first user turn."""
+    sys_txt = ""
+    out = []
+    turns = [m for m in messages if m.get("role") != "system"]
+    for m in messages:
+        if m.get("role") == "system":
+            sys_txt = f"<<SYS>>\n{m.get('content', '')}\n<</SYS>>\n\n"
+    i = 0
+    while i < len(turns):
+        u = turns[i]
+        content = u.get("content", "")
+        if i == 0 and sys_txt:
+            content = sys_txt + content
+        if u.get("role") == "user":
+            seg = f"[INST] {content} [/INST]"
+            if i + 1 < len(turns) and turns[i + 1].get("role") == "assistant":
+                seg += f" {turns[i + 1].get('content', '')} </s><s>"
+                i += 1
+            out.append(seg)
+        i += 1
+    return "".join(out)
+
+
+class _Stats:
+    def __init__(self):
+        self.requests = 0
+        self.errors = 0
+        self.prompt_tokens = 0
+        self.completion_tokens = 0
+        self.ttft: List[float] = []
+        self.itl: List[float] = []
+
+    def observe(self, seq):
+        self.prompt_tokens += len(seq.prompt_ids)
+        self.completion_tokens += len(seq.output_ids)
+        if seq.first_token_time is not None:
+            self.ttft.append(seq.first_token_time - seq.arrival)
+        tt = seq.token_times
+        self.itl.extend(b - a for a, b in zip(tt, tt[1:]))
+        self.ttft = self.ttft[-10000:]
+        self.itl = self.itl[-100000:]
+
+
+def _quantiles(xs, qs=(0.5, 0.9, 0.99)):
+    if not xs:
+        return {q: 0.0 for q in qs}
+    s = sorted(xs)
+    return {q: s[min(len(s) - 1, int(q * len(s)))] for q in qs}
+
+
+def _params(body: Dict[str, Any], eos: Optional[int]) -> SamplingParams:
+    stop_ids = body.get("stop_token_ids") or []
+    return SamplingParams(max_tokens=int(body.get("max_tokens") or 16),
+                          temperature=float(body.get("temperature", 1.0)),
+                          top_p=float(body.get("top_p", 1.0)), top_k=int(body.get("top_k", 0) or 0),
+                          stop_token_ids=list(stop_ids), ignore_eos=bool(body.get("ignore_eos", False)),
+                          seed=body.get("seed"), logprobs=bool(body.get("logprobs", False)))
+
+
+def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
+    eng = aengine.engine
+    name = served_model_name or eng.cfg.model
+    tok = eng.tokenizer
+    stats = _Stats()
+    app = FastAPI(title="lumen OpenAI-compatible server")
+
+    def decode(ids):
+        return tok.decode(ids)
+
+    @app.get("/health")
+    async def health():
+        return {"status": "ok"}
+
+    @app.get("/v1/models")
+    async def models():
+        return {"object": "list", "data": [{"id": name, "object": "model",
+                                            "created": int(time.time()), "owned_by": "lumen",
+                                            "max_model_len": eng.cfg.max_model_len}]}
+
+    @app.get("/metrics")
+    async def metrics():
+        t, i = _quantiles(stats.ttft), _quantiles(stats.itl)
+        lines = [
+            "# TYPE lumen_requests_total counter", f"lumen_requests_total {stats.requests}",
+            "# TYPE lumen_request_errors_total counter", f"lumen_request_errors_total {stats.errors}",
+            "# TYPE lumen_prompt_tokens_total counter", f"lumen_prompt_tokens_total {stats.prompt_tokens}",
+            "# TYPE lumen_generation_tokens_total counter",
+            f"lumen_generation_tokens_total {stats.completion_tokens}",
+            "# TYPE lumen_time_to_first_token_seconds summary",
+            *[f'lumen_time_to_first_token_seconds{{quantile="{q}"}} {v:.6f}' for q, v in t.items()],
+            "# TYPE lumen_inter_token_latency_seconds summary",
+            *[f'lumen_inter_token_latency_seconds{{quantile="{q}"}} {v:.6f}' for q, v in i.items()],
+            "# TYPE lumen_kv_cache_usage_ratio gauge", f"lumen_kv_cache_usage_ratio {eng.blocks.usage():.4f}",
+            "# TYPE lumen_running_requests gauge", f"lumen_running_requests {len(eng.scheduler.running)}",
+            "# TYPE lumen_waiting_requests gauge", f"lumen_waiting_requests {len(eng.scheduler.waiting)}",
+            "# TYPE lumen_preemptions_total counter",
+            f"lumen_preemptions_total {eng.scheduler.num_preemptions}",
+        ]
+        return PlainTextResponse("\n".join(lines) + "\n")
+
+    async def _run(prompt, params, chat: bool, stream: bool, model: str):
+        rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex
+        created = int(time.time())
+        stats.requests += 1
+        obj = "chat.completion" if chat else "text_completion"
+
+        def chunk(delta_text, finish, seq=None):
+            if chat:
+                d = {"content": delta_text} if delta_text else {}
+                ch = {"index": 0, "delta": d, "finish_reason": finish}
+                o = "chat.completion.chunk"
+            else:
+                ch = {"index": 0, "text": delta_text, "logprobs": None, "finish_reason": finish}
+                o = "text_completion"
+            return {"id": rid, "object": o, "created": created, "model": model, "choices": [ch]}
+
+        if stream:
+            async def gen():
+                sent = ""
+                last = None
+                try:
+                    if chat:
+                        first = {"id": rid, "object": "chat.completion.chunk", "created": created,
+                                 "model": model, "choices": [{"index": 0, "delta": {"role": "assistant"},
+                                                              "finish_reason": None}]}
+                        yield f"data: {json.dumps(first)}\n\n"
+                    async for seq in aengine.stream(prompt, params, rid):
+                        last = seq
+                        text = decode(seq.output_ids)
+                        delta = text[len(sent):] if text.startswith(sent) else text
+                        sent = text
+                        fin = seq.finish_reason if seq.finished else None
+                        if delta or fin:
+                            yield f"data: {json.dumps(chunk(delta, fin))}\n\n"
+                    if last is not None:
+                        stats.observe(last)
+                except ValueError as e:
+                    stats.errors += 1
+                    yield f"data: {json.dumps({'error': {'message': str(e)}})}\n\n"
+                yield "data: [DONE]\n\n"
+            return StreamingResponse(gen(), media_type="text/event-stream")
+
+        last = None
+        try:
+            async for seq in aengine.stream(prompt, params, rid):
+                last = seq
+        except ValueError as e:
+            stats.errors += 1
+            raise HTTPException(status_code=400, detail=str(e))
+        stats.observe(last)
+        text = decode(last.output_ids)
+        usage = {"prompt_tokens": len(last.prompt_ids), "completion_tokens": len(last.output_ids),
+                 "total_tokens": last.length}
+        if chat:
+            choice = {"index": 0, "message": {"role": "assistant", "content": text},
+                      "finish_reason": last.finish_reason}
+        else:
+            lp = None
+            if params.logprobs:
+                lp = {"tokens": [decode([t]) for t in last.output_ids],
+                      "token_logprobs": list(last.output_logprobs)}
+            choice = {"index": 0, "text": text, "logprobs": lp, "finish_reason": last.finish_reason}
+        return JSONResponse({"id": rid, "object": obj, "created": created, "model": model,
+                             "choices": [choice], "usage": usage})
+
+    @app.post("/v1/completions")
+    async def completions(req: Request):
+        body = await req.json()
+        prompt: Union[str, List[int], List[str]] = body.get("prompt", "")
+        if isinstance(prompt, list) and prompt and isinstance(prompt[0], str):
+            if len(prompt) != 1:
+                raise HTTPException(status_code=400, detail="batched string prompts: send one per request")
+            prompt = prompt[0]
+        try:
+            params = _params(body, eng.eos_id)
+        except ValueError as e:
+            raise HTTPException(status_code=400, detail=str(e))
+        return await _run(prompt, params, False, bool(body.get("stream", False)),
+                          body.get("model", name))
+
+    @app.post("/v1/chat/completions")
+    async def chat(req: Request):
+        body = await req.json()
+        msgs = body.get("messages") or []
+        if not msgs:
+            raise HTTPException(status_code=400, detail="messages required")
+        try:
+            params = _params(body, eng.eos_id)
+        except ValueError as e:
+            raise HTTPException(status_code=400, detail=str(e))
+        return await _run(llama2_chat_prompt(msgs), params, True, bool(body.get("stream", False)),
+                          body.get("model", name))
+
+    app.state.stats = stats
+    return app

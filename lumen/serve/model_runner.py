@@ -1,0 +1,301 @@
+"""Serving model runner: paged-KV prefill / decode of Llama-family models on MI355X.
+
+Per layer (token-major activations, no autograd):
+    fused add+RMSNorm (HIP) -> q|k|v GEMM (hipBLASLt) -> in-place RoPE on q,k at each token's
+    position (HIP) -> K/V scattered into the paged cache by slot (HIP) -> attention
+    [prefill: PyTorch-ROCm fused SDPA per sequence (causal, GQA); decode: HIP paged-attention]
+    -> o GEMM (+ RCCL all-reduce under TP) -> fused add+RMSNorm -> gate|up GEMM -> SwiGLU (HIP)
+    -> down GEMM (+ all-reduce) ; final norm on the sampled rows only -> LM head -> HIP sampler.
+
+Tensor parallelism: Megatron-style column split of q|k|v and gate|up by
+heads / FFN columns, row split of o and down followed by an all-reduce over the TP group.
+Rank 0 owns the scheduler; every step it broadcasts one int64 metadata tensor (token ids,
+positions, slots, block tables, lengths) so worker ranks run the same kernels (no pickling).
+Decode steps are captured in HIP graphs per batch-size bucket (static input buffers), which
+removes the per-kernel launch cost that otherwise dominates small-batch decode.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence as Seq
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from ..models.config import ModelConfig
+from ..ops._native import native, use_native
+from ..ops.activation import swiglu
+from ..ops.attention import paged_decode, write_kv_cache
+from ..ops.norm import rms_norm
+from ..ops.rope import rope_inplace, rope_tables
+
+
+@dataclass
+class LayerW:
+    ln1: torch.Tensor
+    ln2: torch.Tensor
+    qkv: torch.Tensor
+    o: torch.Tensor
+    gate_up: torch.Tensor
+    down: torch.Tensor
+
+
+class ServeWeights:
+    """Inference weights extracted from a (LoRA-merged) LlamaForCausalLM, TP-sliced."""
+
+    def __init__(self, model, tp_rank: int = 0, tp_size: int = 1):
+        cfg: ModelConfig = model.config
+        if cfg.arch != "llama":
+            raise NotImplementedError("serving supports the Llama family")
+        self.cfg = cfg
+        nh, nkv, D, H, Fd = (cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
+                             cfg.hidden_size, cfg.intermediate_size)
+        if nh % tp_size or nkv % tp_size or Fd % tp_size:
+            raise ValueError(f"TP={tp_size} must divide heads ({nh}/{nkv}) and FFN ({Fd})")
+        self.nh, self.nkv = nh // tp_size, nkv // tp_size
+        self.F = Fd // tp_size
+        r = tp_rank
+        qs, ks = nh * D, nkv * D
+        lq, lk, lf = self.nh * D, self.nkv * D, self.F
+        self.layers: List[LayerW] = []
+        with torch.no_grad():
+            for L in model.layers:
+                W = L.self_attn.qkv_proj.weight
+                qkv = torch.cat([W[r * lq:(r + 1) * lq], W[qs + r * lk:qs + (r + 1) * lk],
+                                 W[qs + ks + r * lk:qs + ks + (r + 1) * lk]], 0).contiguous()
+                o = L.self_attn.o_proj.weight[:, r * lq:(r + 1) * lq].contiguous()
+                GU = L.mlp.gate_up_proj.weight
+                gu = torch.cat([GU[r * lf:(r + 1) * lf], GU[Fd + r * lf:Fd + (r + 1) * lf]],
+                               0).contiguous()
+                dn = L.mlp.down_proj.weight[:, r * lf:(r + 1) * lf].contiguous()
+                self.layers.append(LayerW(L.input_layernorm.weight, L.post_attention_layernorm.weight,
+                                          qkv, o, gu, dn))
+        self.embed = model.embed_tokens.weight
+        self.norm = model.norm.weight
+        self.lm_head = model.lm_head.weight
+        self.dtype = self.embed.dtype
+
+
+@dataclass
+class StepInput:
+    kind: str                          # prefill | decode
+    tokens: torch.Tensor               # [T] int64 (device)
+    positions: torch.Tensor            # [T] int32
+    slots: torch.Tensor                # [T] int64
+    cu_seqlens: List[int]              # prefill: per-sequence token offsets (host)
+    block_tables: Optional[torch.Tensor] = None  # decode [N, maxb] int32
+    context_lens: Optional[torch.Tensor] = None  # decode [N] int32
+    max_context: int = 0
+
+
+def kv_bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2, tp_size: int = 1) -> int:
+    return 2 * cfg.num_hidden_layers * (cfg.num_key_value_heads // tp_size) * cfg.head_dim * dtype_bytes
+
+
+class ModelRunner:
+    def __init__(self, weights: ServeWeights, num_blocks: int, block_size: int,
+                 device: torch.device, max_model_len: int = 4096, tp_group=None,
+                 use_graphs: bool = True, max_graph_batch: int = 256):
+        self.w = weights
+        self.cfg = weights.cfg
+        self.device = device
+        self.block_size = block_size
+        self.num_blocks = num_blocks
+        self.max_model_len = max_model_len
+        self.tp_group = tp_group
+        self.tp = dist.get_world_size(tp_group) if tp_group is not None else 1
+        cfg = self.cfg
+        D = cfg.head_dim
+        self.q_size, self.kv_size = self.w.nh * D, self.w.nkv * D
+        self.max_blocks = (max_model_len + block_size - 1) // block_size
+        dt = weights.dtype
+        self.k_cache = [torch.zeros(num_blocks, self.w.nkv, block_size, D, dtype=dt, device=device)
+                        for _ in range(cfg.num_hidden_layers)]
+        self.v_cache = [torch.zeros_like(k) for k in self.k_cache]
+        self.cos, self.sin = rope_tables(D, max(cfg.max_position_embeddings, max_model_len),
+                                         cfg.rope_theta, device)
+        self.scale = 1.0 / math.sqrt(D)
+        self.use_graphs = use_graphs and device.type == "cuda"
+        self.graph_buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 96, 128, 160, 192, 224, 256)
+                              if b <= max_graph_batch]
+        self._graphs: Dict[int, tuple] = {}
+        self._graph_pool = None
+        self.partition = 512
+
+    # ------------------------------------------------------------------------------------------
+    def _allreduce(self, x):
+        if self.tp > 1:
+            dist.all_reduce(x, group=self.tp_group)
+        return x
+
+    def _layers(self, h, positions, slots, attn_fn):
+        cfg = self.cfg
+        res = None
+        T = h.shape[0]
+        D = cfg.head_dim
+        for i, L in enumerate(self.w.layers):
+            y, res = rms_norm(h, L.ln1, cfg.rms_norm_eps, res)
+            qkv = torch.matmul(y, L.qkv.t())
+            rope_inplace(qkv, positions, self.w.nh + self.w.nkv, D, self.cos, self.sin)
+            qs, ks = self.q_size, self.kv_size
+            k = qkv[:, qs:qs + ks].view(T, self.w.nkv, D)
+            v = qkv[:, qs + ks:].view(T, self.w.nkv, D)
+            write_kv_cache(k, v, self.k_cache[i], self.v_cache[i], slots)
+            o = attn_fn(qkv, i)
+            a = self._allreduce(torch.matmul(o, L.o.t()))
+            y2, res = rms_norm(a, L.ln2, cfg.rms_norm_eps, res)
+            h = self._allreduce(torch.matmul(swiglu(torch.matmul(y2, L.gate_up.t())), L.down.t()))
+        return h, res
+
+    def _logits(self, h, res, rows):
+        y, _ = rms_norm(h[rows], self.w.norm, self.cfg.rms_norm_eps, res[rows])
+        return torch.matmul(y, self.w.lm_head.t())
+
+    # ---- prefill: whole prompts, packed ----------------------------------------------------
+    @torch.no_grad()
+    def prefill(self, inp: StepInput) -> torch.Tensor:
+        h = F.embedding(inp.tokens, self.w.embed)
+        cu = inp.cu_seqlens
+        nh, nkv, D = self.w.nh, self.w.nkv, self.cfg.head_dim
+        qs, ks = self.q_size, self.kv_size
+
+        def attn(qkv, i):
+            outs = []
+            for s in range(len(cu) - 1):
+                a, b = cu[s], cu[s + 1]
+                n = b - a
+                q = qkv[a:b, :qs].view(n, nh, D).transpose(0, 1)[None]
+                k = qkv[a:b, qs:qs + ks].view(n, nkv, D).transpose(0, 1)[None]
+                v = qkv[a:b, qs + ks:].view(n, nkv, D).transpose(0, 1)[None]
+                if nkv != nh:
+                    if q.is_cuda:
+                        o = F.scaled_dot_product_attention(q, k, v, is_causal=True,
+                                                           enable_gqa=True)
+                    else:
+                        rep = nh // nkv
+                        o = F.scaled_dot_product_attention(q, k.repeat_interleave(rep, 1),
+                                                           v.repeat_interleave(rep, 1),
+                                                           is_causal=True)
+                else:
+                    o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+                outs.append(o[0].transpose(0, 1).reshape(n, nh * D))
+            return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
+
+        h, res = self._layers(h, inp.positions, inp.slots, attn)
+        last = torch.tensor([c - 1 for c in cu[1:]], device=h.device)
+        return self._logits(h, res, last)
+
+    # ---- decode: one token per sequence ----------------------------------------------------
+    def _decode_eager(self, tokens, positions, slots, block_tables, context_lens, max_context):
+        h = F.embedding(tokens, self.w.embed)
+        N = tokens.shape[0]
+        nh, D = self.w.nh, self.cfg.head_dim
+
+        def attn(qkv, i):
+            q = qkv[:, :self.q_size].reshape(N, nh, D)
+            return paged_decode(q, self.k_cache[i], self.v_cache[i], block_tables, context_lens,
+                                max_context, self.scale, self.partition).view(N, nh * D)
+
+        h, res = self._layers(h, positions, slots, attn)
+        rows = torch.arange(N, device=h.device)
+        y, _ = rms_norm(h, self.w.norm, self.cfg.rms_norm_eps, res)
+        return torch.matmul(y, self.w.lm_head.t())
+
+    @torch.no_grad()
+    def decode(self, inp: StepInput) -> torch.Tensor:
+        N = inp.tokens.shape[0]
+        if not self.use_graphs or N > self.graph_buckets[-1]:
+            return self._decode_eager(inp.tokens, inp.positions, inp.slots, inp.block_tables,
+                                      inp.context_lens, inp.max_context)
+        bucket = next(b for b in self.graph_buckets if b >= N)
+        g = self._graphs.get(bucket)
+        if g is None:
+            g = self._capture(bucket)
+        graph, st, out = g
+        st["tokens"][:N].copy_(inp.tokens)
+        st["positions"][:N].copy_(inp.positions)
+        st["slots"][:N].copy_(inp.slots)
+        nb = inp.block_tables.shape[1]
+        st["block_tables"][:N, :nb].copy_(inp.block_tables)
+        st["context_lens"][:N].copy_(inp.context_lens)
+        if N < bucket:  # padding rows: no cache write, one-token context on block 0
+            st["slots"][N:].fill_(-1)
+            st["context_lens"][N:].fill_(1)
+        graph.replay()
+        return out[:N]
+
+    def _capture(self, bucket: int):
+        dev = self.device
+        st = {"tokens": torch.zeros(bucket, dtype=torch.long, device=dev),
+              "positions": torch.zeros(bucket, dtype=torch.int32, device=dev),
+              "slots": torch.full((bucket,), -1, dtype=torch.long, device=dev),
+              "block_tables": torch.zeros(bucket, self.max_blocks, dtype=torch.int32, device=dev),
+              "context_lens": torch.ones(bucket, dtype=torch.int32, device=dev)}
+        args = (st["tokens"], st["positions"], st["slots"], st["block_tables"],
+                st["context_lens"], self.max_model_len)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up (allocator, hipBLASLt heuristics) outside capture
+                self._decode_eager(*args)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(graph, pool=self._graph_pool):
+            out = self._decode_eager(*args)
+        self._graphs[bucket] = (graph, st, out)
+        return self._graphs[bucket]
+
+    # ---- sampling ----------------------------------------------------------------------------
+    @torch.no_grad()
+    def sample(self, logits: torch.Tensor, temps: Seq[float], top_ps: Seq[float],
+               top_ks: Seq[int], seed: int, offset: int, want_logprobs: bool = True):
+        R = logits.shape[0]
+        dev = logits.device
+        t = torch.tensor(temps, dtype=torch.float32, device=dev)
+        p = torch.tensor(top_ps, dtype=torch.float32, device=dev)
+        k = torch.tensor(top_ks, dtype=torch.int32, device=dev)
+        if use_native(logits):
+            out = torch.empty(R, dtype=torch.long, device=dev)
+            lp = torch.empty(R, dtype=torch.float32, device=dev) if want_logprobs else None
+            native().sample(logits.contiguous(), t, p, k, seed, offset, out, lp)
+            return out, lp
+        return sample_ref(logits, t, p, k, seed, offset)
+
+
+def sample_ref(logits, temps, top_ps, top_ks, seed, offset):
+    """Torch sampler (CPU path): same semantics as kernels/sampling.hip, torch RNG."""
+    R, V = logits.shape
+    g = torch.Generator(device=logits.device).manual_seed((seed * 1000003 + offset) & 0x7FFFFFFF)
+    out = torch.empty(R, dtype=torch.long, device=logits.device)
+    lps = torch.empty(R, dtype=torch.float32, device=logits.device)
+    for i in range(R):
+        z = logits[i].float()
+        T = float(temps[i])
+        if T <= 0:
+            tok = int(z.argmax())
+            zs = z
+        else:
+            zs = z / T
+            probs = torch.softmax(zs, -1)
+            keep = torch.ones(V, dtype=torch.bool, device=z.device)
+            k = int(top_ks[i])
+            if 0 < k < V:
+                thr = torch.topk(zs, k).values[-1]
+                keep &= zs >= thr
+            p = float(top_ps[i])
+            if p < 1.0:
+                sp, idx = torch.sort(probs, descending=True)
+                c = torch.cumsum(sp, 0)
+                cut = int((c < p).sum()) + 1
+                m = torch.zeros(V, dtype=torch.bool, device=z.device)
+                m[idx[:cut]] = True
+                keep &= m
+            pr = torch.where(keep, probs, torch.zeros_like(probs))
+            tok = int(torch.multinomial(pr / pr.sum(), 1, generator=g))
+        out[i] = tok
+        lps[i] = torch.log_softmax(zs, -1)[tok]
+    return out, lps

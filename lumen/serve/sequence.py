@@ -1,0 +1,84 @@
+"""Request / sequence state for the serving engine."""
+from __future__ import annotations
+
+import enum
+import itertools
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+
+@dataclass
+class SamplingParams:
+    max_tokens: int = 16
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = 0            # 0 = disabled
+    stop_token_ids: List[int] = field(default_factory=list)
+    ignore_eos: bool = False
+    seed: Optional[int] = None
+    logprobs: bool = False
+
+    def __post_init__(self):
+        if self.max_tokens < 1:
+            raise ValueError("max_tokens must be >= 1")
+        if self.temperature < 0:
+            raise ValueError("temperature must be >= 0")
+        if not 0.0 < self.top_p <= 1.0:
+            raise ValueError("top_p must be in (0, 1]")
+
+
+class Status(enum.Enum):
+    WAITING = 0
+    RUNNING = 1
+    FINISHED = 2
+
+
+_ids = itertools.count()
+
+
+@dataclass
+class Sequence:
+    prompt_ids: List[int]
+    params: SamplingParams
+    request_id: str = ""
+    seq_id: int = field(default_factory=lambda: next(_ids))
+    output_ids: List[int] = field(default_factory=list)
+    output_logprobs: List[float] = field(default_factory=list)
+    status: Status = Status.WAITING
+    finish_reason: Optional[str] = None
+    arrival: float = field(default_factory=time.perf_counter)
+    first_token_time: Optional[float] = None
+    last_token_time: Optional[float] = None
+    token_times: List[float] = field(default_factory=list)
+    num_cached: int = 0          # tokens whose K/V are in the cache
+    preemptions: int = 0
+
+    @property
+    def all_ids(self) -> List[int]:
+        return self.prompt_ids + self.output_ids
+
+    @property
+    def length(self) -> int:
+        return len(self.prompt_ids) + len(self.output_ids)
+
+    @property
+    def finished(self) -> bool:
+        return self.status == Status.FINISHED
+
+    def append(self, tok: int, logprob: Optional[float], eos_id: Optional[int]) -> None:
+        now = time.perf_counter()
+        if self.first_token_time is None:
+            self.first_token_time = now
+        self.last_token_time = now
+        self.token_times.append(now)
+        self.output_ids.append(tok)
+        if logprob is not None:
+            self.output_logprobs.append(logprob)
+        p = self.params
+        if not p.ignore_eos and eos_id is not None and tok == eos_id:
+            self.status, self.finish_reason = Status.FINISHED, "stop"
+        elif tok in p.stop_token_ids:
+            self.status, self.finish_reason = Status.FINISHED, "stop"
+        elif len(self.output_ids) >= p.max_tokens:
+            self.status, self.finish_reason = Status.FINISHED, "length"

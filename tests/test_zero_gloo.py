@@ -77,4 +77,5 @@ def test_zero2_cpu_offload_optimizer(tmp_path):
     ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama", micro=4, accum=1, steps=2)
     r = _run(2, 2, str(tmp_path / "b"), model="tiny-llama", micro=2, accum=1, steps=2,
              extra={"offload": True})
-    _close(r["sd"], ref["sd"])
+    # C++ AVX-512 AdamW vs torch AdamW: same math, different rounding order
+    _close(r["sd"], ref["sd"], tol=3e-4)
