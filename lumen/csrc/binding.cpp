@@ -39,6 +39,10 @@ hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, 
                                    int, int, int, int, long long, long long, int, hipStream_t);
 hipError_t lumen_sample(int, const void*, const float*, const float*, const int*,
                         unsigned long long, long long, long long*, float*, int, int, hipStream_t);
+hipError_t lumen_flash_attn(int, int, int, int, const void*, const void*, const void*, long long,
+                            long long, long long, void*, long long, float*, const int*, const int*,
+                            int, int, int, int, float, const void*, long long, void*, void*, void*,
+                            long long, long long, long long, const float*, hipStream_t);
 void lumen_cpu_adamw(float*, const float*, float*, float*, long long, float, float, float, float,
                      float, float, float, float);
 int lumen_cpu_has_avx512();
@@ -230,6 +234,28 @@ void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::T
         "sample");
 }
 
+// which: 0 fwd, 1 delta, 2 dK/dV, 3 dQ.  q/k/v/o/dout/dq/dk/dv are (possibly strided) 2-D views
+// [T, cols]: the kernels address head h at column h*128 with the given row strides.
+void flash_attn(int64_t which, bool causal, int64_t mt, const at::Tensor& q, const at::Tensor& k,
+                const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
+                const at::Tensor& cu, const at::Tensor& tiles, int64_t nh, int64_t nkv,
+                double scale, const std::optional<at::Tensor>& dout,
+                const std::optional<at::Tensor>& dq, const std::optional<at::Tensor>& dk,
+                const std::optional<at::Tensor>& dv, const std::optional<at::Tensor>& delta) {
+  if (!q.is_cuda()) throw std::invalid_argument("lumen: flash_attn needs GPU tensors");
+  auto st = [](const std::optional<at::Tensor>& t) -> long long { return t.has_value() ? t->stride(0) : 0; };
+  const int T = static_cast<int>(q.size(0));
+  const int ntiles = static_cast<int>(tiles.numel() / 2);
+  check(lumen_flash_attn(dcode(q), static_cast<int>(which), causal ? 1 : 0, static_cast<int>(mt),
+                         q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
+                         v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr<float>(),
+                         cu.data_ptr<int>(), tiles.data_ptr<int>(), ntiles, static_cast<int>(nh),
+                         static_cast<int>(nkv), T, static_cast<float>(scale), ptr(dout), st(dout),
+                         ptr(dq), ptr(dk), ptr(dv), st(dq), st(dk), st(dv), ptr<const float>(delta),
+                         cur_stream()),
+        "flash_attn");
+}
+
 void cpu_adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, double lr, double b1,
                double b2, double eps, double wd, double bc1, double bc2, double grad_scale) {
   if (p.is_cuda() || g.is_cuda()) throw std::invalid_argument("lumen: cpu_adamw takes host tensors");
@@ -257,6 +283,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("paged_attention_decode", &paged_attention_decode);
   m.def("reshape_and_cache", &reshape_and_cache);
   m.def("sample", &sample);
+  m.def("flash_attn", &flash_attn);
   m.def("cpu_adamw", &cpu_adamw);
   m.def("cpu_has_avx512", &lumen_cpu_has_avx512);
 }

@@ -1,0 +1,658 @@
+// Flash attention forward + backward for gfx950, varlen + causal + GQA.
+//
+// Reference behaviour: torch SDPA inside transformers' Llama attention (the model loaded at
+// training/train_baseline.py:122), preceded by a [B,S,H,D] -> [B,H,S,D] transpose of q/k/v and
+// followed by the inverse transpose before o_proj.
+//
+// Here attention reads q/k/v IN PLACE from the fused token-major QKV GEMM output
+// [T, (nh + 2 nkv) * D] (head h of q at column h*D, of k at (nh + h)*D, ...) and writes O
+// token-major [T, nh*D] = exactly the o_proj input, so the split/transpose copies disappear.
+// Sequences are packed back to back (cu_seqlens); the host passes the list of (sequence,
+// row-start) tiles, heaviest causal tiles first.
+//
+// Tiling (D = 128, wave64, MFMA v_mfma_f32_16x16x32_{bf16,f16}):
+//  fwd   workgroup = 4 waves x (16*MT) query rows; K/V tiles of 64 keys staged in LDS as
+//        "dual-use" images (XOR-swizzled 256-byte rows: conflict-free ds_read_b128 row reads
+//        for K^T operands AND ds_read_b64_tr_b16 transposed reads for V operands); online
+//        softmax in exp2 domain on the MFMA accumulators; P goes through a small per-wave LDS
+//        tile (8-byte writes, transposed reads) to become the A operand of P.V.
+//  bwd   two kernels, no atomics: dK/dV per 64-key tile (each wave 16 keys, K and V fragments
+//        in registers, loops over query tiles and the GQA group's heads), and dQ per 64-query
+//        tile (loops over key tiles); the softmax row statistics come from the forward's LSE
+//        and delta = rowsum(dO * O) (preprocess kernel).
+#include "common.h"
+
+namespace lumen {
+namespace fa {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int D = 128;     // head dim (Llama family)
+constexpr int BN = 64;     // keys per tile
+constexpr int IMG = BN * D * 2;  // bytes of one [64][128] 16-bit LDS image
+
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16> {
+  static __device__ __forceinline__ f32x4 run(uint4 a, uint4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<fp16> {
+  static __device__ __forceinline__ f32x4 run(uint4 a, uint4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+// ---- LDS image of a [rows][128] 16-bit tile: 256-byte rows, 16-byte chunks XOR-swizzled ----
+__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int img_off(int row, int chunk) {
+  return row * 256 + ((chunk ^ swz(row)) << 4);
+}
+
+// stage rows [r0, r0+64) x 128 cols of a token-major matrix (row stride ld elements) into img;
+// rows >= rmax are zero-filled.  256 threads x 4 chunks of 16 bytes.
+template <typename T>
+__device__ __forceinline__ void stage64(char* img, const T* base, long long ld, int r0, int rmax) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + i * 256;
+    const int row = idx >> 4, ch = idx & 15;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + row < rmax) v = *reinterpret_cast<const uint4*>(base + (long long)(r0 + row) * ld + ch * 8);
+    *reinterpret_cast<uint4*>(img + img_off(row, ch)) = v;
+  }
+}
+
+// Asynchronous variant: global_load_lds (LDS-DMA, 16 B per lane, no VGPRs) into the same
+// swizzled image.  One wave-instruction fills 1 KiB = 4 image rows; wave w issues rows
+// [16w, 16w+16) in 4 instructions.  The swizzle moves to the per-lane SOURCE address (the LDS side
+// of an LDS-DMA is lane-linear).  Rows >= rmax are clamped to row rmax-1 (finite data; the
+// softmax masks those keys).  Completion: the issuing wave's vmcnt, then a barrier.
+template <typename T>
+__device__ __forceinline__ void stage64_async(char* img, const T* base, long long ld, int r0,
+                                              int rmax) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ swz(row);
+    int gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)(base + (long long)gr * ld + ch * 8),
+        (__attribute__((address_space(3))) void*)(img + (wid * 4 + i) * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_vm_8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+__device__ __forceinline__ void lds_fence_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 16-byte row read: 8 consecutive columns [8*chunk, 8*chunk+8) of `row`
+__device__ __forceinline__ uint4 row_read(const char* img, int row, int chunk) {
+  return *reinterpret_cast<const uint4*>(img + img_off(row, chunk));
+}
+
+__device__ __forceinline__ uint2 tr_read_raw(const char* p) {
+  s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+  return __builtin_bit_cast(uint2, r);
+}
+
+// B operand (k = rows, n = cols) of a 16x16x32 MFMA from an image whose rows are the k axis:
+// lane (L = lane&15, g = lane>>4) gets col n0 + L, rows k0 + 8g + 0..7.
+__device__ __forceinline__ uint4 tr_read_img(const char* img, int k0, int n0, int lane) {
+  const int L = lane & 15, g = lane >> 4;
+  const int col = n0 + 4 * (L & 3);
+  const int ch = col >> 3, half = (col >> 2) & 1;
+  const int r = k0 + 8 * g + (L >> 2);
+  const uint2 lo = tr_read_raw(img + img_off(r, ch) + 8 * half);
+  const uint2 hi = tr_read_raw(img + img_off(r + 4, ch) + 8 * half);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+// Per-wave scratch Y[rows k][cols m] (plain row-major, `cols` 16-bit elements per row): C tiles are
+// written transposed with 8-byte stores and read back as A operands (row m, 8 consecutive k).
+// Y rows are padded by 4 elements (8 bytes) so the 16 rows of one 8-byte transposed store land on
+// distinct banks.
+__device__ __forceinline__ uint4 tr_read_y(const char* y, int cols, int k0, int m0, int lane) {
+  const int L = lane & 15, g = lane >> 4;
+  const int r = k0 + 8 * g + (L >> 2);
+  const int c = m0 + 4 * (L & 3);
+  const int ld = cols + 4;
+  const uint2 lo = tr_read_raw(y + (r * ld + c) * 2);
+  const uint2 hi = tr_read_raw(y + ((r + 4) * ld + c) * 2);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+// write a 16x16 C tile (lane: col = lane&15, rows 4*(lane>>4)+0..3) transposed into Y at
+// Y[k = k0 + col][m = m0 + 4*(lane>>4) .. +3] as one 8-byte store
+template <typename T>
+__device__ __forceinline__ void y_store(char* y, int cols, int k0, int m0, int lane, float v0,
+                                        float v1, float v2, float v3) {
+  T t[4] = {from_f32<T>(v0), from_f32<T>(v1), from_f32<T>(v2), from_f32<T>(v3)};
+  *reinterpret_cast<uint2*>(y + ((k0 + (lane & 15)) * (cols + 4) + m0 + 4 * (lane >> 4)) * 2) =
+      *reinterpret_cast<uint2*>(t);
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 gload16(const T* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+}
+
+// Row reductions over the 16 lanes that share a 16x16 C-tile row, on the DPP cross-lane path
+// (quad_perm xor1, xor2, row_half_mirror, row_mirror): 4 VALU ops instead of 4 LDS-routed
+// ds_bpermute shuffles per reduction.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+__device__ __forceinline__ float red16_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp<0x141>(v));  // row_half_mirror
+  v = fmaxf(v, dpp<0x140>(v));  // row_mirror
+  return v;
+}
+__device__ __forceinline__ float red16_sum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x140>(v);
+  return v;
+}
+
+struct Args {
+  const void* q; const void* k; const void* v;  // token-major bases (head 0)
+  long long ldq, ldk, ldv;
+  void* o; long long ldo;
+  float* lse;                                     // [nh][T] (log2 domain)
+  const int* cu;                                  // [nseq + 1]
+  const int* tiles;                               // [ntiles][2] = (seq, row start)
+  int nh, nkv, T;
+  float scale, scale_log2;
+  // backward
+  const void* dout; long long lddo;
+  void* dq; void* dk; void* dv; long long lddq, lddk, lddv;
+  const float* delta;                             // [nh][T]
+};
+
+// =============================================================================================
+// forward
+// =============================================================================================
+template <typename T, bool CAUSAL, int MT>
+__global__ void __launch_bounds__(256, 2) fwd_kernel(Args a) {
+  constexpr int QW = 16 * MT;        // query rows per wave
+  constexpr int BM = 4 * QW;         // query rows per workgroup
+  constexpr int YCOLS = QW;          // P^T scratch: [64 keys][QW queries]
+  constexpr int YB = BN * (YCOLS + 4) * 2;  // bytes of one wave's Y scratch
+  // [K0 | V0 | K1 | V1 | Y x 4]: K/V double-buffered, filled by LDS-DMA one tile ahead
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 4 * YB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  char* y = smem + 4 * IMG + wid * YB;
+  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
+  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const int wq0 = q0 + wid * QW;     // first query row of this wave
+
+  uint4 qf[MT][4];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = wq0 + mt * 16 + lr;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      qf[mt][ks] = gload16(Q + (long long)row * a.ldq + (4 * ks + lg) * 8, row < L);
+  }
+  f32x4 acc[MT][8];
+  float m_i[MT][4], l_i[MT][4];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[mt][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { m_i[mt][r] = -INFINITY; l_i[mt][r] = 0.f; }
+  }
+  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
+  if (kv_end > 0) {
+    stage64_async(smem, K, a.ldk, 0, L);
+    stage64_async(smem + IMG, V, a.ldv, 0, L);
+  }
+  int it = 0;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
+    char* kimg = smem + (it & 1) * 2 * IMG;
+    char* vimg = kimg + IMG;
+    if (kv0 + BN < kv_end) {  // prefetch the next tile into the other buffer, then wait for this one
+      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
+      stage64_async(nk, K, a.ldk, kv0 + BN, L);
+      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
+      wait_vm_8();
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+    // S = Q K^T   [QW x 64] per wave
+    f32x4 s[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) s[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const uint4 b = row_read(kimg, nt * 16 + lr, 4 * ks + lg);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) s[mt][nt] = Mfma<T>::run(qf[mt][ks], b, s[mt][nt]);
+      }
+    }
+    // online softmax (exp2 domain); rows of this lane: wq0 + 16mt + 4lg + r
+    // masking only where a key can be past the sequence end or above this wave's first row
+    const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float pr[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qrow = wq0 + mt * 16 + 4 * lg + r;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          float x = s[mt][nt][r] * a.scale_log2;
+          if (need_mask) {
+            const int kpos = kv0 + nt * 16 + lr;
+            if (kpos >= L || (CAUSAL && kpos > qrow)) x = -INFINITY;
+          }
+          pr[nt][r] = x;
+          mx = fmaxf(mx, x);
+        }
+        mx = red16_max(mx);
+        const float m_new = fmaxf(m_i[mt][r], mx);
+        const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_i[mt][r] - m_new);
+        float rs = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const float p = (m_new == -INFINITY) ? 0.f : exp2f(pr[nt][r] - m_new);
+          pr[nt][r] = p;
+          rs += p;
+        }
+        rs = red16_sum(rs);
+        l_i[mt][r] = l_i[mt][r] * alpha + rs;
+        m_i[mt][r] = m_new;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) acc[mt][n][r] *= alpha;
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        y_store<T>(y, YCOLS, nt * 16, mt * 16, lane, pr[nt][0], pr[nt][1], pr[nt][2], pr[nt][3]);
+    }
+    // Y is per-wave: the wave's own LDS writes must land before its transposed reads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // O += P V
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 pa[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) pa[mt] = tr_read_y(y, YCOLS, 32 * ks, mt * 16, lane);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const uint4 b = tr_read_img(vimg, 32 * ks, n * 16, lane);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt][n] = Mfma<T>::run(pa[mt], b, acc[mt][n]);
+      }
+    }
+    lds_fence_barrier();  // every wave is done with this K/V buffer before it is refilled
+  }
+  // epilogue: O /= l ; LSE (log2) per row
+  T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qrow = wq0 + mt * 16 + 4 * lg + r;
+      if (qrow >= L) continue;
+      const float inv = l_i[mt][r] > 0.f ? 1.f / l_i[mt][r] : 0.f;
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        O[(long long)qrow * a.ldo + n * 16 + lr] = from_f32<T>(acc[mt][n][r] * inv);
+      if (lr == 0 && a.lse)
+        a.lse[(long long)head * a.T + s0 + qrow] =
+            l_i[mt][r] > 0.f ? m_i[mt][r] + __log2f(l_i[mt][r]) : INFINITY;
+    }
+  }
+}
+
+// =============================================================================================
+// backward: delta = rowsum(dO * O)
+// =============================================================================================
+template <typename T>
+__global__ void __launch_bounds__(256) delta_kernel(Args a) {
+  const long long tid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (tid >= (long long)a.T * a.nh) return;
+  const int t = (int)(tid / a.nh), h = (int)(tid % a.nh);
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (long long)t * a.lddo + h * D;
+  const T* O = reinterpret_cast<const T*>(a.o) + (long long)t * a.ldo + h * D;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < D; c += 8) {
+    float x[8], y[8];
+    load8(dO + c, x);
+    load8(O + c, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+  }
+  const_cast<float*>(a.delta)[(long long)h * a.T + t] = s;
+}
+
+// =============================================================================================
+// backward: dK, dV  (workgroup = 64 keys of one kv head; loops over q tiles and group heads)
+// =============================================================================================
+template <typename T, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
+  constexpr int YC = 16;  // Y scratch: [64 queries][16 keys] per wave (P^T, then dS^T)
+  constexpr int YB = 64 * (YC + 4) * 2;
+  constexpr int STAGE = 2 * IMG + 512;  // Q image | dO image | lse[64] | delta[64]
+  // two stages filled by LDS-DMA one (head, q-tile) step ahead, then the per-wave Y scratch
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 4 * YB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  char* y = smem + 2 * STAGE + wid * YB;
+  const int seq = a.tiles[2 * blockIdx.x], k0 = a.tiles[2 * blockIdx.x + 1];
+  const int kvh = blockIdx.y;
+  const int grp = a.nh / a.nkv;
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const int wk0 = k0 + wid * 16;  // this wave's 16 keys
+  uint4 kf[4], vf[4];
+  {
+    const int row = wk0 + lr;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      kf[ks] = gload16(K + (long long)row * a.ldk + (4 * ks + lg) * 8, row < L);
+      vf[ks] = gload16(V + (long long)row * a.ldv + (4 * ks + lg) * 8, row < L);
+    }
+  }
+  wait_vm_all();
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) { dk[n] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[n] = dk[n]; }
+  const int qstart = CAUSAL ? (k0 / 64) * 64 : 0;
+  const int nq = qstart < L ? (L - qstart + 63) / 64 : 0;
+  const int nsteps = grp * nq;  // (group head, query tile) pairs
+  // stage step j: Q / dO tiles via 8 DMA instructions per wave, lse / delta via one 4-byte DMA
+  // instruction on waves 0 / 1 (the DMA ring stays the only in-loop global traffic, so the
+  // counted vmcnt waits below stay exact: every wave keeps the same count per step, waves 0/1
+  // issue one more, waited with vmcnt(0) on the last step only)
+  auto stage = [&](int j, char* st) {
+    const int hh = j / nq, q0 = qstart + (j % nq) * 64;
+    const int head = kvh * grp + hh;
+    stage64_async(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
+                  q0, L);
+    stage64_async(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D,
+                  a.lddo, q0, L);
+    if (wid < 2) {
+      const float* src = (wid == 0 ? a.lse : a.delta) + (long long)head * a.T + s0;
+      int qr = q0 + lane;
+      qr = qr < L ? qr : L - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(src + qr),
+                                       (__attribute__((address_space(3))) void*)(st + 2 * IMG + wid * 256),
+                                       4, 0, 0);
+    }
+  };
+  if (nsteps > 0) stage(0, smem);
+  for (int j = 0; j < nsteps; ++j) {
+    char* st = smem + (j & 1) * STAGE;
+    char* qimg = st;
+    char* oimg = st + IMG;
+    const float* s_lse = reinterpret_cast<const float*>(st + 2 * IMG);
+    const float* s_del = s_lse + 64;
+    const int q0 = qstart + (j % nq) * 64;
+    if (j + 1 < nsteps) {
+      stage(j + 1, smem + ((j + 1) & 1) * STAGE);
+      if (wid < 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+    // S^T = K Q^T and dP^T = V dO^T   [16 keys x 64 queries]
+    f32x4 st_[4], dpt[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) { st_[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dpt[nt] = st_[nt]; }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        st_[nt] = Mfma<T>::run(kf[ks], row_read(qimg, nt * 16 + lr, 4 * ks + lg), st_[nt]);
+        dpt[nt] = Mfma<T>::run(vf[ks], row_read(oimg, nt * 16 + lr, 4 * ks + lg), dpt[nt]);
+      }
+    }
+    // P^T (to Y) ; lane: query col = q0 + 16nt + lr, key rows = wk0 + 4lg + r
+    float ds[4][4];
+    const bool need_mask = (q0 + 64 > L) || (CAUSAL && wk0 + 15 > q0);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int qc = nt * 16 + lr;
+      const float lq = s_lse[qc], dq = s_del[qc];
+      float p[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pv = exp2f(st_[nt][r] * a.scale_log2 - lq);
+        if (need_mask) {
+          const int krow = wk0 + 4 * lg + r;
+          if (krow >= L || q0 + qc >= L || (CAUSAL && krow > q0 + qc)) pv = 0.f;
+        }
+        p[r] = pv;
+        ds[nt][r] = pv * (dpt[nt][r] - dq);
+      }
+      y_store<T>(y, YC, nt * 16, 0, lane, p[0], p[1], p[2], p[3]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // dV += P^T dO
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint4 pa = tr_read_y(y, YC, 32 * ks, 0, lane);
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        dv[n] = Mfma<T>::run(pa, tr_read_img(oimg, 32 * ks, n * 16, lane), dv[n]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P^T reads done before dS^T overwrites Y
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+      y_store<T>(y, YC, nt * 16, 0, lane, ds[nt][0], ds[nt][1], ds[nt][2], ds[nt][3]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // dK += dS^T Q
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint4 da = tr_read_y(y, YC, 32 * ks, 0, lane);
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        dk[n] = Mfma<T>::run(da, tr_read_img(qimg, 32 * ks, n * 16, lane), dk[n]);
+    }
+    lds_fence_barrier();  // stage buffer free for the DMA two steps ahead
+  }
+  // write dK (x softmax scale), dV : rows wk0 + 4lg + r, cols 16n + lr
+  T* dK = reinterpret_cast<T*>(a.dk) + (long long)s0 * a.lddk + kvh * D;
+  T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int krow = wk0 + 4 * lg + r;
+    if (krow >= L) continue;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      dK[(long long)krow * a.lddk + n * 16 + lr] = from_f32<T>(dk[n][r] * a.scale);
+      dV[(long long)krow * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
+    }
+  }
+}
+
+// =============================================================================================
+// backward: dQ  (workgroup = 64 queries of one head; loops over key tiles)
+// =============================================================================================
+template <typename T, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) bwd_dq_kernel(Args a) {
+  constexpr int YC = 16;  // Y scratch: [64 keys][16 queries] per wave
+  constexpr int YB = 64 * (YC + 4) * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 4 * YB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  char* y = smem + 4 * IMG + wid * YB;
+  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
+  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const int wq0 = q0 + wid * 16;
+  uint4 qf[4], of[4];
+  {
+    const int row = wq0 + lr;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qf[ks] = gload16(Q + (long long)row * a.ldq + (4 * ks + lg) * 8, row < L);
+      of[ks] = gload16(dO + (long long)row * a.lddo + (4 * ks + lg) * 8, row < L);
+    }
+  }
+  float lse_r[4], del_r[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qrow = wq0 + 4 * lg + r;
+    lse_r[r] = qrow < L ? a.lse[(long long)head * a.T + s0 + qrow] : INFINITY;
+    del_r[r] = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
+  }
+  f32x4 dq[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) dq[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kv_end = CAUSAL ? min(L, q0 + 64) : L;
+  wait_vm_all();  // Q / dO fragments and row statistics are in registers before the DMA ring starts
+  if (kv_end > 0) {
+    stage64_async(smem, K, a.ldk, 0, L);
+    stage64_async(smem + IMG, V, a.ldv, 0, L);
+  }
+  int it = 0;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
+    char* kimg = smem + (it & 1) * 2 * IMG;
+    char* vimg = kimg + IMG;
+    if (kv0 + BN < kv_end) {
+      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
+      stage64_async(nk, K, a.ldk, kv0 + BN, L);
+      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
+      wait_vm_8();
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) { s[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[nt] = s[nt]; }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        s[nt] = Mfma<T>::run(qf[ks], row_read(kimg, nt * 16 + lr, 4 * ks + lg), s[nt]);
+        dp[nt] = Mfma<T>::run(of[ks], row_read(vimg, nt * 16 + lr, 4 * ks + lg), dp[nt]);
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int kpos = kv0 + nt * 16 + lr;
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qrow = wq0 + 4 * lg + r;
+        float pv = exp2f(s[nt][r] * a.scale_log2 - lse_r[r]);
+        if (kpos >= L || qrow >= L || (CAUSAL && kpos > qrow)) pv = 0.f;
+        ds[r] = pv * (dp[nt][r] - del_r[r]);
+      }
+      y_store<T>(y, YC, nt * 16, 0, lane, ds[0], ds[1], ds[2], ds[3]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint4 da = tr_read_y(y, YC, 32 * ks, 0, lane);
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        dq[n] = Mfma<T>::run(da, tr_read_img(kimg, 32 * ks, n * 16, lane), dq[n]);
+    }
+    lds_fence_barrier();
+  }
+  T* dQ = reinterpret_cast<T*>(a.dq) + (long long)s0 * a.lddq + head * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qrow = wq0 + 4 * lg + r;
+    if (qrow >= L) continue;
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+      dQ[(long long)qrow * a.lddq + n * 16 + lr] = from_f32<T>(dq[n][r] * a.scale);
+  }
+}
+
+template <typename T>
+static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& a, hipStream_t st) {
+  dim3 block(256);
+  if (which == 0) {
+    dim3 grid(ntiles, a.nh);
+    if (causal) {
+      if (mt == 2) hipLaunchKernelGGL((fwd_kernel<T, true, 2>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((fwd_kernel<T, true, 1>), grid, block, 0, st, a);
+    } else {
+      if (mt == 2) hipLaunchKernelGGL((fwd_kernel<T, false, 2>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((fwd_kernel<T, false, 1>), grid, block, 0, st, a);
+    }
+  } else if (which == 1) {
+    dim3 grid((unsigned)(((long long)a.T * a.nh + 255) / 256));
+    hipLaunchKernelGGL(delta_kernel<T>, grid, block, 0, st, a);
+  } else if (which == 2) {
+    dim3 grid(ntiles, a.nkv);
+    if (causal) hipLaunchKernelGGL((bwd_dkdv_kernel<T, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((bwd_dkdv_kernel<T, false>), grid, block, 0, st, a);
+  } else if (which == 3) {
+    dim3 grid(ntiles, a.nh);
+    if (causal) hipLaunchKernelGGL((bwd_dq_kernel<T, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((bwd_dq_kernel<T, false>), grid, block, 0, st, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fa
+}  // namespace lumen
+
+// which: 0 = forward (tiles of 64*mt query rows), 1 = delta, 2 = dK/dV (64-key tiles),
+//        3 = dQ (64-query tiles)
+extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
+                                       const void* q, const void* k, const void* v,
+                                       long long ldq, long long ldk, long long ldv, void* o,
+                                       long long ldo, float* lse, const int* cu,
+                                       const int* tiles, int ntiles, int nh, int nkv, int T,
+                                       float scale, const void* dout, long long lddo, void* dq,
+                                       void* dk, void* dv, long long lddq, long long lddk,
+                                       long long lddv, const float* delta, hipStream_t st) {
+  if (nkv <= 0 || nh % nkv != 0) return hipErrorInvalidValue;
+  if (which != 1 && ntiles == 0) return hipSuccess;
+  lumen::fa::Args a;
+  a.q = q; a.k = k; a.v = v; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.o = o; a.ldo = ldo;
+  a.lse = lse; a.cu = cu; a.tiles = tiles; a.nh = nh; a.nkv = nkv; a.T = T;
+  a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
+  a.dout = dout; a.lddo = lddo; a.dq = dq; a.dk = dk; a.dv = dv; a.lddq = lddq; a.lddk = lddk;
+  a.lddv = lddv; a.delta = delta;
+  if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
+  if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
+  return hipErrorInvalidValue;
+}

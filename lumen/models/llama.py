@@ -20,9 +20,9 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
 from ..ops.activation import swiglu
-from ..ops.attention import causal_attention
+from ..ops.attention import causal_attention, flash_attention_qkv
 from ..ops.loss import lm_head_cross_entropy
-from ..ops.rope import qkv_rope_split, rope_tables
+from ..ops.rope import qkv_rope_split, rope_qkv_, rope_tables
 from .config import ModelConfig
 from .layers import Linear, RMSNorm
 
@@ -39,12 +39,33 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x2d: torch.Tensor, B: int, S: int, pos: Optional[torch.Tensor] = None):
         c = self.cfg
+        nh, nkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
         qkv = self.qkv_proj(x2d)
-        cos, sin = rope_tables(c.head_dim, c.max_position_embeddings, c.rope_theta, x2d.device)
-        q, k, v = qkv_rope_split(qkv, B, S, c.num_attention_heads, c.num_key_value_heads,
-                                 c.head_dim, cos, sin, pos)
+        cos, sin = rope_tables(D, c.max_position_embeddings, c.rope_theta, x2d.device)
+        if qkv.is_cuda and D == 128 and USE_FLASH:
+            # HIP path: RoPE in place on the fused buffer, flash attention reads q/k/v from it and
+            # writes O token-major (no split / transpose copies)
+            if pos is None:
+                pos = _positions(B, S, x2d.device)
+            qkv = rope_qkv_(qkv, pos, nh, nkv, D, cos, sin)
+            o = flash_attention_qkv(qkv, tuple(range(0, B * S + 1, S)), nh, nkv, D, True)
+            return self.o_proj(o)
+        q, k, v = qkv_rope_split(qkv, B, S, nh, nkv, D, cos, sin, pos)
         o = causal_attention(q, k, v)
         return self.o_proj(o)
+
+
+USE_FLASH = True
+_POS = {}
+
+
+def _positions(B: int, S: int, device) -> torch.Tensor:
+    key = (B, S, str(device))
+    t = _POS.get(key)
+    if t is None:
+        t = torch.arange(S, dtype=torch.int32, device=device).repeat(B)
+        _POS[key] = t
+    return t
 
 
 class LlamaMLP(nn.Module):

@@ -99,3 +99,111 @@ def write_kv_cache(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor,
     blk, off = sm // bs, sm % bs
     k_cache[blk, :, off] = k[valid].to(k_cache.dtype)
     v_cache[blk, :, off] = v[valid].to(v_cache.dtype)
+
+
+# ------------------------------------------------------------------------------------------------
+# HIP flash attention over the fused token-major QKV buffer (kernels/flash_attn.hip)
+# ------------------------------------------------------------------------------------------------
+
+_TILE_CACHE = {}
+
+
+def _tiles(cu: tuple, rows: int, device, heavy_first: bool = True) -> torch.Tensor:
+    key = (cu, rows, str(device), heavy_first)
+    t = _TILE_CACHE.get(key)
+    if t is None:
+        lst = []
+        for s in range(len(cu) - 1):
+            L = cu[s + 1] - cu[s]
+            lst += [(s, r) for r in range(0, L, rows)]
+        if heavy_first:  # causal: the last tiles of a sequence carry the most keys
+            lst.sort(key=lambda x: -x[1])
+        t = torch.tensor(lst if lst else [(0, 0)], dtype=torch.int32, device=device).reshape(-1)
+        if not lst:
+            t = t[:0]
+        if len(_TILE_CACHE) > 256:
+            _TILE_CACHE.clear()
+        _TILE_CACHE[key] = t
+    return t
+
+
+def _cu_tensor(cu: tuple, device) -> torch.Tensor:
+    key = ("cu", cu, str(device))
+    t = _TILE_CACHE.get(key)
+    if t is None:
+        t = torch.tensor(cu, dtype=torch.int32, device=device)
+        _TILE_CACHE[key] = t
+    return t
+
+
+import os as _os
+FA_MT = int(_os.environ.get("LUMEN_FA_MT", "1"))  # query m-tiles (16 rows) per wave in the fwd
+
+
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cu, nh, nkv, D, causal):
+        C = native()
+        T = qkv.shape[0]
+        q = qkv[:, :nh * D]
+        k = qkv[:, nh * D:(nh + nkv) * D]
+        v = qkv[:, (nh + nkv) * D:]
+        o = torch.empty(T, nh * D, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
+        cut = _cu_tensor(cu, qkv.device)
+        scale = 1.0 / math.sqrt(D)
+        C.flash_attn(0, causal, FA_MT, q, k, v, o, lse, cut, _tiles(cu, 64 * FA_MT, qkv.device),
+                     nh, nkv, scale, None, None, None, None, None)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.meta = (cu, nh, nkv, D, causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        C = native()
+        qkv, o, lse = ctx.saved_tensors
+        cu, nh, nkv, D, causal, scale = ctx.meta
+        do = do.contiguous()
+        T = qkv.shape[0]
+        q = qkv[:, :nh * D]
+        k = qkv[:, nh * D:(nh + nkv) * D]
+        v = qkv[:, (nh + nkv) * D:]
+        dqkv = torch.empty_like(qkv)
+        dq = dqkv[:, :nh * D]
+        dk = dqkv[:, nh * D:(nh + nkv) * D]
+        dv = dqkv[:, (nh + nkv) * D:]
+        delta = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
+        cut = _cu_tensor(cu, qkv.device)
+        C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
+                     scale, do, None, None, None, delta)
+        C.flash_attn(2, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
+                     scale, do, dq, dk, dv, delta)
+        C.flash_attn(3, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
+                     scale, do, dq, dk, dv, delta)
+        return dqkv, None, None, None, None, None
+
+
+def flash_attention_qkv(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int,
+                        causal: bool = True) -> torch.Tensor:
+    """Causal attention straight from the fused token-major QKV buffer [T, (nh+2nkv)*D]
+    (q/k already rotated); returns O token-major [T, nh*D].  ``cu_seqlens``: sequence offsets."""
+    cu = tuple(int(c) for c in cu_seqlens)
+    if use_native(qkv) and D == 128:
+        return _FlashAttn.apply(qkv, cu, nh, nkv, D, causal)
+    return flash_attention_ref(qkv, cu, nh, nkv, D, causal)
+
+
+def flash_attention_ref(qkv, cu, nh, nkv, D, causal=True):
+    outs = []
+    for s in range(len(cu) - 1):
+        a, b = cu[s], cu[s + 1]
+        n = b - a
+        q = qkv[a:b, :nh * D].view(n, nh, D).transpose(0, 1)[None]
+        k = qkv[a:b, nh * D:(nh + nkv) * D].view(n, nkv, D).transpose(0, 1)[None]
+        v = qkv[a:b, (nh + nkv) * D:].view(n, nkv, D).transpose(0, 1)[None]
+        if nkv != nh:
+            rep = nh // nkv
+            k, v = k.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=causal)
+        outs.append(o[0].transpose(0, 1).reshape(n, nh * D))
+    return torch.cat(outs, 0)

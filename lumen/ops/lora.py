@@ -200,12 +200,14 @@ class _Linear(torch.autograd.Function):
 def linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor] = None,
            w_param: Optional[torch.Tensor] = None) -> torch.Tensor:
     shp = x.shape
-    x2d = x.reshape(-1, shp[-1])
+    x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
     if use_native(x2d):
         y = _Linear.apply(x2d.contiguous(), weight_fn, bias, w_param)
     else:
         y = F.linear(x2d, _frozen(weight_fn()), bias)
-    return y.view(*shp[:-1], y.shape[-1])
+    # 2-D in -> return the Function output itself (not a view): a view would make a later
+    # in-place op on it (RoPE on the fused QKV buffer) go through autograd's CopySlices
+    return y if x.dim() == 2 else y.view(*shp[:-1], y.shape[-1])
 
 
 def _frozen(W: torch.Tensor) -> torch.Tensor:
@@ -218,13 +220,13 @@ def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: tor
                 B: torch.Tensor, segs: List[Seg], r: int, scale: float, p: float, seed: int,
                 w_param: Optional[torch.Tensor] = None) -> torch.Tensor:
     shp = x.shape
-    x2d = x.reshape(-1, shp[-1])
+    x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
     if use_native(x2d):
         y = _LoraLinear.apply(x2d.contiguous(), weight_fn, bias, A, B, segs, r, scale, p, seed,
                               w_param)
     else:
         y = lora_linear_ref(x2d, _frozen(weight_fn()), bias, A, B, segs, r, scale, p, seed)
-    return y.view(*shp[:-1], y.shape[-1])
+    return y if x.dim() == 2 else y.view(*shp[:-1], y.shape[-1])
 
 
 def lora_linear_ref(x2d, W, bias, A, B, segs, r, scale, p, seed):

@@ -107,3 +107,50 @@ def rope_inplace(x2d: torch.Tensor, pos: torch.Tensor, nheads: int, D: int,
     p = pos.long()
     cos, sin = cos_t[p][:, None], sin_t[p][:, None]
     view.copy_(_rotate_ref(view, cos, sin))
+
+
+_NEG_SIN = {}
+
+
+def _neg(sin_t):
+    k = (sin_t.data_ptr(), sin_t.shape, str(sin_t.device))
+    t = _NEG_SIN.get(k)
+    if t is None:
+        t = (-sin_t).contiguous()
+        _NEG_SIN[k] = t
+    return t
+
+
+class _RopeQKV(torch.autograd.Function):
+    """In-place RoPE on the q and k heads of the fused QKV buffer (training path of the HIP
+    flash attention); backward = the inverse rotation (sin -> -sin) applied in place."""
+
+    @staticmethod
+    def forward(ctx, qkv, pos, nqk, D, cos_t, sin_t):
+        native().rope_inplace(qkv, pos, cos_t, sin_t, qkv.shape[0], qkv.stride(0), nqk, D)
+        ctx.mark_dirty(qkv)
+        ctx.save_for_backward(pos)
+        ctx.meta = (nqk, D, cos_t, sin_t)
+        return qkv
+
+    @staticmethod
+    def backward(ctx, g):
+        (pos,) = ctx.saved_tensors
+        nqk, D, cos_t, sin_t = ctx.meta
+        # g is the flash-attention backward's fresh dQKV buffer (sole consumer): rotate it in
+        # place instead of copying 3*T*H*2 bytes
+        g = g if g.is_contiguous() else g.contiguous()
+        native().rope_inplace(g, pos, cos_t, _neg(sin_t), g.shape[0], g.stride(0), nqk, D)
+        return g, None, None, None, None, None
+
+
+def rope_qkv_(qkv: torch.Tensor, pos: torch.Tensor, nh: int, nkv: int, D: int, cos_t, sin_t):
+    """Rotate q and k heads of qkv [T, (nh+2nkv)*D] in place (autograd-aware)."""
+    if use_native(qkv):
+        return _RopeQKV.apply(qkv, pos.to(torch.int32).contiguous(), nh + nkv, D, cos_t, sin_t)
+    T = qkv.shape[0]
+    out = qkv.clone()
+    view = out[:, :(nh + nkv) * D].view(T, nh + nkv, D)
+    p = pos.long()
+    rot = _rotate_ref(view, cos_t[p][:, None], sin_t[p][:, None])
+    return torch.cat([rot.reshape(T, -1), out[:, (nh + nkv) * D:]], 1)

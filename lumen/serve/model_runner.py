@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from ..models.config import ModelConfig
 from ..ops._native import native, use_native
 from ..ops.activation import swiglu
-from ..ops.attention import paged_decode, write_kv_cache
+from ..ops.attention import flash_attention_qkv, paged_decode, write_kv_cache
 from ..ops.norm import rms_norm
 from ..ops.rope import rope_inplace, rope_tables
 
@@ -162,6 +162,9 @@ class ModelRunner:
         qs, ks = self.q_size, self.kv_size
 
         def attn(qkv, i):
+            if qkv.is_cuda and D == 128:
+                # packed varlen causal flash attention straight from the QKV buffer (HIP)
+                return flash_attention_qkv(qkv, cu, nh, nkv, D, True)
             outs = []
             for s in range(len(cu) - 1):
                 a, b = cu[s], cu[s + 1]
