@@ -20,7 +20,28 @@ namespace lumen {
 
 constexpr int kMaxGroup = 8;
 
-template <typename T, int D>
+template <int W>
+__device__ __forceinline__ float wave_sum_width(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Row reduction over the 16 lanes of a DPP row (quad_perm xor1/xor2, half-mirror, mirror).
+template <int CTRL>
+__device__ __forceinline__ float pa_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+__device__ __forceinline__ float pa_red16(float v) {
+  v += pa_dpp<0xB1>(v);
+  v += pa_dpp<0x4E>(v);
+  v += pa_dpp<0x141>(v);
+  v += pa_dpp<0x140>(v);
+  return v;
+}
+
+template <typename T, int D, int G>
 __global__ void __launch_bounds__(256) pa_decode_kernel(
     T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
     const T* __restrict__ vc, const int* __restrict__ block_tables,
@@ -28,130 +49,129 @@ __global__ void __launch_bounds__(256) pa_decode_kernel(
     float scale, float* __restrict__ tmp_m, float* __restrict__ tmp_l, float* __restrict__ tmp_o,
     int PART) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int LPT = D / 8;        // lanes per cache row
-  constexpr int RPS = 256 / LPT;    // rows per step
+  constexpr int LPT = D / 8;        // lanes per cache row (16-byte chunk each)
+  constexpr int RPS = 256 / LPT;    // rows per workgroup step
+  constexpr int U = 4;              // rows in flight per thread (memory-level parallelism)
   const int seq = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
   const int ctx = context_lens[seq];
   const int start = part * PART;
   if (start >= ctx) return;
   const int end = min(ctx, start + PART);
   const int n = end - start;
-  const int g = nh / nkv;
-  float* q_s = smem;                  // [g][D]
-  float* sc = q_s + kMaxGroup * D;    // [g][PART]
-  float* ml = sc + kMaxGroup * PART;  // [2][g]
-  float* red = ml + 2 * kMaxGroup;    // [4 waves][g][D]
+  float* sc = smem;                  // [G][PART] scores, then probabilities
+  float* red = sc + G * PART;        // [4 waves][G][D] PV partials
+  float* ml = red + 4 * G * D;       // [2][G] + scratch [8]
   const int tid = threadIdx.x;
-  for (int i = tid; i < g * D; i += 256) {
-    const int h = i / D, d = i % D;
-    q_s[i] = to_f32(q[(static_cast<size_t>(seq) * nh + kvh * g + h) * D + d]) * scale;
-  }
-  __syncthreads();
+  const int lane = tid & 63, wid = tid >> 6;
   const int rsub = tid / LPT, d0 = (tid % LPT) * 8;
+  // this lane's 8 q values for each head of the group (f32, pre-scaled)
+  float qv[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    load8(q + (static_cast<size_t>(seq) * nh + kvh * G + h) * D + d0, qv[h]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[h][j] *= scale;
+  }
   const int* bt = block_tables + static_cast<size_t>(seq) * max_blocks;
-  // scores
-  // groups of LPT lanes share t, so a group is entirely active or inactive and the xor-shuffle
-  // reduction below never mixes groups
-  for (int t = start + rsub; t < end; t += RPS) {
-    float part_s[kMaxGroup];
-    {
-      const int blk = bt[t / BS], slot = t % BS;
-      const T* kr = kc + ((static_cast<size_t>(blk) * nkv + kvh) * BS + slot) * D + d0;
-      float kv[8];
-      load8(kr, kv);
+  const size_t head_off = static_cast<size_t>(kvh) * BS * D;
+  const size_t blk_stride = static_cast<size_t>(nkv) * BS * D;
+  // ---- scores: U independent 16-byte K loads in flight per thread ----
+  for (int t0 = start + rsub; t0 < end; t0 += RPS * U) {
+    float kv[U][8];
 #pragma unroll
-      for (int h = 0; h < kMaxGroup; ++h) {
-        float s = 0.f;
-        if (h < g) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) s += kv[j] * q_s[h * D + d0 + j];
-        }
-        part_s[h] = s;
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * RPS;
+      if (t < end) {
+        const T* kr = kc + bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
+        load8(kr, kv[u]);
       }
     }
 #pragma unroll
-    for (int h = 0; h < kMaxGroup; ++h) {
-      float s = part_s[h];
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * RPS;
 #pragma unroll
-      for (int o = LPT / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-      part_s[h] = s;
-    }
-    if ((tid % LPT) == 0) {
+      for (int h = 0; h < G; ++h) {
+        float s = 0.f;
 #pragma unroll
-      for (int h = 0; h < kMaxGroup; ++h)
-        if (h < g) sc[h * PART + (t - start)] = part_s[h];
+        for (int j = 0; j < 8; ++j) s += kv[u][j] * qv[h][j];
+        s = LPT == 16 ? pa_red16(s) : wave_sum_width<LPT>(s);
+        if (t < end && (tid % LPT) == 0) sc[h * PART + (t - start)] = s;
+      }
     }
   }
   __syncthreads();
-  // softmax per head: one wave per head
-  const int lane = tid & 63, wid = tid >> 6;
-  for (int h = wid; h < g; h += 4) {
+  // ---- softmax over the partition (every wave covers a slice of the scores) ----
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
     float m = -INFINITY;
-    for (int i = lane; i < n; i += 64) m = fmaxf(m, sc[h * PART + i]);
-    m = wave_max(m);
+    for (int i = tid; i < n; i += 256) m = fmaxf(m, sc[h * PART + i]);
+    m = block_max<256>(m, ml + 2 * G);
     float l = 0.f;
-    for (int i = lane; i < n; i += 64) {
+    for (int i = tid; i < n; i += 256) {
       const float p = __expf(sc[h * PART + i] - m);
       sc[h * PART + i] = p;
       l += p;
     }
-    l = wave_sum(l);
-    if (lane == 0) { ml[h] = m; ml[kMaxGroup + h] = l; }
+    l = block_sum<256>(l, ml + 2 * G);
+    if (tid == 0) { ml[h] = m; ml[G + h] = l; }
   }
   __syncthreads();
-  // P.V
-  float acc[kMaxGroup][8];
+  // ---- P.V: U independent V loads in flight ----
+  float acc[G][8];
 #pragma unroll
-  for (int h = 0; h < kMaxGroup; ++h)
+  for (int h = 0; h < G; ++h)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
-  for (int t = start + rsub; t < end; t += RPS) {
-    const int blk = bt[t / BS], slot = t % BS;
-    const T* vr = vc + ((static_cast<size_t>(blk) * nkv + kvh) * BS + slot) * D + d0;
-    float vv[8];
-    load8(vr, vv);
+  for (int t0 = start + rsub; t0 < end; t0 += RPS * U) {
+    float vv[U][8];
 #pragma unroll
-    for (int h = 0; h < kMaxGroup; ++h) {
-      if (h < g) {
-        const float p = sc[h * PART + (t - start)];
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * RPS;
+      if (t < end) {
+        const T* vr = vc + bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
+        load8(vr, vv[u]);
+      }
+    }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[h][j] += p * vv[j];
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * RPS;
+      if (t < end) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          const float p = sc[h * PART + (t - start)];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[h][j] += p * vv[u][j];
+        }
       }
     }
   }
-  // reduce the 64/LPT row groups of each wave with shuffles, then the 4 waves through LDS
+  // reduce the 64/LPT row groups of each wave, then the 4 waves through LDS
 #pragma unroll
-  for (int h = 0; h < kMaxGroup; ++h) {
+  for (int h = 0; h < G; ++h)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float a = acc[h][j];
+      float x = acc[h][j];
 #pragma unroll
-      for (int o = LPT; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
-      acc[h][j] = a;
+      for (int o = LPT; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+      acc[h][j] = x;
     }
-  }
   if (lane < LPT) {
 #pragma unroll
-    for (int h = 0; h < kMaxGroup; ++h) {
-      if (h < g) {
+    for (int h = 0; h < G; ++h)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) red[(wid * g + h) * D + d0 + j] = acc[h][j];
-      }
-    }
+      for (int j = 0; j < 8; ++j) red[(wid * G + h) * D + d0 + j] = acc[h][j];
   }
   __syncthreads();
-  for (int i = tid; i < g * D; i += 256) {
-    float o = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) o += red[r * g * D + i];
+  for (int i = tid; i < G * D; i += 256) {
+    const float o = red[i] + red[G * D + i] + red[2 * G * D + i] + red[3 * G * D + i];
     const int h = i / D, d = i % D;
-    const int head = kvh * g + h;
+    const int head = kvh * G + h;
     if (max_parts == 1) {
-      out[(static_cast<size_t>(seq) * nh + head) * D + d] = from_f32<T>(o / ml[kMaxGroup + h]);
+      out[(static_cast<size_t>(seq) * nh + head) * D + d] = from_f32<T>(o / ml[G + h]);
     } else {
       const size_t mi = (static_cast<size_t>(seq) * nh + head) * max_parts + part;
       tmp_o[mi * D + d] = o;
-      if (d == 0) { tmp_m[mi] = ml[h]; tmp_l[mi] = ml[kMaxGroup + h]; }
+      if (d == 0) { tmp_m[mi] = ml[h]; tmp_l[mi] = ml[G + h]; }
     }
   }
 }
@@ -200,24 +220,36 @@ __global__ void __launch_bounds__(256) cache_write_kernel(
       *reinterpret_cast<const uint4*>(v + t * v_stride + static_cast<long long>(h) * D + c * 8);
 }
 
+template <typename T, int D>
+static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out, const void* q,
+                        const void* kc, const void* vc, const int* bt, const int* cl, int nh,
+                        int nkv, int BS, int max_blocks, int max_parts, float scale, float* tm,
+                        float* tl, void* to, int PART) {
+#define LUMEN_PA_G(GG)                                                                         \
+  hipLaunchKernelGGL((pa_decode_kernel<T, D, GG>), grid, dim3(256), smem, st, (T*)out,         \
+                     (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks,  \
+                     max_parts, scale, tm, tl, (float*)to, PART)
+  if (G == 1) LUMEN_PA_G(1);
+  else if (G == 2) LUMEN_PA_G(2);
+  else if (G == 4) LUMEN_PA_G(4);
+  else LUMEN_PA_G(8);
+#undef LUMEN_PA_G
+}
+
 template <typename T>
 static hipError_t launch_pa(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, const int* cl, int nseq, int nh, int nkv, int D, int BS,
                             int max_blocks, int max_parts, float scale, float* tm, float* tl,
                             void* to, int PART, hipStream_t st) {
-  dim3 grid(nseq, nkv, max_parts), block(256);
-  const size_t smem = (kMaxGroup * D + kMaxGroup * PART + 2 * kMaxGroup +
-                       static_cast<size_t>(4) * (nh / nkv) * D) * sizeof(float);
-#define LUMEN_PA(DD)                                                                           \
-  hipLaunchKernelGGL((pa_decode_kernel<T, DD>), grid, block, smem, st, (T*)out, (const T*)q,     \
-                     (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, \
-                     tm, tl, (float*)to, PART)
-  if (D == 128) LUMEN_PA(128);
-  else if (D == 64) LUMEN_PA(64);
-  else if (D == 256) LUMEN_PA(256);
-  else if (D == 32) LUMEN_PA(32);
+  const int G = nh / nkv;
+  if (G != 1 && G != 2 && G != 4 && G != 8) return hipErrorInvalidValue;
+  dim3 grid(nseq, nkv, max_parts);
+  const size_t smem = (static_cast<size_t>(G) * PART + 4 * G * D + 2 * G + 8) * sizeof(float);
+  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
+  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
+  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
+  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
   else return hipErrorInvalidValue;
-#undef LUMEN_PA
   if (max_parts > 1) {
     dim3 g2(nseq, nh), b2(128);
     hipLaunchKernelGGL(pa_reduce_kernel<T>, g2, b2, 0, st, (T*)out, cl, tm, tl,
