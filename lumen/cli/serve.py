@@ -16,11 +16,11 @@ def build_parser():
     ap = argparse.ArgumentParser(description="lumen OpenAI-compatible server (MI355X)")
     ap.add_argument("--model", default="meta-llama/Llama-2-7b-hf",
                     help="preset / hub id (random init offline) or local HF checkpoint dir")
-    ap.add_argument("--adapter", default=None, help="PEFT LoRA adapter dir to merge")
+    ap.add_argument("--adapter", "--lora", default=None, help="PEFT LoRA adapter dir to merge")
     ap.add_argument("--served-model-name", default=None)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
-    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (= world size)")
+    ap.add_argument("--tp", "--tensor-parallel-size", "--tensor_parallel_size", type=int, default=1, help="tensor-parallel degree (= world size)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-num-seqs", type=int, default=256)

@@ -48,11 +48,19 @@ def env_ints():
 
 
 def init(backend: Optional[str] = None, device: Optional[str] = None,
-         timeout_s: int = 1800) -> DistEnv:
-    """Initialise (idempotent).  backend None -> 'nccl' (RCCL) when GPUs are visible, else gloo."""
+         timeout_s: Optional[int] = None) -> DistEnv:
+    """Initialise (idempotent).  backend None -> 'nccl' (RCCL) when GPUs are visible, else gloo.
+
+    A hung collective fails after ``LUMEN_DIST_TIMEOUT`` seconds (default 1800) with async error
+    handling on, so a dead peer ends the job instead of stalling it."""
     global _ENV
     if _ENV is not None:
         return _ENV
+    from ..utils.debug import apply_debug_env
+
+    apply_debug_env()  # before the first HIP call
+    if timeout_s is None:
+        timeout_s = int(os.environ.get("LUMEN_DIST_TIMEOUT", "1800"))
     rank, world, local, local_world = env_ints()
     want_gpu = device != "cpu" and (device == "cuda" or torch.cuda.is_available())
     if want_gpu:

@@ -21,6 +21,7 @@ from ..data import CausalLMCollator, ShardedSampler, build_dataset, load_tokeniz
 from ..lora import LoraConfig, apply_lora, print_trainable_parameters, save_adapter
 from ..models import build_model, get_config
 from ..parallel.dist import DistEnv, all_reduce_scalar, barrier
+from ..utils.debug import StepProfiler, check_finite, maybe_inject_fault
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 from .config import DSConfig
 from .engine import ZeroEngine
@@ -132,6 +133,7 @@ class Trainer:
         self.print(f"[lumen] ZeRO-{ds.stage} world={env.world_size} micro={ds.micro_batch} "
                    f"accum={ds.grad_accum} effective batch={ds.train_batch_size} "
                    f"steps={total_steps}")
+        prof = StepProfiler(env.rank, self.print)
         t_start = time.time()
         tokens = 0
         samples = 0
@@ -149,6 +151,7 @@ class Trainer:
                 produced += 1
                 b = self._to_device(self.collator(raw))
                 loss = eng.forward(b)
+                check_finite("loss", loss, eng.global_step, env.rank)
                 eng.backward(loss)
                 loss_acc += loss.detach().float()
                 loss_n += 1
@@ -156,6 +159,9 @@ class Trainer:
                 samples += len(raw)
                 samples_in_epoch += len(raw)
                 if eng.step():
+                    prof.step()
+                    if ds.dtype != "fp16":  # fp16 overflow is handled by the loss scaler
+                        check_finite("grad_norm", eng.last_grad_norm, eng.global_step, env.rank)
                     if eng.global_step % a.logging_steps == 0 or eng.global_step == total_steps:
                         l = all_reduce_scalar(float(loss_acc.item()) / max(loss_n, 1)) / env.world_size
                         gn = float(eng.last_grad_norm.item()) if eng.last_grad_norm is not None else 0.0
@@ -166,12 +172,17 @@ class Trainer:
                         rec["tokens_per_second"] = round(tokens * env.world_size / max(el, 1e-9), 1)
                         self.log_history.append(rec)
                         self.print(json.dumps(rec))
+                        if ds.wall_clock_breakdown:
+                            br = eng.timers.pop()
+                            self.print("[lumen] time (ms) | " + " | ".join(
+                                f"{k}: {v * 1e3:.2f}" for k, v in sorted(br.items())))
                         last_loss = l
                         loss_acc.zero_()
                         loss_n = 0
                     if (a.save_strategy == "steps" and a.save_steps > 0
                             and eng.global_step % a.save_steps == 0):
                         self._save(epoch, samples_in_epoch)
+                    maybe_inject_fault(eng.global_step, env.rank)
                     if eng.global_step >= total_steps:
                         done = True
                         break
@@ -181,6 +192,7 @@ class Trainer:
             if not done and a.save_strategy == "epoch":
                 self._save(epoch + 1, 0)
             epoch += 1
+        prof.close()
         if env.device.type == "cuda":
             torch.cuda.synchronize()
         elapsed = time.time() - t_start

@@ -99,3 +99,50 @@ def test_cli_baseline_single_process(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     rows = list(csv.DictReader(open(tmp_path / "m.csv")))
     assert rows[-1]["experiment"] == "baseline" and rows[-1]["strategy"] == "pytorch_lora"
+
+
+def _zero2_cmd(out, csvp, steps, resume=False):
+    cmd = [sys.executable, "-m", "lumen.launch", "--nproc_per_node", "2", "--master_port",
+           str(_port()), "--grace", "5", os.path.join(ROOT, "training", "train_deepspeed_zero2.py"),
+           "--model_name", "tiny-llama", "--synthetic", "--synthetic_samples", "64",
+           "--max_length", "16", "--max_steps", str(steps), "--logging_steps", "1",
+           "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "2",
+           "--lora_r", "4", "--save_steps", "2", "--device", "cpu", "--output_dir", out,
+           "--metrics_csv", csvp, "--seed", "5",
+           "--deepspeed_config", os.path.join(ROOT, "configs", "ds_config_zero2.json")]
+    if resume:
+        cmd.append("--resume_from_checkpoint")
+    return cmd
+
+
+def test_fault_injection_kill_and_resume_matches(tmp_path):
+    """Rank 1 dies after step 3 (LUMEN_FAULT_STEP), the launcher tears rank 0 down, and a resumed
+    run from checkpoint-2 ends with the same adapter as an uninterrupted run."""
+    from safetensors.torch import load_file
+
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    csvp = str(tmp_path / "m.csv")
+    full = str(tmp_path / "full")
+    r = subprocess.run(_zero2_cmd(full, csvp, 6), capture_output=True, text=True, timeout=600,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+    part = str(tmp_path / "part")
+    fenv = dict(env, LUMEN_FAULT_STEP="3", LUMEN_FAULT_RANK="1")
+    r = subprocess.run(_zero2_cmd(part, csvp, 6), capture_output=True, text=True, timeout=600,
+                       env=fenv, cwd=ROOT)
+    assert r.returncode == 17, (r.returncode, r.stderr[-3000:])
+    assert "rank 1 exited with code 17" in r.stderr
+    assert latest_checkpoint(part).endswith("checkpoint-2")
+    assert not os.path.exists(os.path.join(part, "final"))
+
+    r = subprocess.run(_zero2_cmd(part, csvp, 6, resume=True), capture_output=True, text=True,
+                       timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "resumed from" in r.stdout
+    a = load_file(os.path.join(full, "final", "adapter_model.safetensors"))
+    b = load_file(os.path.join(part, "final", "adapter_model.safetensors"))
+    assert a.keys() == b.keys()
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=0, atol=1e-6)

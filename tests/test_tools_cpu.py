@@ -1,0 +1,213 @@
+"""CPU tests for the tooling around the engine: dataset prep, scaling comparison, the launcher,
+the Locust profile and LoRA merge/export."""
+import csv
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def test_format_and_prepare_dataset(tmp_path):
+    from lumen.data.prepare import dataset_dir_name, format_conversation_for_llama2
+
+    assert format_conversation_for_llama2({"question": " q? ", "answer": "a."}) == \
+        {"text": "<s>[INST] q? [/INST] a.</s>"}
+    assert dataset_dir_name(None) == "glaive_code_full"
+    assert dataset_dir_name(5000) == "glaive_code_5k"
+
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/prepare_dataset.py"),
+                          "--num_samples", "2000", "--output_dir", str(tmp_path)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    path = tmp_path / "glaive_code_2k"
+    from datasets import load_from_disk
+
+    ds = load_from_disk(str(path))
+    assert len(ds) == 2000 and ds.column_names == ["text"]
+    assert ds[0]["text"].startswith("<s>[INST] ") and ds[0]["text"].endswith("</s>")
+    # the training data path reads it back and tokenizes with truncation
+    from lumen.data.datasets import build_dataset
+    from lumen.data.tokenizer import ByteTokenizer
+
+    tok = ByteTokenizer()
+    d = build_dataset(str(path), tok, 64, False, 0, tok.vocab_size)
+    assert len(d) == 2000 and max(len(d[i]["input_ids"]) for i in range(20)) <= 64
+
+
+def test_prepare_from_local_jsonl(tmp_path):
+    import json
+
+    from lumen.data.prepare import prepare_dataset
+
+    src = tmp_path / "src.jsonl"
+    with open(src, "w") as f:
+        for i in range(10):
+            f.write(json.dumps({"question": f"q{i}", "answer": f"a{i}"}) + "\n")
+    out = prepare_dataset(str(tmp_path / "data"), None, str(src))
+    from datasets import load_from_disk
+
+    ds = load_from_disk(out)
+    assert ds[3]["text"] == "<s>[INST] q3 [/INST] a3</s>"
+
+
+def test_compare_training(tmp_path):
+    from lumen.utils.compare import compare
+    from lumen.utils.metrics import save_training_metrics
+
+    p = str(tmp_path / "m.csv")
+    rows = [("baseline", 1, 0, 2.0, 100.0), ("zero2_1gpu", 1, 2, 1.8, 110.0),
+            ("zero2_2gpu", 2, 2, 1.0, 200.0), ("zero2_4gpu", 4, 2, 0.6, 330.0)]
+    for name, n, st, hours, tok in rows:
+        save_training_metrics({"experiment": name, "num_gpus": n, "zero_stage": st,
+                               "strategy": "baseline" if st == 0 else f"ZeRO-{st}",
+                               "training_time_hours": hours, "samples_per_second": 1.0,
+                               "peak_memory_gb": 10.0 / n, "final_loss": 1.0,
+                               "tokens_per_second": tok}, p)
+    res = compare(p, str(tmp_path / "plots" / "cmp.png"))
+    df = res["table"].set_index("experiment")
+    assert df.loc["zero2_2gpu", "speedup"] == pytest.approx(2.0)
+    assert df.loc["zero2_4gpu", "efficiency"] == pytest.approx(2.0 / 0.6 / 4 * 100)
+    assert df.loc["zero2_4gpu", "token_speedup"] == pytest.approx(3.3)
+    assert res["plot"] is None or os.path.isfile(res["plot"])
+    # CLI without a CSV is a no-op message, not a crash
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/compare_training.py"),
+                          "--csv", str(tmp_path / "missing.csv")], capture_output=True, text=True)
+    assert out.returncode == 0 and "No metrics" in out.stdout
+
+
+def _write(path, body):
+    path.write_text(textwrap.dedent(body))
+    return str(path)
+
+
+def test_launch_env_and_local_rank(tmp_path):
+    script = _write(tmp_path / "w.py", """
+        import os, sys, json
+        out = sys.argv[1]
+        with open(os.path.join(out, "r%s.json" % os.environ["RANK"]), "w") as f:
+            json.dump({k: os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                       "MASTER_ADDR", "MASTER_PORT")} | {"argv": sys.argv[2:]}, f)
+        """)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0,1,2")
+    out = subprocess.run([sys.executable, "-m", "lumen.launch", "--nproc_per_node", "2",
+                          "--master_port", "29555", script, str(tmp_path)], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    import json
+
+    r1 = json.load(open(tmp_path / "r1.json"))
+    assert r1["LOCAL_RANK"] == "1" and r1["WORLD_SIZE"] == "2"
+    assert r1["MASTER_ADDR"] == "127.0.0.1" and r1["MASTER_PORT"] == "29555"
+    assert r1["argv"] == ["--local_rank=1"]
+
+
+def test_launch_refuses_to_widen_visible_devices(tmp_path):
+    script = _write(tmp_path / "w.py", "print('should not run')\n")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0")
+    out = subprocess.run([sys.executable, "-m", "lumen.launch", "--num_gpus", "2", script],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=60)
+    assert out.returncode != 0 and "refusing to widen" in out.stderr
+    assert "should not run" not in out.stdout
+
+
+def test_launch_fail_fast(tmp_path):
+    script = _write(tmp_path / "w.py", """
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(300)
+        """)
+    import time
+
+    t0 = time.time()
+    out = subprocess.run([sys.executable, "-m", "lumen.launch", "--nproc_per_node", "2",
+                          "--no_local_rank_arg", "--grace", "2", script], cwd=ROOT,
+                         env=dict(os.environ, HIP_VISIBLE_DEVICES="0,1"), capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 3
+    assert time.time() - t0 < 60
+    assert "rank 1 exited with code 3" in out.stderr
+
+
+def test_launch_slurm_env():
+    from lumen.launch import build_rank_envs, parse_args
+
+    a = parse_args(["--nproc_per_node", "2", "x.py"])
+    envs = build_rank_envs(a, {"SLURM_NNODES": "2", "SLURM_NODEID": "1",
+                               "SLURM_JOB_NODELIST": "gpu[07-08]", "ROCR_VISIBLE_DEVICES": "0,1"})
+    assert [e["RANK"] for e in envs] == ["2", "3"]
+    assert envs[0]["WORLD_SIZE"] == "4" and envs[0]["MASTER_ADDR"].startswith("gpu")
+
+
+def test_locust_payload():
+    import random
+
+    from lumen.bench.locustfile import make_payload, parse_sse_line
+
+    b = make_payload(random.Random(0), chat=False, prompt_tokens=8, max_tokens=4)
+    assert b["stream"] and b["max_tokens"] == 4 and len(b["prompt"].split()) == 8
+    c = make_payload(random.Random(0), chat=True, prompt_tokens=8, max_tokens=4)
+    assert c["messages"][0]["role"] == "user"
+    assert parse_sse_line(b'data: {"a": 1}') == {"a": 1}
+    assert parse_sse_line(b"data: [DONE]") is None and parse_sse_line(b"") is None
+
+
+def test_merge_lora_export(tmp_path):
+    from lumen.lora import LoraConfig, apply_lora, save_adapter
+    from lumen.models import build_model
+
+    torch.manual_seed(0)
+    m = build_model("tiny-llama", dtype=torch.float32, device=torch.device("cpu"))
+    apply_lora(m, LoraConfig(r=4, lora_dropout=0.0))
+    for n, p in m.named_parameters():
+        if p.requires_grad:
+            p.data.normal_(0, 0.05)
+    m.eval()
+    ids = torch.randint(3, m.config.vocab_size, (2, 12))
+    with torch.no_grad():
+        ref = m(ids)["logits"] if isinstance(m(ids), dict) else m(ids)
+    save_adapter(m, str(tmp_path / "adapter"), "tiny-llama")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/merge_lora.py"), "--model",
+                          "tiny-llama", "--adapter", str(tmp_path / "adapter"), "--output_dir",
+                          str(tmp_path / "merged"), "--dtype", "fp32"], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    merged = build_model(str(tmp_path / "merged"), dtype=torch.float32,
+                         device=torch.device("cpu"))
+    merged.eval()
+    with torch.no_grad():
+        got = merged(ids)
+        got = got["logits"] if isinstance(got, dict) else got
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_profiler_and_debug_guards(tmp_path, monkeypatch):
+    from lumen.parallel.dist import init
+    from lumen.train.config import load_ds_config
+    from lumen.train.trainer import TrainArgs, Trainer
+    from lumen.utils.debug import NonFiniteError, check_finite
+
+    monkeypatch.setenv("LUMEN_PROFILE", "1")
+    monkeypatch.setenv("LUMEN_PROFILE_WAIT", "1")
+    monkeypatch.setenv("LUMEN_PROFILE_ACTIVE", "2")
+    monkeypatch.setenv("LUMEN_PROFILE_DIR", str(tmp_path / "prof"))
+    monkeypatch.setenv("LUMEN_DEBUG", "1")
+    env = init(device="cpu")
+    ds = load_ds_config({"zero_optimization": {"stage": 1}, "wall_clock_breakdown": True}, 2, 1,
+                        1, 1e-3, dtype_override="fp32")
+    a = TrainArgs(model_name="tiny-llama", synthetic=True, synthetic_samples=16, max_length=16,
+                  per_device_train_batch_size=2, max_steps=5, logging_steps=1, lora_r=4,
+                  save_strategy="no", output_dir=str(tmp_path / "o"), save_final=False)
+    lines = []
+    t = Trainer(a, ds, env, printer=lambda *x, **k: lines.append(" ".join(map(str, x))))
+    t.train()
+    assert os.path.isfile(tmp_path / "prof" / "trace_rank0.json")
+    assert any(l.startswith("[lumen] time (ms)") and "fwd" in l for l in lines)
+    with pytest.raises(NonFiniteError):
+        check_finite("x", torch.tensor([1.0, float("nan")]))
