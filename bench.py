@@ -43,6 +43,11 @@ def main():
     ap.add_argument("--lora_r", type=int, default=16)
     ap.add_argument("--gradient_checkpointing", action="store_true")
     ap.add_argument("--profile_dir", default=None, help="write a torch.profiler trace here")
+    ap.add_argument("--gemm_table", default=None,
+                    help="TunableOp table to load ('off' = library heuristics); default "
+                         "configs/tunableop/mi355x_gemms.csv when present")
+    ap.add_argument("--tune_gemms", default=None, metavar="OUT_CSV",
+                    help="tune the GEMM shapes during warmup and write the table at exit")
     args = ap.parse_args()
 
     import torch
@@ -69,6 +74,13 @@ def main():
 
     env = init()
     world = env.world_size
+    from lumen.utils.gemm_tuning import load_tuned_gemms, start_gemm_tuning, tuned_entries
+
+    if args.tune_gemms:
+        start_gemm_tuning(args.tune_gemms)
+        gemm_table = "tuning"
+    else:
+        gemm_table = "tuned" if load_tuned_gemms(args.gemm_table) else "heuristic"
     if world != args.gpus and env.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     ds = load_ds_config(args.config, args.micro_batch, args.grad_accum, world, 2e-4)
@@ -112,6 +124,10 @@ def main():
 
     loss = run_steps(args.warmup, 0)
     sync()
+    if args.tune_gemms:  # timed steps use the tuned solutions, no tuning inside the timing
+        import torch.cuda.tunable as tn
+
+        tn.tuning_enable(False)
     prof = None
     if args.profile_dir and env.is_main:
         from torch.profiler import ProfilerActivity, profile
@@ -171,6 +187,8 @@ def main():
                 "setup_s": round(setup_s, 1),
                 "zero3_keep_gathered": bool(engine.coordinator.keep) if engine.coordinator else None,
                 "baseline_tok_s": BASELINE_TOK_S,
+                "gemm_algos": gemm_table,
+                "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,
             },
         }
         print(json.dumps(out), flush=True)

@@ -72,9 +72,32 @@ class Linear(nn.Module):
         self.seg_names = list(seg_names) if seg_names else ["proj"]
         self.lora: Optional[LoRAAdapter] = None
         self.lora_enabled = True
+        self.transpose_bwd = False      # keep W^T for a K-contiguous (TN) input-gradient GEMM
+        self._wt: Optional[torch.Tensor] = None
+        self._wt_key = None
 
     def weight_fn(self) -> torch.Tensor:
         return self.weight
+
+    def weight_t_fn(self) -> Optional[torch.Tensor]:
+        """Cached contiguous W^T [in, out] for the backward dX = dY @ W, or None.
+
+        hipBLASLt runs dY[T,N] @ W[N,K] (reduction over W's row index) markedly slower than the
+        TN form dY @ (W^T)^T with both operands K-contiguous (lumen/bench/gemm_bench.py), so
+        frozen persistent weights keep a transposed copy (288 GB HBM affords it).  ZeRO-3
+        gathered weights are excluded: a per-step transpose would cost about what it saves."""
+        W = self.weight
+        if not self.transpose_bwd or W.requires_grad or getattr(W, "_lumen_gathered", False):
+            return None
+        key = (W.data_ptr(), tuple(W.shape), W.dtype)
+        if self._wt is None or self._wt_key != key:
+            with torch.no_grad():
+                self._wt = W.detach().t().contiguous()
+            self._wt_key = key
+        return self._wt
+
+    def invalidate_weight_cache(self):
+        self._wt, self._wt_key = None, None
 
     def seg_offset(self, name: str) -> Tuple[int, int]:
         i = self.seg_names.index(name)
@@ -96,8 +119,11 @@ class Linear(nn.Module):
             # before recomputing, so the recomputed forward regenerates the same dropout mask
             seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
             return lora_linear(x, self.weight_fn, self.bias, lo.lora_A, lo.lora_B, lo.segs, lo.r,
-                               lo.scale, p, seed, self.weight)
-        return linear(x, self.weight_fn, self.bias, self.weight)
+                               lo.scale, p, seed, self.weight, self._wt_fn())
+        return linear(x, self.weight_fn, self.bias, self.weight, self._wt_fn())
+
+    def _wt_fn(self):
+        return self.weight_t_fn if (self.transpose_bwd and torch.is_grad_enabled()) else None
 
     @torch.no_grad()
     def merge_lora(self):
@@ -111,6 +137,37 @@ class Linear(nn.Module):
             B = lo.lora_B[b_off:b_off + n_len].float()
             W[n_off:n_off + n_len] = (W[n_off:n_off + n_len].float() + lo.scale * (B @ A)).to(W.dtype)
         self.lora = None
+        self.invalidate_weight_cache()
+
+
+def configure_backward_layout(model: nn.Module, policy=None) -> int:
+    """Enable the transposed-weight (TN) input-gradient GEMM on the linears whose first segment
+    name is in ``policy`` (env ``LUMEN_BWD_WT``: comma list, ``all`` or ``none``; default
+    ``all``: in-situ on MI355X the TN form won for every Llama-2-7B projection -- step time
+    104.6 ms vs 110.0 ms with none, profiles/r01_tuned).  Returns the count enabled."""
+    import os
+
+    if policy is None:
+        policy = os.environ.get("LUMEN_BWD_WT", "all")
+    if isinstance(policy, str):
+        policy = policy.strip()
+        names = None if policy == "all" else set() if policy in ("", "none") else set(policy.split(","))
+    else:
+        names = set(policy)
+    n = 0
+    for name, m in model.named_modules():
+        if isinstance(m, Linear):
+            on = not name.endswith("lm_head") and (names is None or m.seg_names[0] in names)
+            m.transpose_bwd = on
+            m.invalidate_weight_cache()
+            n += int(on)
+    return n
+
+
+def invalidate_weight_caches(model: nn.Module) -> None:
+    for m in model.modules():
+        if isinstance(m, Linear):
+            m.invalidate_weight_cache()
 
 
 class RMSNorm(nn.Module):

@@ -87,6 +87,9 @@ def load_hf_weights(model: nn.Module, path: str, strict: bool = True) -> None:
         if tuple(t.shape) != tuple(dst.shape):
             raise ValueError(f"{ours}: checkpoint {tuple(t.shape)} != model {tuple(dst.shape)}")
         dst.copy_(t.to(dst.dtype))
+    from .layers import invalidate_weight_caches
+
+    invalidate_weight_caches(model)
 
 
 @torch.no_grad()

@@ -144,13 +144,14 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
 
 class _LoraLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param):
+    def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param, wt_fn):
         W = weight_fn()
         y = torch.matmul(x2d, W.t())
         if bias is not None:
             y.add_(bias)
         Z = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed)
         ctx.weight_fn = weight_fn
+        ctx.wt_fn = wt_fn
         ctx.meta = (segs, r, scale, p, seed)
         ctx.w_grad = w_param is not None and w_param.requires_grad
         ctx.b_grad = bias is not None and bias.requires_grad
@@ -162,25 +163,25 @@ class _LoraLinear(torch.autograd.Function):
         x2d, A, B, Z = ctx.saved_tensors
         segs, r, scale, p, seed = ctx.meta
         dy = dy.contiguous()
-        W = ctx.weight_fn()
-        dx = torch.matmul(dy, W) if ctx.needs_input_grad[0] else None
+        dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
         dA, dB = lora_bwd_native(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed,
                                  ctx.needs_input_grad[3], ctx.needs_input_grad[4])
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
-        return dx, None, db, dA, dB, None, None, None, None, None, dw
+        return dx, None, db, dA, dB, None, None, None, None, None, dw, None
 
 
 class _Linear(torch.autograd.Function):
     """Plain (frozen or trainable) linear whose weight is re-fetched at backward."""
 
     @staticmethod
-    def forward(ctx, x2d, weight_fn, bias, w_param):
+    def forward(ctx, x2d, weight_fn, bias, w_param, wt_fn):
         W = weight_fn()
         y = torch.matmul(x2d, W.t())
         if bias is not None:
             y.add_(bias)
         ctx.weight_fn = weight_fn
+        ctx.wt_fn = wt_fn
         ctx.w_grad = w_param is not None and w_param.requires_grad
         ctx.b_grad = bias is not None and bias.requires_grad
         ctx.save_for_backward(x2d if ctx.w_grad else torch.empty(0))
@@ -189,20 +190,27 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (x2d,) = ctx.saved_tensors
-        W = ctx.weight_fn()
         dy = dy.contiguous()
-        dx = torch.matmul(dy, W) if ctx.needs_input_grad[0] else None
+        dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
-        return dx, None, db, dw
+        return dx, None, db, dw, None
+
+
+def _input_grad(ctx, dy):
+    """dX = dY @ W, as the TN GEMM dY @ (W^T)^T when the layer keeps a transposed copy."""
+    Wt = ctx.wt_fn() if ctx.wt_fn is not None else None
+    if Wt is not None:
+        return torch.matmul(dy, Wt.t())
+    return torch.matmul(dy, ctx.weight_fn())
 
 
 def linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor] = None,
-           w_param: Optional[torch.Tensor] = None) -> torch.Tensor:
+           w_param: Optional[torch.Tensor] = None, wt_fn=None) -> torch.Tensor:
     shp = x.shape
     x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
     if use_native(x2d):
-        y = _Linear.apply(x2d.contiguous(), weight_fn, bias, w_param)
+        y = _Linear.apply(x2d.contiguous(), weight_fn, bias, w_param, wt_fn)
     else:
         y = F.linear(x2d, _frozen(weight_fn()), bias)
     # 2-D in -> return the Function output itself (not a view): a view would make a later
@@ -218,12 +226,12 @@ def _frozen(W: torch.Tensor) -> torch.Tensor:
 
 def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: torch.Tensor,
                 B: torch.Tensor, segs: List[Seg], r: int, scale: float, p: float, seed: int,
-                w_param: Optional[torch.Tensor] = None) -> torch.Tensor:
+                w_param: Optional[torch.Tensor] = None, wt_fn=None) -> torch.Tensor:
     shp = x.shape
     x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
     if use_native(x2d):
         y = _LoraLinear.apply(x2d.contiguous(), weight_fn, bias, A, B, segs, r, scale, p, seed,
-                              w_param)
+                              w_param, wt_fn)
     else:
         y = lora_linear_ref(x2d, _frozen(weight_fn()), bias, A, B, segs, r, scale, p, seed)
     return y if x.dim() == 2 else y.view(*shp[:-1], y.shape[-1])

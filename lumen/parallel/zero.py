@@ -239,6 +239,7 @@ class ParamCoordinator:
             del flat
             for p in u.params:
                 p.data = torch.empty(0, dtype=u.dtype, device=p.device)
+                p._lumen_gathered = True  # storage swapped per gather: no derived caches
         self.total_numel = total
         self.keep = total <= max_live   # whole model fits the live budget: gather once per micro-step
         # prefetch depth: upcoming units whose gathered size fits the prefetch bucket (>= 1)

@@ -79,6 +79,10 @@ class ZeroEngine:
                 cfg.stage3_max_live_parameters, cfg.stage3_prefetch_bucket_size,
                 offload_param=cfg.offload_param == "cpu", pin_memory=cfg.offload_param_pin)
             model.coordinator = self.coordinator
+        if self.device.type == "cuda":
+            from ..models.layers import configure_backward_layout
+
+            configure_backward_layout(model)  # TN input-gradient GEMMs for persistent weights
         bucket = cfg.reduce_bucket_size if self.stage >= 1 else int(2.5e7)
         self.flat = FlatTrainable(trainable, env, max(bucket, 1), self.device)
         # broadcast adapter init from rank 0 (only the trainable 32 MiB, not 13.5 GB)

@@ -315,3 +315,30 @@ def test_llama_layer_flash_vs_sdpa_path():
     assert abs(res[True][0] - res[False][0]) < 1e-2
     for a, b in zip(res[True][1], res[False][1]):
         assert rel(a, b) < 5e-2
+
+
+@pytest.mark.gpu
+def test_transposed_weight_backward_matches():
+    """TN input-gradient path (cached W^T) gives the same dX / adapter grads as the NN path."""
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+    from lumen.models.layers import configure_backward_layout
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    m = build_model("tiny-llama", dtype=torch.bfloat16, device=dev)
+    apply_lora(m, LoraConfig(r=8, lora_dropout=0.0))
+    m.train()
+    ids = torch.randint(3, m.config.vocab_size, (2, 64), device=dev)
+    labels = torch.roll(ids, -1, 1)
+    grads = []
+    for pol in ("none", "all"):
+        assert configure_backward_layout(m, pol) == (0 if pol == "none" else 8)
+        for p in m.parameters():
+            p.grad = None
+        loss = m(ids, labels=labels)
+        loss.backward()
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 0
+    for k in grads[0]:
+        torch.testing.assert_close(grads[1][k], grads[0][k], rtol=2e-2, atol=2e-3)
