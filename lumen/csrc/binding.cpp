@@ -32,6 +32,10 @@ hipError_t lumen_lora_gemm(int, int, int, const void*, const void*, void*, long 
                            long long, long long, float, int, unsigned long long, unsigned int, float,
                            long long, int, const long long*, const long long*, const long long*,
                            const int*, const int*, const int*, hipStream_t);
+hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long long, void*,
+                       long long, long long, float, int, int, int, unsigned long long, unsigned int,
+                       float, long long, long long, int, const long long*, const long long*,
+                       const long long*, const int*, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
                                         float, float*, float*, void*, int, hipStream_t);
@@ -189,6 +193,38 @@ void lora_gemm(int64_t act_dtype, int64_t mode, int64_t bn, const at::Tensor& X,
         "lora_gemm");
 }
 
+// segs: (big_off, small_off, out_off, ncols) per segment
+void lora2(int64_t dtype, int64_t kind, int64_t flag, const at::Tensor& big, int64_t ldb,
+           const at::Tensor& small, int64_t lds, at::Tensor& out, int64_t cs0, int64_t cs1,
+           double alpha, int64_t T, int64_t J, int64_t split, int64_t seed, int64_t drop_thresh,
+           double drop_scale, int64_t drop_ld, int64_t drop_col0,
+           const std::vector<std::vector<int64_t>>& segs) {
+  if (!big.is_cuda() || !small.is_cuda() || !out.is_cuda())
+    throw std::invalid_argument("lumen: lora2 needs GPU tensors");
+  if (small.scalar_type() != at::kFloat)
+    throw std::invalid_argument("lumen: lora2 small operand must be f32");
+  if (kind == 2 ? (big.scalar_type() != at::kFloat || out.scalar_type() == at::kFloat)
+                : out.scalar_type() != at::kFloat)
+    throw std::invalid_argument("lumen: lora2 UP takes f32 adapter weights and a 16-bit output; "
+                                "DOWN/WGRAD write f32");
+  const int nseg = static_cast<int>(segs.size());
+  if (nseg < 1 || nseg > 4) throw std::invalid_argument("lumen: lora2 needs 1..4 segments");
+  long long bo[4] = {0}, so[4] = {0}, oo[4] = {0};
+  int nc[4] = {0};
+  for (int i = 0; i < nseg; ++i) {
+    if (segs[i].size() != 4) throw std::invalid_argument("lumen: lora2 segment = (big_off, small_off, out_off, ncols)");
+    bo[i] = segs[i][0]; so[i] = segs[i][1]; oo[i] = segs[i][2];
+    nc[i] = static_cast<int>(segs[i][3]);
+  }
+  check(lumen_lora2(static_cast<int>(dtype), static_cast<int>(kind), static_cast<int>(flag),
+                    big.data_ptr(), ldb, small.data_ptr<float>(), lds, out.data_ptr(), cs0,
+                    cs1, static_cast<float>(alpha), static_cast<int>(T), static_cast<int>(J),
+                    static_cast<int>(split), static_cast<unsigned long long>(seed),
+                    static_cast<unsigned int>(drop_thresh), static_cast<float>(drop_scale),
+                    drop_ld, drop_col0, nseg, bo, so, oo, nc, cur_stream()),
+        "lora2");
+}
+
 void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
                             const at::Tensor& v_cache, const at::Tensor& block_tables,
                             const at::Tensor& context_lens, int64_t num_kv_heads, int64_t block_size,
@@ -280,6 +316,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm_sq", &grad_norm_sq);
   m.def("adamw", &adamw);
   m.def("lora_gemm", &lora_gemm);
+  m.def("lora2", &lora2);
   m.def("paged_attention_decode", &paged_attention_decode);
   m.def("reshape_and_cache", &reshape_and_cache);
   m.def("sample", &sample);

@@ -338,23 +338,31 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(Args a) {
 // =============================================================================================
 // backward: delta = rowsum(dO * O)
 // =============================================================================================
+// One wave per token row: lane l reads the 16-byte chunks l*8 + 512*i (coalesced 1 KiB per
+// instruction); with D = 128 the 16 lanes of a row-group share one head per i, so a 16-lane
+// butterfly finishes each head's sum.
 template <typename T>
 __global__ void __launch_bounds__(256) delta_kernel(Args a) {
-  const long long tid = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (tid >= (long long)a.T * a.nh) return;
-  const int t = (int)(tid / a.nh), h = (int)(tid % a.nh);
-  const T* dO = reinterpret_cast<const T*>(a.dout) + (long long)t * a.lddo + h * D;
-  const T* O = reinterpret_cast<const T*>(a.o) + (long long)t * a.ldo + h * D;
-  float s = 0.f;
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= a.T) return;
+  const int H = a.nh * D;
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (long long)t * a.lddo;
+  const T* O = reinterpret_cast<const T*>(a.o) + (long long)t * a.ldo;
+  for (int base = 0; base < H; base += 512) {
+    const int e = base + lane * 8;
+    float s = 0.f;
+    if (e < H) {
+      float x[8], y[8];
+      load8(dO + e, x);
+      load8(O + e, y);
 #pragma unroll
-  for (int c = 0; c < D; c += 8) {
-    float x[8], y[8];
-    load8(dO + c, x);
-    load8(O + c, y);
+      for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 16);
+    if ((lane & 15) == 0 && e < H) const_cast<float*>(a.delta)[(long long)(e / D) * a.T + t] = s;
   }
-  const_cast<float*>(a.delta)[(long long)h * a.T + t] = s;
 }
 
 // =============================================================================================
@@ -615,7 +623,7 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
       else hipLaunchKernelGGL((fwd_kernel<T, false, 1>), grid, block, 0, st, a);
     }
   } else if (which == 1) {
-    dim3 grid((unsigned)(((long long)a.T * a.nh + 255) / 256));
+    dim3 grid((unsigned)((a.T + 3) / 4));
     hipLaunchKernelGGL(delta_kernel<T>, grid, block, 0, st, a);
   } else if (which == 2) {
     dim3 grid(ntiles, a.nkv);

@@ -91,6 +91,32 @@ def _lora_gemm(act, mode, X, W, Cm, ldx, ldw, cs_m, cs_n, alpha, segs6, ksplit, 
                        [list(map(int, s)) for s in segs6])
 
 
+import os as _os
+
+USE_V2 = _os.environ.get("LUMEN_LORA_V2", "1") != "0"
+
+
+def _v2_ok(r: int, R: int, *mats) -> bool:
+    """The 16-bit-MFMA kernels (kernels/lora_v2.hip) take ranks that are multiples of 16 up to
+    64 stacked rows and 8-element aligned rows; anything else uses the f32-MFMA kernel."""
+    return (USE_V2 and r % 16 == 0 and R % 16 == 0 and R <= 64
+            and all(m.stride(0) % 8 == 0 and m.stride(1) == 1 for m in mats))
+
+
+def _split(blocks_per_split: int, reduce_len: int, chunk: int, target: int = 512) -> int:
+    s = max(1, math.ceil(target / max(blocks_per_split, 1)))
+    return int(max(1, min(s, reduce_len // chunk)))
+
+
+def _lora2(kind, flag, big, small, out, cs0, cs1, alpha, T, J, split, segs4, seed=0, p=0.0,
+           drop_ld=0):
+    dt = DTYPE_CODE[out.dtype if kind == 2 else big.dtype]
+    native().lora2(dt, kind, flag, big, big.stride(0), small, small.stride(0), out, cs0, cs1, float(alpha), T, J, int(split),
+                   int(seed) & 0x7FFFFFFFFFFFFFFF, drop_threshold(p),
+                   1.0 / (1.0 - p) if p > 0 else 1.0, drop_ld, 0,
+                   [list(map(int, s)) for s in segs4])
+
+
 def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed):
     """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place)."""
     T, K = x2d.shape
@@ -98,9 +124,18 @@ def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed):
     Ntot = y.shape[1]
     act = DTYPE_CODE[x2d.dtype]
     Z = torch.zeros(T, R, device=x2d.device, dtype=torch.float32)
-    bn = _bn(R)
-    _lora_gemm(act, 1, x2d, A, Z, K, K, R, 1, 1.0, [(0, 0, 0, T, R, K)],
-               _ksplit(T, R, K, bn), seed, p, K)
+    if _v2_ok(r, R, x2d):
+        _lora2(0, 1, x2d, A, Z, R, 1, 1.0, T, R, _split(math.ceil(T / 64), K, 256),
+               [(0, 0, 0, K)], seed, p, K)
+    else:
+        _lora_gemm(act, 1, x2d, A, Z, K, K, R, 1, 1.0, [(0, 0, 0, T, R, K)],
+                   _ksplit(T, R, K, _bn(R)), seed, p, K)
+    if _v2_ok(r, R, x2d, y) and all(s[0] % 8 == 0 and s[1] % 8 == 0 for s in segs):
+        for i in range(0, len(segs), 4):
+            ch = segs[i:i + 4]
+            _lora2(2, 1, B, Z, y, y.stride(0), 1, scale, T, r, 1,
+                   [(b_off * r, r_off, n_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+        return Z
     segs6 = [(r_off, b_off * r, n_off, T, n_len, r) for (n_off, n_len, r_off, b_off) in segs]
     for i in range(0, len(segs6), 4):
         _lora_gemm(act, 6, Z, B, y, R, r, Ntot, 1, scale, segs6[i:i + 4], 1)
@@ -115,26 +150,52 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
     Ntot = dy.shape[1]
     act = DTYPE_CODE[dy.dtype]
     dev = dy.device
-    dZ = torch.zeros(T, R, device=dev, dtype=torch.float32)
-    s2 = [(n_off, b_off * r, r_off, T, r, n_len) for (n_off, n_len, r_off, b_off) in segs]
-    for i in range(0, len(s2), 4):
-        chunk = s2[i:i + 4]
-        _lora_gemm(act, 2, dy, B, dZ, Ntot, r, R, 1, scale, chunk,
-                   _ksplit(T, r, max(s[5] for s in chunk), 16, len(chunk)))
+    # one zero-filled workspace for dZ, dA and dB (the kernels accumulate with atomics)
+    nA = R * K if need_dA else 0
+    nB = B.shape[0] * r if need_dB else 0
+    ws = torch.zeros(T * R + nA + nB, device=dev, dtype=torch.float32)
+    dZ = ws[:T * R].view(T, R)
+    v2 = _v2_ok(r, R, x2d, dy)
+    if v2:
+        for i in range(0, len(segs), 4):
+            ch = segs[i:i + 4]
+            _lora2(0, 0, dy, B, dZ, R, 1, scale, T, r,
+                   _split(math.ceil(T / 64) * len(ch), max(s[1] for s in ch), 256),
+                   [(n_off, b_off * r, r_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+    else:
+        s2 = [(n_off, b_off * r, r_off, T, r, n_len) for (n_off, n_len, r_off, b_off) in segs]
+        for i in range(0, len(s2), 4):
+            chunk = s2[i:i + 4]
+            _lora_gemm(act, 2, dy, B, dZ, Ntot, r, R, 1, scale, chunk,
+                       _ksplit(T, r, max(s[5] for s in chunk), 16, len(chunk)))
     dA = dB = None
     if need_dA:
-        dA = torch.zeros(R, K, device=dev, dtype=torch.float32)
-        _lora_gemm(act, 3, dZ, x2d, dA, R, K, K, 1, 1.0, [(0, 0, 0, R, K, T)],
-                   _ksplit(R, K, T, 64), seed, p, K)
+        dA = ws[T * R:T * R + nA].view(R, K)
+        if v2:
+            _lora2(1, 1, x2d, dZ, dA, 1, K, 1.0, T, R, _split(math.ceil(K / 128), T, 128),
+                   [(0, 0, 0, K)], seed, p, K)
+        else:
+            _lora_gemm(act, 3, dZ, x2d, dA, R, K, K, 1, 1.0, [(0, 0, 0, R, K, T)],
+                       _ksplit(R, K, T, 64), seed, p, K)
     if need_dB:
-        dB = torch.zeros(B.shape[0], r, device=dev, dtype=torch.float32)
-        s4 = [(n_off, r_off, b_off * r, n_len, r, T) for (n_off, n_len, r_off, b_off) in segs]
-        for i in range(0, len(s4), 4):
-            chunk = s4[i:i + 4]
-            _lora_gemm(act, 4, dy, Z, dB, Ntot, R, r, 1, scale, chunk,
-                       _ksplit(max(s[3] for s in chunk), r, T, 16, len(chunk)))
+        dB = ws[T * R + nA:].view(B.shape[0], r)
+        if v2:
+            for i in range(0, len(segs), 4):
+                ch = segs[i:i + 4]
+                _lora2(1, 0, dy, Z, dB, r, 1, scale, T, r,
+                       _split(sum(math.ceil(s[1] / 128) for s in ch), T, 128),
+                       [(n_off, r_off, b_off * r, n_len) for (n_off, n_len, r_off, b_off) in ch])
+        else:
+            s4 = [(n_off, r_off, b_off * r, n_len, r, T) for (n_off, n_len, r_off, b_off) in segs]
+            for i in range(0, len(s4), 4):
+                chunk = s4[i:i + 4]
+                _lora_gemm(act, 4, dy, Z, dB, Ntot, R, r, 1, scale, chunk,
+                           _ksplit(max(s[3] for s in chunk), r, T, 16, len(chunk)))
     if dx is not None:
-        _lora_gemm(act, 5, dZ, A, dx, R, K, K, 1, 1.0, [(0, 0, 0, T, K, R)], 1, seed, p, K)
+        if v2 and _v2_ok(r, R, dx):
+            _lora2(2, 0, A, dZ, dx, dx.stride(0), 1, 1.0, T, R, 1, [(0, 0, 0, K)], seed, p, K)
+        else:
+            _lora_gemm(act, 5, dZ, A, dx, R, K, K, 1, 1.0, [(0, 0, 0, T, K, R)], 1, seed, p, K)
     return dA, dB
 
 

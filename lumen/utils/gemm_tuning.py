@@ -40,9 +40,18 @@ def load_tuned_gemms(path: Optional[str] = None) -> bool:
     return ok
 
 
-def start_gemm_tuning(out_path: str, max_ms: int = 60) -> None:
-    """Tune every GEMM shape met from now on; results are written to ``out_path`` at exit."""
+def start_gemm_tuning(out_path: str, max_ms: int = 60, rotating_mb: Optional[int] = None) -> None:
+    """Tune every GEMM shape met from now on; results are written to ``out_path`` at exit.
+
+    Candidates are timed over a rotating set of operand buffers larger than the 256 MB
+    Infinity Cache (``rotating_mb``, env ``LUMEN_TUNE_ROTATING_MB``, default 1024), i.e. with
+    weights streaming from HBM as they do inside a training step, not from a warm cache."""
     import torch.cuda.tunable as tn
+
+    if rotating_mb is None:
+        rotating_mb = int(os.environ.get("LUMEN_TUNE_ROTATING_MB", "1024"))
+    if rotating_mb > 0:
+        tn.set_rotating_buffer_size(rotating_mb)
 
     os.makedirs(os.path.dirname(os.path.abspath(out_path)), exist_ok=True)
     tn.enable(True)

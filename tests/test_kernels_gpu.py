@@ -158,8 +158,13 @@ def test_grad_norm_and_adamw():
 
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
-def test_lora_linear_fwd_bwd(segs_kind, p_drop):
+@pytest.mark.parametrize("impl", ["v2", "f32"])
+def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch):
+    """impl v2: 16-bit MFMA kernels (lora_v2.hip); f32: exact-f32 MFMA kernel (lora.hip)."""
+    import lumen.ops.lora as lora_mod
     from lumen.ops.lora import lora_linear, lora_linear_ref
+
+    monkeypatch.setattr(lora_mod, "USE_V2", impl == "v2")
 
     T, K, r = 512 + 64, 1024, 16
     if segs_kind == "qkv":
