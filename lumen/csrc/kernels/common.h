@@ -116,9 +116,24 @@ __device__ __forceinline__ uint32_t rng_u32(uint32_t seed32, uint64_t idx) {
   return h;
 }
 
-// keep-probability test: returns true when the element survives dropout with prob (1-p).
-__device__ __forceinline__ bool dropout_keep(uint32_t seed32, uint64_t idx, uint32_t thresh) {
-  return rng_u32(seed32, idx) >= thresh;
+// keep-probability test with a 16-bit threshold (p * 65536): one 32-bit hash of the pair index
+// idx >> 1 serves two consecutive elements (low half for the even one, high half for the odd),
+// halving the hashing work of the mask-regenerating kernels.
+__device__ __forceinline__ bool dropout_keep(uint32_t seed32, uint64_t idx, uint32_t thresh16) {
+  const uint32_t h = rng_u32(seed32, idx >> 1);
+  return ((h >> ((idx & 1) * 16)) & 0xFFFFu) >= thresh16;
+}
+
+// masks of 8 consecutive elements starting at an even index: bit e set = element e kept
+__device__ __forceinline__ uint32_t dropout_keep8(uint32_t seed32, uint64_t idx0, uint32_t thresh16) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t h = rng_u32(seed32, (idx0 >> 1) + e);
+    m |= ((h & 0xFFFFu) >= thresh16 ? 1u : 0u) << (2 * e);
+    m |= ((h >> 16) >= thresh16 ? 1u : 0u) << (2 * e + 1);
+  }
+  return m;
 }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }

@@ -89,8 +89,9 @@ __device__ __forceinline__ void store_big(char* img, uint4 (&v)[4], int r0, int 
       unpack8<T>(u, f);
       const unsigned long long i0 =
           static_cast<unsigned long long>(r0 + row) * d.ld + dcol0 + c0 + ch * 8;
+      const uint32_t keep = dropout_keep8(d.seed, i0, d.thresh);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = dropout_keep(d.seed, i0 + e, d.thresh) ? f[e] * d.scale : 0.f;
+      for (int e = 0; e < 8; ++e) f[e] = (keep >> e) & 1u ? f[e] * d.scale : 0.f;
       u = pack8<T>(f);
     }
     *reinterpret_cast<uint4*>(img + img_off(row, ch)) = u;
@@ -397,12 +398,14 @@ __global__ void __launch_bounds__(256) up_kernel(Args a) {
         T* po = out + (long long)t * a.cs0 + c;
         float y[8];
         load8(po, y);
+        const uint32_t keep = DROP ? dropout_keep8(a.drop.seed,
+                                                   (unsigned long long)t * a.drop.ld + a.drop_col0 + c,
+                                                   a.drop.thresh)
+                                   : 0xFFu;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float add = a.alpha * sc[rr * kUC + cc + e];
-          if (DROP)
-            add = dropout_keep(a.drop.seed, (unsigned long long)t * a.drop.ld + a.drop_col0 + c + e,
-                               a.drop.thresh) ? add * a.drop.scale : 0.f;
+          if (DROP) add = (keep >> e) & 1u ? add * a.drop.scale : 0.f;
           y[e] += add;
         }
         store8(po, y);

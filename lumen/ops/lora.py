@@ -50,13 +50,16 @@ def rng_u32_ref(seed: int, idx: torch.Tensor) -> torch.Tensor:
 
 
 def drop_threshold(p: float) -> int:
-    return min(int(p * 4294967296.0), 0xFFFFFFFF) if p > 0 else 0
+    """16-bit drop threshold: element dropped when its 16-bit hash slice < p * 65536."""
+    return min(int(round(p * 65536.0)), 0xFFFF) if p > 0 else 0
 
 
 def dropout_mask_ref(seed: int, T: int, K: int, p: float, device=None) -> torch.Tensor:
-    """Keep-mask [T, K] (bool) identical to the kernel's."""
+    """Keep-mask [T, K] (bool) identical to the kernels': one 32-bit hash per element pair
+    (index >> 1), low 16 bits for the even element, high 16 bits for the odd one."""
     idx = torch.arange(T * K, dtype=torch.int64, device=device).view(T, K)
-    return rng_u32_ref(seed, idx) >= drop_threshold(p)
+    h = rng_u32_ref(seed, idx >> 1)
+    return ((h >> ((idx & 1) * 16)) & 0xFFFF) >= drop_threshold(p)
 
 
 def _apply_dropout_ref(x, p, seed):
