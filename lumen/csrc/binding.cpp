@@ -36,6 +36,7 @@ hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long
                        long long, long long, float, int, int, int, unsigned long long, unsigned int,
                        float, long long, long long, int, const long long*, const long long*,
                        const long long*, const int*, hipStream_t);
+hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
                                         float, float*, float*, void*, int, hipStream_t);
@@ -225,6 +226,16 @@ void lora2(int64_t dtype, int64_t kind, int64_t flag, const at::Tensor& big, int
         "lora2");
 }
 
+void transpose2d(const at::Tensor& in, at::Tensor& out) {
+  if (!in.is_cuda() || !out.is_cuda() || in.dim() != 2 || out.dim() != 2)
+    throw std::invalid_argument("lumen: transpose2d needs 2-D GPU tensors");
+  if (in.stride(1) != 1 || out.stride(1) != 1 || out.size(0) != in.size(1) || out.size(1) != in.size(0))
+    throw std::invalid_argument("lumen: transpose2d shape/stride mismatch");
+  check(lumen_transpose(dcode(in), in.data_ptr(), out.data_ptr(), static_cast<int>(in.size(0)),
+                        static_cast<int>(in.size(1)), in.stride(0), out.stride(0), cur_stream()),
+        "transpose2d");
+}
+
 void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
                             const at::Tensor& v_cache, const at::Tensor& block_tables,
                             const at::Tensor& context_lens, int64_t num_kv_heads, int64_t block_size,
@@ -317,6 +328,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("adamw", &adamw);
   m.def("lora_gemm", &lora_gemm);
   m.def("lora2", &lora2);
+  m.def("transpose2d", &transpose2d);
   m.def("paged_attention_decode", &paged_attention_decode);
   m.def("reshape_and_cache", &reshape_and_cache);
   m.def("sample", &sample);

@@ -336,6 +336,173 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(Args a) {
 }
 
 // =============================================================================================
+// forward, transposed formulation
+// =============================================================================================
+// S^T = K Q^T puts one query per lane column: lane (L, g) holds 16 scores of query L (keys
+// nt*16 + 4g + r), so the row max / sum are 15 in-register ops plus two cross-lane steps, the
+// online-softmax rescale is a per-lane scalar, and P never leaves registers: it is directly the
+// B operand of O^T += V^T P^T once V's transposed LDS reads use the same key order
+// (k-slot 8g + e <-> key 32ks + 4g + e for e < 4, 32ks + 16 + 4g + (e - 4) otherwise).
+// Removes the P round trip through LDS and ~3/4 of the softmax VALU work of fwd_kernel.
+
+// V^T operand rows for the permuted key order: lane (L, g) gets column n0 + L of rows
+// rlo + 0..3 (lo) and rhi + 0..3 (hi)
+__device__ __forceinline__ uint4 tr_read_img2(const char* img, int rlo, int rhi, int n0, int lane) {
+  const int L = lane & 15;
+  const int col = n0 + 4 * (L & 3);
+  const int ch = col >> 3, half = (col >> 2) & 1;
+  const uint2 lo = tr_read_raw(img + img_off(rlo + (L >> 2), ch) + 8 * half);
+  const uint2 hi = tr_read_raw(img + img_off(rhi + (L >> 2), ch) + 8 * half);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 pack_p(const f32x4& a, const f32x4& b) {
+  struct alignas(16) P8 { T v[8]; } o;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { o.v[r] = from_f32<T>(a[r]); o.v[4 + r] = from_f32<T>(b[r]); }
+  return __builtin_bit_cast(uint4, o);
+}
+
+template <typename T, bool CAUSAL, int QG>
+__global__ void __launch_bounds__(256, 2) fwd_t_kernel(Args a) {
+  constexpr int BM = 64 * QG;        // query rows per workgroup (16 * QG per wave)
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [K0 | V0 | K1 | V1]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
+  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const int wq0 = q0 + wid * 16 * QG;  // first query row of this wave
+
+  uint4 qf[QG][4];
+  int qrow[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    qrow[qg] = wq0 + qg * 16 + lr;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      qf[qg][ks] = gload16(Q + (long long)qrow[qg] * a.ldq + (4 * ks + lg) * 8, qrow[qg] < L);
+  }
+  f32x4 acc[QG][8];
+  float m_i[QG], l_i[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[qg][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_i[qg] = -INFINITY;
+    l_i[qg] = 0.f;
+  }
+  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
+  if (kv_end > 0) {
+    stage64_async(smem, K, a.ldk, 0, L);
+    stage64_async(smem + IMG, V, a.ldv, 0, L);
+  }
+  int it = 0;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
+    char* kimg = smem + (it & 1) * 2 * IMG;
+    char* vimg = kimg + IMG;
+    if (kv0 + BN < kv_end) {
+      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
+      stage64_async(nk, K, a.ldk, kv0 + BN, L);
+      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
+      wait_vm_8();
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+    // S^T = K Q^T: per query group 4 key tiles of 16
+    f32x4 st[QG][4];
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) st[qg][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const uint4 kf = row_read(kimg, nt * 16 + lr, 4 * ks + lg);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) st[qg][nt] = Mfma<T>::run(kf, qf[qg][ks], st[qg][nt]);
+      }
+    }
+    const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
+    uint4 pf[QG][2];
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = st[qg][nt][r] * a.scale_log2;
+          if (need_mask) {
+            const int kpos = kv0 + nt * 16 + 4 * lg + r;
+            if (kpos >= L || (CAUSAL && kpos > qrow[qg])) x = -INFINITY;
+          }
+          st[qg][nt][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_i[qg], mx);
+      const float mref = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = exp2f(m_i[qg] - mref);
+      float rs = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(st[qg][nt][r] - mref);
+          st[qg][nt][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16);
+      rs += __shfl_xor(rs, 32);
+      l_i[qg] = l_i[qg] * alpha + rs;
+      m_i[qg] = m_new;
+      if (__any(alpha != 1.f)) {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) acc[qg][n] *= alpha;
+      }
+      pf[qg][0] = pack_p<T>(st[qg][0], st[qg][1]);
+      pf[qg][1] = pack_p<T>(st[qg][2], st[qg][3]);
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const uint4 vf = tr_read_img2(vimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) acc[qg][n] = Mfma<T>::run(vf, pf[qg][ks], acc[qg][n]);
+      }
+    }
+    lds_fence_barrier();  // every wave is done with this K/V buffer before it is refilled
+  }
+  // epilogue: lane (L, g) holds O[query L][d = 16n + 4g + r]
+  T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D;
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    if (qrow[qg] >= L) continue;
+    const float inv = l_i[qg] > 0.f ? 1.f / l_i[qg] : 0.f;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      struct alignas(8) O4 { T v[4]; } o4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o4.v[r] = from_f32<T>(acc[qg][n][r] * inv);
+      *reinterpret_cast<O4*>(O + (long long)qrow[qg] * a.ldo + n * 16 + 4 * lg) = o4;
+    }
+    if (lg == 0 && a.lse)
+      a.lse[(long long)head * a.T + s0 + qrow[qg]] =
+          l_i[qg] > 0.f ? m_i[qg] + __log2f(l_i[qg]) : INFINITY;
+  }
+}
+
+// =============================================================================================
 // backward: delta = rowsum(dO * O)
 // =============================================================================================
 // One wave per token row: lane l reads the 16-byte chunks l*8 + 512*i (coalesced 1 KiB per
@@ -615,7 +782,16 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
   dim3 block(256);
   if (which == 0) {
     dim3 grid(ntiles, a.nh);
-    if (causal) {
+    if (mt >= 10) {  // transposed-formulation kernel, QG = mt - 10 query groups per wave
+      const int qg = mt - 10;
+      if (causal) {
+        if (qg == 2) hipLaunchKernelGGL((fwd_t_kernel<T, true, 2>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((fwd_t_kernel<T, true, 1>), grid, block, 0, st, a);
+      } else {
+        if (qg == 2) hipLaunchKernelGGL((fwd_t_kernel<T, false, 2>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((fwd_t_kernel<T, false, 1>), grid, block, 0, st, a);
+      }
+    } else if (causal) {
       if (mt == 2) hipLaunchKernelGGL((fwd_kernel<T, true, 2>), grid, block, 0, st, a);
       else hipLaunchKernelGGL((fwd_kernel<T, true, 1>), grid, block, 0, st, a);
     } else {
@@ -642,7 +818,8 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 }  // namespace fa
 }  // namespace lumen
 
-// which: 0 = forward (tiles of 64*mt query rows), 1 = delta, 2 = dK/dV (64-key tiles),
+// which: 0 = forward (tiles of 64*mt query rows; mt >= 10 selects the transposed-formulation
+//        kernel with 64*(mt-10)-row tiles), 1 = delta, 2 = dK/dV (64-key tiles),
 //        3 = dQ (64-query tiles)
 extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
                                        const void* q, const void* k, const void* v,

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.lora import lora_linear, linear
+from ..ops.transpose import transpose_2d
 from ..ops.norm import rms_norm
 
 
@@ -73,6 +74,7 @@ class Linear(nn.Module):
         self.lora: Optional[LoRAAdapter] = None
         self.lora_enabled = True
         self.transpose_bwd = False      # keep W^T for a K-contiguous (TN) input-gradient GEMM
+        self.transpose_gathered = False  # ... also for ZeRO-3-gathered weights (per step)
         self._wt: Optional[torch.Tensor] = None
         self._wt_key = None
 
@@ -80,19 +82,22 @@ class Linear(nn.Module):
         return self.weight
 
     def weight_t_fn(self) -> Optional[torch.Tensor]:
-        """Cached contiguous W^T [in, out] for the backward dX = dY @ W, or None.
+        """Contiguous W^T [in, out] for the backward dX = dY @ W, or None.
 
         hipBLASLt runs dY[T,N] @ W[N,K] (reduction over W's row index) markedly slower than the
         TN form dY @ (W^T)^T with both operands K-contiguous (lumen/bench/gemm_bench.py), so
         frozen persistent weights keep a transposed copy (288 GB HBM affords it).  ZeRO-3
-        gathered weights are excluded: a per-step transpose would cost about what it saves."""
+        gathered weights change storage every step: they are transposed on the fly, and only
+        where the GEMM saving beats the transpose's HBM traffic (``transpose_gathered``)."""
         W = self.weight
-        if not self.transpose_bwd or W.requires_grad or getattr(W, "_lumen_gathered", False):
+        if not self.transpose_bwd or W.requires_grad:
             return None
+        if getattr(W, "_lumen_gathered", False):
+            return transpose_2d(W.detach()) if self.transpose_gathered else None
         key = (W.data_ptr(), tuple(W.shape), W.dtype)
         if self._wt is None or self._wt_key != key:
             with torch.no_grad():
-                self._wt = W.detach().t().contiguous()
+                self._wt = transpose_2d(W.detach())
             self._wt_key = key
         return self._wt
 
@@ -140,6 +145,9 @@ class Linear(nn.Module):
         self.invalidate_weight_cache()
 
 
+GATHERED_TN = ("q_proj", "down_proj", "fc2")
+
+
 def configure_backward_layout(model: nn.Module, policy=None) -> int:
     """Enable the transposed-weight (TN) input-gradient GEMM on the linears whose first segment
     name is in ``policy`` (env ``LUMEN_BWD_WT``: comma list, ``all`` or ``none``; default
@@ -159,6 +167,9 @@ def configure_backward_layout(model: nn.Module, policy=None) -> int:
         if isinstance(m, Linear):
             on = not name.endswith("lm_head") and (names is None or m.seg_names[0] in names)
             m.transpose_bwd = on
+            # per-step transposes of gathered weights pay off where the NN GEMM is slowest
+            # relative to the transpose's traffic (q|k|v: 299 -> 188 us, down: 277 -> 200 us)
+            m.transpose_gathered = on and m.seg_names[0] in GATHERED_TN
             m.invalidate_weight_cache()
             n += int(on)
     return n

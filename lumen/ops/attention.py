@@ -137,7 +137,12 @@ def _cu_tensor(cu: tuple, device) -> torch.Tensor:
 
 
 import os as _os
-FA_MT = int(_os.environ.get("LUMEN_FA_MT", "1"))  # query m-tiles (16 rows) per wave in the fwd
+FA_MT = int(_os.environ.get("LUMEN_FA_MT", "1"))  # query m-tiles (16 rows) per wave (old fwd)
+# forward kernel: "t1"/"t2" = transposed formulation with 1/2 query groups per wave (P stays in
+# registers), "old" = fwd_kernel with FA_MT
+_FWD = _os.environ.get("LUMEN_FA_FWD", "t1")
+FA_FWD_MT = {"t1": 11, "t2": 12}.get(_FWD, FA_MT)
+FA_FWD_ROWS = 64 * (FA_FWD_MT - 10 if FA_FWD_MT >= 10 else FA_FWD_MT)
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -152,8 +157,9 @@ class _FlashAttn(torch.autograd.Function):
         lse = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
         cut = _cu_tensor(cu, qkv.device)
         scale = 1.0 / math.sqrt(D)
-        C.flash_attn(0, causal, FA_MT, q, k, v, o, lse, cut, _tiles(cu, 64 * FA_MT, qkv.device),
-                     nh, nkv, scale, None, None, None, None, None)
+        C.flash_attn(0, causal, FA_FWD_MT, q, k, v, o, lse, cut,
+                     _tiles(cu, FA_FWD_ROWS, qkv.device), nh, nkv, scale, None, None, None, None,
+                     None)
         ctx.save_for_backward(qkv, o, lse)
         ctx.meta = (cu, nh, nkv, D, causal, scale)
         return o

@@ -266,8 +266,14 @@ def test_sampling_greedy_and_topk():
 
 @pytest.mark.parametrize("nh,nkv,lens", [(8, 8, [512, 512]), (8, 2, [512, 300, 77]),
                                          (4, 4, [1000, 64, 129])])
-def test_flash_attention_fwd_bwd(nh, nkv, lens):
+@pytest.mark.parametrize("fwd", ["t1", "t2", "old"])
+def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, monkeypatch):
+    import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
+
+    mt = {"t1": 11, "t2": 12, "old": 1}[fwd]
+    monkeypatch.setattr(att, "FA_FWD_MT", mt)
+    monkeypatch.setattr(att, "FA_FWD_ROWS", 64 * (mt - 10 if mt >= 10 else mt))
 
     D = 128
     cu = [0]
@@ -347,3 +353,11 @@ def test_transposed_weight_backward_matches():
     assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 0
     for k in grads[0]:
         torch.testing.assert_close(grads[1][k], grads[0][k], rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("shape", [(4096, 12288), (11008, 4096), (72, 200), (136, 64)])
+def test_transpose_2d(shape):
+    from lumen.ops.transpose import transpose_2d
+
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    torch.testing.assert_close(transpose_2d(x), x.t().contiguous(), rtol=0, atol=0)
