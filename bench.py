@@ -182,6 +182,7 @@ def main():
             },
             "extra": {
                 "tflops_per_gpu": round(tflops, 1),
+                "samples_per_second": round(B * ds.grad_accum * world * args.steps / dt, 2),
                 "peak_mem_gb_rank0": round(peak_gb, 2),
                 "final_loss": round(final_loss, 4),
                 "setup_s": round(setup_s, 1),

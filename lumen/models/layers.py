@@ -162,10 +162,16 @@ def configure_backward_layout(model: nn.Module, policy=None) -> int:
         names = None if policy == "all" else set() if policy in ("", "none") else set(policy.split(","))
     else:
         names = set(policy)
+    budget = _transpose_budget(model)
     n = 0
     for name, m in model.named_modules():
         if isinstance(m, Linear):
             on = not name.endswith("lm_head") and (names is None or m.seg_names[0] in names)
+            gathered = getattr(m.weight, "_lumen_gathered", False)
+            if on and not gathered:  # persistent copies must fit the HBM budget
+                need = m.weight.numel() * m.weight.element_size()
+                on = need <= budget
+                budget -= need if on else 0
             m.transpose_bwd = on
             # per-step transposes of gathered weights pay off where the NN GEMM is slowest
             # relative to the transpose's traffic (q|k|v: 299 -> 188 us, down: 277 -> 200 us)
@@ -173,6 +179,19 @@ def configure_backward_layout(model: nn.Module, policy=None) -> int:
             m.invalidate_weight_cache()
             n += int(on)
     return n
+
+
+def _transpose_budget(model: nn.Module) -> float:
+    """Bytes of HBM the persistent W^T copies may take: free memory minus a reserve for
+    activations (max(48 GiB, 25% of the device)); unlimited off-GPU."""
+    import os
+
+    dev = next((p.device for p in model.parameters() if p.device.type == "cuda"), None)
+    if dev is None:
+        return float("inf")
+    free, total = torch.cuda.mem_get_info(dev)
+    reserve = float(os.environ.get("LUMEN_BWD_WT_RESERVE_GB", "0")) * 2**30 or max(48 * 2**30, 0.25 * total)
+    return max(0.0, free - reserve)
 
 
 def invalidate_weight_caches(model: nn.Module) -> None:
