@@ -74,7 +74,12 @@ class ServeWeights:
                                           qkv, o, gu, dn))
         self.embed = model.embed_tokens.weight
         self.norm = model.norm.weight
-        self.lm_head = model.lm_head.weight
+        # vocab-parallel LM head: each rank scores V/TP rows, logits all-gathered
+        V = cfg.vocab_size
+        self.vocab_shard = V // tp_size if V % tp_size == 0 else V
+        lm = model.lm_head.weight
+        self.lm_head = (lm[r * self.vocab_shard:(r + 1) * self.vocab_shard].contiguous()
+                        if self.vocab_shard != V else lm)
         self.dtype = self.embed.dtype
 
 
@@ -149,9 +154,23 @@ class ModelRunner:
             h = self._allreduce(torch.matmul(swiglu(torch.matmul(y2, L.gate_up.t())), L.down.t()))
         return h, res
 
+    def _vocab_gather(self, logits):
+        """[R, V/TP] local logits -> [R, V] on every rank (vocab-parallel LM head)."""
+        if self.tp == 1 or self.w.vocab_shard == self.cfg.vocab_size:
+            return logits
+        R, Vs = logits.shape
+        if logits.is_cuda:
+            buf = torch.empty(self.tp, R, Vs, dtype=logits.dtype, device=logits.device)
+            dist.all_gather_into_tensor(buf, logits.contiguous(), group=self.tp_group)
+            parts = buf.unbind(0)
+        else:
+            parts = [torch.empty_like(logits) for _ in range(self.tp)]
+            dist.all_gather(parts, logits.contiguous(), group=self.tp_group)
+        return torch.cat(parts, 1)
+
     def _logits(self, h, res, rows):
         y, _ = rms_norm(h[rows], self.w.norm, self.cfg.rms_norm_eps, res[rows])
-        return torch.matmul(y, self.w.lm_head.t())
+        return self._vocab_gather(torch.matmul(y, self.w.lm_head.t()))
 
     # ---- prefill: whole prompts, packed ----------------------------------------------------
     @torch.no_grad()
@@ -202,9 +221,8 @@ class ModelRunner:
                                 max_context, self.scale, self.partition).view(N, nh * D)
 
         h, res = self._layers(h, positions, slots, attn)
-        rows = torch.arange(N, device=h.device)
         y, _ = rms_norm(h, self.w.norm, self.cfg.rms_norm_eps, res)
-        return torch.matmul(y, self.w.lm_head.t())
+        return self._vocab_gather(torch.matmul(y, self.w.lm_head.t()))
 
     @torch.no_grad()
     def decode(self, inp: StepInput) -> torch.Tensor:

@@ -38,3 +38,46 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
         torch.save({"sd": sd, "losses": [r["loss"] for r in t.log_history], "res": res},
                    os.path.join(outdir, f"result_stage{stage}_w{world}.pt"))
     shutdown()
+
+
+def serve_tp_worker(rank, world, port, outdir):
+    """TP serving on gloo: rank 0 runs the engine, rank 1 the worker loop; greedy outputs of
+    rank 0 are saved for comparison with a single-process engine."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import torch
+
+    torch.set_num_threads(1)
+    from lumen.parallel.dist import init, shutdown
+    from lumen.serve.engine import EngineConfig, LLMEngine
+    from lumen.serve.sequence import SamplingParams
+    from lumen.serve.tp import worker_loop
+
+    init(device="cpu")
+    model = _tp_test_model()
+    cfg = EngineConfig(model="tiny-llama-gqa", device="cpu", max_model_len=128, block_size=4,
+                       use_graphs=False, num_blocks=128, tp_size=world)
+    eng = LLMEngine(cfg, model=model)
+    if rank == 0:
+        prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
+        seqs = eng.generate(prompts, SamplingParams(max_tokens=8, temperature=0.0,
+                                                    ignore_eos=True))
+        eng.shutdown()
+        torch.save([s.output_ids for s in seqs], os.path.join(outdir, "tp_out.pt"))
+    else:
+        worker_loop(eng.runner)
+    shutdown()
+
+
+def _tp_test_model():
+    import torch
+
+    from lumen.models import build_model
+
+    m = build_model("tiny-llama-gqa", dtype=torch.float32, device="cpu", init="random", seed=1)
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.dim() == 2:
+                p.mul_(5.0)
+    m.eval()
+    return m

@@ -126,3 +126,25 @@ def test_openai_api_surface(model):
     finally:
         ae.shutdown()
     assert llama2_chat_prompt([{"role": "user", "content": "q"}]) == "[INST] q [/INST]"
+
+
+def test_tensor_parallel_serving_gloo(tmp_path):
+    """TP=2 over gloo (head/FFN-sharded layers, row-parallel all-reduce, vocab-parallel LM head,
+    step broadcast to the worker) reproduces single-process greedy decoding."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from tests._dist_worker import _tp_test_model, serve_tp_worker
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(serve_tp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    got = torch.load(tmp_path / "tp_out.pt", weights_only=True)
+    ref_model = _tp_test_model()
+    prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
+    for p, out in zip(prompts, got):
+        assert out == naive_greedy(ref_model, p, 8), p
