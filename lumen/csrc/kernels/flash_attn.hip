@@ -537,14 +537,14 @@ __global__ void __launch_bounds__(256) delta_kernel(Args a) {
 // =============================================================================================
 template <typename T, bool CAUSAL>
 __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
-  constexpr int YC = 16;  // Y scratch: [64 queries][16 keys] per wave (P^T, then dS^T)
-  constexpr int YB = 64 * (YC + 4) * 2;
   constexpr int STAGE = 2 * IMG + 512;  // Q image | dO image | lse[64] | delta[64]
-  // two stages filled by LDS-DMA one (head, q-tile) step ahead, then the per-wave Y scratch
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 4 * YB];
+  // two stages filled by LDS-DMA one (head, q-tile) step ahead.  S = Q K^T and dP = dO V^T are
+  // computed with the queries as MFMA rows, so the accumulator lane (key L, queries 4g + r of each
+  // 16-query tile) already holds P^T / dS^T rows in the permuted-k order of the fwd_t kernel:
+  // they feed dV += P^T dO and dK += dS^T Q straight from registers (no LDS round trip).
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  char* y = smem + 2 * STAGE + wid * YB;
   const int seq = a.tiles[2 * blockIdx.x], k0 = a.tiles[2 * blockIdx.x + 1];
   const int kvh = blockIdx.y;
   const int grp = a.nh / a.nkv;
@@ -552,13 +552,13 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
   const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
   const int wk0 = k0 + wid * 16;  // this wave's 16 keys
+  const int krow = wk0 + lr;      // the key of this lane's accumulator column
   uint4 kf[4], vf[4];
   {
-    const int row = wk0 + lr;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      kf[ks] = gload16(K + (long long)row * a.ldk + (4 * ks + lg) * 8, row < L);
-      vf[ks] = gload16(V + (long long)row * a.ldv + (4 * ks + lg) * 8, row < L);
+      kf[ks] = gload16(K + (long long)krow * a.ldk + (4 * ks + lg) * 8, krow < L);
+      vf[ks] = gload16(V + (long long)krow * a.ldv + (4 * ks + lg) * 8, krow < L);
     }
   }
   wait_vm_all();
@@ -604,59 +604,44 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
       wait_vm_all();
     }
     lds_fence_barrier();
-    // S^T = K Q^T and dP^T = V dO^T   [16 keys x 64 queries]
-    f32x4 st_[4], dpt[4];
+    // S = Q K^T and dP = dO V^T: [64 queries x 16 keys] per wave as 4 query tiles
+    f32x4 sc[4], dp[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) { st_[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dpt[nt] = st_[nt]; }
+    for (int nt = 0; nt < 4; ++nt) { sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[nt] = sc[nt]; }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        st_[nt] = Mfma<T>::run(kf[ks], row_read(qimg, nt * 16 + lr, 4 * ks + lg), st_[nt]);
-        dpt[nt] = Mfma<T>::run(vf[ks], row_read(oimg, nt * 16 + lr, 4 * ks + lg), dpt[nt]);
+        sc[nt] = Mfma<T>::run(row_read(qimg, nt * 16 + lr, 4 * ks + lg), kf[ks], sc[nt]);
+        dp[nt] = Mfma<T>::run(row_read(oimg, nt * 16 + lr, 4 * ks + lg), vf[ks], dp[nt]);
       }
     }
-    // P^T (to Y) ; lane: query col = q0 + 16nt + lr, key rows = wk0 + 4lg + r
-    float ds[4][4];
+    // lane: key krow, queries q0 + 16nt + 4lg + r
     const bool need_mask = (q0 + 64 > L) || (CAUSAL && wk0 + 15 > q0);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int qc = nt * 16 + lr;
-      const float lq = s_lse[qc], dq = s_del[qc];
-      float p[4];
+      const float4 l4 = *reinterpret_cast<const float4*>(s_lse + nt * 16 + 4 * lg);
+      const float4 d4 = *reinterpret_cast<const float4*>(s_del + nt * 16 + 4 * lg);
+      const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float pv = exp2f(st_[nt][r] * a.scale_log2 - lq);
-        if (need_mask) {
-          const int krow = wk0 + 4 * lg + r;
-          if (krow >= L || q0 + qc >= L || (CAUSAL && krow > q0 + qc)) pv = 0.f;
-        }
-        p[r] = pv;
-        ds[nt][r] = pv * (dpt[nt][r] - dq);
+        const int qc = nt * 16 + 4 * lg + r;
+        float pv = exp2f(sc[nt][r] * a.scale_log2 - lq[r]);
+        if (need_mask && (krow >= L || q0 + qc >= L || (CAUSAL && krow > q0 + qc))) pv = 0.f;
+        sc[nt][r] = pv;
+        dp[nt][r] = pv * (dp[nt][r] - dq4[r]);
       }
-      y_store<T>(y, YC, nt * 16, 0, lane, p[0], p[1], p[2], p[3]);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // dV += P^T dO
+    // dV += P^T dO ; dK += dS^T Q   (k = queries in the permuted order)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const uint4 pa = tr_read_y(y, YC, 32 * ks, 0, lane);
+      const uint4 pa = pack_p<T>(sc[2 * ks], sc[2 * ks + 1]);
+      const uint4 da = pack_p<T>(dp[2 * ks], dp[2 * ks + 1]);
 #pragma unroll
-      for (int n = 0; n < 8; ++n)
-        dv[n] = Mfma<T>::run(pa, tr_read_img(oimg, 32 * ks, n * 16, lane), dv[n]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P^T reads done before dS^T overwrites Y
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-      y_store<T>(y, YC, nt * 16, 0, lane, ds[nt][0], ds[nt][1], ds[nt][2], ds[nt][3]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // dK += dS^T Q
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint4 da = tr_read_y(y, YC, 32 * ks, 0, lane);
-#pragma unroll
-      for (int n = 0; n < 8; ++n)
-        dk[n] = Mfma<T>::run(da, tr_read_img(qimg, 32 * ks, n * 16, lane), dk[n]);
+      for (int n = 0; n < 8; ++n) {
+        dv[n] = Mfma<T>::run(pa, tr_read_img2(oimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dv[n]);
+        dk[n] = Mfma<T>::run(da, tr_read_img2(qimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dk[n]);
+      }
     }
     lds_fence_barrier();  // stage buffer free for the DMA two steps ahead
   }
@@ -665,12 +650,12 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int krow = wk0 + 4 * lg + r;
-    if (krow >= L) continue;
+    const int kr = wk0 + 4 * lg + r;
+    if (kr >= L) continue;
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
-      dK[(long long)krow * a.lddk + n * 16 + lr] = from_f32<T>(dk[n][r] * a.scale);
-      dV[(long long)krow * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
+      dK[(long long)kr * a.lddk + n * 16 + lr] = from_f32<T>(dk[n][r] * a.scale);
+      dV[(long long)kr * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
     }
   }
 }
@@ -680,12 +665,11 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
 // =============================================================================================
 template <typename T, bool CAUSAL>
 __global__ void __launch_bounds__(256, 2) bwd_dq_kernel(Args a) {
-  constexpr int YC = 16;  // Y scratch: [64 keys][16 queries] per wave
-  constexpr int YB = 64 * (YC + 4) * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 4 * YB];
+  // S^T = K Q^T and dP^T = V dO^T with the keys as MFMA rows: lane (query L, keys 4g + r) holds
+  // its query's dS row in the permuted-k order, the A operand of dQ += dS K without LDS.
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  char* y = smem + 4 * IMG + wid * YB;
   const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
   const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
   const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
@@ -694,22 +678,15 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_kernel(Args a) {
   const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
   const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
   const int wq0 = q0 + wid * 16;
+  const int qrow = wq0 + lr;  // this lane's query
   uint4 qf[4], of[4];
-  {
-    const int row = wq0 + lr;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qf[ks] = gload16(Q + (long long)row * a.ldq + (4 * ks + lg) * 8, row < L);
-      of[ks] = gload16(dO + (long long)row * a.lddo + (4 * ks + lg) * 8, row < L);
-    }
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = gload16(Q + (long long)qrow * a.ldq + (4 * ks + lg) * 8, qrow < L);
+    of[ks] = gload16(dO + (long long)qrow * a.lddo + (4 * ks + lg) * 8, qrow < L);
   }
-  float lse_r[4], del_r[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qrow = wq0 + 4 * lg + r;
-    lse_r[r] = qrow < L ? a.lse[(long long)head * a.T + s0 + qrow] : INFINITY;
-    del_r[r] = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
-  }
+  const float lse_q = qrow < L ? a.lse[(long long)head * a.T + s0 + qrow] : INFINITY;
+  const float del_q = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
   f32x4 dq[8];
 #pragma unroll
   for (int n = 0; n < 8; ++n) dq[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -739,41 +716,38 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_kernel(Args a) {
     for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        s[nt] = Mfma<T>::run(qf[ks], row_read(kimg, nt * 16 + lr, 4 * ks + lg), s[nt]);
-        dp[nt] = Mfma<T>::run(of[ks], row_read(vimg, nt * 16 + lr, 4 * ks + lg), dp[nt]);
+        s[nt] = Mfma<T>::run(row_read(kimg, nt * 16 + lr, 4 * ks + lg), qf[ks], s[nt]);
+        dp[nt] = Mfma<T>::run(row_read(vimg, nt * 16 + lr, 4 * ks + lg), of[ks], dp[nt]);
       }
     }
+    const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int kpos = kv0 + nt * 16 + lr;
-      float ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int qrow = wq0 + 4 * lg + r;
-        float pv = exp2f(s[nt][r] * a.scale_log2 - lse_r[r]);
-        if (kpos >= L || qrow >= L || (CAUSAL && kpos > qrow)) pv = 0.f;
-        ds[r] = pv * (dp[nt][r] - del_r[r]);
+        const int kpos = kv0 + nt * 16 + 4 * lg + r;
+        float pv = exp2f(s[nt][r] * a.scale_log2 - lse_q);
+        if (need_mask && (kpos >= L || qrow >= L || (CAUSAL && kpos > qrow))) pv = 0.f;
+        s[nt][r] = pv * (dp[nt][r] - del_q);
       }
-      y_store<T>(y, YC, nt * 16, 0, lane, ds[0], ds[1], ds[2], ds[3]);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const uint4 da = tr_read_y(y, YC, 32 * ks, 0, lane);
+      const uint4 da = pack_p<T>(s[2 * ks], s[2 * ks + 1]);
 #pragma unroll
       for (int n = 0; n < 8; ++n)
-        dq[n] = Mfma<T>::run(da, tr_read_img(kimg, 32 * ks, n * 16, lane), dq[n]);
+        dq[n] = Mfma<T>::run(da, tr_read_img2(kimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dq[n]);
     }
     lds_fence_barrier();
   }
   T* dQ = reinterpret_cast<T*>(a.dq) + (long long)s0 * a.lddq + head * D;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int qrow = wq0 + 4 * lg + r;
-    if (qrow >= L) continue;
+    const int qr = wq0 + 4 * lg + r;
+    if (qr >= L) continue;
 #pragma unroll
     for (int n = 0; n < 8; ++n)
-      dQ[(long long)qrow * a.lddq + n * 16 + lr] = from_f32<T>(dq[n][r] * a.scale);
+      dQ[(long long)qr * a.lddq + n * 16 + lr] = from_f32<T>(dq[n][r] * a.scale);
   }
 }
 
