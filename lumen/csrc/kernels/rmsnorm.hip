@@ -74,30 +74,37 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ s, const T* __restrict__ w,
     const float* __restrict__ rstd, const T* __restrict__ ds_res, T* __restrict__ dx,
     float* __restrict__ dw, int rows, int H) {
+  // All row loads (dy, s and the residual-stream gradient) are issued up front and kept packed
+  // (16-bit) in registers, so the reduction and the write-back never wait on a second round of
+  // HBM latency and the VGPR budget leaves room for 3-4 waves per SIMD.
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const size_t base = static_cast<size_t>(row) * H;
   const float rs = rstd[row];
-  float g[VPL][8], xh[VPL][8];
+  uint4 dyr[VPL], sr[VPL], rr[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * 8;
+    const bool ok = c < H;
+    dyr[i] = ok ? *reinterpret_cast<const uint4*>(dy + base + c) : make_uint4(0, 0, 0, 0);
+    sr[i] = ok ? *reinterpret_cast<const uint4*>(s + base + c) : make_uint4(0, 0, 0, 0);
+    rr[i] = (ok && ds_res) ? *reinterpret_cast<const uint4*>(ds_res + base + c) : make_uint4(0, 0, 0, 0);
+  }
   float dot = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = (lane + i * 64) * 8;
     if (c < H) {
-      float dyv[8], sv[8], wv[8];
-      load8(dy + base + c, dyv);
-      load8(s + base + c, sv);
+      const T* dyv = reinterpret_cast<const T*>(&dyr[i]);
+      const T* sv = reinterpret_cast<const T*>(&sr[i]);
+      float wv[8];
       load8(w + c, wv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        xh[i][j] = sv[j] * rs;
-        g[i][j] = dyv[j] * wv[j];
-        dot += g[i][j] * xh[i][j];
-      }
+      for (int j = 0; j < 8; ++j) dot += to_f32(dyv[j]) * wv[j] * (to_f32(sv[j]) * rs);
       if (dw) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(dw + c + j, dyv[j] * xh[i][j]);
+        for (int j = 0; j < 8; ++j) atomicAdd(dw + c + j, to_f32(dyv[j]) * to_f32(sv[j]) * rs);
       }
     }
   }
@@ -106,14 +113,15 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
   for (int i = 0; i < VPL; ++i) {
     const int c = (lane + i * 64) * 8;
     if (c < H) {
-      float o[8];
+      const T* dyv = reinterpret_cast<const T*>(&dyr[i]);
+      const T* sv = reinterpret_cast<const T*>(&sr[i]);
+      const T* rv = reinterpret_cast<const T*>(&rr[i]);
+      float wv[8], o[8];
+      load8(w + c, wv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - xh[i][j] * dot);
-      if (ds_res) {
-        float r[8];
-        load8(ds_res + base + c, r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] += r[j];
+      for (int j = 0; j < 8; ++j) {
+        o[j] = rs * (to_f32(dyv[j]) * wv[j] - to_f32(sv[j]) * rs * dot);
+        if (ds_res) o[j] += to_f32(rv[j]);
       }
       store8(dx + base + c, o);
     }

@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
+from ..ops.lora import arena_reset
 from ..ops.activation import swiglu
 from ..ops.attention import causal_attention, flash_attention_qkv
 from ..ops.loss import lm_head_cross_entropy
@@ -150,6 +151,8 @@ class LlamaForCausalLM(nn.Module):
 
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
                 n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None):
+        if self.training and torch.is_grad_enabled():
+            arena_reset(input_ids.device)  # adapter scratch of the previous micro-step is dead
         h, res = self.hidden_states(input_ids, pos)
         last = len(self.layers) + 1
 

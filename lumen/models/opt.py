@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
+from ..ops.lora import arena_reset
 from ..ops.attention import causal_attention
 from ..ops.loss import lm_head_cross_entropy
 from ..ops.norm import layer_norm
@@ -91,6 +92,8 @@ class OPTForCausalLM(nn.Module):
 
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
                 n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None):
+        if self.training and torch.is_grad_enabled():
+            arena_reset(input_ids.device)  # adapter scratch of the previous micro-step is dead
         B, S = input_ids.shape
         if pos is None:
             pos = torch.arange(S, device=input_ids.device).expand(B, S)

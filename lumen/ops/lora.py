@@ -120,13 +120,64 @@ def _lora2(kind, flag, big, small, out, cs0, cs1, alpha, T, J, split, segs4, see
                    [list(map(int, s)) for s in segs4])
 
 
-def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed):
+class ZeroArena:
+    """Pre-zeroed f32 scratch for the adapter kernels' atomic accumulators (Z, dZ).
+
+    Every adapted linear needs two zero-initialised [T, R] buffers per micro-step; handing out
+    slices of one buffer that is zeroed once per forward (``reset``) replaces ~128 fill kernels
+    per Llama-2-7B step with one.  A cycle that outgrows the buffer falls back to torch.zeros
+    and the next ``reset`` reallocates to the measured demand.  Slices stay valid until the next
+    ``reset``, i.e. through the backward of the same micro-step."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+        self.off = 0      # bytes handed out of buf (in elements)
+        self.used = 0     # demand of the current cycle, including fallbacks
+
+    def reset(self, device) -> None:
+        if self.buf is None or self.buf.device != device or self.buf.numel() < self.used:
+            self.buf = (torch.zeros(self.used, device=device, dtype=torch.float32)
+                        if self.used else None)
+        elif self.off:
+            self.buf[:self.off].zero_()
+        self.off = 0
+        self.used = 0
+
+    def zeros(self, *shape, device) -> torch.Tensor:
+        n = math.prod(shape)
+        n_al = (n + 63) // 64 * 64
+        self.used += n_al
+        if self.buf is not None and self.buf.device == device and self.off + n_al <= self.buf.numel():
+            t = self.buf[self.off:self.off + n].view(*shape)
+            self.off += n_al
+            return t
+        return torch.zeros(*shape, device=device, dtype=torch.float32)
+
+
+ARENA = ZeroArena()
+USE_ARENA = _os.environ.get("LUMEN_LORA_ARENA", "1") != "0"
+_IN_BACKWARD = [False]
+
+
+def arena_reset(device) -> None:
+    """Start of a training forward (called by the model); no-op unless enabled on a GPU."""
+    if USE_ARENA and device.type == "cuda":
+        ARENA.reset(device)
+
+
+def _zeros(*shape, device, train: bool = False):
+    if USE_ARENA and device.type == "cuda" and (train or _IN_BACKWARD[0]):
+        return ARENA.zeros(*shape, device=device)
+    return torch.zeros(*shape, device=device, dtype=torch.float32)
+
+
+def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train: bool = False):
     """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place)."""
     T, K = x2d.shape
     R = A.shape[0]
     Ntot = y.shape[1]
     act = DTYPE_CODE[x2d.dtype]
-    Z = torch.zeros(T, R, device=x2d.device, dtype=torch.float32)
+    Z = _zeros(T, R, device=x2d.device, train=train)
     if _v2_ok(r, R, x2d):
         _lora2(0, 1, x2d, A, Z, R, 1, 1.0, T, R, _split(math.ceil(T / 64), K, 256),
                [(0, 0, 0, K)], seed, p, K)
@@ -153,12 +204,14 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
     Ntot = dy.shape[1]
     act = DTYPE_CODE[dy.dtype]
     dev = dy.device
-    # one zero-filled workspace for dZ, dA and dB (the kernels accumulate with atomics)
-    nA = R * K if need_dA else 0
-    nB = B.shape[0] * r if need_dB else 0
-    ws = torch.zeros(T * R + nA + nB, device=dev, dtype=torch.float32)
-    dZ = ws[:T * R].view(T, R)
     v2 = _v2_ok(r, R, x2d, dy)
+    # dA / dB accumulate straight into the parameters' .grad (views of the engine's flat f32
+    # gradient buffer) when they exist: no zero-filled temporaries and no autograd add kernels
+    direct = v2 and DIRECT_GRAD and _direct_ok(A) and _direct_ok(B)
+    nA = R * K if need_dA and not direct else 0
+    nB = B.shape[0] * r if need_dB and not direct else 0
+    ws = _zeros(T * R + nA + nB, device=dev)
+    dZ = ws[:T * R].view(T, R)
     if v2:
         for i in range(0, len(segs), 4):
             ch = segs[i:i + 4]
@@ -173,7 +226,7 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
                        _ksplit(T, r, max(s[5] for s in chunk), 16, len(chunk)))
     dA = dB = None
     if need_dA:
-        dA = ws[T * R:T * R + nA].view(R, K)
+        dA = A.grad if direct else ws[T * R:T * R + nA].view(R, K)
         if v2:
             _lora2(1, 1, x2d, dZ, dA, 1, K, 1.0, T, R, _split(math.ceil(K / 128), T, 128),
                    [(0, 0, 0, K)], seed, p, K)
@@ -181,7 +234,7 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
             _lora_gemm(act, 3, dZ, x2d, dA, R, K, K, 1, 1.0, [(0, 0, 0, R, K, T)],
                        _ksplit(R, K, T, 64), seed, p, K)
     if need_dB:
-        dB = ws[T * R + nA:].view(B.shape[0], r)
+        dB = B.grad if direct else ws[T * R + nA:].view(B.shape[0], r)
         if v2:
             for i in range(0, len(segs), 4):
                 ch = segs[i:i + 4]
@@ -199,7 +252,22 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
             _lora2(2, 0, A, dZ, dx, dx.stride(0), 1, 1.0, T, R, 1, [(0, 0, 0, K)], seed, p, K)
         else:
             _lora_gemm(act, 5, dZ, A, dx, R, K, K, 1, 1.0, [(0, 0, 0, T, K, R)], 1, seed, p, K)
+    if direct:
+        for prm, need in ((A, need_dA), (B, need_dB)):
+            cb = getattr(prm, "_lumen_grad_ready", None)
+            if need and cb is not None:
+                cb(prm)
+        return None, None
     return dA, dB
+
+
+DIRECT_GRAD = _os.environ.get("LUMEN_LORA_DIRECT_GRAD", "1") != "0"
+
+
+def _direct_ok(prm: torch.Tensor) -> bool:
+    g = prm.grad
+    return (getattr(prm, "_lumen_direct_grad", False) and g is not None
+            and g.dtype == torch.float32 and g.is_contiguous() and g.shape == prm.shape)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -208,12 +276,14 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
 
 class _LoraLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param, wt_fn):
+    def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param, wt_fn, train):
+        ctx.train = train
         W = weight_fn()
         y = torch.matmul(x2d, W.t())
         if bias is not None:
             y.add_(bias)
-        Z = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed)
+        # autograd runs Function.forward with grad disabled: the training flag is passed in
+        Z = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed, train=ctx.train)
         ctx.weight_fn = weight_fn
         ctx.wt_fn = wt_fn
         ctx.meta = (segs, r, scale, p, seed)
@@ -228,11 +298,15 @@ class _LoraLinear(torch.autograd.Function):
         segs, r, scale, p, seed = ctx.meta
         dy = dy.contiguous()
         dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
-        dA, dB = lora_bwd_native(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed,
-                                 ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+        _IN_BACKWARD[0] = True
+        try:
+            dA, dB = lora_bwd_native(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed,
+                                     ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+        finally:
+            _IN_BACKWARD[0] = False
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
-        return dx, None, db, dA, dB, None, None, None, None, None, dw, None
+        return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None
 
 
 class _Linear(torch.autograd.Function):
@@ -295,7 +369,7 @@ def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: tor
     x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
     if use_native(x2d):
         y = _LoraLinear.apply(x2d.contiguous(), weight_fn, bias, A, B, segs, r, scale, p, seed,
-                              w_param, wt_fn)
+                              w_param, wt_fn, torch.is_grad_enabled())
     else:
         y = lora_linear_ref(x2d, _frozen(weight_fn()), bias, A, B, segs, r, scale, p, seed)
     return y if x.dim() == 2 else y.view(*shp[:-1], y.shape[-1])

@@ -106,6 +106,8 @@ class ZeroEngine:
                                             cfg.hysteresis, cfg.min_loss_scale, cfg.loss_scale)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._works: List = []
+        for prm in trainable:  # .grad is a view of flat.grad: kernels may accumulate into it
+            prm._lumen_direct_grad = True
         if self.sharded and self.stage >= 2 and cfg.overlap_comm:
             self._install_bucket_hooks()
 
@@ -124,7 +126,10 @@ class ZeroEngine:
     def _install_bucket_hooks(self):
         for b in self.flat.buckets:
             for p in b.params:
-                p.register_post_accumulate_grad_hook(self._make_ready_hook(b))
+                hook = self._make_ready_hook(b)
+                p.register_post_accumulate_grad_hook(hook)
+                # kernels that accumulate into .grad directly (lora_bwd_native) report here
+                p._lumen_grad_ready = hook
 
     def _make_ready_hook(self, b):
         def hook(p):

@@ -361,3 +361,39 @@ def test_transpose_2d(shape):
 
     x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
     torch.testing.assert_close(transpose_2d(x), x.t().contiguous(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("direct,arena", [(False, False), (True, True)])
+def test_engine_lora_grad_paths_match(direct, arena, monkeypatch):
+    """Direct .grad accumulation + zero arena give the same training trajectory as the plain
+    path (adapter grads returned to autograd, torch.zeros scratch)."""
+    import lumen.ops.lora as lora_mod
+    from lumen.lora import LoraConfig, adapter_state_dict, apply_lora
+    from lumen.models import build_model
+    from lumen.parallel.dist import init
+    from lumen.train.config import load_ds_config
+    from lumen.train.engine import ZeroEngine
+
+    def run(direct_, arena_):
+        monkeypatch.setattr(lora_mod, "DIRECT_GRAD", direct_)
+        monkeypatch.setattr(lora_mod, "USE_ARENA", arena_)
+        torch.manual_seed(0)
+        m = build_model("tiny-llama", dtype=torch.bfloat16, device=torch.device("cuda"), seed=3)
+        apply_lora(m, LoraConfig(r=16, lora_dropout=0.1))
+        m.train()
+        env = init()
+        ds = load_ds_config({"zero_optimization": {"stage": 1}}, 2, 2, 1, 1e-3)
+        eng = ZeroEngine(m, ds, env)
+        g = torch.Generator(device="cpu").manual_seed(5)
+        for _ in range(6):
+            ids = torch.randint(3, m.config.vocab_size, (2, 64), generator=g).cuda()
+            labels = torch.roll(ids, -1, 1)
+            loss = eng.forward({"input_ids": ids, "labels": labels})
+            eng.backward(loss)
+            eng.step()
+        return adapter_state_dict(m)
+
+    ref = run(False, False)
+    got = run(direct, arena)
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k], rtol=1e-3, atol=1e-5)
