@@ -87,8 +87,9 @@ class Scheduler:
         if not self.running:
             return None
         ready: List[Sequence] = []
+        preempted = set()
         for s in list(self.running):
-            if s not in self.running:
+            if s.seq_id in preempted:
                 continue
             while True:
                 try:
@@ -98,6 +99,7 @@ class Scheduler:
                 except RuntimeError:
                     victim = self.running[-1]
                     self._preempt(victim)
+                    preempted.add(victim.seq_id)
                     if victim is s:
                         break
                     if victim in ready:
@@ -119,8 +121,9 @@ class Scheduler:
 
     def finish(self, batch: Batch) -> List[Sequence]:
         done = [s for s in batch.seqs if s.finished]
-        for s in done:
-            if s in self.running:
-                self.running.remove(s)
-            self.blocks.free_seq(s.seq_id)
+        if done:
+            ids = {s.seq_id for s in done}
+            self.running = [s for s in self.running if s.seq_id not in ids]
+            for s in done:
+                self.blocks.free_seq(s.seq_id)
         return done

@@ -63,6 +63,10 @@ class Sequence:
         return len(self.prompt_ids) + len(self.output_ids)
 
     @property
+    def last_token(self) -> int:
+        return self.output_ids[-1] if self.output_ids else self.prompt_ids[-1]
+
+    @property
     def finished(self) -> bool:
         return self.status == Status.FINISHED
 
