@@ -61,6 +61,10 @@ class LLMEngine:
         else:
             dev = torch.device("cpu")
         self.device = dev
+        if dev.type == "cuda":
+            from ..utils.gemm_tuning import load_tuned_gemms
+
+            load_tuned_gemms()  # tuned hipBLASLt algorithms for the prefill/decode GEMM shapes
         dt = _DT[cfg.dtype] if dev.type == "cuda" else torch.float32
         if model is None:
             model = build_model(cfg.model, dtype=dt, device=dev, init=cfg.init, seed=cfg.seed)

@@ -73,6 +73,10 @@ class Trainer:
         self.args, self.ds, self.env = args, ds, env
         self.print = printer or (lambda *a, **k: print(*a, **k, flush=True) if env.is_main else None)
         torch.manual_seed(args.seed)
+        if env.device.type == "cuda":
+            from ..utils.gemm_tuning import load_tuned_gemms
+
+            load_tuned_gemms()
         dt = ds.torch_dtype
         cfg = get_config(args.model_name)
         self.model_cfg = cfg
