@@ -29,6 +29,9 @@ def build_parser():
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--in-process", action="store_true",
+                    help="run the HTTP server on a thread of the GPU process (default: the API "
+                         "runs in its own process and talks to the engine core over queues)")
     return ap
 
 
@@ -36,7 +39,24 @@ def main(argv=None):
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     sys.path.insert(0, root)
     a = build_parser().parse_args(argv)
-    import torch
+    from lumen.models import get_config
+
+    rank = int(os.environ.get("RANK", "0"))
+    api = req_q = out_q = None
+    if rank == 0 and not a.in_process:
+        # OpenAI HTTP front-end in a spawned process (no GPU, its own GIL), started before this
+        # process initialises the GPU; it talks to the engine core below over two queues
+        import multiprocessing as mp
+
+        from lumen.serve.frontend import api_process_main
+
+        mcfg = get_config(a.model)
+        ctx = mp.get_context("spawn")
+        req_q, out_q = ctx.Queue(), ctx.Queue()
+        api = ctx.Process(target=api_process_main, name="lumen-api",
+                          args=(req_q, out_q, a.model, a.max_model_len, a.host, a.port,
+                                a.served_model_name, mcfg.vocab_size), daemon=True)
+        api.start()
 
     from lumen.parallel.dist import init
     from lumen.serve.engine import AsyncEngine, EngineConfig, LLMEngine
@@ -55,16 +75,35 @@ def main(argv=None):
 
         worker_loop(eng.runner)
         return
-    import uvicorn
-
-    from lumen.serve.api_server import create_app
-
-    app = create_app(AsyncEngine(eng), a.served_model_name)
     print(f"[lumen.serve] {cfg.model} tp={a.tp} kv_blocks={eng.blocks.num_blocks} "
           f"on http://{a.host}:{a.port}", flush=True)
+    if a.in_process:
+        import uvicorn
+
+        from lumen.serve.api_server import create_app
+
+        app = create_app(AsyncEngine(eng), a.served_model_name)
+        try:
+            uvicorn.run(app, host=a.host, port=a.port, log_level="warning")
+        finally:
+            eng.shutdown()
+        return
+    import signal
+
+    from lumen.serve.frontend import run_engine_core
+
+    def _term(signum, frame):  # SIGTERM -> unwind through finally: stop the API process too
+        raise SystemExit(0)
+
+    signal.signal(signal.SIGTERM, _term)
     try:
-        uvicorn.run(app, host=a.host, port=a.port, log_level="warning")
+        run_engine_core(eng, req_q, out_q)
+    except KeyboardInterrupt:
+        pass
     finally:
+        out_q.put(None)
+        api.terminate()
+        api.join(10)
         eng.shutdown()
 
 

@@ -17,7 +17,6 @@ from typing import Any, Dict, List, Optional, Union
 from fastapi import FastAPI, HTTPException, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 
-from .engine import AsyncEngine
 from .sequence import SamplingParams
 
 
@@ -81,10 +80,33 @@ def _params(body: Dict[str, Any], eos: Optional[int]) -> SamplingParams:
                           seed=body.get("seed"), logprobs=bool(body.get("logprobs", False)))
 
 
-def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
-    eng = aengine.engine
-    name = served_model_name or eng.cfg.model
-    tok = eng.tokenizer
+class IncrementalDetokenizer:
+    """Streaming text deltas in O(window) per token (re-decoding the whole output every token
+    is O(n^2) per stream).  Holds back output while the last piece decodes to an incomplete
+    UTF-8 / merge sequence (U+FFFD), like vLLM's prefix/read-offset scheme."""
+
+    def __init__(self, tok):
+        self.tok = tok
+        self.prefix = 0
+        self.read = 0
+
+    def step(self, ids: List[int]) -> str:
+        prefix_text = self.tok.decode(ids[self.prefix:self.read])
+        new_text = self.tok.decode(ids[self.prefix:])
+        if len(new_text) > len(prefix_text) and not new_text.endswith("\ufffd"):
+            self.prefix, self.read = self.read, len(ids)
+            return new_text[len(prefix_text):]
+        return ""
+
+    def flush(self, ids: List[int]) -> str:
+        return self.tok.decode(ids[self.prefix:])[len(self.tok.decode(ids[self.prefix:self.read])):]
+
+
+def create_app(aengine, served_model_name: Optional[str] = None):
+    """``aengine``: ``AsyncEngine`` (engine thread in this process) or
+    ``frontend.EngineCoreClient`` (engine core in the GPU process)."""
+    name = served_model_name or aengine.model_name
+    tok = aengine.tokenizer
     stats = _Stats()
     app = FastAPI(title="lumen OpenAI-compatible server")
 
@@ -99,11 +121,12 @@ def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
     async def models():
         return {"object": "list", "data": [{"id": name, "object": "model",
                                             "created": int(time.time()), "owned_by": "lumen",
-                                            "max_model_len": eng.cfg.max_model_len}]}
+                                            "max_model_len": aengine.max_model_len}]}
 
     @app.get("/metrics")
     async def metrics():
         t, i = _quantiles(stats.ttft), _quantiles(stats.itl)
+        live = aengine.live_stats()
         lines = [
             "# TYPE lumen_requests_total counter", f"lumen_requests_total {stats.requests}",
             "# TYPE lumen_request_errors_total counter", f"lumen_request_errors_total {stats.errors}",
@@ -114,11 +137,11 @@ def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
             *[f'lumen_time_to_first_token_seconds{{quantile="{q}"}} {v:.6f}' for q, v in t.items()],
             "# TYPE lumen_inter_token_latency_seconds summary",
             *[f'lumen_inter_token_latency_seconds{{quantile="{q}"}} {v:.6f}' for q, v in i.items()],
-            "# TYPE lumen_kv_cache_usage_ratio gauge", f"lumen_kv_cache_usage_ratio {eng.blocks.usage():.4f}",
-            "# TYPE lumen_running_requests gauge", f"lumen_running_requests {len(eng.scheduler.running)}",
-            "# TYPE lumen_waiting_requests gauge", f"lumen_waiting_requests {len(eng.scheduler.waiting)}",
+            "# TYPE lumen_kv_cache_usage_ratio gauge", f"lumen_kv_cache_usage_ratio {live['kv_usage']:.4f}",
+            "# TYPE lumen_running_requests gauge", f"lumen_running_requests {live['running']}",
+            "# TYPE lumen_waiting_requests gauge", f"lumen_waiting_requests {live['waiting']}",
             "# TYPE lumen_preemptions_total counter",
-            f"lumen_preemptions_total {eng.scheduler.num_preemptions}",
+            f"lumen_preemptions_total {live['preemptions']}",
         ]
         return PlainTextResponse("\n".join(lines) + "\n")
 
@@ -140,8 +163,8 @@ def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
 
         if stream:
             async def gen():
-                sent = ""
                 last = None
+                detok = IncrementalDetokenizer(tok)
                 try:
                     if chat:
                         first = {"id": rid, "object": "chat.completion.chunk", "created": created,
@@ -150,10 +173,10 @@ def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
                         yield f"data: {json.dumps(first)}\n\n"
                     async for seq in aengine.stream(prompt, params, rid):
                         last = seq
-                        text = decode(seq.output_ids)
-                        delta = text[len(sent):] if text.startswith(sent) else text
-                        sent = text
                         fin = seq.finish_reason if seq.finished else None
+                        delta = detok.step(seq.output_ids)
+                        if fin:
+                            delta += detok.flush(seq.output_ids)
                         if delta or fin:
                             yield f"data: {json.dumps(chunk(delta, fin))}\n\n"
                     if last is not None:
@@ -196,7 +219,7 @@ def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
                 raise HTTPException(status_code=400, detail="batched string prompts: send one per request")
             prompt = prompt[0]
         try:
-            params = _params(body, eng.eos_id)
+            params = _params(body, aengine.eos_id)
         except ValueError as e:
             raise HTTPException(status_code=400, detail=str(e))
         return await _run(prompt, params, False, bool(body.get("stream", False)),
@@ -209,7 +232,7 @@ def create_app(aengine: AsyncEngine, served_model_name: Optional[str] = None):
         if not msgs:
             raise HTTPException(status_code=400, detail="messages required")
         try:
-            params = _params(body, eng.eos_id)
+            params = _params(body, aengine.eos_id)
         except ValueError as e:
             raise HTTPException(status_code=400, detail=str(e))
         return await _run(llama2_chat_prompt(msgs), params, True, bool(body.get("stream", False)),

@@ -284,6 +284,28 @@ class AsyncEngine:
             for s in seqs:
                 self._push(s.request_id, ("token", s))
 
+    # -- interface shared with frontend.EngineCoreClient (what the API server reads) ---------
+    @property
+    def tokenizer(self):
+        return self.engine.tokenizer
+
+    @property
+    def model_name(self) -> str:
+        return self.engine.cfg.model
+
+    @property
+    def max_model_len(self) -> int:
+        return self.engine.cfg.max_model_len
+
+    @property
+    def eos_id(self):
+        return self.engine.eos_id
+
+    def live_stats(self) -> dict:
+        sch = self.engine.scheduler
+        return {"kv_usage": self.engine.blocks.usage(), "running": len(sch.running),
+                "waiting": len(sch.waiting), "preemptions": sch.num_preemptions}
+
     def _push(self, rid, item):
         st = self._streams.get(rid)
         if st is None:

@@ -148,3 +148,53 @@ def test_tensor_parallel_serving_gloo(tmp_path):
     prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
     for p, out in zip(prompts, got):
         assert out == naive_greedy(ref_model, p, 8), p
+
+
+def test_serve_cli_engine_core_split(tmp_path):
+    """scripts/serve.py on CPU: API in a spawned process, engine core in the main one."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+    import urllib.request
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    proc = subprocess.Popen([sys.executable, os.path.join(root, "scripts", "serve.py"), "--model",
+                             "tiny-llama", "--port", str(port), "--max-model-len", "256"],
+                            env=dict(os.environ, PYTHONPATH=root), stdout=subprocess.PIPE,
+                            stderr=subprocess.STDOUT)
+    url = f"http://127.0.0.1:{port}"
+    try:
+        t0 = time.time()
+        while True:
+            try:
+                urllib.request.urlopen(url + "/health", timeout=2)
+                break
+            except Exception:
+                assert proc.poll() is None, proc.stdout.read().decode()[-3000:]
+                assert time.time() - t0 < 180, "server did not come up"
+                time.sleep(0.5)
+
+        def post(path, body):
+            req = urllib.request.Request(url + path, data=json.dumps(body).encode(),
+                                         headers={"Content-Type": "application/json"})
+            return urllib.request.urlopen(req, timeout=60).read().decode()
+
+        r = json.loads(post("/v1/completions", {"prompt": [5, 6, 7], "max_tokens": 5,
+                                                "temperature": 0, "ignore_eos": True}))
+        assert r["usage"]["completion_tokens"] == 5
+        body = post("/v1/completions", {"prompt": "hello", "max_tokens": 4, "temperature": 0,
+                                        "ignore_eos": True, "stream": True})
+        events = [l for l in body.splitlines() if l.startswith("data: ")]
+        assert events[-1] == "data: [DONE]"
+        assert json.loads(events[-2][6:])["choices"][0]["finish_reason"] == "length"
+        m = urllib.request.urlopen(url + "/metrics", timeout=10).read().decode()
+        assert "lumen_requests_total 2" in m
+    finally:
+        proc.terminate()
+        proc.wait(30)
