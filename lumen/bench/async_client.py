@@ -80,9 +80,8 @@ async def one_request(session, url: str, prompt, max_tokens: int, model: str) ->
                 j = json.loads(data)
                 if "error" in j:
                     return ReqResult(False, error=j["error"]["message"])
-                ch = j["choices"][0]
                 now = time.perf_counter()
-                if ch.get("text") or ch.get("finish_reason"):
+                if j.get("choices"):  # one event per generated-token step (text may be empty)
                     if first is None:
                         first = now
                     else:

@@ -177,8 +177,10 @@ def create_app(aengine, served_model_name: Optional[str] = None):
                         delta = detok.step(seq.output_ids)
                         if fin:
                             delta += detok.flush(seq.output_ids)
-                        if delta or fin:
-                            yield f"data: {json.dumps(chunk(delta, fin))}\n\n"
+                        # one event per engine step that produced tokens, even when the text
+                        # delta is still empty (incomplete UTF-8 / special ids): clients see
+                        # token timing (TTFT, inter-token latency) as OpenAI streams show it
+                        yield f"data: {json.dumps(chunk(delta, fin))}\n\n"
                     if last is not None:
                         stats.observe(last)
                 except ValueError as e:
