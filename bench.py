@@ -93,7 +93,9 @@ def main():
     model.train()
     n_tr, n_all = count_parameters(model)
     engine = ZeroEngine(model, ds, env)
-    torch.cuda.synchronize()
+    on_gpu = env.device.type == "cuda"
+    if on_gpu:
+        torch.cuda.synchronize()
     setup_s = time.time() - t0
 
     B, S = ds.micro_batch, args.seq_len
@@ -117,10 +119,14 @@ def main():
         return loss
 
     def sync():
-        torch.cuda.synchronize()
-        if dist.is_initialized():
-            dist.barrier(device_ids=[env.local_rank])
+        from lumen.parallel.dist import barrier
+
+        if on_gpu:
             torch.cuda.synchronize()
+        if dist.is_initialized():
+            barrier()  # device-bound barrier on RCCL, plain on gloo (CPU plumbing runs)
+            if on_gpu:
+                torch.cuda.synchronize()
 
     loss = run_steps(args.warmup, 0)
     sync()
@@ -151,7 +157,7 @@ def main():
     final_loss = float(loss.item())
     tokens = world * B * ds.grad_accum * S * args.steps
     value = tokens / dt
-    peak_gb = torch.cuda.max_memory_allocated() / 1e9
+    peak_gb = torch.cuda.max_memory_allocated() / 1e9 if on_gpu else 0.0
     if env.is_main:
         from lumen.train.trainer import model_flops_per_token
 
@@ -168,7 +174,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_TOK_S, 2),
             "dtype": ds.dtype,
-            "data": "synthetic (uniform random token ids, seq 512); random-init weights",
+            "data": f"synthetic (uniform random token ids, seq {S}); random-init weights",
             "config": {
                 "model": cfg.name,
                 "global_batch": B * ds.grad_accum * world,
@@ -194,7 +200,9 @@ def main():
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
-        dist.barrier(device_ids=[env.local_rank])
+        from lumen.parallel.dist import barrier
+
+        barrier()
         dist.destroy_process_group()
 
 

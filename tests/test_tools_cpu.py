@@ -211,3 +211,32 @@ def test_profiler_and_debug_guards(tmp_path, monkeypatch):
     assert any(l.startswith("[lumen] time (ms)") and "fwd" in l for l in lines)
     with pytest.raises(NonFiniteError):
         check_finite("x", torch.tensor([1.0, float("nan")]))
+
+
+def test_bench_contract_torchrun_world2():
+    """bench.py under torch.distributed.run (2 ranks, gloo, tiny model): one JSON line from
+    rank 0 with the driver's fields, whole-job tokens/s, ZeRO-3 partitioning active."""
+    import json
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                          str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                          "--warmup", "1", "--model", "tiny-llama", "--seq_len", "32",
+                          "--micro_batch", "2"], capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    j = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in j, k
+    assert j["n_gpus"] == 2 and j["steps"] == 2 and j["scaling"] == "weak"
+    assert j["config"]["global_batch"] == 4 and j["config"]["parallelism"] == "dp2-zero3"
+    assert j["extra"]["zero3_keep_gathered"] is True
+    assert abs(j["value"] - 4 * 32 * 2 / (j["ms_per_step"] * 2 / 1000)) / j["value"] < 0.02
