@@ -43,7 +43,7 @@ def main():
         for impl in ("f32", "v2"):
             L.USE_V2 = impl == "v2"
             fwd = _time(lambda: L.lora_fwd_native(x, y, A, B, segs, r, 2.0, 0.05, 123))
-            Z = L.lora_fwd_native(x, y, A, B, segs, r, 2.0, 0.05, 123)
+            Z = L.lora_fwd_native(x, y, A, B, segs, r, 2.0, 0.05, 123)[0]
             bwd = _time(lambda: L.lora_bwd_native(dy, x, A, B, Z, dx, segs, r, 2.0, 0.05, 123))
             print(f"{name:4s} {impl:4s} fwd {fwd:7.1f} us  bwd {bwd:7.1f} us", flush=True)
 

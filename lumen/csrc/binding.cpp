@@ -35,7 +35,8 @@ hipError_t lumen_lora_gemm(int, int, int, const void*, const void*, void*, long 
 hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long long, void*,
                        long long, long long, float, int, int, int, unsigned long long, unsigned int,
                        float, long long, long long, int, const long long*, const long long*,
-                       const long long*, const int*, hipStream_t);
+                       const long long*, const int*, const float*, const float*, const int*, int,
+                       hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
@@ -199,7 +200,9 @@ void lora2(int64_t dtype, int64_t kind, int64_t flag, const at::Tensor& big, int
            const at::Tensor& small, int64_t lds, at::Tensor& out, int64_t cs0, int64_t cs1,
            double alpha, int64_t T, int64_t J, int64_t split, int64_t seed, int64_t drop_thresh,
            double drop_scale, int64_t drop_ld, int64_t drop_col0,
-           const std::vector<std::vector<int64_t>>& segs) {
+           const std::vector<std::vector<int64_t>>& segs, const c10::optional<at::Tensor>& rope_cos,
+           const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& rope_pos,
+           int64_t rope_mask) {
   if (!big.is_cuda() || !small.is_cuda() || !out.is_cuda())
     throw std::invalid_argument("lumen: lora2 needs GPU tensors");
   if (small.scalar_type() != at::kFloat)
@@ -222,7 +225,11 @@ void lora2(int64_t dtype, int64_t kind, int64_t flag, const at::Tensor& big, int
                     cs1, static_cast<float>(alpha), static_cast<int>(T), static_cast<int>(J),
                     static_cast<int>(split), static_cast<unsigned long long>(seed),
                     static_cast<unsigned int>(drop_thresh), static_cast<float>(drop_scale),
-                    drop_ld, drop_col0, nseg, bo, so, oo, nc, cur_stream()),
+                    drop_ld, drop_col0, nseg, bo, so, oo, nc,
+                    rope_cos ? rope_cos->data_ptr<float>() : nullptr,
+                    rope_sin ? rope_sin->data_ptr<float>() : nullptr,
+                    rope_pos ? rope_pos->data_ptr<int>() : nullptr, static_cast<int>(rope_mask),
+                    cur_stream()),
         "lora2");
 }
 

@@ -54,6 +54,12 @@ struct Args {
   long long drop_col0;     // dropout feature index of big column 0 (segment offsets added)
   Drop drop;
   Seg4 seg;
+  // UP only: rotary embedding fused into the write-back of the segments in rope_mask (q|k heads
+  // of the fused QKV output, head dim 128): out = rope(out + delta) at position rope_pos[t]
+  const float* rope_cos;   // [max_pos][64]
+  const float* rope_sin;
+  const int* rope_pos;     // [T]
+  int rope_mask;
 };
 
 // ---- software-pipelined staging ------------------------------------------------------------
@@ -389,27 +395,59 @@ __global__ void __launch_bounds__(256) up_kernel(Args a) {
       for (int r = 0; r < 4; ++r) sc[(g * 4 + r) * kUC + n * 16 + L] = acc[n][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scratch writes land before the reads
     // 16 rows x 128 cols = 256 vectors of 8; 4 per lane
+    const bool rope = (a.rope_mask >> seg) & 1;
+    // issue every global load of the write-back (4 output vectors per lane and, for RoPE
+    // segments, their cos/sin) before any arithmetic, so one memory latency covers the tile
+    uint4 yr[4];
+    float4 cr[4][2], sr[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int v = lane + i * 64;
       const int rr = v >> 4, cc = (v & 15) * 8;
       const int t = t0 + wid * 16 + rr, c = c0 + cc;
-      if (t < a.T && c < NC) {
-        T* po = out + (long long)t * a.cs0 + c;
-        float y[8];
-        load8(po, y);
-        const uint32_t keep = DROP ? dropout_keep8(a.drop.seed,
-                                                   (unsigned long long)t * a.drop.ld + a.drop_col0 + c,
-                                                   a.drop.thresh)
-                                   : 0xFFu;
+      const bool ok = t < a.T && c < NC;
+      yr[i] = ok ? *reinterpret_cast<const uint4*>(out + (long long)t * a.cs0 + c) : make_uint4(0, 0, 0, 0);
+      if (rope) {
+        const long long p = (ok ? a.rope_pos[t] : 0) * 64LL + (cc & 63);
+        cr[i][0] = *reinterpret_cast<const float4*>(a.rope_cos + p);
+        cr[i][1] = *reinterpret_cast<const float4*>(a.rope_cos + p + 4);
+        sr[i][0] = *reinterpret_cast<const float4*>(a.rope_sin + p);
+        sr[i][1] = *reinterpret_cast<const float4*>(a.rope_sin + p + 4);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = lane + i * 64;
+      const int rr = v >> 4, cc = (v & 15) * 8;
+      const int t = t0 + wid * 16 + rr, c = c0 + cc;
+      const bool ok = t < a.T && c < NC;
+      float y[8];
+      unpack8<T>(yr[i], y);
+      const uint32_t keep = DROP ? dropout_keep8(a.drop.seed,
+                                                 (unsigned long long)t * a.drop.ld + a.drop_col0 + c,
+                                                 a.drop.thresh)
+                                 : 0xFFu;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float add = a.alpha * sc[rr * kUC + cc + e];
+        if (DROP) add = (keep >> e) & 1u ? add * a.drop.scale : 0.f;
+        y[e] += add;
+      }
+      if (rope) {  // block-uniform: the 128 columns of this block are one head
+        // rotate_half partner of column cc is cc ^ 64, held by lane ^ 8 of the same 16-lane row
+        const float sg = cc < 64 ? -1.f : 1.f;
+        const float cs[8] = {cr[i][0].x, cr[i][0].y, cr[i][0].z, cr[i][0].w,
+                             cr[i][1].x, cr[i][1].y, cr[i][1].z, cr[i][1].w};
+        const float sn[8] = {sr[i][0].x, sr[i][0].y, sr[i][0].z, sr[i][0].w,
+                             sr[i][1].x, sr[i][1].y, sr[i][1].z, sr[i][1].w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float add = a.alpha * sc[rr * kUC + cc + e];
-          if (DROP) add = (keep >> e) & 1u ? add * a.drop.scale : 0.f;
-          y[e] += add;
+          const float partner = __builtin_bit_cast(
+              float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, y[e]), 0x128, 0xF, 0xF, false));
+          y[e] = y[e] * cs[e] + sg * partner * sn[e];
         }
-        store8(po, y);
       }
+      if (ok) store8(out + (long long)t * a.cs0 + c, y);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
   }
@@ -463,7 +501,9 @@ extern "C" hipError_t lumen_lora2(int dtype, int kind, int flag, const void* big
                                   unsigned long long seed, unsigned int drop_thresh,
                                   float drop_scale, long long drop_ld, long long drop_col0,
                                   int nseg, const long long* big_off, const long long* small_off,
-                                  const long long* out_off, const int* ncols, hipStream_t st) {
+                                  const long long* out_off, const int* ncols, const float* rope_cos,
+                                  const float* rope_sin, const int* rope_pos, int rope_mask,
+                                  hipStream_t st) {
   if (nseg < 1 || nseg > 4 || split < 1 || J < 16 || J > 64 || (J & 15) || T <= 0)
     return hipErrorInvalidValue;
   lumen::lv2::Args a;
@@ -471,6 +511,8 @@ extern "C" hipError_t lumen_lora2(int dtype, int kind, int flag, const void* big
   a.alpha = alpha; a.T = T; a.J = J; a.split = split; a.drop_col0 = drop_col0;
   a.drop.seed = static_cast<unsigned int>(seed) ^ static_cast<unsigned int>(seed >> 32);
   a.drop.thresh = drop_thresh; a.drop.scale = drop_scale; a.drop.ld = drop_ld;
+  a.rope_cos = rope_cos; a.rope_sin = rope_sin; a.rope_pos = rope_pos;
+  a.rope_mask = (kind == 2 && rope_cos && rope_sin && rope_pos) ? rope_mask : 0;
   a.seg.nseg = nseg;
   int maxc = 0;
   for (int i = 0; i < 4; ++i) {

@@ -116,7 +116,12 @@ class Linear(nn.Module):
                                 device=self.weight.device)
         return self.lora
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    @property
+    def has_active_lora(self) -> bool:
+        return self.lora is not None and self.lora_enabled
+
+    def forward(self, x: torch.Tensor, rope=None) -> torch.Tensor:
+        """``rope`` (only with an active adapter on the GPU path): see ``lora_linear``."""
         lo = self.lora
         if lo is not None and self.lora_enabled:
             p = lo.dropout if self.training else 0.0
@@ -124,7 +129,9 @@ class Linear(nn.Module):
             # before recomputing, so the recomputed forward regenerates the same dropout mask
             seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
             return lora_linear(x, self.weight_fn, self.bias, lo.lora_A, lo.lora_B, lo.segs, lo.r,
-                               lo.scale, p, seed, self.weight, self._wt_fn())
+                               lo.scale, p, seed, self.weight, self._wt_fn(), rope)
+        if rope is not None:
+            raise ValueError("fused RoPE needs an active LoRA adapter on this linear")
         return linear(x, self.weight_fn, self.bias, self.weight, self._wt_fn())
 
     def _wt_fn(self):

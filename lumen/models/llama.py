@@ -41,22 +41,28 @@ class LlamaAttention(nn.Module):
     def forward(self, x2d: torch.Tensor, B: int, S: int, pos: Optional[torch.Tensor] = None):
         c = self.cfg
         nh, nkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
-        qkv = self.qkv_proj(x2d)
         cos, sin = rope_tables(D, c.max_position_embeddings, c.rope_theta, x2d.device)
-        if qkv.is_cuda and D == 128 and USE_FLASH:
-            # HIP path: RoPE in place on the fused buffer, flash attention reads q/k/v from it and
-            # writes O token-major (no split / transpose copies)
+        if x2d.is_cuda and D == 128 and USE_FLASH:
+            # HIP path: RoPE in place on the fused buffer (inside the adapter write-back when
+            # q|k are adapted), flash attention reads q/k/v from it and writes O token-major
+            # (no split / transpose copies)
             if pos is None:
                 pos = _positions(B, S, x2d.device)
-            qkv = rope_qkv_(qkv, pos, nh, nkv, D, cos, sin)
+            pos = pos.to(torch.int32).contiguous()
+            if self.qkv_proj.has_active_lora and FUSED_ROPE:
+                qkv = self.qkv_proj(x2d, rope=(pos, cos, sin, (nh + nkv) * D))
+            else:
+                qkv = rope_qkv_(self.qkv_proj(x2d), pos, nh, nkv, D, cos, sin)
             o = flash_attention_qkv(qkv, tuple(range(0, B * S + 1, S)), nh, nkv, D, True)
             return self.o_proj(o)
+        qkv = self.qkv_proj(x2d)
         q, k, v = qkv_rope_split(qkv, B, S, nh, nkv, D, cos, sin, pos)
         o = causal_attention(q, k, v)
         return self.o_proj(o)
 
 
 USE_FLASH = True
+FUSED_ROPE = True  # RoPE inside the q|k|v adapter write-back (lora_v2 UP kernel)
 _POS = {}
 
 

@@ -175,6 +175,7 @@ class _FlashAttn(torch.autograd.Function):
         k = qkv[:, nh * D:(nh + nkv) * D]
         v = qkv[:, (nh + nkv) * D:]
         dqkv = torch.empty_like(qkv)
+        dqkv._lumen_scratch = True  # fresh buffer: consumers may transform it in place
         dq = dqkv[:, :nh * D]
         dk = dqkv[:, nh * D:(nh + nkv) * D]
         dv = dqkv[:, (nh + nkv) * D:]

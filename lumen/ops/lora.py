@@ -112,12 +112,13 @@ def _split(blocks_per_split: int, reduce_len: int, chunk: int, target: int = 512
 
 
 def _lora2(kind, flag, big, small, out, cs0, cs1, alpha, T, J, split, segs4, seed=0, p=0.0,
-           drop_ld=0):
+           drop_ld=0, rope=None):
     dt = DTYPE_CODE[out.dtype if kind == 2 else big.dtype]
     native().lora2(dt, kind, flag, big, big.stride(0), small, small.stride(0), out, cs0, cs1, float(alpha), T, J, int(split),
                    int(seed) & 0x7FFFFFFFFFFFFFFF, drop_threshold(p),
                    1.0 / (1.0 - p) if p > 0 else 1.0, drop_ld, 0,
-                   [list(map(int, s)) for s in segs4])
+                   [list(map(int, s)) for s in segs4],
+                   *(rope if rope is not None else (None, None, None, 0)))
 
 
 class ZeroArena:
@@ -171,8 +172,13 @@ def _zeros(*shape, device, train: bool = False):
     return torch.zeros(*shape, device=device, dtype=torch.float32)
 
 
-def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train: bool = False):
-    """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place)."""
+def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train: bool = False,
+                    rope=None):
+    """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place).
+
+    ``rope`` = (pos int32 [T], cos, sin, ncols): also rotate columns [0, ncols) of y (q|k heads,
+    head dim 128) in the same pass when adapter segments cover exactly that range.  Returns
+    (Z, rope_done)."""
     T, K = x2d.shape
     R = A.shape[0]
     Ntot = y.shape[1]
@@ -185,15 +191,32 @@ def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train:
         _lora_gemm(act, 1, x2d, A, Z, K, K, R, 1, 1.0, [(0, 0, 0, T, R, K)],
                    _ksplit(T, R, K, _bn(R)), seed, p, K)
     if _v2_ok(r, R, x2d, y) and all(s[0] % 8 == 0 and s[1] % 8 == 0 for s in segs):
+        fuse = rope is not None and len(segs) <= 4 and _rope_covered(segs, rope[3])
         for i in range(0, len(segs), 4):
             ch = segs[i:i + 4]
+            rp = None
+            if fuse:
+                mask = sum(1 << j for j, sg in enumerate(ch) if sg[0] + sg[1] <= rope[3])
+                rp = (rope[1], rope[2], rope[0], mask)
             _lora2(2, 1, B, Z, y, y.stride(0), 1, scale, T, r, 1,
-                   [(b_off * r, r_off, n_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
-        return Z
+                   [(b_off * r, r_off, n_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
+                   rope=rp)
+        return Z, fuse
     segs6 = [(r_off, b_off * r, n_off, T, n_len, r) for (n_off, n_len, r_off, b_off) in segs]
     for i in range(0, len(segs6), 4):
         _lora_gemm(act, 6, Z, B, y, R, r, Ntot, 1, scale, segs6[i:i + 4], 1)
-    return Z
+    return Z, False
+
+
+def _rope_covered(segs, ncols: int) -> bool:
+    """Adapter segments tile [0, ncols) exactly in 128-column heads (fused RoPE precondition)."""
+    cov = sorted((s[0], s[0] + s[1]) for s in segs if s[0] < ncols)
+    cur = 0
+    for a, b in cov:
+        if a != cur or b > ncols or a % 128 or b % 128:
+            return False
+        cur = b
+    return cur == ncols
 
 
 def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed,
@@ -276,14 +299,19 @@ def _direct_ok(prm: torch.Tensor) -> bool:
 
 class _LoraLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param, wt_fn, train):
+    def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param, wt_fn, train,
+                rope):
         ctx.train = train
         W = weight_fn()
         y = torch.matmul(x2d, W.t())
         if bias is not None:
             y.add_(bias)
         # autograd runs Function.forward with grad disabled: the training flag is passed in
-        Z = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed, train=ctx.train)
+        Z, rope_done = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed, train=ctx.train,
+                                       rope=rope)
+        if rope is not None and not rope_done:
+            _rope_(y, rope, inverse=False)
+        ctx.rope = rope
         ctx.weight_fn = weight_fn
         ctx.wt_fn = wt_fn
         ctx.meta = (segs, r, scale, p, seed)
@@ -297,6 +325,13 @@ class _LoraLinear(torch.autograd.Function):
         x2d, A, B, Z = ctx.saved_tensors
         segs, r, scale, p, seed = ctx.meta
         dy = dy.contiguous()
+        if ctx.rope is not None:
+            # y was rotated in the forward: d(pre-rope) = inverse rotation of the incoming grad.
+            # In place when the grad is a scratch buffer nothing else reads (the flash-attention
+            # backward's fresh dQKV, marked), otherwise on a copy.
+            if not getattr(dy, "_lumen_scratch", False):
+                dy = dy.clone()
+            _rope_(dy, ctx.rope, inverse=True)
         dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
         _IN_BACKWARD[0] = True
         try:
@@ -306,7 +341,7 @@ class _LoraLinear(torch.autograd.Function):
             _IN_BACKWARD[0] = False
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
-        return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None
+        return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None, None
 
 
 class _Linear(torch.autograd.Function):
@@ -333,6 +368,15 @@ class _Linear(torch.autograd.Function):
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
         return dx, None, db, dw, None
+
+
+def _rope_(x2d, rope, inverse: bool):
+    """RoPE over columns [0, ncols) of x2d in place (rope = (pos, cos, sin, ncols), D = 128)."""
+    from .rope import _neg
+
+    pos, cos, sin, ncols = rope
+    native().rope_inplace(x2d, pos, cos, _neg(sin) if inverse else sin, x2d.shape[0],
+                          x2d.stride(0), ncols // 128, 128)
 
 
 def _input_grad(ctx, dy):
@@ -364,12 +408,14 @@ def _frozen(W: torch.Tensor) -> torch.Tensor:
 
 def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: torch.Tensor,
                 B: torch.Tensor, segs: List[Seg], r: int, scale: float, p: float, seed: int,
-                w_param: Optional[torch.Tensor] = None, wt_fn=None) -> torch.Tensor:
+                w_param: Optional[torch.Tensor] = None, wt_fn=None, rope=None) -> torch.Tensor:
+    """``rope`` (GPU path only) = (pos int32 [T], cos, sin, ncols): the output's columns
+    [0, ncols) come back rotated (RoPE fused into the adapter write-back when possible)."""
     shp = x.shape
     x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
     if use_native(x2d):
         y = _LoraLinear.apply(x2d.contiguous(), weight_fn, bias, A, B, segs, r, scale, p, seed,
-                              w_param, wt_fn, torch.is_grad_enabled())
+                              w_param, wt_fn, torch.is_grad_enabled(), rope)
     else:
         y = lora_linear_ref(x2d, _frozen(weight_fn()), bias, A, B, segs, r, scale, p, seed)
     return y if x.dim() == 2 else y.view(*shp[:-1], y.shape[-1])

@@ -397,3 +397,31 @@ def test_engine_lora_grad_paths_match(direct, arena, monkeypatch):
     got = run(direct, arena)
     for k in ref:
         torch.testing.assert_close(got[k], ref[k], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("nh,nkv", [(8, 8), (8, 2)])
+def test_lora_linear_fused_rope(nh, nkv):
+    """RoPE fused into the q|k adapter write-back == lora_linear followed by RoPE (fwd + grads)."""
+    from lumen.ops.lora import lora_linear
+    from lumen.ops.rope import rope_qkv_, rope_tables
+
+    D, K, T, r = 128, 512, 320, 16
+    N = (nh + 2 * nkv) * D
+    segs = [(0, nh * D, 0, 0), (nh * D, nkv * D, 16, nh * D), ((nh + nkv) * D, nkv * D, 32, (nh + nkv) * D)]
+    torch.manual_seed(0)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    A = (torch.randn(48, K, device=DEV) / math.sqrt(K)).requires_grad_(True)
+    B = (torch.randn(N, r, device=DEV) * 0.1).requires_grad_(True)
+    cos, sin = rope_tables(D, 4096, 10000.0, DEV)
+    pos = (torch.arange(T, device=DEV, dtype=torch.int32) * 7) % 1000
+    y1 = lora_linear(x, lambda: W, None, A, B, segs, r, 2.0, 0.0, 0, rope=(pos, cos, sin, (nh + nkv) * D))
+    x2, A2, B2 = (t.detach().clone().requires_grad_(True) for t in (x, A, B))
+    y2 = rope_qkv_(lora_linear(x2, lambda: W, None, A2, B2, segs, r, 2.0, 0.0, 0), pos, nh, nkv, D,
+                   cos, sin)
+    assert rel(y1, y2) < 1e-2
+    dy = torch.randn_like(y1)
+    y1.backward(dy)
+    y2.backward(dy.clone())
+    for a, b in ((x.grad, x2.grad), (A.grad, A2.grad), (B.grad, B2.grad)):
+        assert rel(a, b) < 2e-2
