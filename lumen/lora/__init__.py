@@ -102,13 +102,15 @@ def adapter_state_dict(model: nn.Module) -> Dict[str, torch.Tensor]:
     return sd
 
 
-def save_adapter(model: nn.Module, path: str, base_model_name: str = "") -> None:
+def save_adapter(model: nn.Module, path: str, base_model_name: str = "",
+                 state: Optional[Dict[str, torch.Tensor]] = None) -> None:
+    """PEFT layout; ``state`` = a precomputed (e.g. host-side snapshot) adapter_state_dict."""
     from safetensors.torch import save_file
 
     os.makedirs(path, exist_ok=True)
     cfg: LoraConfig = getattr(model, "lora_config", LoraConfig())
-    save_file(adapter_state_dict(model), os.path.join(path, "adapter_model.safetensors"),
-              metadata={"format": "pt"})
+    save_file(state if state is not None else adapter_state_dict(model),
+              os.path.join(path, "adapter_model.safetensors"), metadata={"format": "pt"})
     conf = {
         "alpha_pattern": {}, "auto_mapping": None, "base_model_name_or_path": base_model_name,
         "bias": cfg.bias, "fan_in_fan_out": False, "inference_mode": True,

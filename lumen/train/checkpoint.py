@@ -16,6 +16,12 @@ lumen writes the same directory shape with its own shard format:
         Python values only, so it loads with ``torch.load(weights_only=True)``)
     checkpoint-N/latest                                             ("global_stepN")
 Resume is resolved on EVERY rank (fixes reference quirk 7: rank-0-only discovery).
+
+``AsyncCheckpointer`` snapshots the state to host memory on the training
+thread and writes the files on a side thread; ranks signal completion with marker files, and
+rank 0 writes ``trainer_state.json`` -- the completeness marker ``latest_checkpoint`` looks
+for -- only after every rank's shard is on disk, so a crash mid-save never yields a checkpoint
+that resume would pick.  No collective runs off the training thread.
 """
 from __future__ import annotations
 
@@ -23,11 +29,13 @@ import json
 import os
 import re
 import shutil
+import threading
+import time
 from typing import Dict, Optional
 
 import torch
 
-from ..lora import load_adapter, save_adapter
+from ..lora import adapter_state_dict, load_adapter, save_adapter
 from ..parallel.dist import barrier
 
 _CKPT_RE = re.compile(r"^checkpoint-(\d+)$")
@@ -99,3 +107,76 @@ def load_checkpoint(path: str, engine, model, env) -> Dict:
             torch.cuda.set_rng_state(st["cuda"])
     with open(os.path.join(path, "trainer_state.json")) as f:
         return json.load(f)
+
+
+def _to_host(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().to("cpu", copy=True)
+    if isinstance(obj, dict):
+        return {k: _to_host(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_host(v) for v in obj)
+    return obj
+
+
+class AsyncCheckpointer:
+    """Background checkpoint writer with the same on-disk layout as ``save_checkpoint``."""
+
+    def __init__(self, timeout_s: float = 3600.0):
+        self.thread: Optional[threading.Thread] = None
+        self.error: Optional[BaseException] = None
+        self.timeout_s = timeout_s
+
+    def wait(self) -> None:
+        if self.thread is not None:
+            self.thread.join()
+            self.thread = None
+        if self.error is not None:
+            err, self.error = self.error, None
+            raise RuntimeError("asynchronous checkpoint save failed") from err
+
+    def save(self, output_dir: str, engine, model, trainer_state: Dict, env,
+             save_total_limit: Optional[int] = None, base_model_name: str = "") -> str:
+        self.wait()  # one save in flight at a time
+        step = engine.global_step
+        path = os.path.join(output_dir, f"checkpoint-{step}")
+        gs = os.path.join(path, f"global_step{step}")
+        os.makedirs(gs, exist_ok=True)
+        sd = _to_host(engine.state_dict())        # device -> host snapshot on this thread
+        rng = _rng_state()
+        adapter = {k: v.to("cpu", copy=True) for k, v in adapter_state_dict(model).items()} \
+            if env.rank == 0 else None
+        state = json.loads(json.dumps(trainer_state))
+        rank, world = env.rank, env.world_size
+
+        def work():
+            try:
+                torch.save(sd, os.path.join(gs, f"zero_pp_rank_{rank}_mp_rank_00_optim_states.pt"))
+                torch.save(rng, os.path.join(path, f"rng_state_{rank}.pth"))
+                with open(os.path.join(gs, f".done_{rank}"), "w") as f:
+                    f.write("ok")
+                if rank != 0:
+                    return
+                deadline = time.time() + self.timeout_s
+                while not all(os.path.exists(os.path.join(gs, f".done_{r}")) for r in range(world)):
+                    if time.time() > deadline:
+                        raise TimeoutError(f"ranks did not finish writing {path}")
+                    time.sleep(0.05)
+                save_adapter(model, path, base_model_name, state=adapter)
+                with open(os.path.join(path, "latest"), "w") as f:
+                    f.write(f"global_step{step}")
+                with open(os.path.join(path, "trainer_state.json"), "w") as f:
+                    json.dump(state, f, indent=2)
+                for r in range(world):
+                    os.remove(os.path.join(gs, f".done_{r}"))
+                if save_total_limit:
+                    done = [c for c in list_checkpoints(output_dir)
+                            if os.path.exists(os.path.join(c[1], "trainer_state.json"))]
+                    for _, old in done[:-save_total_limit]:
+                        shutil.rmtree(old, ignore_errors=True)
+            except BaseException as e:  # noqa: BLE001 - re-raised on the training thread
+                self.error = e
+
+        self.thread = threading.Thread(target=work, name=f"lumen-ckpt-{step}", daemon=True)
+        self.thread.start()
+        return path

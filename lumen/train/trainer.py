@@ -22,7 +22,7 @@ from ..lora import LoraConfig, apply_lora, print_trainable_parameters, save_adap
 from ..models import build_model, get_config
 from ..parallel.dist import DistEnv, all_reduce_scalar, barrier
 from ..utils.debug import StepProfiler, check_finite, maybe_inject_fault
-from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+from .checkpoint import AsyncCheckpointer, latest_checkpoint, load_checkpoint, save_checkpoint
 from .config import DSConfig
 from .engine import ZeroEngine
 
@@ -57,6 +57,7 @@ class TrainArgs:
     strategy: str = ""
     save_final: bool = True
     log_file: Optional[str] = None
+    async_save: bool = True
 
 
 def model_flops_per_token(cfg, seq_len: int, lora: bool = True) -> float:
@@ -101,6 +102,7 @@ class Trainer:
         self.collator = CausalLMCollator(pad_id=pad, max_length=args.max_length)
         self.sampler = ShardedSampler(len(self.dataset), env.rank, env.world_size, seed=args.seed)
         self.log_history: List[Dict] = []
+        self.ckpt = AsyncCheckpointer() if args.async_save else None
         self.flops_per_token = model_flops_per_token(cfg, args.max_length)
 
     # ---------------------------------------------------------------------------------------
@@ -186,6 +188,8 @@ class Trainer:
                     if (a.save_strategy == "steps" and a.save_steps > 0
                             and eng.global_step % a.save_steps == 0):
                         self._save(epoch, samples_in_epoch)
+                    if self.ckpt is not None and os.environ.get("LUMEN_FAULT_STEP"):
+                        self.ckpt.wait()  # injected crashes hit after the last save landed
                     maybe_inject_fault(eng.global_step, env.rank)
                     if eng.global_step >= total_steps:
                         done = True
@@ -197,6 +201,8 @@ class Trainer:
                 self._save(epoch + 1, 0)
             epoch += 1
         prof.close()
+        if self.ckpt is not None:
+            self.ckpt.wait()  # the last periodic checkpoint is complete before we report / exit
         if env.device.type == "cuda":
             torch.cuda.synchronize()
         elapsed = time.time() - t_start
@@ -220,10 +226,11 @@ class Trainer:
                 "train_batch_size": self.ds.train_batch_size, "args": asdict(self.args)}
 
     def _save(self, epoch: int, samples_in_epoch: int):
-        p = save_checkpoint(self.args.output_dir, self.engine, self.model,
-                            self._trainer_state(epoch, samples_in_epoch), self.env,
-                            self.args.save_total_limit, self.args.model_name)
-        self.print(f"[lumen] saved {p}")
+        save = self.ckpt.save if self.ckpt is not None else save_checkpoint
+        p = save(self.args.output_dir, self.engine, self.model,
+                 self._trainer_state(epoch, samples_in_epoch), self.env,
+                 self.args.save_total_limit, self.args.model_name)
+        self.print(f"[lumen] {'saving' if self.ckpt is not None else 'saved'} {p}")
 
     def save_final(self):
         final = os.path.join(self.args.output_dir, "final")

@@ -146,3 +146,25 @@ def test_fault_injection_kill_and_resume_matches(tmp_path):
     assert a.keys() == b.keys()
     for k in a:
         torch.testing.assert_close(a[k], b[k], rtol=0, atol=1e-6)
+
+
+def test_async_checkpoint_layout_and_resume(tmp_path):
+    """The side-thread writer produces the same layout and resumes bit-exactly."""
+    from lumen.train.checkpoint import AsyncCheckpointer
+
+    full = _trainer(str(tmp_path / "full"), 6, save_steps=100)
+    full.args.async_save = False
+    full.train()
+    ref = adapter_state_dict(full.model)
+    part = _trainer(str(tmp_path / "part"), 4, save_steps=2, limit=1)
+    assert isinstance(part.ckpt, AsyncCheckpointer)
+    part.train()
+    steps = [s for s, _ in list_checkpoints(str(tmp_path / "part"))]
+    assert steps == [4], steps
+    ck = latest_checkpoint(str(tmp_path / "part"))
+    assert not [f for f in os.listdir(os.path.join(ck, "global_step4")) if f.startswith(".done")]
+    second = _trainer(str(tmp_path / "part"), 6, resume=True, save_steps=100)
+    second.train()
+    got = adapter_state_dict(second.model)
+    for k in ref:
+        assert torch.allclose(ref[k], got[k], atol=1e-6), k
