@@ -17,6 +17,9 @@ def build_parser():
     ap.add_argument("--model", default="meta-llama/Llama-2-7b-hf",
                     help="preset / hub id (random init offline) or local HF checkpoint dir")
     ap.add_argument("--adapter", "--lora", default=None, help="PEFT LoRA adapter dir to merge")
+    ap.add_argument("--lora-modules", nargs="*", default=None, metavar="NAME=PATH",
+                    help="serve these PEFT adapters un-merged; requests pick one with 'model'")
+    ap.add_argument("--max-loras", type=int, default=4)
     ap.add_argument("--served-model-name", default=None)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
@@ -51,11 +54,12 @@ def main(argv=None):
         from lumen.serve.frontend import api_process_main
 
         mcfg = get_config(a.model)
+        lora_names = [m.split("=", 1)[0] for m in (a.lora_modules or [])]
         ctx = mp.get_context("spawn")
         req_q, out_q = ctx.Queue(), ctx.Queue()
         api = ctx.Process(target=api_process_main, name="lumen-api",
                           args=(req_q, out_q, a.model, a.max_model_len, a.host, a.port,
-                                a.served_model_name, mcfg.vocab_size), daemon=True)
+                                a.served_model_name, mcfg.vocab_size, lora_names), daemon=True)
         api.start()
 
     from lumen.parallel.dist import init
@@ -68,7 +72,9 @@ def main(argv=None):
                        max_model_len=a.max_model_len, block_size=a.block_size,
                        gpu_memory_utilization=a.gpu_memory_utilization,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_num_batched_tokens,
-                       tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs)
+                       tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs,
+                       lora_modules=dict(m.split("=", 1) for m in a.lora_modules)
+                       if a.lora_modules else None, max_loras=a.max_loras)
     eng = LLMEngine(cfg)
     if env.rank != 0:
         from lumen.serve.tp import worker_loop

@@ -117,11 +117,16 @@ def create_app(aengine, served_model_name: Optional[str] = None):
     async def health():
         return {"status": "ok"}
 
+    loras = list(getattr(aengine, "lora_names", []) or [])
+
     @app.get("/v1/models")
     async def models():
-        return {"object": "list", "data": [{"id": name, "object": "model",
-                                            "created": int(time.time()), "owned_by": "lumen",
-                                            "max_model_len": aengine.max_model_len}]}
+        now = int(time.time())
+        data = [{"id": name, "object": "model", "created": now, "owned_by": "lumen",
+                 "max_model_len": aengine.max_model_len}]
+        data += [{"id": n, "object": "model", "created": now, "owned_by": "lumen", "root": name,
+                  "parent": name, "max_model_len": aengine.max_model_len} for n in loras]
+        return {"object": "list", "data": data}
 
     @app.get("/metrics")
     async def metrics():
@@ -147,6 +152,7 @@ def create_app(aengine, served_model_name: Optional[str] = None):
 
     async def _run(prompt, params, chat: bool, stream: bool, model: str):
         rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex
+        lora = model if model in loras else None  # OpenAI "model" selects a served adapter
         created = int(time.time())
         stats.requests += 1
         obj = "chat.completion" if chat else "text_completion"
@@ -171,7 +177,7 @@ def create_app(aengine, served_model_name: Optional[str] = None):
                                  "model": model, "choices": [{"index": 0, "delta": {"role": "assistant"},
                                                               "finish_reason": None}]}
                         yield f"data: {json.dumps(first)}\n\n"
-                    async for seq in aengine.stream(prompt, params, rid):
+                    async for seq in aengine.stream(prompt, params, rid, lora):
                         last = seq
                         fin = seq.finish_reason if seq.finished else None
                         delta = detok.step(seq.output_ids)
@@ -191,7 +197,7 @@ def create_app(aengine, served_model_name: Optional[str] = None):
 
         last = None
         try:
-            async for seq in aengine.stream(prompt, params, rid):
+            async for seq in aengine.stream(prompt, params, rid, lora):
                 last = seq
         except ValueError as e:
             stats.errors += 1

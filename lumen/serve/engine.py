@@ -44,6 +44,9 @@ class EngineConfig:
     use_graphs: bool = True
     device: Optional[str] = None
     init: str = "auto"
+    # multi-LoRA serving (vLLM --enable-lora): {served name: PEFT adapter dir}, kept un-merged
+    lora_modules: Optional[Dict[str, str]] = None
+    max_loras: int = 4
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -82,6 +85,13 @@ class LLMEngine:
         self.runner = ModelRunner(self.weights, nb, cfg.block_size, dev, cfg.max_model_len,
                                   tp_group, use_graphs=cfg.use_graphs and self.tp == 1,
                                   max_graph_batch=min(256, cfg.max_num_seqs))
+        self.lora_names: List[str] = []
+        if cfg.lora_modules:
+            from .multi_lora import MultiLoRA
+
+            self.runner.lora = MultiLoRA(model.config, cfg.lora_modules, cfg.max_loras, self.rank,
+                                         self.tp, dev, dt)
+            self.lora_names = list(self.runner.lora.names)
         self._pinned: Optional[torch.Tensor] = None
         self._pinned_ready = None
         self.scheduler = Scheduler(SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,
@@ -118,7 +128,7 @@ class LLMEngine:
         return list(prompt)
 
     def add_request(self, prompt: Union[str, List[int]], params: Optional[SamplingParams] = None,
-                    request_id: Optional[str] = None) -> Sequence:
+                    request_id: Optional[str] = None, lora: Optional[str] = None) -> Sequence:
         params = params or SamplingParams()
         ids = self.encode(prompt)
         if not ids:
@@ -130,6 +140,10 @@ class LLMEngine:
         if params.max_tokens > budget:
             params.max_tokens = budget
         seq = Sequence(ids, params, request_id or uuid.uuid4().hex)
+        if lora:
+            if self.runner.lora is None or lora not in self.lora_names:
+                raise ValueError(f"unknown LoRA adapter '{lora}' (serving: {self.lora_names})")
+            seq.lora_slot = self.runner.lora.slot_of(lora)
         self.scheduler.add(seq)
         self.stats["requests"] += 1
         return seq
@@ -160,9 +174,14 @@ class LLMEngine:
                 slots.append(tbl[p // bs] * bs + p % bs)
                 cu.append(cu[-1] + n)
             T = cu[-1]
-            host = np.concatenate(toks + pos + slots)
+            extra = []
+            if self.runner.lora is not None:
+                extra = [np.repeat(np.array([s.lora_slot for s in batch.seqs], dtype=np.int64),
+                                   np.diff(np.asarray(cu)))]
+            host = np.concatenate(toks + pos + slots + extra)
             dev = self._to_device(host)
-            return StepInput("prefill", dev[:T], dev[T:2 * T].int(), dev[2 * T:3 * T], cu)
+            return StepInput("prefill", dev[:T], dev[T:2 * T].int(), dev[2 * T:3 * T], cu,
+                             lora_ids=dev[3 * T:4 * T].int() if extra else None)
         N = len(batch.seqs)
         tables = [bm.tables[s.seq_id] for s in batch.seqs]
         lens = np.fromiter((s.length for s in batch.seqs), dtype=np.int64, count=N)
@@ -173,11 +192,16 @@ class LLMEngine:
             bt[i, :len(t)] = t
         pos = lens - 1
         slots = bt[np.arange(N), pos // bs] * bs + pos % bs
-        host = np.concatenate([toks, pos, slots, lens, bt.reshape(-1)])
+        parts = [toks, pos, slots, lens, bt.reshape(-1)]
+        if self.runner.lora is not None:
+            parts.append(np.fromiter((s.lora_slot for s in batch.seqs), dtype=np.int64, count=N))
+        host = np.concatenate(parts)
         dev = self._to_device(host)
+        e = 4 * N + N * maxb
         return StepInput("decode", dev[:N], dev[N:2 * N].int(), dev[2 * N:3 * N], [],
-                         dev[4 * N:].view(N, maxb).int(), dev[3 * N:4 * N].int(),
-                         int(lens.max()))
+                         dev[4 * N:e].view(N, maxb).int(), dev[3 * N:4 * N].int(),
+                         int(lens.max()),
+                         lora_ids=dev[e:e + N].int() if self.runner.lora is not None else None)
 
     def _to_device(self, host: "np.ndarray") -> torch.Tensor:
         t = torch.from_numpy(host)
@@ -262,9 +286,9 @@ class AsyncEngine:
                 while True:
                     op = self._inbox.get_nowait()
                     if op[0] == "add":
-                        _, prompt, params, rid = op
+                        _, prompt, params, rid, lora = op
                         try:
-                            seq = eng.add_request(prompt, params, rid)
+                            seq = eng.add_request(prompt, params, rid, lora)
                             self._push(rid, ("start", seq))
                         except Exception as e:  # bad request -> report to its stream
                             self._push(rid, ("error", str(e)))
@@ -313,12 +337,17 @@ class AsyncEngine:
         loop, q = st
         loop.call_soon_threadsafe(q.put_nowait, item)
 
-    async def stream(self, prompt, params: SamplingParams, request_id: Optional[str] = None):
+    @property
+    def lora_names(self) -> List[str]:
+        return list(self.engine.lora_names)
+
+    async def stream(self, prompt, params: SamplingParams, request_id: Optional[str] = None,
+                     lora: Optional[str] = None):
         """Async generator of (sequence, new_token_count) updates until finished."""
         rid = request_id or uuid.uuid4().hex
         q: asyncio.Queue = asyncio.Queue()
         self._streams[rid] = (asyncio.get_running_loop(), q)
-        self._inbox.put(("add", prompt, params, rid))
+        self._inbox.put(("add", prompt, params, rid, lora))
         kind, payload = "start", None
         try:
             while True:

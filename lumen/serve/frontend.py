@@ -9,7 +9,8 @@ client-side inter-token latency (1.2 s vs 22 ms engine-side).  The split keeps t
 loop free of HTTP work, as vLLM's engine-core process does.
 
 Protocol (all plain tuples/lists, pickled by multiprocessing):
-  front -> core: ("add", rid, prompt_ids, params_dict, arrival) | ("abort", rid) | ("stop",)
+  front -> core: ("add", rid, prompt_ids, params_dict, arrival, lora_name|None) | ("abort", rid)
+                 | ("stop",)
   core -> front: ("step", [(rid, new_ids, new_logprobs, finish_reason|None), ...], stats)
                  ("error", rid, message)
 """
@@ -45,9 +46,9 @@ def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
             block = False
             kind = op[0]
             if kind == "add":
-                _, rid, ids, pdict, arrival = op
+                _, rid, ids, pdict, arrival, lora = op
                 try:
-                    seq = engine.add_request(ids, SamplingParams(**pdict), rid)
+                    seq = engine.add_request(ids, SamplingParams(**pdict), rid, lora)
                     seq.arrival = arrival
                     live[rid] = seq
                     sent[rid] = 0
@@ -120,8 +121,9 @@ class EngineCoreClient:
     engine core in another process."""
 
     def __init__(self, req_q, out_q, tokenizer, model_name: str, max_model_len: int,
-                 eos_id: Optional[int]):
+                 eos_id: Optional[int], lora_names: Optional[List[str]] = None):
         self.req_q, self.out_q = req_q, out_q
+        self.lora_names = list(lora_names or [])
         self.tokenizer = tokenizer
         self.model_name = model_name
         self.max_model_len = max_model_len
@@ -156,7 +158,8 @@ class EngineCoreClient:
                 if st is not None:
                     st[0].call_soon_threadsafe(_deliver, [(st[1], ("error", msg[2]))])
 
-    async def stream(self, prompt, params: SamplingParams, request_id: Optional[str] = None):
+    async def stream(self, prompt, params: SamplingParams, request_id: Optional[str] = None,
+                     lora: Optional[str] = None):
         rid = request_id or uuid.uuid4().hex
         ids = self.tokenizer.encode(prompt) if isinstance(prompt, str) else list(prompt)
         if not ids:
@@ -167,7 +170,7 @@ class EngineCoreClient:
         q: asyncio.Queue = asyncio.Queue()
         self._streams[rid] = (asyncio.get_running_loop(), q)
         view = SeqView(ids, rid, time.perf_counter())
-        self.req_q.put(("add", rid, ids, dataclasses.asdict(params), view.arrival))
+        self.req_q.put(("add", rid, ids, dataclasses.asdict(params), view.arrival, lora))
         try:
             while True:
                 kind, payload = await q.get()
@@ -198,7 +201,8 @@ def _deliver(items):
 
 
 def api_process_main(req_q, out_q, model: str, max_model_len: int, host: str, port: int,
-                     served_model_name: Optional[str], vocab_size: int) -> None:
+                     served_model_name: Optional[str], vocab_size: int,
+                     lora_names: Optional[List[str]] = None) -> None:
     """Entry point of the spawned HTTP process (no GPU)."""
     import os
 
@@ -218,6 +222,7 @@ def api_process_main(req_q, out_q, model: str, max_model_len: int, host: str, po
 
     tok = load_tokenizer(model, vocab_size)
     eos = getattr(tok, "eos_token_id", None)
-    client = EngineCoreClient(req_q, out_q, tok, served_model_name or model, max_model_len, eos)
+    client = EngineCoreClient(req_q, out_q, tok, served_model_name or model, max_model_len, eos,
+                              lora_names)
     app = create_app(client, served_model_name)
     uvicorn.run(app, host=host, port=port, log_level="warning")

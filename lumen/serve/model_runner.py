@@ -93,6 +93,7 @@ class StepInput:
     block_tables: Optional[torch.Tensor] = None  # decode [N, maxb] int32
     context_lens: Optional[torch.Tensor] = None  # decode [N] int32
     max_context: int = 0
+    lora_ids: Optional[torch.Tensor] = None      # [T] int32 adapter slot per token (multi-LoRA)
 
 
 def kv_bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2, tp_size: int = 1) -> int:
@@ -128,6 +129,7 @@ class ModelRunner:
         self._graphs: Dict[int, tuple] = {}
         self._graph_pool = None
         self.partition = 512
+        self.lora = None  # serve.multi_lora.MultiLoRA when adapters are served un-merged
 
     # ------------------------------------------------------------------------------------------
     def _allreduce(self, x):
@@ -135,14 +137,18 @@ class ModelRunner:
             dist.all_reduce(x, group=self.tp_group)
         return x
 
-    def _layers(self, h, positions, slots, attn_fn):
+    def _layers(self, h, positions, slots, attn_fn, lora_ids=None):
         cfg = self.cfg
         res = None
         T = h.shape[0]
         D = cfg.head_dim
+        ml = self.lora if lora_ids is not None else None
+        masks = {n: ml.mask(lora_ids, n) for n in (1, 2, 3)} if ml is not None else None
         for i, L in enumerate(self.w.layers):
             y, res = rms_norm(h, L.ln1, cfg.rms_norm_eps, res)
             qkv = torch.matmul(y, L.qkv.t())
+            if ml is not None:
+                ml.apply(i, "qkv", y, qkv, masks)
             rope_inplace(qkv, positions, self.w.nh + self.w.nkv, D, self.cos, self.sin)
             qs, ks = self.q_size, self.kv_size
             k = qkv[:, qs:qs + ks].view(T, self.w.nkv, D)
@@ -150,8 +156,16 @@ class ModelRunner:
             write_kv_cache(k, v, self.k_cache[i], self.v_cache[i], slots)
             o = attn_fn(qkv, i)
             a = self._allreduce(torch.matmul(o, L.o.t()))
+            if ml is not None:
+                ml.apply(i, "o", o, a, masks, self.tp_group, self.tp)
             y2, res = rms_norm(a, L.ln2, cfg.rms_norm_eps, res)
-            h = self._allreduce(torch.matmul(swiglu(torch.matmul(y2, L.gate_up.t())), L.down.t()))
+            gu = torch.matmul(y2, L.gate_up.t())
+            if ml is not None:
+                ml.apply(i, "gate_up", y2, gu, masks)
+            act = swiglu(gu)
+            h = self._allreduce(torch.matmul(act, L.down.t()))
+            if ml is not None:
+                ml.apply(i, "down", act, h, masks, self.tp_group, self.tp)
         return h, res
 
     def _vocab_gather(self, logits):
@@ -205,12 +219,13 @@ class ModelRunner:
                 outs.append(o[0].transpose(0, 1).reshape(n, nh * D))
             return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
 
-        h, res = self._layers(h, inp.positions, inp.slots, attn)
+        h, res = self._layers(h, inp.positions, inp.slots, attn, inp.lora_ids)
         last = torch.tensor([c - 1 for c in cu[1:]], device=h.device)
         return self._logits(h, res, last)
 
     # ---- decode: one token per sequence ----------------------------------------------------
-    def _decode_eager(self, tokens, positions, slots, block_tables, context_lens, max_context):
+    def _decode_eager(self, tokens, positions, slots, block_tables, context_lens, max_context,
+                      lora_ids=None):
         h = F.embedding(tokens, self.w.embed)
         N = tokens.shape[0]
         nh, D = self.w.nh, self.cfg.head_dim
@@ -220,7 +235,7 @@ class ModelRunner:
             return paged_decode(q, self.k_cache[i], self.v_cache[i], block_tables, context_lens,
                                 max_context, self.scale, self.partition).view(N, nh * D)
 
-        h, res = self._layers(h, positions, slots, attn)
+        h, res = self._layers(h, positions, slots, attn, lora_ids)
         y, _ = rms_norm(h, self.w.norm, self.cfg.rms_norm_eps, res)
         return self._vocab_gather(torch.matmul(y, self.w.lm_head.t()))
 
@@ -229,7 +244,7 @@ class ModelRunner:
         N = inp.tokens.shape[0]
         if not self.use_graphs or N > self.graph_buckets[-1]:
             return self._decode_eager(inp.tokens, inp.positions, inp.slots, inp.block_tables,
-                                      inp.context_lens, inp.max_context)
+                                      inp.context_lens, inp.max_context, inp.lora_ids)
         bucket = next(b for b in self.graph_buckets if b >= N)
         g = self._graphs.get(bucket)
         if g is None:
@@ -241,6 +256,8 @@ class ModelRunner:
         nb = inp.block_tables.shape[1]
         st["block_tables"][:N, :nb].copy_(inp.block_tables)
         st["context_lens"][:N].copy_(inp.context_lens)
+        if self.lora is not None:
+            st["lora_ids"][:N].copy_(inp.lora_ids)
         if N < bucket:  # padding rows: no cache write, one-token context on block 0
             st["slots"][N:].fill_(-1)
             st["context_lens"][N:].fill_(1)
@@ -254,8 +271,10 @@ class ModelRunner:
               "slots": torch.full((bucket,), -1, dtype=torch.long, device=dev),
               "block_tables": torch.zeros(bucket, self.max_blocks, dtype=torch.int32, device=dev),
               "context_lens": torch.ones(bucket, dtype=torch.int32, device=dev)}
+        if self.lora is not None:
+            st["lora_ids"] = torch.zeros(bucket, dtype=torch.int32, device=dev)
         args = (st["tokens"], st["positions"], st["slots"], st["block_tables"],
-                st["context_lens"], self.max_model_len)
+                st["context_lens"], self.max_model_len, st.get("lora_ids"))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

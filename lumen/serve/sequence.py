@@ -53,6 +53,7 @@ class Sequence:
     token_times: List[float] = field(default_factory=list)
     num_cached: int = 0          # tokens whose K/V are in the cache
     preemptions: int = 0
+    lora_slot: int = 0           # multi-LoRA serving: adapter slot (0 = base model)
 
     @property
     def all_ids(self) -> List[int]:

@@ -34,6 +34,9 @@ def pack_step(inp: Optional[StepInput], device) -> None:
         N, nb = inp.block_tables.shape
         parts += [inp.block_tables.long().reshape(-1), inp.context_lens.long()]
         hdr[:5] = torch.tensor([KIND["decode"], T, N, nb, inp.max_context])
+    if inp.lora_ids is not None:  # multi-LoRA: per-token adapter slots ride at the end
+        parts.append(inp.lora_ids.long())
+        hdr[5] = 1
     payload = torch.cat(parts)
     hdr[7] = payload.numel()
     dist.broadcast(hdr, src=0)
@@ -51,13 +54,14 @@ def recv_step(device) -> Optional[StepInput]:
     T = h[1]
     tok, pos, slots = payload[:T], payload[T:2 * T].int(), payload[2 * T:3 * T]
     rest = payload[3 * T:]
+    lora = payload[-T:].int() if h[5] else None
     if h[0] == KIND["prefill"]:
         cu = rest[:h[2]].tolist()
-        return StepInput("prefill", tok, pos, slots, cu)
+        return StepInput("prefill", tok, pos, slots, cu, lora_ids=lora)
     N, nb, maxc = h[2], h[3], h[4]
     bt = rest[:N * nb].view(N, nb).int()
     cl = rest[N * nb:N * nb + N].int()
-    return StepInput("decode", tok, pos, slots, [], bt, cl, maxc)
+    return StepInput("decode", tok, pos, slots, [], bt, cl, maxc, lora_ids=lora)
 
 
 def worker_loop(runner) -> None:

@@ -40,7 +40,7 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
     shutdown()
 
 
-def serve_tp_worker(rank, world, port, outdir):
+def serve_tp_worker(rank, world, port, outdir, loras=None):
     """TP serving on gloo: rank 0 runs the engine, rank 1 the worker loop; greedy outputs of
     rank 0 are saved for comparison with a single-process engine."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -56,12 +56,16 @@ def serve_tp_worker(rank, world, port, outdir):
     init(device="cpu")
     model = _tp_test_model()
     cfg = EngineConfig(model="tiny-llama-gqa", device="cpu", max_model_len=128, block_size=4,
-                       use_graphs=False, num_blocks=128, tp_size=world)
+                       use_graphs=False, num_blocks=128, tp_size=world, lora_modules=loras)
     eng = LLMEngine(cfg, model=model)
     if rank == 0:
         prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
-        seqs = eng.generate(prompts, SamplingParams(max_tokens=8, temperature=0.0,
-                                                    ignore_eos=True))
+        sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+        names = list(loras or {}) + [None] * 3
+        seqs = [eng.add_request(p, SamplingParams(**vars(sp)), lora=names[i])
+                for i, p in enumerate(prompts)]
+        while any(not s.finished for s in seqs):
+            eng.step()
         eng.shutdown()
         torch.save([s.output_ids for s in seqs], os.path.join(outdir, "tp_out.pt"))
     else:
