@@ -363,8 +363,9 @@ def test_transpose_2d(shape):
     torch.testing.assert_close(transpose_2d(x), x.t().contiguous(), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("direct,arena", [(False, False), (True, True)])
-def test_engine_lora_grad_paths_match(direct, arena, monkeypatch):
+@pytest.mark.parametrize("direct,arena,ckpt", [(False, False, False), (True, True, False),
+                                               (True, True, True)])
+def test_engine_lora_grad_paths_match(direct, arena, ckpt, monkeypatch):
     """Direct .grad accumulation + zero arena give the same training trajectory as the plain
     path (adapter grads returned to autograd, torch.zeros scratch)."""
     import lumen.ops.lora as lora_mod
@@ -374,12 +375,13 @@ def test_engine_lora_grad_paths_match(direct, arena, monkeypatch):
     from lumen.train.config import load_ds_config
     from lumen.train.engine import ZeroEngine
 
-    def run(direct_, arena_):
+    def run(direct_, arena_, ckpt_=False):
         monkeypatch.setattr(lora_mod, "DIRECT_GRAD", direct_)
         monkeypatch.setattr(lora_mod, "USE_ARENA", arena_)
         torch.manual_seed(0)
-        m = build_model("tiny-llama", dtype=torch.bfloat16, device=torch.device("cuda"), seed=3)
+        m = build_model("small-llama", dtype=torch.bfloat16, device=torch.device("cuda"), seed=3)
         apply_lora(m, LoraConfig(r=16, lora_dropout=0.1))
+        m.gradient_checkpointing = ckpt_
         m.train()
         env = init()
         ds = load_ds_config({"zero_optimization": {"stage": 1}}, 2, 2, 1, 1e-3)
@@ -394,7 +396,7 @@ def test_engine_lora_grad_paths_match(direct, arena, monkeypatch):
         return adapter_state_dict(m)
 
     ref = run(False, False)
-    got = run(direct, arena)
+    got = run(direct, arena, ckpt)
     for k in ref:
         torch.testing.assert_close(got[k], ref[k], rtol=1e-3, atol=1e-5)
 
