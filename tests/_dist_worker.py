@@ -85,3 +85,30 @@ def _tp_test_model():
                 p.mul_(5.0)
     m.eval()
     return m
+
+
+def eval_worker(rank, world, port, outdir):
+    """Data-parallel evaluate_loss on a fixed tiny model; rank 0 writes the result."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import json
+
+    import torch
+    import torch.distributed as dist
+
+    torch.set_num_threads(1)
+    from lumen.data.collator import CausalLMCollator
+    from lumen.data.datasets import SyntheticTokenDataset
+    from lumen.eval import evaluate_loss
+    from lumen.models import build_model
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = build_model("tiny-llama", dtype=torch.float32, device=torch.device("cpu"), seed=3)
+    ds = SyntheticTokenDataset(7, 24, m.config.vocab_size, seed=5, min_len=8)
+    res = evaluate_loss(m, ds, CausalLMCollator(pad_id=2), batch_size=2, rank=rank, world=world)
+    if rank == 0:
+        with open(os.path.join(outdir, f"eval_w{world}.json"), "w") as f:
+            json.dump(res, f)
+    if world > 1:
+        dist.destroy_process_group()
