@@ -49,6 +49,18 @@ hipError_t lumen_flash_attn(int, int, int, int, const void*, const void*, const 
                             long long, long long, void*, long long, float*, const int*, const int*,
                             int, int, int, int, float, const void*, long long, void*, void*, void*,
                             long long, long long, long long, const float*, hipStream_t);
+long long lumen_car_signal_bytes();
+int lumen_car_max_blocks();
+int lumen_car_max_ranks();
+hipError_t lumen_car_alloc(long long, int, void**);
+hipError_t lumen_car_free(void*);
+hipError_t lumen_car_get_handle(void*, void*);
+int lumen_car_handle_bytes();
+hipError_t lumen_car_open_handle(const void*, void**);
+hipError_t lumen_car_close_handle(void*);
+hipError_t lumen_car_read_err(void*, unsigned int*);
+hipError_t lumen_car_allreduce(int, const long long*, const long long*, int, int, const void*,
+                               void*, long long, int, int, double, hipStream_t);
 void lumen_cpu_adamw(float*, const float*, float*, float*, long long, float, float, float, float,
                      float, float, float, float);
 int lumen_cpu_has_avx512();
@@ -323,6 +335,54 @@ void cpu_adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
 
 }  // namespace
 
+// ---- custom all-reduce (kernels/custom_ar.hip): raw device pointers travel as Python ints
+int64_t car_alloc(int64_t bytes, bool cached) {
+  void* p = nullptr;
+  check(lumen_car_alloc(bytes, cached ? 1 : 0, &p), "car_alloc");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void car_free(int64_t p) { check(lumen_car_free(reinterpret_cast<void*>(p)), "car_free"); }
+
+py::bytes car_handle(int64_t p) {
+  std::string h(lumen_car_handle_bytes(), '\0');
+  check(lumen_car_get_handle(reinterpret_cast<void*>(p), h.data()), "car_handle");
+  return py::bytes(h);
+}
+
+int64_t car_open(const py::bytes& handle) {
+  std::string h = handle;
+  if ((int)h.size() != lumen_car_handle_bytes()) throw std::invalid_argument("lumen: bad IPC handle");
+  void* p = nullptr;
+  check(lumen_car_open_handle(h.data(), &p), "car_open");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void car_close(int64_t p) { check(lumen_car_close_handle(reinterpret_cast<void*>(p)), "car_close"); }
+
+int64_t car_err(int64_t sig) {
+  unsigned int e = 0;
+  check(lumen_car_read_err(reinterpret_cast<void*>(sig), &e), "car_err");
+  return e;
+}
+
+void car_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>& sig, int rank,
+                   const at::Tensor& in, at::Tensor& out, bool two_shot, int blocks,
+                   double timeout_s) {
+  need_cuda(in, "in");
+  need_cuda(out, "out");
+  const int world = (int)data.size();
+  if ((int)sig.size() != world || rank < 0 || rank >= world)
+    throw std::invalid_argument("lumen: car_allreduce peer tables do not match");
+  if (in.numel() != out.numel() || in.scalar_type() != out.scalar_type() || (in.numel() & 7))
+    throw std::invalid_argument("lumen: car_allreduce needs same-shape tensors with numel % 8 == 0");
+  std::vector<long long> d(data.begin(), data.end()), s(sig.begin(), sig.end());
+  check(lumen_car_allreduce(dcode(in), d.data(), s.data(), rank, world, in.data_ptr(),
+                            out.data_ptr(), in.numel(), two_shot ? 1 : 0, blocks, timeout_s,
+                            cur_stream()),
+        "car_allreduce");
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "lumen native ops for MI355X (gfx950)";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
@@ -340,6 +400,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("reshape_and_cache", &reshape_and_cache);
   m.def("sample", &sample);
   m.def("flash_attn", &flash_attn);
+  m.def("car_alloc", &car_alloc);
+  m.def("car_free", &car_free);
+  m.def("car_handle", &car_handle);
+  m.def("car_open", &car_open);
+  m.def("car_close", &car_close);
+  m.def("car_err", &car_err);
+  m.def("car_allreduce", &car_allreduce);
+  m.def("car_signal_bytes", &lumen_car_signal_bytes);
+  m.def("car_max_blocks", &lumen_car_max_blocks);
+  m.def("car_max_ranks", &lumen_car_max_ranks);
   m.def("cpu_adamw", &cpu_adamw);
   m.def("cpu_has_avx512", &lumen_cpu_has_avx512);
 }

@@ -82,9 +82,18 @@ class LLMEngine:
         self.weights = ServeWeights(model, self.rank, self.tp)
         nb = cfg.num_blocks or self._auto_blocks(dt)
         self.blocks = BlockManager(nb, cfg.block_size)
+        car = None
+        if self.tp > 1 and dev.type == "cuda":
+            # TP decode: row-parallel sums on the custom IPC all-reduce, which also lets the
+            # decode buckets be captured in hipGraphs (collective: every rank builds it here)
+            from ..parallel.custom_ar import maybe_custom_allreduce
+
+            esz = torch.empty((), dtype=dt).element_size()
+            car = maybe_custom_allreduce(
+                tp_group, dev, max(8 << 20, min(256, cfg.max_num_seqs) * model.config.hidden_size * esz))
         self.runner = ModelRunner(self.weights, nb, cfg.block_size, dev, cfg.max_model_len,
-                                  tp_group, use_graphs=cfg.use_graphs and self.tp == 1,
-                                  max_graph_batch=min(256, cfg.max_num_seqs))
+                                  tp_group, use_graphs=cfg.use_graphs,
+                                  max_graph_batch=min(256, cfg.max_num_seqs), custom_ar=car)
         self.lora_names: List[str] = []
         if cfg.lora_modules:
             from .multi_lora import MultiLoRA

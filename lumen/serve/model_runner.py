@@ -103,7 +103,7 @@ def kv_bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2, tp_size: int = 1)
 class ModelRunner:
     def __init__(self, weights: ServeWeights, num_blocks: int, block_size: int,
                  device: torch.device, max_model_len: int = 4096, tp_group=None,
-                 use_graphs: bool = True, max_graph_batch: int = 256):
+                 use_graphs: bool = True, max_graph_batch: int = 256, custom_ar=None):
         self.w = weights
         self.cfg = weights.cfg
         self.device = device
@@ -123,9 +123,19 @@ class ModelRunner:
         self.cos, self.sin = rope_tables(D, max(cfg.max_position_embeddings, max_model_len),
                                          cfg.rope_theta, device)
         self.scale = 1.0 / math.sqrt(D)
-        self.use_graphs = use_graphs and device.type == "cuda"
-        self.graph_buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 96, 128, 160, 192, 224, 256)
-                              if b <= max_graph_batch]
+        # TP: row-parallel sums go through the custom all-reduce (IPC peer memory, one kernel,
+        # graph-capturable) when it is up; RCCL otherwise (and then decode runs eagerly)
+        self.car = custom_ar
+        self.use_graphs = (use_graphs and device.type == "cuda"
+                           and (self.tp == 1 or self.car is not None))
+        buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 96, 128, 160, 192, 224, 256)
+                   if b <= max_graph_batch]
+        if self.tp > 1 and self.car is not None:
+            # a captured bucket may only hold custom all-reduces (RCCL cannot be captured)
+            row_bytes = cfg.hidden_size * torch.empty((), dtype=dt).element_size()
+            buckets = [b for b in buckets if b * row_bytes <= self.car.max_bytes]
+        self.graph_buckets = buckets
+        self.use_graphs = self.use_graphs and bool(buckets)
         self._graphs: Dict[int, tuple] = {}
         self._graph_pool = None
         self.partition = 512
@@ -134,7 +144,10 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------------
     def _allreduce(self, x):
         if self.tp > 1:
-            dist.all_reduce(x, group=self.tp_group)
+            if self.car is not None and self.car.eligible(x):
+                self.car.all_reduce(x)
+            else:
+                dist.all_reduce(x, group=self.tp_group)
         return x
 
     def _layers(self, h, positions, slots, attn_fn, lora_ids=None):
@@ -157,7 +170,7 @@ class ModelRunner:
             o = attn_fn(qkv, i)
             a = self._allreduce(torch.matmul(o, L.o.t()))
             if ml is not None:
-                ml.apply(i, "o", o, a, masks, self.tp_group, self.tp)
+                ml.apply(i, "o", o, a, masks, self._allreduce)
             y2, res = rms_norm(a, L.ln2, cfg.rms_norm_eps, res)
             gu = torch.matmul(y2, L.gate_up.t())
             if ml is not None:
@@ -165,7 +178,7 @@ class ModelRunner:
             act = swiglu(gu)
             h = self._allreduce(torch.matmul(act, L.down.t()))
             if ml is not None:
-                ml.apply(i, "down", act, h, masks, self.tp_group, self.tp)
+                ml.apply(i, "down", act, h, masks, self._allreduce)
         return h, res
 
     def _vocab_gather(self, logits):
@@ -225,7 +238,7 @@ class ModelRunner:
 
     # ---- decode: one token per sequence ----------------------------------------------------
     def _decode_eager(self, tokens, positions, slots, block_tables, context_lens, max_context,
-                      lora_ids=None):
+                      lora_ids=None, gather: bool = True):
         h = F.embedding(tokens, self.w.embed)
         N = tokens.shape[0]
         nh, D = self.w.nh, self.cfg.head_dim
@@ -237,7 +250,8 @@ class ModelRunner:
 
         h, res = self._layers(h, positions, slots, attn, lora_ids)
         y, _ = rms_norm(h, self.w.norm, self.cfg.rms_norm_eps, res)
-        return self._vocab_gather(torch.matmul(y, self.w.lm_head.t()))
+        logits = torch.matmul(y, self.w.lm_head.t())
+        return self._vocab_gather(logits) if gather else logits
 
     @torch.no_grad()
     def decode(self, inp: StepInput) -> torch.Tensor:
@@ -262,7 +276,8 @@ class ModelRunner:
             st["slots"][N:].fill_(-1)
             st["context_lens"][N:].fill_(1)
         graph.replay()
-        return out[:N]
+        # the vocab-parallel gather (RCCL) stays outside the graph
+        return self._vocab_gather(out[:N])
 
     def _capture(self, bucket: int):
         dev = self.device
@@ -274,7 +289,7 @@ class ModelRunner:
         if self.lora is not None:
             st["lora_ids"] = torch.zeros(bucket, dtype=torch.int32, device=dev)
         args = (st["tokens"], st["positions"], st["slots"], st["block_tables"],
-                st["context_lens"], self.max_model_len, st.get("lora_ids"))
+                st["context_lens"], self.max_model_len, st.get("lora_ids"), False)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

@@ -21,10 +21,9 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import torch
-import torch.distributed as dist
 
 _HF = {"q": "self_attn.q_proj", "k": "self_attn.k_proj", "v": "self_attn.v_proj",
        "o": "self_attn.o_proj", "gate": "mlp.gate_proj", "up": "mlp.up_proj",
@@ -128,14 +127,16 @@ class MultiLoRA:
         return (cs[None, :] == ids.to(torch.int32)[:, None]).to(self.dtype)
 
     def apply(self, layer: int, proj: str, x: torch.Tensor, y: torch.Tensor, masks: dict,
-              tp_group=None, tp: int = 1) -> None:
-        """y += (x A^T * mask) B^T for one projection (in place); no-op when absent."""
+              allreduce: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> None:
+        """y += (x A^T * mask) B^T for one projection (in place); no-op when absent.
+        ``allreduce`` sums the row-parallel partial Z over the TP group (the runner's: custom
+        all-reduce inside graphs, RCCL otherwise)."""
         p = self.layers[layer].get(proj)
         if p is None:
             return
         z = torch.matmul(x, p.A.t())
-        if p.row_parallel and tp > 1:
-            dist.all_reduce(z, group=tp_group)
+        if p.row_parallel and allreduce is not None:
+            allreduce(z)
         nseg = p.A.shape[0] // (self.slots * self.r)
         z.mul_(masks[nseg])
         y.add_(torch.matmul(z, p.B.t()))

@@ -112,3 +112,88 @@ def eval_worker(rank, world, port, outdir):
             json.dump(res, f)
     if world > 1:
         dist.destroy_process_group()
+
+
+def car_worker(rank, world, port, outdir):
+    """Custom all-reduce on ONE GPU shared by `world` processes (gloo only exchanges the IPC
+    handles): every dtype / size / one-shot / two-shot / graph case checked bit-exactly against
+    the same f32 sum in rank order, computed on the host."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import json
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lumen.parallel.custom_ar import CustomAllReduce
+
+    dev = torch.device("cuda", 0)
+    car = CustomAllReduce(dist.group.WORLD, dev, max_bytes=4 << 20, timeout_s=20.0)
+    res = {"cases": [], "timing_us": {}}
+
+    def inputs(case, n, dt):
+        xs = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * case + q)).to(dt)
+              for q in range(world)]
+        acc = xs[0].float()
+        for q in range(1, world):
+            acc = acc + xs[q].float()
+        return xs[rank], acc.to(dt)
+
+    case = 0
+    for dt, n in ((torch.bfloat16, 8), (torch.bfloat16, 4096), (torch.float32, 12345 * 8),
+                  (torch.float16, 65536), (torch.bfloat16, 1 << 20), (torch.float32, 8 * 1001)):
+        for two in (False, True):
+            for blocks in (None, 1, 7):
+                case += 1
+                x, want = inputs(case, n, dt)
+                xd = x.to(dev)
+                inplace = case % 2 == 0
+                out = xd if inplace else torch.empty_like(xd)
+                car.all_reduce(xd, out=out, two_shot=two, blocks=blocks)
+                got = out.cpu()
+                bad = int((got.float() != want.float()).sum())
+                res["cases"].append({"dtype": str(dt), "n": n, "two_shot": two, "blocks": blocks,
+                                     "inplace": inplace, "mismatches": bad})
+    # hipGraph capture + replay with new inputs each time
+    n = 65536
+    xs = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    ys = torch.empty_like(xs)
+    xs.fill_(1.0)
+    car.all_reduce(xs, out=ys)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            car.all_reduce(xs, out=ys)
+    graph_bad = 0
+    for it in range(3):
+        case += 1
+        x, want = inputs(case, n, torch.bfloat16)
+        xs.copy_(x.to(dev))
+        g.replay()
+        graph_bad += int((ys.cpu().float() != want.float()).sum())
+    res["graph_mismatches"] = graph_bad
+    # latency on a shared GPU (not an xGMI number: both ranks sit on one device)
+    for nbytes in (8 << 10, 256 << 10, 2 << 20):
+        t = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=dev)
+        for _ in range(5):
+            car.all_reduce(t)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(50):
+            car.all_reduce(t)
+        torch.cuda.synchronize()
+        res["timing_us"][str(nbytes)] = (time.perf_counter() - t0) / 50 * 1e6
+    car.check()
+    res["err"] = 0
+    dist.barrier()
+    car.close()
+    if rank == 0:
+        with open(os.path.join(outdir, "car.json"), "w") as f:
+            json.dump(res, f)
+    dist.destroy_process_group()
