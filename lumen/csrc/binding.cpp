@@ -61,6 +61,8 @@ hipError_t lumen_car_close_handle(void*);
 hipError_t lumen_car_read_err(void*, unsigned int*);
 hipError_t lumen_car_allreduce(int, const long long*, const long long*, int, int, const void*,
                                void*, long long, int, int, double, hipStream_t);
+hipError_t lumen_car_allgather(int, const long long*, const long long*, int, int, const void*,
+                               void*, long long, long long, int, double, hipStream_t);
 void lumen_cpu_adamw(float*, const float*, float*, float*, long long, float, float, float, float,
                      float, float, float, float);
 int lumen_cpu_has_avx512();
@@ -360,6 +362,22 @@ int64_t car_open(const py::bytes& handle) {
 
 void car_close(int64_t p) { check(lumen_car_close_handle(reinterpret_cast<void*>(p)), "car_close"); }
 
+void car_allgather(const std::vector<int64_t>& data, const std::vector<int64_t>& sig, int rank,
+                   const at::Tensor& in, at::Tensor& out, int blocks, double timeout_s) {
+  need_cuda(in, "in");
+  need_cuda(out, "out");
+  const int world = (int)data.size();
+  if ((int)sig.size() != world || rank < 0 || rank >= world || in.dim() != 2 || out.dim() != 2)
+    throw std::invalid_argument("lumen: car_allgather needs 2-D tensors and matching peer tables");
+  if (out.size(0) != in.size(0) || out.size(1) != in.size(1) * world || (in.size(1) & 7) ||
+      in.scalar_type() != out.scalar_type())
+    throw std::invalid_argument("lumen: car_allgather shapes: in [R, Vs], out [R, W*Vs], Vs % 8 == 0");
+  std::vector<long long> d(data.begin(), data.end()), s(sig.begin(), sig.end());
+  check(lumen_car_allgather(dcode(in), d.data(), s.data(), rank, world, in.data_ptr(),
+                            out.data_ptr(), in.size(0), in.size(1), blocks, timeout_s, cur_stream()),
+        "car_allgather");
+}
+
 int64_t car_err(int64_t sig) {
   unsigned int e = 0;
   check(lumen_car_read_err(reinterpret_cast<void*>(sig), &e), "car_err");
@@ -407,6 +425,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("car_close", &car_close);
   m.def("car_err", &car_err);
   m.def("car_allreduce", &car_allreduce);
+  m.def("car_allgather", &car_allgather);
   m.def("car_signal_bytes", &lumen_car_signal_bytes);
   m.def("car_max_blocks", &lumen_car_max_blocks);
   m.def("car_max_ranks", &lumen_car_max_ranks);

@@ -158,6 +158,44 @@ allreduce_kernel(Peers P, const T* __restrict__ in, T* __restrict__ out, long lo
   if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
 }
 
+// All-gather of row-major shards: rank q holds in[R, Vs]; out[R, W*Vs] gets shard q in columns
+// [q*Vs, (q+1)*Vs) on every rank (the vocab-parallel LM head's logits).  Same staging buffers
+// and barriers as the all-reduce; the interleaving into `out` is done by the stores, so no
+// separate concatenation pass is needed.  vs8 = Vs / 8.
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+allgather_kernel(Peers P, const T* __restrict__ in, T* __restrict__ out, long long rows, int vs8,
+                 int rank, int world, uint64_t deadline_ticks) {
+  Signal* self = P.sig[rank];
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  const long long n8 = rows * vs8;
+  const int G = gridDim.x;
+  const long long lo = n8 * blockIdx.x / G, hi = n8 * (blockIdx.x + 1) / G;
+  T* mine = reinterpret_cast<T*>(P.data[rank]);
+  for (long long u = lo + threadIdx.x; u < hi; u += kThreads) {
+    float v[8];
+    load8<T>(in + u * 8, v);
+    store8<T>(mine + u * 8, v);
+  }
+  block_barrier(P, self, 0, rank, world, epoch, deadline_ticks);
+  const long long ld = (long long)world * vs8 * 8;
+  for (int k = 0; k < world; ++k) {
+    const int q = (rank + k) % world;
+    const T* theirs = reinterpret_cast<const T*>(P.data[q]);
+    for (long long u = lo + threadIdx.x; u < hi; u += kThreads) {
+      const long long r = u / vs8, c = u - r * vs8;
+      float v[8];
+      load8<T>(theirs + u * 8, v);
+      store8<T>(out + r * ld + (long long)q * vs8 * 8 + c * 8, v);
+    }
+  }
+  block_barrier(P, self, 2, rank, world, epoch, deadline_ticks);
+  if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
+}
+
 template <typename T, int W>
 hipError_t launch_w(const Peers& P, const void* in, void* out, long long n8, int rank, int world,
                     int two_shot, int blocks, uint64_t ticks, hipStream_t st) {
@@ -240,6 +278,36 @@ hipError_t lumen_car_allreduce(int dtype, const long long* data, const long long
     case 2: return launch<bf16>(P, in, out, numel, rank, world, two_shot, blocks, timeout_s, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t lumen_car_allgather(int dtype, const long long* data, const long long* sig, int rank,
+                               int world, const void* in, void* out, long long rows,
+                               long long shard_cols, int blocks, double timeout_s, hipStream_t st) {
+  if (world < 1 || world > kMaxRanks || blocks < 1 || blocks > kMaxBlocks || (shard_cols & 7))
+    return hipErrorInvalidValue;
+  Peers P{};
+  for (int i = 0; i < world; ++i) {
+    P.data[i] = reinterpret_cast<void*>(data[i]);
+    P.sig[i] = reinterpret_cast<Signal*>(sig[i]);
+  }
+  const uint64_t ticks = (uint64_t)(timeout_s * 1.0e8);
+  const int vs8 = (int)(shard_cols / 8);
+  switch (dtype) {
+    case 0:
+      hipLaunchKernelGGL(allgather_kernel<float>, dim3(blocks), dim3(kThreads), 0, st, P,
+                         (const float*)in, (float*)out, rows, vs8, rank, world, ticks);
+      break;
+    case 1:
+      hipLaunchKernelGGL(allgather_kernel<fp16>, dim3(blocks), dim3(kThreads), 0, st, P,
+                         (const fp16*)in, (fp16*)out, rows, vs8, rank, world, ticks);
+      break;
+    case 2:
+      hipLaunchKernelGGL(allgather_kernel<bf16>, dim3(blocks), dim3(kThreads), 0, st, P,
+                         (const bf16*)in, (bf16*)out, rows, vs8, rank, world, ticks);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 }  // extern "C"

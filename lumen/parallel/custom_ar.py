@@ -139,6 +139,24 @@ class CustomAllReduce:
         self.calls += 1
         return out
 
+    def gather_eligible(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dim() == 2 and t.dtype in _DTYPES and t.is_contiguous()
+                and t.shape[1] % 8 == 0 and 0 < t.numel() * t.element_size() <= self.max_bytes)
+
+    def all_gather_cols(self, t: torch.Tensor, out: Optional[torch.Tensor] = None,
+                        blocks: Optional[int] = None) -> torch.Tensor:
+        """[R, Vs] shards -> [R, W*Vs] with rank q's shard in columns q*Vs .. (q+1)*Vs."""
+        if not self.gather_eligible(t):
+            raise ValueError(f"tensor not eligible for the custom all-gather: {tuple(t.shape)}")
+        R, Vs = t.shape
+        if out is None:
+            out = torch.empty(R, Vs * self.world, dtype=t.dtype, device=t.device)
+        units = t.numel() // 8
+        nb = blocks if blocks is not None else max(1, min(self.max_blocks, -(-units // 512)))
+        self.C.car_allgather(self.data, self.sig, self.rank, t, out, int(nb), self.timeout_s)
+        self.calls += 1
+        return out
+
     def check(self) -> None:
         """Raise if any barrier of this rank timed out (a peer never arrived).  Syncs."""
         err = self.C.car_err(self._sig)

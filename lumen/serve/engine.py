@@ -89,8 +89,11 @@ class LLMEngine:
             from ..parallel.custom_ar import maybe_custom_allreduce
 
             esz = torch.empty((), dtype=dt).element_size()
+            rows = min(256, cfg.max_num_seqs)
+            vshard = model.config.vocab_size // self.tp
             car = maybe_custom_allreduce(
-                tp_group, dev, max(8 << 20, min(256, cfg.max_num_seqs) * model.config.hidden_size * esz))
+                tp_group, dev, max(8 << 20, rows * model.config.hidden_size * esz,
+                                   rows * vshard * esz))
         self.runner = ModelRunner(self.weights, nb, cfg.block_size, dev, cfg.max_model_len,
                                   tp_group, use_graphs=cfg.use_graphs,
                                   max_graph_batch=min(256, cfg.max_num_seqs), custom_ar=car)

@@ -136,6 +136,12 @@ class ModelRunner:
             buckets = [b for b in buckets if b * row_bytes <= self.car.max_bytes]
         self.graph_buckets = buckets
         self.use_graphs = self.use_graphs and bool(buckets)
+        # the vocab gather joins the graph when every bucket's logits shard fits the staging
+        # buffer (then a decode step is one graph replay; otherwise an RCCL gather follows it)
+        self._graph_gathers = self.tp == 1 or self.w.vocab_shard == cfg.vocab_size or (
+            self.car is not None and self.w.vocab_shard % 8 == 0
+            and max(buckets or [1]) * self.w.vocab_shard * torch.empty((), dtype=dt).element_size()
+            <= self.car.max_bytes)
         self._graphs: Dict[int, tuple] = {}
         self._graph_pool = None
         self.partition = 512
@@ -186,6 +192,8 @@ class ModelRunner:
         if self.tp == 1 or self.w.vocab_shard == self.cfg.vocab_size:
             return logits
         R, Vs = logits.shape
+        if self.car is not None and self.car.gather_eligible(logits):
+            return self.car.all_gather_cols(logits.contiguous())
         if logits.is_cuda:
             buf = torch.empty(self.tp, R, Vs, dtype=logits.dtype, device=logits.device)
             dist.all_gather_into_tensor(buf, logits.contiguous(), group=self.tp_group)
@@ -276,7 +284,9 @@ class ModelRunner:
             st["slots"][N:].fill_(-1)
             st["context_lens"][N:].fill_(1)
         graph.replay()
-        # the vocab-parallel gather (RCCL) stays outside the graph
+        if self._graph_gathers:
+            return out[:N]
+        # the vocab-parallel gather stays outside the graph when it would need RCCL
         return self._vocab_gather(out[:N])
 
     def _capture(self, bucket: int):
@@ -289,7 +299,7 @@ class ModelRunner:
         if self.lora is not None:
             st["lora_ids"] = torch.zeros(bucket, dtype=torch.int32, device=dev)
         args = (st["tokens"], st["positions"], st["slots"], st["block_tables"],
-                st["context_lens"], self.max_model_len, st.get("lora_ids"), False)
+                st["context_lens"], self.max_model_len, st.get("lora_ids"), self._graph_gathers)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

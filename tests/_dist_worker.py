@@ -197,3 +197,87 @@ def car_worker(rank, world, port, outdir):
         with open(os.path.join(outdir, "car.json"), "w") as f:
             json.dump(res, f)
     dist.destroy_process_group()
+
+
+def serve_tp_gpu_worker(rank, world, port, outdir):
+    """TP=2 serving with both ranks on the ONE GPU (gloo carries the step broadcast and the
+    vocab gather; the row-parallel sums take the custom IPC all-reduce, so decode buckets run
+    as hipGraphs).  Rank 0 saves greedy outputs + which paths were active."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
+    import torch
+
+    from lumen.parallel.dist import init, shutdown
+    from lumen.serve.engine import EngineConfig, LLMEngine
+    from lumen.serve.sequence import SamplingParams
+    from lumen.serve.tp import worker_loop
+
+    init(backend="gloo", device="cuda")
+    model = _tp_test_model().to("cuda")
+    model = model.to(torch.bfloat16)  # the paged-KV kernels are 16-bit
+    cfg = EngineConfig(model="tiny-llama-gqa", device="cuda:0", dtype="bf16", max_model_len=128,
+                       block_size=16, use_graphs=True, num_blocks=64, tp_size=world,
+                       max_num_seqs=8)
+    eng = LLMEngine(cfg, model=model)
+    info = {"car": eng.runner.car is not None, "graphs": eng.runner.use_graphs}
+    if rank == 0:
+        prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
+        sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+        seqs = [eng.add_request(p, SamplingParams(**vars(sp))) for p in prompts]
+        while any(not s.finished for s in seqs):
+            eng.step()
+        eng.shutdown()
+        info["captured"] = sorted(eng.runner._graphs)
+        info["car_calls"] = eng.runner.car.calls if eng.runner.car is not None else 0
+        eng.runner.car.check()
+        torch.save({"out": [s.output_ids for s in seqs], "info": info},
+                   os.path.join(outdir, "tp_gpu_out.pt"))
+    else:
+        worker_loop(eng.runner)
+    shutdown()
+
+
+def car_gather_worker(rank, world, port, outdir):
+    """Custom column all-gather ([R, Vs] shards -> [R, W*Vs]) on one shared GPU, incl. graph."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import json
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lumen.parallel.custom_ar import CustomAllReduce
+
+    dev = torch.device("cuda", 0)
+    car = CustomAllReduce(dist.group.WORLD, dev, max_bytes=2 << 20, timeout_s=20.0)
+    bad = 0
+    for i, (R, Vs, dt, blocks) in enumerate(((1, 8, torch.bfloat16, None), (3, 256, torch.float32, 5),
+                                             (37, 4000, torch.bfloat16, None),
+                                             (256, 2000, torch.float16, 128))):
+        shards = [torch.randn(R, Vs, generator=torch.Generator().manual_seed(100 * i + q)).to(dt)
+                  for q in range(world)]
+        want = torch.cat(shards, 1)
+        got = car.all_gather_cols(shards[rank].to(dev), blocks=blocks).cpu()
+        bad += int((got != want).sum())
+    x = torch.zeros(16, 512, dtype=torch.bfloat16, device=dev)
+    car.all_gather_cols(x)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(torch.cuda.Stream()):
+        with torch.cuda.graph(g):
+            y = car.all_gather_cols(x)
+    for it in range(2):
+        shards = [torch.full((16, 512), float(10 * it + q), dtype=torch.bfloat16)
+                  for q in range(world)]
+        x.copy_(shards[rank].to(dev))
+        g.replay()
+        bad += int((y.cpu() != torch.cat(shards, 1)).sum())
+    car.check()
+    dist.barrier()
+    car.close()
+    if rank == 0:
+        with open(os.path.join(outdir, "gather.json"), "w") as f:
+            json.dump({"mismatches": bad}, f)
+    dist.destroy_process_group()

@@ -10,7 +10,7 @@ import socket
 import pytest
 import torch.multiprocessing as mp
 
-from tests._dist_worker import car_worker
+from tests._dist_worker import car_gather_worker, car_worker
 
 pytestmark = pytest.mark.gpu
 
@@ -28,3 +28,44 @@ def test_custom_allreduce_two_processes_one_gpu(tmp_path):
     assert res["graph_mismatches"] == 0
     assert res["err"] == 0
     print("custom all-reduce latency on a shared GPU (us):", res["timing_us"])
+
+
+def test_custom_allgather_columns(tmp_path):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(car_gather_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    assert json.loads((tmp_path / "gather.json").read_text())["mismatches"] == 0
+
+
+def test_tp2_serving_on_one_gpu_matches_single_process(tmp_path):
+    """TP=2 engine + worker on the same GPU (bf16): custom all-reduce + graph-captured decode
+    follow the un-sharded f32 model's greedy choice (teacher-forced, so one bf16 near-tie
+    cannot derail the rest of a sequence)."""
+    import torch
+
+    from tests._dist_worker import _tp_test_model, serve_tp_gpu_worker
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(serve_tp_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    got = torch.load(tmp_path / "tp_gpu_out.pt", weights_only=True)
+    info = got["info"]
+    assert info["car"] and info["graphs"] and info["captured"], info
+    assert info["car_calls"] > 0
+    ref_model = _tp_test_model()
+    prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
+    agree, total = 0, 0
+    for p, out in zip(prompts, got["out"]):
+        assert len(out) == 8
+        with torch.no_grad():
+            logits = ref_model(torch.tensor(p + out)[None]).float().reshape(len(p) + 8, -1)
+        pred = logits.argmax(-1)[len(p) - 1:len(p) - 1 + 8].tolist()
+        assert pred[0] == out[0], (p, pred, out)
+        agree += sum(int(a == b) for a, b in zip(pred, out))
+        total += 8
+    assert agree / total >= 0.85, (agree, total)
