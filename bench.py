@@ -140,6 +140,8 @@ def main():
 
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
+    coord = engine.coordinator
+    gb0 = coord.gathered_bytes if coord else 0
     t1 = time.perf_counter()
     loss = run_steps(args.steps, args.warmup)
     sync()
@@ -192,7 +194,9 @@ def main():
                 "peak_mem_gb_rank0": round(peak_gb, 2),
                 "final_loss": round(final_loss, 4),
                 "setup_s": round(setup_s, 1),
-                "zero3_keep_gathered": bool(engine.coordinator.keep) if engine.coordinator else None,
+                "zero3_schedule": coord.schedule if coord else None,
+                "zero3_gathered_gb_per_step": (round((coord.gathered_bytes - gb0) / 1e9
+                                                     / args.steps, 2) if coord else 0.0),
                 "baseline_tok_s": BASELINE_TOK_S,
                 "gemm_algos": gemm_table,
                 "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,

@@ -93,6 +93,9 @@ class Linear(nn.Module):
         if not self.transpose_bwd or W.requires_grad:
             return None
         if getattr(W, "_lumen_gathered", False):
+            wt = getattr(W, "_lumen_wt", None)  # transposed by the ZeRO-3 coordinator off-path
+            if wt is not None:
+                return wt
             return transpose_2d(W.detach()) if self.transpose_gathered else None
         key = (W.data_ptr(), tuple(W.shape), W.dtype)
         if self._wt is None or self._wt_key != key:

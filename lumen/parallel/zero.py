@@ -164,6 +164,35 @@ class FlatTrainable:
 # ZeRO-3 parameter coordinator (frozen/base weights)
 # ================================================================================================
 
+class _LocalGather:
+    """World-1 stand-in for an async ``all_gather_into_tensor`` (the shard IS the whole unit):
+    a copy on a side stream ordered after the issuing stream, with ``wait()`` making the
+    current stream wait on it -- the same stream semantics ProcessGroupNCCL gives, so the
+    coordinator's schedule can be exercised on one GPU (``LUMEN_ZERO3_SINGLE=1``)."""
+
+    _stream = None
+
+    def __init__(self, out: torch.Tensor, shard: torch.Tensor):
+        if out.is_cuda:
+            if _LocalGather._stream is None:
+                _LocalGather._stream = torch.cuda.Stream(device=out.device)
+            s = _LocalGather._stream
+            s.wait_stream(torch.cuda.current_stream(out.device))
+            with torch.cuda.stream(s):
+                out.copy_(shard, non_blocking=True)
+                self.ev = torch.cuda.Event()
+                self.ev.record(s)
+            shard.record_stream(s)
+            out.record_stream(s)
+        else:
+            out.copy_(shard)
+            self.ev = None
+
+    def wait(self):
+        if self.ev is not None:
+            torch.cuda.current_stream().wait_event(self.ev)
+
+
 class _Unit:
     def __init__(self, idx):
         self.idx = idx
@@ -171,28 +200,51 @@ class _Unit:
         self.deps: List[int] = []
         self.numel = 0
         self.padded = 0
-        self.shard: Optional[torch.Tensor] = None     # [padded / W] (device, or pinned host)
-        self.full: Optional[torch.Tensor] = None      # [padded] gathered (device)
-        self.work = None
-        self.state = "released"                       # released | inflight | ready
+        self.shard: Optional[torch.Tensor] = None      # [padded / W] (device, or pinned host)
+        self.bufs: List[Optional[torch.Tensor]] = []   # per slot: [padded] gathered (device)
+        self.works: List[Optional[object]] = []
+        self.states: List[str] = []                    # per slot: empty | inflight | ready
+        self.bound = -1                                # slot the params currently view, or -1
         self.dtype = None
+        # W^T copies made off the critical path (keep / pipelined): (param idx, off, wt_off)
+        self.tn: List[tuple] = []
+        self.wt_numel = 0
+        self.wt_bufs: List[Optional[torch.Tensor]] = []
+        self.wt_events: List[Optional[object]] = []
 
 
 class ParamCoordinator:
     """Gathers / releases ZeRO-3 partitioned units around the model's unit loop.
 
     The model calls ``pre_forward(i)`` / ``post_forward(i, out)``; gradient hooks on unit outputs
-    call ``pre_backward(i)``.  All collectives are ``all_gather_into_tensor`` on the process
-    group's RCCL stream; the compute stream waits on them only right before the unit runs.
+    call ``pre_backward(i)`` (before unit i's backward runs); the engine calls
+    ``end_micro_step()`` after ``loss.backward()``.  Every gather is one
+    ``all_gather_into_tensor`` of a unit's shards on the process group's RCCL stream; the compute
+    stream waits on it only right before the unit runs.  The shards are the only persistent copy
+    of the frozen weights: every micro-step re-materialises every unit over xGMI.
+
+    Schedules (chosen from ``stage3_max_live_parameters``, DeepSpeed's live-parameter budget):
+
+    * ``release`` (budget < model): gather before use, prefetch the next ``depth`` units, free
+      after the forward, gather again for the backward (DeepSpeed's schedule).
+    * ``keep`` (model <= budget < 2x model): one buffer per unit, gathered once per micro-step
+      and kept from the forward through the backward.  As soon as unit i's backward has run,
+      its buffer is re-gathered for the next micro-step (the frozen values cannot change in
+      between), so the next step's gathers overlap this step's backward.
+    * ``pipelined`` (budget >= 2x model, the 7B-on-288 GB case): two buffers per unit; the
+      whole next micro-step's gathers are issued, in forward order, when the current one
+      starts, so one step of compute hides one step of xGMI traffic.  This is what makes
+      2-4 GPU ZeRO-3 compute-bound: a 2-GPU all-gather of 6.3 GB crosses ONE xGMI link.
     """
 
     def __init__(self, model: nn.Module, env: DistEnv, persistence_threshold: int,
                  max_live: int, prefetch_numel: int, offload_param: bool = False,
-                 pin_memory: bool = True):
+                 pin_memory: bool = True, schedule: Optional[str] = None):
         self.env = env
         self.model = model
         self.offload = offload_param
         W = env.world_size
+        self.local = not (dist.is_available() and dist.is_initialized()) and W == 1
         mark_zero_shapes(model)
         units_mods = model.zero_units()
         owner: Dict[int, int] = {}
@@ -241,8 +293,23 @@ class ParamCoordinator:
                 p.data = torch.empty(0, dtype=u.dtype, device=p.device)
                 p._lumen_gathered = True  # storage swapped per gather: no derived caches
         self.total_numel = total
-        self.keep = total <= max_live   # whole model fits the live budget: gather once per micro-step
-        # prefetch depth: upcoming units whose gathered size fits the prefetch bucket (>= 1)
+        if schedule is None:
+            schedule = ("pipelined" if 2 * total <= max_live else
+                        "keep" if total <= max_live else "release")
+        assert schedule in ("release", "keep", "pipelined"), schedule
+        self.schedule = schedule
+        self.keep = schedule != "release"
+        n_slots = 2 if schedule == "pipelined" else 1
+        for u in self.units:
+            u.bufs = [None] * n_slots
+            u.works = [None] * n_slots
+            u.states = ["empty"] * n_slots
+            u.wt_bufs = [None] * n_slots
+            u.wt_events = [None] * n_slots
+        self._tstream = None
+        self.transposed_numel = 0
+        self.slot = 0
+        # prefetch depth (release mode): upcoming units whose gathered size fits the bucket
         sizes = [u.padded for u in self.units if u.padded]
         avg = (sum(sizes) / len(sizes)) if sizes else 1
         self.depth = max(1, int(prefetch_numel // max(avg, 1)))
@@ -251,75 +318,183 @@ class ParamCoordinator:
         self.last = len(self.units) - 1
         self.device = env.device
         self._bwd_seen = set()
-        self.gathered_bytes = 0
+        self._in_step = False
+        self.gathered_bytes = 0    # bytes materialised by gathers (all ranks' shards)
+        self.gathers = 0
 
-    # ---- gather / release ----------------------------------------------------------------
-    def _issue(self, i: int):
+    # ---- gather / bind / release ------------------------------------------------------------
+    def _issue(self, i: int, slot: Optional[int] = None):
         if i < 0 or i > self.last:
             return
+        slot = self.slot if slot is None else slot
         u = self.units[i]
         for d in u.deps:
-            self._issue(d)
-        if not u.params or u.state != "released":
+            self._issue(d, slot)
+        if not u.params or u.states[slot] != "empty":
             return
-        if u.full is None:
-            u.full = torch.empty(u.padded, dtype=u.dtype, device=self.device)
+        if u.bufs[slot] is None:
+            u.bufs[slot] = torch.empty(u.padded, dtype=u.dtype, device=self.device)
         shard = u.shard
         if self.offload:
             shard = shard.to(self.device, non_blocking=True)
-        u.work = dist.all_gather_into_tensor(u.full, shard, async_op=True)
-        self.gathered_bytes += u.padded * u.full.element_size()
-        u.state = "inflight"
+        if self.local:
+            u.works[slot] = _LocalGather(u.bufs[slot], shard)
+        else:
+            u.works[slot] = dist.all_gather_into_tensor(u.bufs[slot], shard, async_op=True)
+        self.gathered_bytes += u.padded * u.bufs[slot].element_size()
+        self.gathers += 1
+        u.states[slot] = "inflight"
+        if u.tn:
+            self._transpose_after_gather(u, slot)
+
+    def _transpose_after_gather(self, u: _Unit, slot: int):
+        """On a side stream: wait for the gather, write W^T of the unit's projections (for the
+        backward's TN input-gradient GEMMs).  Overlaps compute instead of sitting in the
+        backward; the compute stream waits on the event only when it binds the unit."""
+        from ..ops.transpose import transpose_2d
+
+        cur = torch.cuda.current_stream(self.device)
+        if self._tstream is None:
+            self._tstream = torch.cuda.Stream(device=self.device)
+        side = self._tstream
+        if u.wt_bufs[slot] is None:
+            u.wt_bufs[slot] = torch.empty(u.wt_numel, dtype=u.dtype, device=self.device)
+        side.wait_stream(cur)      # earlier readers of this slot's W^T are done
+        with torch.cuda.stream(side):
+            u.works[slot].wait()   # side stream waits on the collective
+            full, wt = u.bufs[slot], u.wt_bufs[slot]
+            for k, off, wt_off in u.tn:
+                rows, cols = u.params[k]._zero_shape
+                transpose_2d(full[off:off + rows * cols].view(rows, cols),
+                             out=wt[wt_off:wt_off + rows * cols].view(cols, rows))
+            ev = torch.cuda.Event()
+            ev.record(side)
+        u.wt_events[slot] = ev
+
+    def enable_transposes(self, params: Sequence[nn.Parameter]) -> int:
+        """Keep W^T of these gathered weights next to the gathered buffer (keep / pipelined
+        schedules, when HBM allows: one more copy of the projections per slot).  Returns the
+        number of weights covered."""
+        if self.schedule == "release" or self.device.type != "cuda":
+            return 0
+        want = {id(p) for p in params}
+        need = 0
+        plan = []
+        for u in self.units:
+            tn, o, wo = [], 0, 0
+            for k, p in enumerate(u.params):
+                shape = p._zero_shape
+                n = math.prod(shape)
+                if (id(p) in want and len(shape) == 2 and shape[0] % 8 == 0
+                        and shape[1] % 8 == 0 and p.dtype in (torch.bfloat16, torch.float16)):
+                    tn.append((k, o, wo))
+                    wo += n
+                o += n
+            plan.append((u, tn, wo))
+            need += wo * (u.dtype.itemsize if u.dtype is not None else 2) * len(u.bufs)
+        free, total = torch.cuda.mem_get_info(self.device)
+        # the gathered buffers themselves are not allocated yet: keep room for them and for
+        # activations (max(48 GiB, 25% of HBM))
+        gathered = sum(u.padded * u.dtype.itemsize for u in self.units if u.params) * len(
+            self.units[0].bufs)
+        if need + gathered > free - max(48 * 2**30, 0.25 * total):
+            return 0
+        n = 0
+        for u, tn, wo in plan:
+            u.tn, u.wt_numel = tn, wo
+            n += len(tn)
+            self.transposed_numel += wo
+        return n
 
     def _wait(self, i: int):
+        """Make unit i's params view the current slot's gathered buffer."""
         u = self.units[i]
         for d in u.deps:
             self._wait(d)
         if not u.params:
             return
-        if u.state == "released":
-            self._issue(i)
-        if u.state == "inflight":
-            u.work.wait()
-            u.work = None
+        s = self.slot
+        if u.states[s] == "empty":
+            self._issue(i, s)
+        if u.states[s] == "inflight":
+            u.works[s].wait()
+            u.works[s] = None
+            u.states[s] = "ready"
+        if u.bound != s:
             o = 0
+            full = u.bufs[s]
             for p in u.params:
                 shape = p._zero_shape
                 n = math.prod(shape)
-                p.data = u.full[o:o + n].view(shape)
+                p.data = full[o:o + n].view(shape)
                 o += n
-            u.state = "ready"
+            if u.tn:
+                if u.wt_events[s] is not None:
+                    torch.cuda.current_stream(self.device).wait_event(u.wt_events[s])
+                    u.wt_events[s] = None
+                wt = u.wt_bufs[s]
+                for k, off, wt_off in u.tn:
+                    rows, cols = u.params[k]._zero_shape
+                    u.params[k]._lumen_wt = wt[wt_off:wt_off + rows * cols].view(cols, rows)
+            u.bound = s
+
+    def _unbind(self, u: _Unit):
+        if u.bound >= 0:
+            for p in u.params:
+                p.data = torch.empty(0, dtype=u.dtype, device=p.device)
+                p._lumen_wt = None
+            u.bound = -1
 
     def _release(self, i: int):
+        """Drop unit i's current-slot contents (release schedule: free the memory too)."""
         if i < 0 or i > self.last:
             return
         u = self.units[i]
-        if not u.params or u.state == "released":
+        if not u.params:
             return
-        if u.state == "inflight":
-            u.work.wait()
-            u.work = None
-        for p in u.params:
-            p.data = torch.empty(0, dtype=u.dtype, device=p.device)
-        if not self.keep:
-            u.full = None  # return memory to the caching allocator (stream-ordered)
-        u.state = "released"
+        s = self.slot
+        if u.states[s] == "inflight":
+            u.works[s].wait()
+            u.works[s] = None
+        self._unbind(u)
+        if self.schedule == "release":
+            u.bufs[s] = None  # return memory to the caching allocator (stream-ordered)
+        u.states[s] = "empty"
+
+    def _refresh(self, i: int):
+        """keep schedule: unit i is done for this micro-step -> re-gather it for the next one
+        into the same buffer (issued after the compute that read it, on the RCCL stream)."""
+        if i < 1 or i > self.last:
+            return
+        u = self.units[i]
+        if not u.params or u.states[self.slot] != "ready":
+            return
+        self._release(i)
+        self._issue(i)
 
     # ---- model hooks ------------------------------------------------------------------------
     def begin_micro_step(self):
         self._bwd_seen.clear()
-        for i in range(min(self.depth, self.last + 1)):
-            self._issue(i)
+        self._in_step = True
+        if self.schedule == "pipelined":
+            for i in range(self.last + 1):
+                self._issue(i, self.slot)
+            for i in range(self.last + 1):
+                self._issue(i, 1 - self.slot)  # next micro-step, behind this one's
+        else:
+            for i in range(min(self.depth, self.last + 1)):
+                self._issue(i)
 
     def pre_forward(self, i: int):
-        if i == 0:
+        if i == 0 and not self._in_step:
             self.begin_micro_step()
         self._wait(i)
-        for j in range(i + 1, min(i + 1 + self.depth, self.last + 1)):
-            self._issue(j)
+        if self.schedule != "pipelined":
+            for j in range(i + 1, min(i + 1 + self.depth, self.last + 1)):
+                self._issue(j)
 
     def post_forward(self, i: int, out):
-        if not self.keep and i != self.last:
+        if self.schedule == "release" and i != self.last:
             self._release(i)
         if torch.is_grad_enabled():
             tensors = out if isinstance(out, (tuple, list)) else (out,)
@@ -337,21 +512,45 @@ class ParamCoordinator:
         return hook
 
     def pre_backward(self, i: int):
+        """Runs when the gradient of unit i's output is complete, i.e. after unit i+1's backward
+        and before unit i's."""
         if i in self._bwd_seen:
             return
+        if not self._bwd_seen:
+            # first hook of this backward: close the micro-step when the whole pass is done
+            # (unit 1's backward runs after the last hook fires)
+            torch.autograd.Variable._execution_engine.queue_callback(self.end_micro_step)
         self._bwd_seen.add(i)
-        if not self.keep:
+        if self.schedule == "release":
             self._release(i + 1)
+        elif self.schedule == "keep":
+            self._refresh(i + 1)
         self._wait(i)
-        for j in range(i - 1, max(i - 1 - self.depth, -1), -1):
-            if j >= 1:  # unit 0 (embedding) has no backward
-                self._issue(j)
-        if i <= 1:
-            self.end_micro_step()
+        if self.schedule == "release":
+            for j in range(i - 1, max(i - 1 - self.depth, -1), -1):
+                if j >= 1:  # unit 0 (embedding) has no backward
+                    self._issue(j)
 
     def end_micro_step(self):
-        for i in range(self.last + 1):
-            self._release(i)
+        """After the backward (or a no-grad forward): nothing of this micro-step is read any
+        more.  Idempotent (the autograd callback and the engine both call it)."""
+        if not self._in_step:
+            return
+        self._in_step = False
+        if self.schedule == "keep":
+            for i in range(self.last + 1):  # units without a backward, then unit 1
+                u = self.units[i]
+                if u.params and u.states[self.slot] == "ready":
+                    self._release(i)
+                    self._issue(i)
+        elif self.schedule == "pipelined":
+            for u in self.units:
+                self._unbind(u)
+                u.states[self.slot] = "empty"   # re-gathered (for micro-step t+2) at t+1's start
+            self.slot = 1 - self.slot
+        else:
+            for i in range(self.last + 1):
+                self._release(i)
 
     def gather_all_full(self) -> None:
         """Materialise every unit (checkpoint save with gather_16bit_weights_on_model_save)."""
@@ -360,7 +559,18 @@ class ParamCoordinator:
             self._wait(i)
 
     def release_all(self):
-        self.end_micro_step()
+        for i in range(self.last + 1):
+            self._release(i)
+        self._in_step = False
+
+    def drain(self):
+        """Complete every in-flight gather (all slots): before process-group teardown."""
+        for u in self.units:
+            for s, w in enumerate(u.works):
+                if w is not None:
+                    w.wait()
+                    u.works[s] = None
+                    u.states[s] = "ready"
 
 
 def mark_zero_shapes(model: nn.Module):

@@ -14,6 +14,7 @@ Engine API (DeepSpeed-like):
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -73,16 +74,31 @@ class ZeroEngine:
             raise ValueError("model has no trainable parameters")
         # ZeRO-3: partition frozen weights first (trainable adapters stay persistent)
         self.coordinator: Optional[ParamCoordinator] = None
-        if self.stage >= 3 and W > 1:
+        # LUMEN_ZERO3_SINGLE=1 partitions at world size 1 too (a one-rank "gather" is a copy on
+        # a side stream): runs the coordinator's schedules on a single-GPU box
+        single = os.environ.get("LUMEN_ZERO3_SINGLE", "0") == "1"
+        if self.stage >= 3 and (W > 1 or single):
             self.coordinator = ParamCoordinator(
                 model, env, cfg.stage3_param_persistence_threshold,
                 cfg.stage3_max_live_parameters, cfg.stage3_prefetch_bucket_size,
-                offload_param=cfg.offload_param == "cpu", pin_memory=cfg.offload_param_pin)
+                offload_param=cfg.offload_param == "cpu", pin_memory=cfg.offload_param_pin,
+                schedule=os.environ.get("LUMEN_ZERO3_SCHEDULE") or None)
             model.coordinator = self.coordinator
         if self.device.type == "cuda":
             from ..models.layers import configure_backward_layout
 
             configure_backward_layout(model)  # TN input-gradient GEMMs for persistent weights
+            # ... and, opt-in, for gathered ones: W^T written on a side stream after each gather.
+            # Measured on one GPU (forced partitioning, profiles/r02_zero3): the side-stream
+            # transposes' HBM traffic costs the compute stream about what the TN GEMMs save
+            # (110.3 vs 109.8 ms/step), so the default keeps on-the-fly q|k|v / down transposes.
+            if (self.coordinator is not None
+                    and os.environ.get("LUMEN_ZERO3_OFFPATH_WT", "0") == "1"):
+                from ..models.layers import Linear
+
+                self.coordinator.enable_transposes(
+                    [m.weight for m in model.modules() if isinstance(m, Linear)
+                     and m.transpose_bwd and getattr(m.weight, "_lumen_gathered", False)])
         bucket = cfg.reduce_bucket_size if self.stage >= 1 else int(2.5e7)
         self.flat = FlatTrainable(trainable, env, max(bucket, 1), self.device)
         # broadcast adapter init from rank 0 (only the trainable 32 MiB, not 13.5 GB)

@@ -1,0 +1,12 @@
+#!/bin/bash
+# ZeRO-3 coordinator schedules on one GPU (forced partitioning), bench with local gathers
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/s2_r3; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_zero3_gpu.py -x -v --timeout 300 --timeout-method thread > $O/zero3_tests.log 2>&1
+rc=$?; echo "zero3 gpu tests rc=$rc"; grep -E "PASS|FAIL|Error|error" $O/zero3_tests.log | tail -20; [ $rc -eq 0 ] || exit $rc
+for sch in pipelined keep; do
+  LUMEN_ZERO3_SINGLE=1 LUMEN_ZERO3_SCHEDULE=$sch timeout -k 10 300 python bench.py --steps 8 --warmup 3 > $O/bench_single_$sch.log 2>&1
+  rc=$?; echo "bench single $sch rc=$rc"; tail -1 $O/bench_single_$sch.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc
+done

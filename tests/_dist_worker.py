@@ -18,6 +18,11 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
     from lumen.train.config import load_ds_config
     from lumen.train.trainer import TrainArgs, Trainer
 
+    saved_env = {k: os.environ.get(k) for k in ("LUMEN_ZERO3_SCHEDULE", "LUMEN_ZERO3_SINGLE")}
+    if extra and extra.get("schedule"):
+        os.environ["LUMEN_ZERO3_SCHEDULE"] = extra["schedule"]
+    if extra and extra.get("single"):
+        os.environ["LUMEN_ZERO3_SINGLE"] = "1"
     env = init(device="cpu")
     raw = {"zero_optimization": {"stage": stage, "reduce_bucket_size": 3000,
                                  "stage3_param_persistence_threshold": 100,
@@ -30,9 +35,18 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
                   per_device_train_batch_size=micro, gradient_accumulation_steps=accum,
                   max_steps=steps, logging_steps=1, lora_r=4, lora_dropout=0.0,
                   save_strategy="no", save_final=False, output_dir=os.path.join(outdir, "ck"),
-                  seed=7)
-    t = Trainer(a, ds, env, printer=lambda *x, **k: None)
-    res = t.train()
+                  seed=7, gradient_checkpointing=bool((extra or {}).get("gc", False)))
+    try:
+        t = Trainer(a, ds, env, printer=lambda *x, **k: None)
+        res = t.train()
+        if extra and extra.get("single"):
+            assert t.engine.coordinator is not None
+    finally:
+        for k, v in saved_env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     if rank == 0:
         sd = adapter_state_dict(t.model)
         torch.save({"sd": sd, "losses": [r["loss"] for r in t.log_history], "res": res},

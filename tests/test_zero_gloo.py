@@ -66,6 +66,27 @@ def test_zero3_release_mode_and_accumulation(tmp_path):
     _close(r["sd"], ref["sd"])
 
 
+@pytest.mark.parametrize("schedule,gc", [("keep", False), ("keep", True), ("pipelined", True),
+                                         ("release", True)])
+def test_zero3_schedules_accumulation_checkpointing(schedule, gc, tmp_path):
+    """Every ZeRO-3 gather schedule (keep: re-gather after each unit's backward; pipelined:
+    next micro-step gathered one step ahead into a second buffer; release) with gradient
+    accumulation, with and without activation checkpointing == single process."""
+    ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama", micro=2, accum=2, steps=2)
+    r = _run(2, 3, str(tmp_path / "b"), model="tiny-llama", micro=1, accum=2, steps=2,
+             extra={"schedule": schedule, "gc": gc})
+    _close(r["sd"], ref["sd"])
+
+
+@pytest.mark.parametrize("schedule", ["keep", "pipelined", "release"])
+def test_zero3_world1_partitioned(schedule, tmp_path):
+    """LUMEN_ZERO3_SINGLE=1: the coordinator at world size 1 (local gathers) == stage 0."""
+    ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama", micro=2, accum=2, steps=2)
+    r = _run(1, 3, str(tmp_path / "b"), model="tiny-llama", micro=2, accum=2, steps=2,
+             extra={"schedule": schedule, "gc": True, "single": True})
+    _close(r["sd"], ref["sd"])
+
+
 def test_zero1_opt125m_style_world2(tmp_path):
     """BASELINE config 1 plumbing: OPT LoRA ZeRO-1 over gloo world_size=2 (tiny OPT)."""
     ref = _run(1, 0, str(tmp_path / "a"), model="tiny-opt", micro=4, accum=1, steps=2)
