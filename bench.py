@@ -195,8 +195,8 @@ def main():
                 "final_loss": round(final_loss, 4),
                 "setup_s": round(setup_s, 1),
                 "zero3_schedule": coord.schedule if coord else None,
-                "zero3_gathered_gb_per_step": (round((coord.gathered_bytes - gb0) / 1e9
-                                                     / args.steps, 2) if coord else 0.0),
+                "zero3_gathered_mb_per_step": (round((coord.gathered_bytes - gb0) / 1e6
+                                                     / args.steps, 1) if coord else 0.0),
                 "baseline_tok_s": BASELINE_TOK_S,
                 "gemm_algos": gemm_table,
                 "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,

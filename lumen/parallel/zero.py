@@ -29,6 +29,7 @@ MI355X-first design (not a DeepSpeed translation):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -293,9 +294,11 @@ class ParamCoordinator:
                 p.data = torch.empty(0, dtype=u.dtype, device=p.device)
                 p._lumen_gathered = True  # storage swapped per gather: no derived caches
         self.total_numel = total
+        self.max_live = max_live if max_live >= 0 else self._hbm_live_budget(units_dtype_bytes(
+            self.units))
         if schedule is None:
-            schedule = ("pipelined" if 2 * total <= max_live else
-                        "keep" if total <= max_live else "release")
+            schedule = ("pipelined" if 2 * total <= self.max_live else
+                        "keep" if total <= self.max_live else "release")
         assert schedule in ("release", "keep", "pipelined"), schedule
         self.schedule = schedule
         self.keep = schedule != "release"
@@ -321,6 +324,21 @@ class ParamCoordinator:
         self._in_step = False
         self.gathered_bytes = 0    # bytes materialised by gathers (all ranks' shards)
         self.gathers = 0
+
+    def _hbm_live_budget(self, elem_bytes: int) -> int:
+        """``stage3_max_live_parameters: "auto"``: elements of gathered weights that fit in the
+        free HBM left after the shards, minus an activation reserve (max(48 GiB, 25% of the
+        device)).  On MI355X (288 GB) that is both buffers of the pipelined schedule for
+        Llama-2-7B and one full copy (keep) for Llama-2-70B.  Unlimited off-GPU."""
+        if self.env.device.type != "cuda":
+            return 1 << 62
+        free, total = torch.cuda.mem_get_info(self.env.device)
+        # blocks the caching allocator holds but no tensor uses (the full weights just sharded)
+        free += torch.cuda.memory_reserved(self.env.device) - torch.cuda.memory_allocated(
+            self.env.device)
+        reserve = float(os.environ.get("LUMEN_ZERO3_RESERVE_GB", "0")) * 2**30 or max(
+            48 * 2**30, 0.25 * total)
+        return max(0, int((free - reserve) // max(elem_bytes, 1)))
 
     # ---- gather / bind / release ------------------------------------------------------------
     def _issue(self, i: int, slot: Optional[int] = None):
@@ -571,6 +589,10 @@ class ParamCoordinator:
                     w.wait()
                     u.works[s] = None
                     u.states[s] = "ready"
+
+
+def units_dtype_bytes(units: Sequence[_Unit]) -> int:
+    return max((u.dtype.itemsize for u in units if u.params), default=2)
 
 
 def mark_zero_shapes(model: nn.Module):

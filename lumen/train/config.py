@@ -134,7 +134,10 @@ def load_ds_config(src, micro_batch: int, grad_accum: int, world_size: int,
     c.stage3_prefetch_bucket_size = int(float(_auto(z.get("stage3_prefetch_bucket_size"), 5e7)))
     c.stage3_param_persistence_threshold = int(float(_auto(
         z.get("stage3_param_persistence_threshold"), 1e5)))
-    c.stage3_max_live_parameters = int(float(_auto(z.get("stage3_max_live_parameters"), 1e9)))
+    # "auto" (lumen extension): size the live-parameter budget from free HBM at engine start
+    # (-1 here; resolved by the ZeRO-3 coordinator once the shards exist)
+    c.stage3_max_live_parameters = (-1 if z.get("stage3_max_live_parameters") == "auto" else
+                                    int(float(z.get("stage3_max_live_parameters", 1e9))))
     c.stage3_max_reuse_distance = int(float(_auto(z.get("stage3_max_reuse_distance"), 1e9)))
     c.stage3_gather_16bit_weights_on_model_save = bool(
         z.get("stage3_gather_16bit_weights_on_model_save", False))

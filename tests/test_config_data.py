@@ -2,6 +2,7 @@
 import csv
 import json
 import math
+import os
 
 import pytest
 import torch
@@ -146,3 +147,14 @@ def test_dropout_mask_rate_and_determinism():
     assert torch.equal(m1, m2)
     assert abs(1 - m1.float().mean().item() - 0.05) < 0.005
     assert not torch.equal(m1, dropout_mask_ref(124, 64, 512, 0.05))
+
+
+def test_stage3_max_live_auto():
+    """lumen extension: "auto" live-parameter budget (sized from free HBM by the coordinator)."""
+    from lumen.train.config import load_ds_config
+
+    c = load_ds_config({"zero_optimization": {"stage": 3, "stage3_max_live_parameters": "auto"}},
+                       1, 1, 1, 1e-4)
+    assert c.stage3_max_live_parameters == -1
+    c = load_ds_config(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "ds_config_zero3_mi355x.json"), 8, 1, 8, 1e-4)
+    assert c.stage3_max_live_parameters == -1 and c.stage == 3

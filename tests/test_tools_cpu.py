@@ -238,5 +238,6 @@ def test_bench_contract_torchrun_world2():
         assert k in j, k
     assert j["n_gpus"] == 2 and j["steps"] == 2 and j["scaling"] == "weak"
     assert j["config"]["global_batch"] == 4 and j["config"]["parallelism"] == "dp2-zero3"
-    assert j["extra"]["zero3_keep_gathered"] is True
+    assert j["extra"]["zero3_schedule"] == "pipelined"
+    assert j["extra"]["zero3_gathered_mb_per_step"] > 0
     assert abs(j["value"] - 4 * 32 * 2 / (j["ms_per_step"] * 2 / 1000)) / j["value"] < 0.02

@@ -9,7 +9,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_wt="none"):
+def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_wt="none",
+           config=None):
     from lumen.lora import LoraConfig, adapter_state_dict, apply_lora
     from lumen.models import build_model
     from lumen.parallel.dist import init
@@ -28,9 +29,13 @@ def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_
     m.gradient_checkpointing = ckpt
     m.train()
     env = init()
-    ds = load_ds_config({"zero_optimization": {"stage": stage,
-                                               "stage3_param_persistence_threshold": 1e4}},
-                        2, accum, 1, 1e-3)
+    if config is not None:
+        ds = load_ds_config(config, 2, accum, 1, 1e-3, dtype_override="bf16")
+        ds.stage3_param_persistence_threshold = int(1e4)
+    else:
+        ds = load_ds_config({"zero_optimization": {"stage": stage,
+                                                   "stage3_param_persistence_threshold": 1e4}},
+                            2, accum, 1, 1e-3)
     eng = ZeroEngine(m, ds, env)
     g = torch.Generator(device="cpu").manual_seed(5)
     losses = []
@@ -75,3 +80,23 @@ def test_zero3_offpath_transposes_match_persistent_layout(schedule, monkeypatch)
     assert sum(len(u.tn) for u in coord.units) == 4 * sum(1 for u in coord.units[1:-1])
     for k in ref:
         torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)
+
+
+def test_reference_zero3_config_with_cpu_offload(monkeypatch):
+    """The reference's configs/ds_config_zero3.json (params AND optimizer offloaded to CPU,
+    pinned) on the GPU path:
+    shards stream H2D per gather, the C++ AdamW updates the host master copy."""
+    import os
+
+    from lumen.train.config import load_ds_config
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    raw = load_ds_config(os.path.join(root, "configs", "ds_config_zero3.json"), 2, 2, 1, 1e-3)
+    assert raw.offload_param == "cpu" and raw.offload_optimizer == "cpu"
+    ref, ref_losses, _ = _train(monkeypatch, 0)
+    got, losses, coord = _train(monkeypatch, 3, config=os.path.join(root, "configs",
+                                                                      "ds_config_zero3.json"))
+    assert coord.offload and coord.units[1].shard.device.type == "cpu"
+    assert coord.units[1].shard.is_pinned()
+    for k in ref:  # host AdamW vs the fused HIP AdamW: same math, different rounding order
+        torch.testing.assert_close(got[k], ref[k], rtol=5e-3, atol=3e-4)
