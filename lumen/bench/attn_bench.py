@@ -24,12 +24,14 @@ def main():
     ap.add_argument("--only", default="all")
     a = ap.parse_args()
     D = 128
+    res = {"fwd_kernel": os.environ.get("LUMEN_FA_FWD", "v32"),
+           "bwd_kernel": os.environ.get("LUMEN_FA_BWD", "mix"), "B": a.B, "S": a.S, "nh": a.nh,
+           "nkv": a.nkv}
     dev = "cuda"
     T = a.B * a.S
     qkv = (torch.randn(T, (a.nh + 2 * a.nkv) * D, device=dev) * 0.5).to(torch.bfloat16)
     cu = list(range(0, T + 1, a.S))
     flops_f = 4 * a.B * a.nh * a.S * a.S * D / 2  # causal
-    res = {}
 
     def timeit(fn, n):
         for _ in range(3):

@@ -172,6 +172,11 @@ __device__ __forceinline__ float red16_sum(float v) {
   return v;
 }
 
+// exp2 on the transcendental unit directly (v_exp_f32): the libm exp2f adds a denormal range
+// fix-up (v_cmp + v_cndmask + v_ldexp per call) that a softmax does not need -- every input is
+// <= 0 and results below 2^-126 are flushed to 0, far beneath bf16 resolution of the row sum.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 struct Args {
   const void* q; const void* k; const void* v;  // token-major bases (head 0)
   long long ldq, ldk, ldv;
@@ -281,11 +286,11 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(Args a) {
         }
         mx = red16_max(mx);
         const float m_new = fmaxf(m_i[mt][r], mx);
-        const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_i[mt][r] - m_new);
+        const float alpha = (m_new == -INFINITY) ? 1.f : fexp2(m_i[mt][r] - m_new);
         float rs = 0.f;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          const float p = (m_new == -INFINITY) ? 0.f : exp2f(pr[nt][r] - m_new);
+          const float p = (m_new == -INFINITY) ? 0.f : fexp2(pr[nt][r] - m_new);
           pr[nt][r] = p;
           rs += p;
         }
@@ -450,13 +455,13 @@ __global__ void __launch_bounds__(256, 2) fwd_t_kernel(Args a) {
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       const float m_new = fmaxf(m_i[qg], mx);
       const float mref = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = exp2f(m_i[qg] - mref);
+      const float alpha = fexp2(m_i[qg] - mref);
       float rs = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(st[qg][nt][r] - mref);
+          const float p = fexp2(st[qg][nt][r] - mref);
           st[qg][nt][r] = p;
           rs += p;
         }
@@ -626,7 +631,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qc = nt * 16 + 4 * lg + r;
-        float pv = exp2f(sc[nt][r] * a.scale_log2 - lq[r]);
+        float pv = fexp2(sc[nt][r] * a.scale_log2 - lq[r]);
         if (need_mask && (krow >= L || q0 + qc >= L || (CAUSAL && krow > q0 + qc))) pv = 0.f;
         sc[nt][r] = pv;
         dp[nt][r] = pv * (dp[nt][r] - dq4[r]);
@@ -726,7 +731,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kpos = kv0 + nt * 16 + 4 * lg + r;
-        float pv = exp2f(s[nt][r] * a.scale_log2 - lse_q);
+        float pv = fexp2(s[nt][r] * a.scale_log2 - lse_q);
         if (need_mask && (kpos >= L || qrow >= L || (CAUSAL && kpos > qrow))) pv = 0.f;
         s[nt][r] = pv * (dp[nt][r] - del_q);
       }
@@ -751,12 +756,485 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_kernel(Args a) {
   }
 }
 
+// =============================================================================================
+// 32x32x16 MFMA kernels (v_mfma_f32_32x32x16_{bf16,f16}): 32 queries (fwd, dQ) or 32 keys
+// (dK/dV) per wave, 4 waves per workgroup.  Same swizzled K/V/Q/dO LDS images as above; every
+// B fragment read from LDS now feeds a 32x32x16 product (32 KFLOP) instead of a 16x16x32 one
+// (16 KFLOP), so the LDS traffic per FLOP halves.  Accumulator layout (verified by
+// scripts/probes/mfma32_layout.hip): lane l, register r = 4j + i holds row 8j + 4(l>>5) + i,
+// column l & 31; A/B lanes hold k = 8(l>>5) + 0..7.  With keys (or queries) on the accumulator
+// ROWS, the registers 8s..8s+7 of a 32-row block are rows {16s + 4hi + 0..3, 16s + 8 + 4hi +
+// 0..3} (hi = l>>5): read the other operand's rows in that order and P / dS feed the next
+// product straight from registers.
+// =============================================================================================
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T> struct Mfma32;
+template <> struct Mfma32<bf16> {
+  static __device__ __forceinline__ f32x16 run(uint4 a, uint4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma32<fp16> {
+  static __device__ __forceinline__ f32x16 run(uint4 a, uint4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// 8 rows of an image, transposed, for a 32x32x16 operand whose k slots follow the register
+// order above: lane (c = lane&31, hi) gets column n0 + c of rows r0 + 4hi + 0..3 and
+// r0 + 8 + 4hi + 0..3 (each 16-lane group reads its own 16 columns).
+__device__ __forceinline__ uint4 tr_read32(const char* img, int r0, int n0, int lane) {
+  const int hi = lane >> 5;
+  return tr_read_img2(img, r0 + 4 * hi, r0 + 8 + 4 * hi, n0 + 16 * ((lane >> 4) & 1), lane);
+}
+
+// registers 8s..8s+7 of a 32x32 accumulator -> 8 packed 16-bit values (a k=16 operand)
+template <typename T>
+__device__ __forceinline__ uint4 pack8(const f32x16& c, int s) {
+  struct alignas(16) P8 { T v[8]; } o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o.v[e] = from_f32<T>(c[8 * s + e]);
+  return __builtin_bit_cast(uint4, o);
+}
+
+// ---- forward: S^T = K Q^T (keys on rows, lane = query), O^T += V^T P^T -----------------------
+// Per-lane LDS byte offsets inside a K/V image, computed once: the swizzle depends only on
+// row & 15, so the key block (kb * 32 rows) and the 16-key slice (16 rows) are immediates.
+struct Off32 {
+  int row[8];   // row_read of row (lane&31), chunk 2ks + hi        (ks = 0..7)
+  int tr[8];    // tr_read32 lo / hi rows for output block n      (index 2n + lohi)
+};
+__device__ __forceinline__ void make_off32(Off32& o, int lane) {
+  const int lq = lane & 31, hi = lane >> 5, L = lane & 15, g16 = (lane >> 4) & 1;
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) o.row[ks] = img_off(lq, 2 * ks + hi);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int ch = 4 * n + 2 * g16 + ((L & 3) >> 1);
+    const int r = 4 * hi + (L >> 2);
+    o.tr[2 * n] = img_off(r, ch) + 8 * (L & 1);
+    o.tr[2 * n + 1] = img_off(r + 8, ch) + 8 * (L & 1);
+  }
+}
+__device__ __forceinline__ uint4 lds16(const char* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ uint4 tr32(const char* img, const Off32& o, int rowbase, int n) {
+  const uint2 lo = tr_read_raw(img + rowbase * 256 + o.tr[2 * n]);
+  const uint2 hi = tr_read_raw(img + rowbase * 256 + o.tr[2 * n + 1]);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+template <typename T, bool CAUSAL, bool MASK>
+__device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, const Off32& off,
+                                           const uint4 (&qf)[8], f32x16 (&acc)[4], float& m_i,
+                                           float& l_i, int kv0, int L, int qrow, int hi,
+                                           float scale_log2) {
+  f32x16 st[2];
+  st[0] = zero16();
+  st[1] = zero16();
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      st[kb] = Mfma32<T>::run(lds16(kimg + kb * 8192 + off.row[ks]), qf[ks], st[kb]);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (MASK) {
+        const int kpos = kv0 + kb * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+        const bool out = (kpos >= L) | (CAUSAL & (kpos > qrow));
+        st[kb][r] = out ? -INFINITY : st[kb][r];
+      }
+      mx = fmaxf(mx, st[kb][r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32)) * scale_log2;
+  // deferred rescale: the running max moves only when a row's new max exceeds it by more than
+  // RESCALE (log2 units), so P stays <= 2^RESCALE and the O / l rescale (64 multiplies per lane)
+  // runs on a handful of tiles per row instead of every tile
+  constexpr float RESCALE = 8.f;
+  const bool bump = mx > m_i + RESCALE;
+  if (__any(bump)) {
+    // lanes that do not move keep alpha = 1 (also when their m_i is still -inf: -inf - -inf)
+    const float alpha = bump ? fexp2(m_i - mx) : 1.f;  // exp2(-inf) = 0 on a row's first tile
+    const float m_new = bump ? mx : m_i;
+    l_i *= alpha;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[n] *= alpha;
+    m_i = m_new;
+  }
+  const float mref = m_i == -INFINITY ? 0.f : m_i;
+  float rs = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = fexp2(fmaf(st[kb][r], scale_log2, -mref));
+      st[kb][r] = p;
+      rs += p;
+    }
+  rs += __shfl_xor(rs, 32);
+  l_i += rs;
+  // O^T[d][q] += V^T[d][key] P^T[key][q], keys in the register order
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint4 pb = pack8<T>(st[kb], s);
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[n] = Mfma32<T>::run(tr32(vimg, off, kb * 32 + 16 * s, n), pb, acc[n]);
+    }
+}
+
+template <typename T, bool CAUSAL>
+__global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
+  constexpr int BM = 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [K0 | V0 | K1 | V1]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lq = lane & 31, hi = lane >> 5;
+  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
+  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const int wq0 = q0 + wid * 32;
+  const int qrow = wq0 + lq;
+  Off32 off;
+  make_off32(off, lane);
+  uint4 qf[8];  // B operand of S^T: Q[qrow][16ks + 8hi .. +7]
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+    qf[ks] = gload16(Q + (long long)qrow * a.ldq + 16 * ks + 8 * hi, qrow < L);
+  f32x16 acc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) acc[n] = zero16();
+  float m_i = -INFINITY, l_i = 0.f;
+  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
+  const int w_end = CAUSAL ? min(kv_end, wq0 + 32) : kv_end;  // keys this wave can see
+  if (kv_end > 0) {
+    stage64_async(smem, K, a.ldk, 0, L);
+    stage64_async(smem + IMG, V, a.ldv, 0, L);
+  }
+  int it = 0;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
+    char* kimg = smem + (it & 1) * 2 * IMG;
+    char* vimg = kimg + IMG;
+    if (kv0 + BN < kv_end) {
+      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
+      stage64_async(nk, K, a.ldk, kv0 + BN, L);
+      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
+      wait_vm_8();
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+    if (kv0 < w_end) {  // (causal: tiles entirely above this wave's rows are skipped)
+      const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
+      if (need_mask)
+        fwd32_tile<T, CAUSAL, true>(kimg, vimg, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
+                                    a.scale_log2);
+      else
+        fwd32_tile<T, CAUSAL, false>(kimg, vimg, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
+                                     a.scale_log2);
+    }
+    lds_fence_barrier();  // every wave is done with this K/V buffer before it is refilled
+  }
+  // epilogue: lane holds O[qrow][32n + 8j + 4hi + i] in acc[n][4j + i]
+  if (qrow < L) {
+    T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D + (long long)qrow * a.ldo;
+    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        struct alignas(8) O4 { T v[4]; } o4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o4.v[i] = from_f32<T>(acc[n][4 * j + i] * inv);
+        *reinterpret_cast<O4*>(O + 32 * n + 8 * j + 4 * hi) = o4;
+      }
+    if (hi == 0 && a.lse)
+      a.lse[(long long)head * a.T + s0 + qrow] = l_i > 0.f ? m_i + __log2f(l_i) : INFINITY;
+  }
+}
+
+template <typename T, bool CAUSAL, bool MASK>
+__device__ __forceinline__ void dkdv32_block(const char* qimg, const char* oimg,
+                                             const float* s_lse, const float* s_del,
+                                             const Off32& off, const uint4 (&kf)[8],
+                                             const uint4 (&vf)[8], f32x16 (&dk)[4],
+                                             f32x16 (&dv)[4], int qb, int q0, int L, int krow,
+                                             int hi, float scale_log2) {
+  f32x16 sc = zero16(), dp = zero16();
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    sc = Mfma32<T>::run(lds16(qimg + qb * 8192 + off.row[ks]), kf[ks], sc);
+    dp = Mfma32<T>::run(lds16(oimg + qb * 8192 + off.row[ks]), vf[ks], dp);
+  }
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int qc = qb * 32 + 8 * jj + 4 * hi;  // rows qc + 0..3 of the staged tile
+    const float4 l4 = *reinterpret_cast<const float4*>(s_lse + qc);
+    const float4 d4 = *reinterpret_cast<const float4*>(s_del + qc);
+    const float lq4[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * jj + i;
+      float pv = fexp2(fmaf(sc[r], scale_log2, -lq4[i]));
+      if (MASK) {
+        const int qpos = q0 + qc + i;
+        const bool out = (krow >= L) | (qpos >= L) | (CAUSAL & (krow > qpos));
+        pv = out ? 0.f : pv;
+      }
+      sc[r] = pv;
+      dp[r] = pv * (dp[r] - dq4[i]);
+    }
+  }
+  // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T += Q^T dS   (q in the register order)
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint4 pb = pack8<T>(sc, s);
+    const uint4 db = pack8<T>(dp, s);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      dv[n] = Mfma32<T>::run(tr32(oimg, off, qb * 32 + 16 * s, n), pb, dv[n]);
+      dk[n] = Mfma32<T>::run(tr32(qimg, off, qb * 32 + 16 * s, n), db, dk[n]);
+    }
+  }
+}
+
+// ---- backward dK/dV: 32 keys per wave, 128 per workgroup ------------------------------------
+// S = Q K^T and dP = dO V^T with the queries on the accumulator rows and lane = key: P and dS
+// are the B operands of dV^T += dO^T P and dK^T += Q^T dS straight from registers.
+template <typename T, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1) bwd_dkdv32_kernel(Args a) {
+  constexpr int STAGE = 2 * IMG + 512;  // Q image | dO image | lse[64] | delta[64]
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lk = lane & 31, hi = lane >> 5;
+  const int seq = a.tiles[2 * blockIdx.x], k0 = a.tiles[2 * blockIdx.x + 1];
+  const int kvh = blockIdx.y;
+  const int grp = a.nh / a.nkv;
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const int wk0 = k0 + wid * 32;
+  const int krow = wk0 + lk;
+  uint4 kf[8], vf[8];  // B operands: K[krow][16ks + 8hi ..], V[krow][...]
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    kf[ks] = gload16(K + (long long)krow * a.ldk + 16 * ks + 8 * hi, krow < L);
+    vf[ks] = gload16(V + (long long)krow * a.ldv + 16 * ks + 8 * hi, krow < L);
+  }
+  wait_vm_all();
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) { dk[n] = zero16(); dv[n] = zero16(); }
+  const int qstart = CAUSAL ? (k0 / 64) * 64 : 0;
+  const int nq = qstart < L ? (L - qstart + 63) / 64 : 0;
+  const int nsteps = grp * nq;
+  auto stage = [&](int j, char* st) {
+    const int hh = j / nq, qq = qstart + (j % nq) * 64;
+    const int head = kvh * grp + hh;
+    stage64_async(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
+                  qq, L);
+    stage64_async(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D,
+                  a.lddo, qq, L);
+    if (wid < 2) {
+      const float* src = (wid == 0 ? a.lse : a.delta) + (long long)head * a.T + s0;
+      int qr = qq + lane;
+      qr = qr < L ? qr : L - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(src + qr),
+                                       (__attribute__((address_space(3))) void*)(st + 2 * IMG + wid * 256),
+                                       4, 0, 0);
+    }
+  };
+  Off32 off;
+  make_off32(off, lane);
+  if (nsteps > 0) stage(0, smem);
+  for (int j = 0; j < nsteps; ++j) {
+    char* st = smem + (j & 1) * STAGE;
+    char* qimg = st;
+    char* oimg = st + IMG;
+    const float* s_lse = reinterpret_cast<const float*>(st + 2 * IMG);
+    const float* s_del = s_lse + 64;
+    const int q0 = qstart + (j % nq) * 64;
+    if (j + 1 < nsteps) {
+      stage(j + 1, smem + ((j + 1) & 1) * STAGE);
+      if (wid < 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int qb0 = q0 + qb * 32;
+      if (CAUSAL && qb0 + 31 < wk0) continue;  // every query of the block is before every key
+      // wave-uniform (the MFMAs read every lane's operands: never branch per lane around them)
+      const bool need_mask = (qb0 + 32 > L) || (wk0 + 32 > L) || (CAUSAL && wk0 + 31 > qb0);
+      if (need_mask)
+        dkdv32_block<T, CAUSAL, true>(qimg, oimg, s_lse, s_del, off, kf, vf, dk, dv, qb, q0, L,
+                                      krow, hi, a.scale_log2);
+      else
+        dkdv32_block<T, CAUSAL, false>(qimg, oimg, s_lse, s_del, off, kf, vf, dk, dv, qb, q0, L,
+                                       krow, hi, a.scale_log2);
+    }
+    lds_fence_barrier();
+  }
+  // lane holds dK^T / dV^T column krow, rows (dims) 32n + 8j + 4hi + i
+  if (krow < L) {
+    T* dK = reinterpret_cast<T*>(a.dk) + (long long)s0 * a.lddk + kvh * D + (long long)krow * a.lddk;
+    T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D + (long long)krow * a.lddv;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        struct alignas(8) O4 { T v[4]; } k4, v4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          k4.v[i] = from_f32<T>(dk[n][4 * jj + i] * a.scale);
+          v4.v[i] = from_f32<T>(dv[n][4 * jj + i]);
+        }
+        *reinterpret_cast<O4*>(dK + 32 * n + 8 * jj + 4 * hi) = k4;
+        *reinterpret_cast<O4*>(dV + 32 * n + 8 * jj + 4 * hi) = v4;
+      }
+  }
+}
+
+template <typename T, bool CAUSAL, bool MASK>
+__device__ __forceinline__ void dq32_tile(const char* kimg, const char* vimg, const Off32& off,
+                                          const uint4 (&qf)[8], const uint4 (&of)[8],
+                                          f32x16 (&dq)[4], int kv0, int L, int qrow, int hi,
+                                          float lse_q, float del_q, float scale_log2) {
+  // one 32-key block at a time: 32 accumulator registers live instead of 64, which keeps the
+  // kernel at two waves per SIMD
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    f32x16 st = zero16(), dpt = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      st = Mfma32<T>::run(lds16(kimg + kb * 8192 + off.row[ks]), qf[ks], st);
+      dpt = Mfma32<T>::run(lds16(vimg + kb * 8192 + off.row[ks]), of[ks], dpt);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float pv = fexp2(fmaf(st[r], scale_log2, -lse_q));
+      if (MASK) {
+        const int kpos = kv0 + kb * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+        const bool out = (kpos >= L) | (qrow >= L) | (CAUSAL & (kpos > qrow));
+        pv = out ? 0.f : pv;
+      }
+      dpt[r] = pv * (dpt[r] - del_q);
+    }
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint4 db = pack8<T>(dpt, s);
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        dq[n] = Mfma32<T>::run(tr32(kimg, off, kb * 32 + 16 * s, n), db, dq[n]);
+    }
+  }
+}
+
+// ---- backward dQ: 32 queries per wave, 128 per workgroup ------------------------------------
+// S^T = K Q^T, dP^T = V dO^T (keys on rows, lane = query); dQ^T += K^T dS^T.
+template <typename T, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
+  constexpr int BM = 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lq = lane & 31, hi = lane >> 5;
+  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
+  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const int wq0 = q0 + wid * 32;
+  const int qrow = wq0 + lq;
+  uint4 qf[8], of[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    qf[ks] = gload16(Q + (long long)qrow * a.ldq + 16 * ks + 8 * hi, qrow < L);
+    of[ks] = gload16(dO + (long long)qrow * a.lddo + 16 * ks + 8 * hi, qrow < L);
+  }
+  const float lse_q = qrow < L ? a.lse[(long long)head * a.T + s0 + qrow] : INFINITY;
+  const float del_q = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
+  f32x16 dq[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) dq[n] = zero16();
+  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
+  const int w_end = CAUSAL ? min(kv_end, wq0 + 32) : kv_end;
+  wait_vm_all();
+  if (kv_end > 0) {
+    stage64_async(smem, K, a.ldk, 0, L);
+    stage64_async(smem + IMG, V, a.ldv, 0, L);
+  }
+  Off32 off;
+  make_off32(off, lane);
+  int it = 0;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
+    char* kimg = smem + (it & 1) * 2 * IMG;
+    char* vimg = kimg + IMG;
+    if (kv0 + BN < kv_end) {
+      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
+      stage64_async(nk, K, a.ldk, kv0 + BN, L);
+      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
+      wait_vm_8();
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+    if (kv0 < w_end) {
+      // wave-uniform (the MFMAs read every lane's operands: never branch per lane around them)
+      const bool need_mask = (kv0 + BN > L) || (wq0 + 32 > L) || (CAUSAL && kv0 + BN - 1 > wq0);
+      if (need_mask)
+        dq32_tile<T, CAUSAL, true>(kimg, vimg, off, qf, of, dq, kv0, L, qrow, hi, lse_q, del_q,
+                                   a.scale_log2);
+      else
+        dq32_tile<T, CAUSAL, false>(kimg, vimg, off, qf, of, dq, kv0, L, qrow, hi, lse_q, del_q,
+                                    a.scale_log2);
+    }
+    lds_fence_barrier();
+  }
+  if (qrow < L) {
+    T* dQ = reinterpret_cast<T*>(a.dq) + (long long)s0 * a.lddq + head * D + (long long)qrow * a.lddq;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        struct alignas(8) O4 { T v[4]; } q4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q4.v[i] = from_f32<T>(dq[n][4 * jj + i] * a.scale);
+        *reinterpret_cast<O4*>(dQ + 32 * n + 8 * jj + 4 * hi) = q4;
+      }
+  }
+}
+
 template <typename T>
 static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& a, hipStream_t st) {
   dim3 block(256);
   if (which == 0) {
     dim3 grid(ntiles, a.nh);
-    if (mt >= 10) {  // transposed-formulation kernel, QG = mt - 10 query groups per wave
+    if (mt == 20) {  // 32x32x16 kernel, 128-row tiles
+      if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((fwd32_kernel<T, false>), grid, block, 0, st, a);
+    } else if (mt >= 10) {  // transposed-formulation kernel, QG = mt - 10 query groups per wave
       const int qg = mt - 10;
       if (causal) {
         if (qg == 2) hipLaunchKernelGGL((fwd_t_kernel<T, true, 2>), grid, block, 0, st, a);
@@ -783,6 +1261,14 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     dim3 grid(ntiles, a.nh);
     if (causal) hipLaunchKernelGGL((bwd_dq_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dq_kernel<T, false>), grid, block, 0, st, a);
+  } else if (which == 4) {  // dK/dV, 32x32x16 kernel, 128-key tiles
+    dim3 grid(ntiles, a.nkv);
+    if (causal) hipLaunchKernelGGL((bwd_dkdv32_kernel<T, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((bwd_dkdv32_kernel<T, false>), grid, block, 0, st, a);
+  } else if (which == 5) {  // dQ, 32x32x16 kernel, 128-query tiles
+    dim3 grid(ntiles, a.nh);
+    if (causal) hipLaunchKernelGGL((bwd_dq32_kernel<T, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((bwd_dq32_kernel<T, false>), grid, block, 0, st, a);
   } else {
     return hipErrorInvalidValue;
   }
@@ -793,8 +1279,9 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 }  // namespace lumen
 
 // which: 0 = forward (tiles of 64*mt query rows; mt >= 10 selects the transposed-formulation
-//        kernel with 64*(mt-10)-row tiles), 1 = delta, 2 = dK/dV (64-key tiles),
-//        3 = dQ (64-query tiles)
+//        kernel with 64*(mt-10)-row tiles; mt == 20 the 32x32x16 kernel, 128-row tiles),
+//        1 = delta, 2 = dK/dV (64-key tiles), 3 = dQ (64-query tiles),
+//        4 = dK/dV (32x32x16, 128-key tiles), 5 = dQ (32x32x16, 128-query tiles)
 extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
                                        const void* q, const void* k, const void* v,
                                        long long ldq, long long ldk, long long ldv, void* o,

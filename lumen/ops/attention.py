@@ -138,11 +138,21 @@ def _cu_tensor(cu: tuple, device) -> torch.Tensor:
 
 import os as _os
 FA_MT = int(_os.environ.get("LUMEN_FA_MT", "1"))  # query m-tiles (16 rows) per wave (old fwd)
-# forward kernel: "t1"/"t2" = transposed formulation with 1/2 query groups per wave (P stays in
-# registers), "old" = fwd_kernel with FA_MT
-_FWD = _os.environ.get("LUMEN_FA_FWD", "t1")
-FA_FWD_MT = {"t1": 11, "t2": 12}.get(_FWD, FA_MT)
-FA_FWD_ROWS = 64 * (FA_FWD_MT - 10 if FA_FWD_MT >= 10 else FA_FWD_MT)
+# forward kernel: "v32" = 32x32x16 MFMA, 32 queries per wave, 128-row tiles (default: 56 vs 71
+# us at B8 S512, 524 vs 668 us at B2 S4096, profiles/r02_fa); "t1"/"t2" = 16x16x32 transposed
+# formulation with 1/2 query groups per wave (P stays in registers), "old" = fwd_kernel
+_FWD = _os.environ.get("LUMEN_FA_FWD", "v32")
+FA_FWD_MT = {"t1": 11, "t2": 12, "v32": 20}.get(_FWD, FA_MT)
+
+
+def _fwd_rows(mt: int) -> int:
+    return 128 if mt == 20 else 64 * (mt - 10 if mt >= 10 else mt)
+
+
+FA_FWD_ROWS = _fwd_rows(FA_FWD_MT)
+# backward kernels: "v16" = 16x16x32 dK/dV (64-key tiles) + dQ (64-query tiles);
+# "v32" = 32x32x16 kernels with 128-row tiles; "mix" = 16x16x32 dK/dV + 32x32x16 dQ
+FA_BWD = _os.environ.get("LUMEN_FA_BWD", "mix")
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -183,9 +193,13 @@ class _FlashAttn(torch.autograd.Function):
         cut = _cu_tensor(cu, qkv.device)
         C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
                      scale, do, None, None, None, delta)
-        C.flash_attn(2, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
+        # dK/dV and dQ kernels per FA_BWD: "v16" both 16x16x32 (64-row tiles), "v32" both
+        # 32x32x16 (128-row tiles), "mix" = 16x16x32 dK/dV + 32x32x16 dQ
+        wkv, rkv = (4, 128) if FA_BWD == "v32" else (2, 64)
+        wq, rq = (5, 128) if FA_BWD in ("v32", "mix") else (3, 64)
+        C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh, nkv,
                      scale, do, dq, dk, dv, delta)
-        C.flash_attn(3, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
+        C.flash_attn(wq, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rq, qkv.device), nh, nkv,
                      scale, do, dq, dk, dv, delta)
         return dqkv, None, None, None, None, None
 

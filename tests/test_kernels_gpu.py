@@ -266,14 +266,16 @@ def test_sampling_greedy_and_topk():
 
 @pytest.mark.parametrize("nh,nkv,lens", [(8, 8, [512, 512]), (8, 2, [512, 300, 77]),
                                          (4, 4, [1000, 64, 129])])
-@pytest.mark.parametrize("fwd", ["t1", "t2", "old"])
-def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, monkeypatch):
+@pytest.mark.parametrize("fwd,bwd", [("t1", "v16"), ("t2", "v16"), ("old", "v16"),
+                                     ("v32", "v32"), ("v32", "mix")])
+def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch):
     import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
 
-    mt = {"t1": 11, "t2": 12, "old": 1}[fwd]
+    mt = {"t1": 11, "t2": 12, "old": 1, "v32": 20}[fwd]
     monkeypatch.setattr(att, "FA_FWD_MT", mt)
-    monkeypatch.setattr(att, "FA_FWD_ROWS", 64 * (mt - 10 if mt >= 10 else mt))
+    monkeypatch.setattr(att, "FA_FWD_ROWS", att._fwd_rows(mt))
+    monkeypatch.setattr(att, "FA_BWD", bwd)
 
     D = 128
     cu = [0]

