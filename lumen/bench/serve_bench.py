@@ -143,7 +143,7 @@ def main():
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-num-seqs", type=int, default=256)
-    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--max-batched-tokens", type=int, default=8192)
     ap.add_argument("--no-graphs", action="store_true")
     a = ap.parse_args()
     res = bench_engine(a) if a.mode == "engine" else bench_http(a)
