@@ -38,6 +38,8 @@ hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long
                        const long long*, const int*, const float*, const float*, const int*, int,
                        hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
+hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
+                             long long, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
                                         float, float*, float*, void*, int, hipStream_t);
@@ -147,6 +149,20 @@ void swiglu(bool bwd, const at::Tensor& gu, const std::optional<at::Tensor>& dac
   check(lumen_swiglu(dcode(gu), bwd ? 1 : 0, gu.data_ptr(), ptr(dact), out.data_ptr(), rows, F,
                      cur_stream()),
         "swiglu");
+}
+
+void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
+  if (!x.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: skinny_gemm needs GPU tensors");
+  need_cuda(w, "w");  // x / y may be row-strided views (unit column stride checked below)
+  if (x.dim() != 2 || w.dim() != 2 || y.dim() != 2 || x.stride(1) != 1 || y.stride(1) != 1 ||
+      !w.is_contiguous() || x.size(1) != w.size(1) || y.size(0) != x.size(0) ||
+      y.size(1) != w.size(0) || x.scalar_type() != w.scalar_type() ||
+      y.scalar_type() != w.scalar_type())
+    throw std::invalid_argument("lumen: skinny_gemm shape/layout mismatch");
+  check(lumen_skinny_gemm(dcode(w), x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                          static_cast<int>(x.size(0)), static_cast<int>(w.size(0)),
+                          static_cast<int>(w.size(1)), x.stride(0), y.stride(0), cur_stream()),
+        "skinny_gemm");
 }
 
 void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
@@ -414,6 +430,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_gemm", &lora_gemm);
   m.def("lora2", &lora2);
   m.def("transpose2d", &transpose2d);
+  m.def("skinny_gemm", &skinny_gemm);
   m.def("paged_attention_decode", &paged_attention_decode);
   m.def("reshape_and_cache", &reshape_and_cache);
   m.def("sample", &sample);

@@ -29,7 +29,13 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
   if (row >= rows) return;
   const size_t base = static_cast<size_t>(row) * H;
   float v[VPL][8];
+  uint4 wraw[VPL];  // weight chunks loaded with the row: one round of memory latency, not two
   float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * 8;
+    if (c < H) wraw[i] = *reinterpret_cast<const uint4*>(w + c);
+  }
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = (lane + i * 64) * 8;
@@ -61,9 +67,63 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
         store8(s_out + base + c, sr);
       }
       float wv[8], o[8];
-      load8(w + c, wv);
+      load8(reinterpret_cast<const T*>(&wraw[i]), wv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[j];
+      store8(y + base + c, o);
+    }
+  }
+}
+
+// Few rows (decode: 1..512 tokens): a whole 256-thread workgroup per row, so each lane issues
+// VPT (= H / 2048) loads instead of H / 512 and the row reaches HBM / L2 with 4x the parallelism
+// (batch-1 decode: 10 -> a few us per call, 65 calls per token).
+template <typename T, int VPT>
+__global__ void __launch_bounds__(256) rmsnorm_fwd_row_kernel(
+    const T* __restrict__ x, const T* __restrict__ residual, const T* __restrict__ w,
+    T* __restrict__ y, T* __restrict__ s_out, float* __restrict__ rstd_out, int rows, int H,
+    float eps) {
+  __shared__ float part[4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row = blockIdx.x;
+  const size_t base = static_cast<size_t>(row) * H;
+  float v[VPT][8], wv[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (tid + i * 256) * 8;
+    if (c < H) {
+      load8(w + c, wv[i]);
+      load8(x + base + c, v[i]);
+      if (residual) {
+        float r[8];
+        load8(residual + base + c, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += r[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = wave_sum(ss);
+  if (lane == 0) part[wid] = ss;
+  __syncthreads();
+  ss = part[0] + part[1] + part[2] + part[3];
+  const float rs = rsqrtf(ss / static_cast<float>(H) + eps);
+  if (tid == 0 && rstd_out) rstd_out[row] = rs;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (tid + i * 256) * 8;
+    if (c < H) {
+      if (s_out) {
+        float sr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sr[j] = to_f32(from_f32<T>(v[i][j]));
+        store8(s_out + base + c, sr);
+      }
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[i][j];
       store8(y + base + c, o);
     }
   }
@@ -131,7 +191,20 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
 template <typename T>
 static hipError_t launch_fwd(const void* x, const void* res, const void* w, void* y, void* s_out,
                              float* rstd, int rows, int H, float eps, hipStream_t st) {
-  dim3 grid((rows + 3) / 4), block(256);
+  dim3 block(256);
+  if (rows < 1024 && H <= 8192) {  // under ~4 waves per CU: one workgroup per row
+    dim3 grid(rows);
+    const int vpt = (H + 2047) / 2048;
+#define LUMEN_RMS_ROW(V)                                                                          \
+  hipLaunchKernelGGL((rmsnorm_fwd_row_kernel<T, V>), grid, block, 0, st, (const T*)x,            \
+                     (const T*)res, (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps)
+    if (vpt <= 1) LUMEN_RMS_ROW(1);
+    else if (vpt <= 2) LUMEN_RMS_ROW(2);
+    else LUMEN_RMS_ROW(4);
+#undef LUMEN_RMS_ROW
+    return hipGetLastError();
+  }
+  dim3 grid((rows + 3) / 4);
   const int vpl = (H + 511) / 512;
 #define LUMEN_RMS_FWD(V)                                                                          \
   hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, V>), grid, block, 0, st, (const T*)x, (const T*)res, \

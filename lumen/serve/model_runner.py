@@ -28,6 +28,7 @@ from ..models.config import ModelConfig
 from ..ops._native import native, use_native
 from ..ops.activation import swiglu
 from ..ops.attention import flash_attention_qkv, paged_decode, write_kv_cache
+from ..ops.gemm import linear_nt
 from ..ops.norm import rms_norm
 from ..ops.rope import rope_inplace, rope_tables
 
@@ -144,7 +145,7 @@ class ModelRunner:
             <= self.car.max_bytes)
         self._graphs: Dict[int, tuple] = {}
         self._graph_pool = None
-        self.partition = 512
+        self.partition = 512  # context tokens per decode workgroup at full batch
         self.lora = None  # serve.multi_lora.MultiLoRA when adapters are served un-merged
 
     # ------------------------------------------------------------------------------------------
@@ -165,7 +166,7 @@ class ModelRunner:
         masks = {n: ml.mask(lora_ids, n) for n in (1, 2, 3)} if ml is not None else None
         for i, L in enumerate(self.w.layers):
             y, res = rms_norm(h, L.ln1, cfg.rms_norm_eps, res)
-            qkv = torch.matmul(y, L.qkv.t())
+            qkv = linear_nt(y, L.qkv)
             if ml is not None:
                 ml.apply(i, "qkv", y, qkv, masks)
             rope_inplace(qkv, positions, self.w.nh + self.w.nkv, D, self.cos, self.sin)
@@ -174,15 +175,15 @@ class ModelRunner:
             v = qkv[:, qs + ks:].view(T, self.w.nkv, D)
             write_kv_cache(k, v, self.k_cache[i], self.v_cache[i], slots)
             o = attn_fn(qkv, i)
-            a = self._allreduce(torch.matmul(o, L.o.t()))
+            a = self._allreduce(linear_nt(o, L.o))
             if ml is not None:
                 ml.apply(i, "o", o, a, masks, self._allreduce)
             y2, res = rms_norm(a, L.ln2, cfg.rms_norm_eps, res)
-            gu = torch.matmul(y2, L.gate_up.t())
+            gu = linear_nt(y2, L.gate_up)
             if ml is not None:
                 ml.apply(i, "gate_up", y2, gu, masks)
             act = swiglu(gu)
-            h = self._allreduce(torch.matmul(act, L.down.t()))
+            h = self._allreduce(linear_nt(act, L.down))
             if ml is not None:
                 ml.apply(i, "down", act, h, masks, self._allreduce)
         return h, res
@@ -254,12 +255,23 @@ class ModelRunner:
         def attn(qkv, i):
             q = qkv[:, :self.q_size].reshape(N, nh, D)
             return paged_decode(q, self.k_cache[i], self.v_cache[i], block_tables, context_lens,
-                                max_context, self.scale, self.partition).view(N, nh * D)
+                                max_context, self.scale, self.decode_partition(N)).view(N, nh * D)
 
         h, res = self._layers(h, positions, slots, attn, lora_ids)
         y, _ = rms_norm(h, self.w.norm, self.cfg.rms_norm_eps, res)
-        logits = torch.matmul(y, self.w.lm_head.t())
+        logits = linear_nt(y, self.w.lm_head)
         return self._vocab_gather(logits) if gather else logits
+
+    def decode_partition(self, n_seqs: int) -> int:
+        """Context tokens per paged-decode workgroup for a batch of ``n_seqs``: 512 once
+        sequences x kv heads alone give >= 2048 workgroups (8 per CU), shorter partitions (down
+        to 64) below that, so a small batch still spreads its KV read over the chip (batch 1 at
+        576 tokens of context: 64 -> 288 workgroups; the kernel went from 53 to a few us)."""
+        pairs = max(1, n_seqs * self.w.nkv)
+        part = self.partition
+        while part > 64 and pairs * (self.partition // part) < 2048:
+            part //= 2
+        return part
 
     @torch.no_grad()
     def decode(self, inp: StepInput) -> torch.Tensor:

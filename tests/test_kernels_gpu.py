@@ -429,3 +429,29 @@ def test_lora_linear_fused_rope(nh, nkv):
     y2.backward(dy.clone())
     for a, b in ((x.grad, x2.grad), (A.grad, A2.grad), (B.grad, B2.grad)):
         assert rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 8, 16])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (1024, 11008)])
+def test_skinny_gemm(M, N, K):
+    """Weight-streaming decode GEMM (kernels/skinny_gemm.hip) vs an f32 reference."""
+    from lumen.ops.gemm import linear_nt, skinny_ok
+
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    from lumen.ops._native import native
+
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    native().skinny_gemm(x, w, y)  # both kernel forms (M <= 4 VALU, M > 4 MFMA)
+    ref = x.float() @ w.float().t()
+    assert rel(y, ref) < 1e-2
+    assert skinny_ok(x, w) == (M == 1 and N <= 4096)
+    y = linear_nt(x, w)
+    ref = x.float() @ w.float().t()
+    assert y.shape == (M, N) and rel(y, ref) < 1e-2
+    # strided activation rows (a view into a wider buffer)
+    xb = torch.randn(M, K + 128, device=DEV).to(torch.bfloat16)
+    xv = xb[:, :K]
+    yv = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    native().skinny_gemm(xv, w, yv)
+    assert rel(yv, xv.float() @ w.float().t()) < 1e-2
