@@ -31,6 +31,19 @@ template <> __device__ __forceinline__ float from_f32<float>(float x) { return x
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return __float2bfloat16(x); }
 template <> __device__ __forceinline__ fp16 from_f32<fp16>(float x) { return __float2half(x); }
 
+// two f32 -> one packed 16-bit pair (element 0 in the low half), round to nearest even.  For
+// bf16 this is ONE v_cvt_pk_bf16_f32; converting the elements one at a time compiles to two
+// conversions plus a shift and an or per pair (4x the VALU in the attention / LoRA inner loops).
+typedef float lumen_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 lumen_bf16x2 __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ unsigned pk2(float a, float b);
+template <> __device__ __forceinline__ unsigned pk2<bf16>(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(lumen_f32x2{a, b}, lumen_bf16x2));
+}
+template <> __device__ __forceinline__ unsigned pk2<fp16>(float a, float b) {
+  return __builtin_bit_cast(unsigned, __floats2half2_rn(a, b));
+}
+
 // 16-byte vector of 8 half-precision elements.
 template <typename T> struct alignas(16) Vec8 { T v[8]; };
 
@@ -52,10 +65,8 @@ __device__ __forceinline__ void load8<float>(const float* __restrict__ p, float 
 
 template <typename T>
 __device__ __forceinline__ void store8(T* __restrict__ p, const float (&in)[8]) {
-  Vec8<T> o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o.v[j] = from_f32<T>(in[j]);
-  *reinterpret_cast<Vec8<T>*>(p) = o;
+  *reinterpret_cast<uint4*>(p) = make_uint4(pk2<T>(in[0], in[1]), pk2<T>(in[2], in[3]),
+                                            pk2<T>(in[4], in[5]), pk2<T>(in[6], in[7]));
 }
 
 template <>

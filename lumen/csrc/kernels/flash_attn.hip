@@ -90,8 +90,12 @@ __device__ __forceinline__ void stage64_async(char* img, const T* base, long lon
   }
 }
 
-__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_vm_8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+// vmcnt waits as the s_waitcnt builtin (gfx9 simm16: vmcnt bits [3:0], expcnt [6:4] = 7,
+// lgkmcnt [11:8] = 15 i.e. "don't care"), NOT inline asm: the compiler's wait-insertion pass
+// sees the builtin, knows that every LDS-DMA older than the newest N has landed, and does not add
+// its own vmcnt(0) in front of the ds_reads of the tile just waited for.
+__device__ __forceinline__ void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0xF70); }
+__device__ __forceinline__ void wait_vm_8() { __builtin_amdgcn_s_waitcnt(0xF78); }
 __device__ __forceinline__ void lds_fence_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -363,10 +367,7 @@ __device__ __forceinline__ uint4 tr_read_img2(const char* img, int rlo, int rhi,
 
 template <typename T>
 __device__ __forceinline__ uint4 pack_p(const f32x4& a, const f32x4& b) {
-  struct alignas(16) P8 { T v[8]; } o;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) { o.v[r] = from_f32<T>(a[r]); o.v[4 + r] = from_f32<T>(b[r]); }
-  return __builtin_bit_cast(uint4, o);
+  return make_uint4(pk2<T>(a[0], a[1]), pk2<T>(a[2], a[3]), pk2<T>(b[0], b[1]), pk2<T>(b[2], b[3]));
 }
 
 template <typename T, bool CAUSAL, int QG>
@@ -801,10 +802,8 @@ __device__ __forceinline__ uint4 tr_read32(const char* img, int r0, int n0, int 
 // registers 8s..8s+7 of a 32x32 accumulator -> 8 packed 16-bit values (a k=16 operand)
 template <typename T>
 __device__ __forceinline__ uint4 pack8(const f32x16& c, int s) {
-  struct alignas(16) P8 { T v[8]; } o;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) o.v[e] = from_f32<T>(c[8 * s + e]);
-  return __builtin_bit_cast(uint4, o);
+  return make_uint4(pk2<T>(c[8 * s], c[8 * s + 1]), pk2<T>(c[8 * s + 2], c[8 * s + 3]),
+                    pk2<T>(c[8 * s + 4], c[8 * s + 5]), pk2<T>(c[8 * s + 6], c[8 * s + 7]));
 }
 
 // ---- forward: S^T = K Q^T (keys on rows, lane = query), O^T += V^T P^T -----------------------
@@ -833,6 +832,41 @@ __device__ __forceinline__ uint4 tr32(const char* img, const Off32& o, int rowba
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
+// LDS reads as inline asm.  The compiler's wait insertion cannot tell that the LDS-DMA prefetch
+// in flight targets the OTHER ping-pong buffer, so before any plain ds_read of the current tile
+// it emits s_waitcnt vmcnt(0) -- waiting for the prefetch it was meant to overlap (seen in the
+// ISA of every kernel in this file).  Inline asm is opaque to that pass; the tile code waits for
+// its own reads with lgkm_wait(), whose register operands order every consumer after it.
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned lds_off(const char* p) {
+  return static_cast<unsigned>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)(p)));
+}
+template <int OFF>
+__device__ __forceinline__ u32x4v ds_b128(unsigned a) {
+  u32x4v r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ u32x2v ds_tr64(unsigned a) {
+  u32x2v r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+__device__ __forceinline__ void lgkm_wait(u32x4v& a, u32x4v& b, u32x4v& c, u32x4v& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ uint4 as_u4(u32x4v v) { return __builtin_bit_cast(uint4, v); }
+// V^T / K^T operand of the 32x32x16 products (tr32 above) for key block rowbase = 16 * RB
+template <int RB>
+__device__ __forceinline__ u32x4v tr32a(unsigned img, const Off32& o, int n) {
+  const u32x2v lo = ds_tr64<RB * 16 * 256>(img + o.tr[2 * n]);
+  const u32x2v hi = ds_tr64<RB * 16 * 256>(img + o.tr[2 * n + 1]);
+  return u32x4v{lo.x, lo.y, hi.x, hi.y};
+}
+
 template <typename T, bool CAUSAL, bool MASK>
 __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, const Off32& off,
                                            const uint4 (&qf)[8], f32x16 (&acc)[4], float& m_i,
@@ -841,11 +875,23 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
   f32x16 st[2];
   st[0] = zero16();
   st[1] = zero16();
+  {
+    const unsigned kb0 = lds_off(kimg);
+    u32x4v kr[2][8];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
+    for (int ks = 0; ks < 8; ++ks) {
+      kr[0][ks] = ds_b128<0>(kb0 + off.row[ks]);
+      kr[1][ks] = ds_b128<8192>(kb0 + off.row[ks]);
+    }
+    lgkm_wait(kr[0][0], kr[0][1], kr[0][2], kr[0][3]);
+    lgkm_wait(kr[0][4], kr[0][5], kr[0][6], kr[0][7]);
+    lgkm_wait(kr[1][0], kr[1][1], kr[1][2], kr[1][3]);
+    lgkm_wait(kr[1][4], kr[1][5], kr[1][6], kr[1][7]);
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-      st[kb] = Mfma32<T>::run(lds16(kimg + kb * 8192 + off.row[ks]), qf[ks], st[kb]);
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) st[kb] = Mfma32<T>::run(as_u4(kr[kb][ks]), qf[ks], st[kb]);
+    }
   }
   float mx = -INFINITY;
 #pragma unroll
@@ -887,21 +933,35 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
   rs += __shfl_xor(rs, 32);
   l_i += rs;
   // O^T[d][q] += V^T[d][key] P^T[key][q], keys in the register order
+  const unsigned vb = lds_off(vimg);
+  u32x4v vr[4][4];  // [16-key slice kb * 2 + s][output block n]
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+  for (int n = 0; n < 4; ++n) {
+    vr[0][n] = tr32a<0>(vb, off, n);
+    vr[1][n] = tr32a<1>(vb, off, n);
+    vr[2][n] = tr32a<2>(vb, off, n);
+    vr[3][n] = tr32a<3>(vb, off, n);
+  }
+  const uint4 pb[4] = {pack8<T>(st[0], 0), pack8<T>(st[0], 1), pack8<T>(st[1], 0),
+                       pack8<T>(st[1], 1)};
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const uint4 pb = pack8<T>(st[kb], s);
+  for (int sl = 0; sl < 4; ++sl) {
+    lgkm_wait(vr[sl][0], vr[sl][1], vr[sl][2], vr[sl][3]);
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-        acc[n] = Mfma32<T>::run(tr32(vimg, off, kb * 32 + 16 * s, n), pb, acc[n]);
-    }
+    for (int n = 0; n < 4; ++n) acc[n] = Mfma32<T>::run(as_u4(vr[sl][n]), pb[sl], acc[n]);
+  }
 }
 
 template <typename T, bool CAUSAL>
 __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   constexpr int BM = 128;
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [K0 | V0 | K1 | V1]
+  // Two SEPARATE LDS objects for the ping-pong K|V buffers, with the loop unrolled by two so
+  // every LDS-DMA and every ds_read names its buffer statically: the compiler's wait insertion
+  // tracks LDS-DMA per LDS object, and with one array indexed by (it & 1) it had to assume the
+  // in-flight prefetch aliases the tile being read and put an s_waitcnt vmcnt(0) in front of the
+  // first ds_read -- which serialised every prefetch against the compute it was meant to hide.
+  __shared__ __attribute__((aligned(16))) char bufA[2 * IMG];  // [K | V]
+  __shared__ __attribute__((aligned(16))) char bufB[2 * IMG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lq = lane & 31, hi = lane >> 5;
   const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
@@ -924,18 +984,16 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   float m_i = -INFINITY, l_i = 0.f;
   const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
   const int w_end = CAUSAL ? min(kv_end, wq0 + 32) : kv_end;  // keys this wave can see
+  wait_vm_all();  // Q fragments in registers before the DMA ring starts (exact vmcnt below)
   if (kv_end > 0) {
-    stage64_async(smem, K, a.ldk, 0, L);
-    stage64_async(smem + IMG, V, a.ldv, 0, L);
+    stage64_async(bufA, K, a.ldk, 0, L);
+    stage64_async(bufA + IMG, V, a.ldv, 0, L);
   }
-  int it = 0;
-  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
-    char* kimg = smem + (it & 1) * 2 * IMG;
-    char* vimg = kimg + IMG;
+  // one K/V tile: prefetch the next into `nxt`, wait for `cur`, compute, release `cur`
+  auto tile = [&](char* cur, char* nxt, int kv0) {
     if (kv0 + BN < kv_end) {
-      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
-      stage64_async(nk, K, a.ldk, kv0 + BN, L);
-      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
+      stage64_async(nxt, K, a.ldk, kv0 + BN, L);
+      stage64_async(nxt + IMG, V, a.ldv, kv0 + BN, L);
       wait_vm_8();
     } else {
       wait_vm_all();
@@ -944,13 +1002,17 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
     if (kv0 < w_end) {  // (causal: tiles entirely above this wave's rows are skipped)
       const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
       if (need_mask)
-        fwd32_tile<T, CAUSAL, true>(kimg, vimg, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
+        fwd32_tile<T, CAUSAL, true>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
                                     a.scale_log2);
       else
-        fwd32_tile<T, CAUSAL, false>(kimg, vimg, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
+        fwd32_tile<T, CAUSAL, false>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
                                      a.scale_log2);
     }
-    lds_fence_barrier();  // every wave is done with this K/V buffer before it is refilled
+    lds_fence_barrier();  // every wave is done with `cur` before it is refilled
+  };
+  for (int kv0 = 0; kv0 < kv_end; kv0 += 2 * BN) {
+    tile(bufA, bufB, kv0);
+    if (kv0 + BN < kv_end) tile(bufB, bufA, kv0 + BN);
   }
   // epilogue: lane holds O[qrow][32n + 8j + 4hi + i] in acc[n][4j + i]
   if (qrow < L) {

@@ -63,10 +63,8 @@ __device__ __forceinline__ uint4 tr_read_img(const char* img, int k0, int n0, in
 // 8 floats -> 8 packed 16-bit values (round to nearest even)
 template <typename T>
 __device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
-  Vec8<T> o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o.v[j] = from_f32<T>(v[j]);
-  return __builtin_bit_cast(uint4, o);
+  return make_uint4(pk2<T>(v[0], v[1]), pk2<T>(v[2], v[3]), pk2<T>(v[4], v[5]),
+                    pk2<T>(v[6], v[7]));
 }
 
 template <typename T>

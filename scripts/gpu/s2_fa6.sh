@@ -2,8 +2,8 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/s2_fa4; mkdir -p $O; rm -f $O/bench.jsonl
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "flash_attention" -x -q --timeout 120 --timeout-method thread > $O/fa_tests.log 2>&1
+O=gpurun_out/s2_fa6; mkdir -p $O; rm -f $O/bench.jsonl
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "flash_attention or rmsnorm or swiglu or lora or rope or cross_entropy" -x -q --timeout 120 --timeout-method thread > $O/fa_tests.log 2>&1
 rc=$?; echo "fa tests rc=$rc"; tail -2 $O/fa_tests.log; [ $rc -eq 0 ] || exit $rc
 for v in "t1 v16" "v32 v32" "v32 mix"; do set -- $v
   LUMEN_FA_FWD=$1 LUMEN_FA_BWD=$2 timeout -k 10 120 python lumen/bench/attn_bench.py --only all >> $O/bench.jsonl 2>$O/bench.err || exit 1
