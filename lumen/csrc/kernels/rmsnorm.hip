@@ -29,13 +29,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
   if (row >= rows) return;
   const size_t base = static_cast<size_t>(row) * H;
   float v[VPL][8];
-  uint4 wraw[VPL];  // weight chunks loaded with the row: one round of memory latency, not two
   float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPL; ++i) {
-    const int c = (lane + i * 64) * 8;
-    if (c < H) wraw[i] = *reinterpret_cast<const uint4*>(w + c);
-  }
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = (lane + i * 64) * 8;
@@ -67,7 +61,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
         store8(s_out + base + c, sr);
       }
       float wv[8], o[8];
-      load8(reinterpret_cast<const T*>(&wraw[i]), wv);
+      load8(w + c, wv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[j];
       store8(y + base + c, o);
