@@ -53,8 +53,12 @@ __attribute__((target("avx512f"))) void adam_avx512(float* p, const float* g, fl
 }
 
 bool has_avx512() {
+#ifdef LUMEN_NO_AVX512  // sanitizer harness: exercise the portable path too
+  return false;
+#else
   static const int cached = __builtin_cpu_supports("avx512f") ? 1 : 0;
   return cached != 0;
+#endif
 }
 
 }  // namespace

@@ -106,8 +106,11 @@ def _v2_ok(r: int, R: int, *mats) -> bool:
             and all(m.stride(0) % 8 == 0 and m.stride(1) == 1 for m in mats))
 
 
-def _split(blocks_per_split: int, reduce_len: int, chunk: int, target: int = 512) -> int:
-    s = max(1, math.ceil(target / max(blocks_per_split, 1)))
+SPLIT_TARGET = int(_os.environ.get("LUMEN_LORA_SPLIT_TARGET", "512"))  # blocks per launch
+
+
+def _split(blocks_per_split: int, reduce_len: int, chunk: int, target: int = 0) -> int:
+    s = max(1, math.ceil((target or SPLIT_TARGET) / max(blocks_per_split, 1)))
     return int(max(1, min(s, reduce_len // chunk)))
 
 
