@@ -324,6 +324,9 @@ class ParamCoordinator:
         self._in_step = False
         self.gathered_bytes = 0    # bytes materialised by gathers (all ranks' shards)
         self.gathers = 0
+        from ..utils.debug import zero3_poison_enabled
+
+        self.poison = zero3_poison_enabled()
 
     def _hbm_live_budget(self, elem_bytes: int) -> int:
         """``stage3_max_live_parameters: "auto"``: elements of gathered weights that fit in the
@@ -352,6 +355,8 @@ class ParamCoordinator:
             return
         if u.bufs[slot] is None:
             u.bufs[slot] = torch.empty(u.padded, dtype=u.dtype, device=self.device)
+        if self.poison:  # race detector: stale reads of this buffer now see NaN
+            u.bufs[slot].fill_(float("nan"))
         shard = u.shard
         if self.offload:
             shard = shard.to(self.device, non_blocking=True)

@@ -15,6 +15,12 @@ pays nothing when they are off:
                            on the flat gradient buffer after every backward, and a device sync
                            around collectives (stream-ordering bugs surface as errors at the
                            offending call instead of wrong numbers later).
+``LUMEN_ZERO3_POISON=1``   race detector for the ZeRO-3 gather schedules (also on under
+                           ``LUMEN_DEBUG``): every gathered-weight buffer is filled with NaN on the
+                           compute stream right before it is (re-)gathered, so a kernel that reads
+                           a buffer outside its live window -- the refresh of the keep schedule, the
+                           next-step slot of the pipelined one -- turns the loss NaN at once
+                           instead of silently reading identical-looking stale weights.
 ``LUMEN_FAULT_STEP=k``     fault injection: the rank(s) in ``LUMEN_FAULT_RANK`` (default 0) exit
                            with code 17 right after optimizer step k (after any checkpoint of
                            that step).  Used by the kill-and-resume equality test.
@@ -129,3 +135,7 @@ def maybe_inject_fault(step: int, rank: int) -> None:
     if rank in ranks:
         print(f"[lumen fault] rank {rank} exiting at step {step}", flush=True)
         os._exit(FAULT_EXIT_CODE)
+
+
+def zero3_poison_enabled() -> bool:
+    return debug_enabled() or os.environ.get("LUMEN_ZERO3_POISON", "0") not in ("", "0")

@@ -3,6 +3,8 @@ backward time through ``weight_fn``), on a one-GPU box: ``LUMEN_ZERO3_SINGLE=1``
 world size 1, where a gather is an async copy on a side stream with the same stream ordering
 as RCCL's.  Every schedule (release / keep / pipelined), with accumulation and activation
 checkpointing, must give the stage-0 trajectory."""
+import math
+
 import pytest
 import torch
 
@@ -105,3 +107,21 @@ def test_reference_zero3_config_with_cpu_offload(monkeypatch):
         d = (got[k] - ref[k]).abs()
         assert d.max().item() < 4e-3, k
         assert (d > 3e-4 + 5e-3 * ref[k].abs()).float().mean().item() < 5e-3, k
+
+
+@pytest.mark.parametrize("schedule", ["keep", "pipelined", "release"])
+def test_zero3_schedules_race_free_under_nan_poison(schedule, monkeypatch):
+    """Race detector: with LUMEN_ZERO3_POISON every buffer is NaN-filled right before each
+    (re-)gather.  A read outside a buffer's live window would make the loss NaN; the run must
+    match the unpoisoned one."""
+    ref, ref_losses, _ = _train(monkeypatch, 3, schedule, ckpt=True, steps=3)
+    monkeypatch.setenv("LUMEN_ZERO3_POISON", "1")
+    got, losses, coord = _train(monkeypatch, 3, schedule, ckpt=True, steps=3)
+    assert coord.poison
+    assert all(math.isfinite(x) for x in losses)
+    # (not bitwise: the LoRA kernels' split-K f32 atomics make run-to-run rounding differ)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 1e-3 * max(1.0, abs(b))
+    for k in ref:
+        assert torch.isfinite(got[k]).all(), k
+        torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)

@@ -79,9 +79,10 @@ def test_zero3_schedules_accumulation_checkpointing(schedule, gc, tmp_path):
 
 
 @pytest.mark.parametrize("schedule", ["keep", "pipelined", "release"])
-def test_zero3_world1_partitioned(schedule, tmp_path):
+def test_zero3_world1_partitioned(schedule, tmp_path, monkeypatch):
     """LUMEN_ZERO3_SINGLE=1: the coordinator at world size 1 (local gathers) == stage 0."""
     ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama", micro=2, accum=2, steps=2)
+    monkeypatch.setenv("LUMEN_ZERO3_POISON", "1")  # NaN-poisoned buffers: no stale reads
     r = _run(1, 3, str(tmp_path / "b"), model="tiny-llama", micro=2, accum=2, steps=2,
              extra={"schedule": schedule, "gc": True, "single": True})
     _close(r["sd"], ref["sd"])
