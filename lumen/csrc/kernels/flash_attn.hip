@@ -867,6 +867,29 @@ __device__ __forceinline__ u32x4v tr32a(unsigned img, const Off32& o, int n) {
   return u32x4v{lo.x, lo.y, hi.x, hi.y};
 }
 
+// xor-32 lane exchange on the VALU (v_permlane32_swap, gfx950) instead of ds_bpermute through
+// LDS: both operands must be distinct registers holding the value (the builtin, given the same
+// value twice, gets them coalesced into one register and returns the lane's own value;
+// scripts/probes/permlane_probe.hip).
+__device__ __forceinline__ void xor32_pair(float v, float& a, float& b) {
+  unsigned x = __builtin_bit_cast(unsigned, v), y = x;
+  // s_nop padding: inline asm is invisible to the compiler's hazard recognizer, and the swap
+  // reads VGPRs a VALU just wrote (and its results feed the next VALU)
+  asm volatile("s_nop 4\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 4" : "+v"(x), "+v"(y));
+  a = __builtin_bit_cast(float, x);
+  b = __builtin_bit_cast(float, y);
+}
+__device__ __forceinline__ float xor32_max(float v) {
+  float a, b;
+  xor32_pair(v, a, b);
+  return fmaxf(a, b);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  float a, b;
+  xor32_pair(v, a, b);
+  return a + b;
+}
+
 template <typename T, bool CAUSAL, bool MASK>
 __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, const Off32& off,
                                            const uint4 (&qf)[8], f32x16 (&acc)[4], float& m_i,
@@ -905,7 +928,7 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
       }
       mx = fmaxf(mx, st[kb][r]);
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 32)) * scale_log2;
+  mx = xor32_max(mx) * scale_log2;
   // deferred rescale: the running max moves only when a row's new max exceeds it by more than
   // RESCALE (log2 units), so P stays <= 2^RESCALE and the O / l rescale (64 multiplies per lane)
   // runs on a handful of tiles per row instead of every tile
@@ -930,8 +953,7 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
       st[kb][r] = p;
       rs += p;
     }
-  rs += __shfl_xor(rs, 32);
-  l_i += rs;
+  l_i += xor32_sum(rs);
   // O^T[d][q] += V^T[d][key] P^T[key][q], keys in the register order
   const unsigned vb = lds_off(vimg);
   u32x4v vr[4][4];  // [16-key slice kb * 2 + s][output block n]
