@@ -7,8 +7,62 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
+def _time(fn, ws, reps=20):
+    import torch
+
+    for w in ws:
+        fn(w)
+    torch.cuda.synchronize()
+    it = reps * len(ws)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(it):
+        fn(ws[i % len(ws)])
+    e1.record()
+    torch.cuda.synchronize()
+    return round(e0.elapsed_time(e1) * 1e3 / it, 2)
+
+
+def m1_forms():
+    """Batch-1 kernel forms: row-group (form 0) vs rows-per-lane (form 1), plain and with the
+    SwiGLU activation fused into the down projection (vs swiglu kernel + GEMV)."""
+    import torch
+
+    from lumen.ops._native import native
+    from lumen.ops.activation import swiglu
+
+    dev = "cuda"
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096),
+              "down": (4096, 11008)}
+    for name, (N, K) in shapes.items():
+        copies = max(2, int(600e6 // (N * K * 2)))
+        ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        x = torch.randn(1, K, device=dev).to(torch.bfloat16)
+        y = torch.empty(1, N, device=dev, dtype=torch.bfloat16)
+        row = {"shape": name, "N": N, "K": K}
+        for form in (0, 1):
+            native().set_gemv_form(form)
+            row[f"form{form}_us"] = _time(lambda w: native().skinny_gemm(x, w, y), ws)
+            row[f"form{form}_TBps"] = round(N * K * 2 / (row[f"form{form}_us"] * 1e-6) / 1e12, 2)
+        row["hipblaslt_us"] = _time(lambda w: torch.matmul(x, w.t()), ws)
+        if name == "down":
+            gu = torch.randn(1, 2 * K, device=dev).to(torch.bfloat16)
+            for form in (0, 1):
+                native().set_gemv_form(form)
+                row[f"swiglu_fused_form{form}_us"] = _time(
+                    lambda w: native().gemv_swiglu(gu, w, y), ws)
+                row[f"swiglu_then_gemv_form{form}_us"] = _time(
+                    lambda w: native().skinny_gemm(swiglu(gu), w, y), ws)
+        native().set_gemv_form(1)
+        print(json.dumps(row), flush=True)
+        del ws
+
+
 def main():
     import torch
+
+    if "--m1-forms" in sys.argv:
+        return m1_forms()
 
     from lumen.ops._native import native
     from lumen.utils.gemm_tuning import load_tuned_gemms

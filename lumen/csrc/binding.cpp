@@ -38,11 +38,16 @@ hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long
                        const long long*, const int*, const float*, const float*, const int*, int,
                        hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
+hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, const float*, void*,
+                            void*, const long long*, int, int, int, int, int, hipStream_t);
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
+hipError_t lumen_gemv_swiglu(int, const void*, const void*, void*, int, int, long long, long long,
+                             hipStream_t);
+void lumen_set_gemv_form(int);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
-                                        float, float*, float*, void*, int, hipStream_t);
+                                        float, float*, float*, void*, int, unsigned*, hipStream_t);
 hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, const long long*,
                                    int, int, int, int, long long, long long, int, hipStream_t);
 hipError_t lumen_sample(int, const void*, const float*, const float*, const int*,
@@ -165,6 +170,22 @@ void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
         "skinny_gemm");
 }
 
+// y[1, N] = swiglu(gu[1, 2F]) @ w[N, F]^T with the activation formed inside the weight stream
+void gemv_swiglu(const at::Tensor& gu, const at::Tensor& w, at::Tensor& y) {
+  if (!gu.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: gemv_swiglu needs GPU tensors");
+  need_cuda(w, "w");
+  if (gu.dim() != 2 || w.dim() != 2 || y.dim() != 2 || gu.size(0) != 1 || y.size(0) != 1 ||
+      gu.stride(1) != 1 || y.stride(1) != 1 || !w.is_contiguous() ||
+      gu.size(1) != 2 * w.size(1) || y.size(1) != w.size(0) || w.size(0) % 4 != 0 ||
+      w.size(1) % 8 != 0 || gu.scalar_type() != w.scalar_type() ||
+      y.scalar_type() != w.scalar_type())
+    throw std::invalid_argument("lumen: gemv_swiglu shape/layout mismatch");
+  check(lumen_gemv_swiglu(dcode(w), gu.data_ptr(), w.data_ptr(), y.data_ptr(),
+                          static_cast<int>(w.size(0)), static_cast<int>(w.size(1)), gu.stride(0),
+                          y.stride(0), cur_stream()),
+        "gemv_swiglu");
+}
+
 void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
                    const std::optional<at::Tensor>& row_loss, int64_t ignore_index, double scale,
                    bool write_grad) {
@@ -277,11 +298,20 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                             const at::Tensor& v_cache, const at::Tensor& block_tables,
                             const at::Tensor& context_lens, int64_t num_kv_heads, int64_t block_size,
                             int64_t max_blocks_per_seq, double scale, at::Tensor& tmp_m,
-                            at::Tensor& tmp_l, at::Tensor& tmp_o, int64_t partition_size) {
+                            at::Tensor& tmp_l, at::Tensor& tmp_o, int64_t partition_size,
+                            const std::optional<at::Tensor>& counters) {
   need_cuda(q, "q"); need_cuda(out, "out");
   const int num_seqs = static_cast<int>(q.size(0));
   const int nh = static_cast<int>(q.size(1));
   const int D = static_cast<int>(q.size(2));
+  unsigned* cnt = nullptr;
+  if (counters.has_value()) {
+    const at::Tensor& c = *counters;
+    need_cuda(c, "counters");
+    if (c.scalar_type() != at::kInt || c.numel() < static_cast<int64_t>(num_seqs) * num_kv_heads)
+      throw std::invalid_argument("lumen: paged_attention_decode counters must be int32 >= nseq*nkv");
+    cnt = reinterpret_cast<unsigned*>(c.data_ptr<int>());
+  }
   check(lumen_paged_attention_decode(dcode(q), out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
                                      v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                      context_lens.data_ptr<int>(), num_seqs, nh,
@@ -289,7 +319,8 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                                      static_cast<int>(max_blocks_per_seq),
                                      static_cast<int>(tmp_m.size(-1)), static_cast<float>(scale),
                                      tmp_m.data_ptr<float>(), tmp_l.data_ptr<float>(),
-                                     tmp_o.data_ptr(), static_cast<int>(partition_size), cur_stream()),
+                                     tmp_o.data_ptr(), static_cast<int>(partition_size), cnt,
+                                     cur_stream()),
         "paged_attention_decode");
 }
 
@@ -302,6 +333,29 @@ void reshape_and_cache(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_c
                                 static_cast<int>(num_kv_heads), static_cast<int>(D),
                                 static_cast<int>(block_size), k_stride, v_stride, 0, cur_stream()),
         "reshape_and_cache");
+}
+
+void rope_cache_write(at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos_t,
+                      const at::Tensor& sin_t, at::Tensor& k_cache, at::Tensor& v_cache,
+                      const at::Tensor& slots, int64_t nh, int64_t nkv, int64_t D,
+                      int64_t block_size) {
+  if (!qkv.is_cuda() || qkv.dim() != 2 || qkv.stride(1) != 1)
+    throw std::invalid_argument("lumen: rope_cache_write needs a 2-D GPU qkv with unit column stride");
+  need_cuda(pos, "pos"); need_cuda(cos_t, "cos"); need_cuda(sin_t, "sin");
+  need_cuda(k_cache, "k_cache"); need_cuda(v_cache, "v_cache"); need_cuda(slots, "slots");
+  if (pos.scalar_type() != at::kInt || slots.scalar_type() != at::kLong ||
+      cos_t.scalar_type() != at::kFloat || sin_t.scalar_type() != at::kFloat ||
+      qkv.size(1) < (nh + 2 * nkv) * D || pos.numel() < qkv.size(0) ||
+      slots.numel() < qkv.size(0))
+    throw std::invalid_argument("lumen: rope_cache_write argument mismatch");
+  check(lumen_rope_cache(dcode(qkv), qkv.data_ptr(), qkv.stride(0), pos.data_ptr<int>(),
+                         cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), k_cache.data_ptr(),
+                         v_cache.data_ptr(),
+                         reinterpret_cast<const long long*>(slots.data_ptr<int64_t>()),
+                         static_cast<int>(qkv.size(0)), static_cast<int>(nh),
+                         static_cast<int>(nkv), static_cast<int>(D),
+                         static_cast<int>(block_size), cur_stream()),
+        "rope_cache_write");
 }
 
 void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& top_p,
@@ -431,6 +485,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora2", &lora2);
   m.def("transpose2d", &transpose2d);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("gemv_swiglu", &gemv_swiglu);
+  m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
+  m.def("rope_cache_write", &rope_cache_write);
   m.def("paged_attention_decode", &paged_attention_decode);
   m.def("reshape_and_cache", &reshape_and_cache);
   m.def("sample", &sample);

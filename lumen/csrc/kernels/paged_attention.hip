@@ -41,13 +41,20 @@ __device__ __forceinline__ float pa_red16(float v) {
   return v;
 }
 
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T, int D, int G>
 __global__ void __launch_bounds__(256) pa_decode_kernel(
     T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
     const T* __restrict__ vc, const int* __restrict__ block_tables,
     const int* __restrict__ context_lens, int nh, int nkv, int BS, int max_blocks, int max_parts,
     float scale, float* __restrict__ tmp_m, float* __restrict__ tmp_l, float* __restrict__ tmp_o,
-    int PART) {
+    int PART, unsigned* __restrict__ counters) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int LPT = D / 8;        // lanes per cache row (16-byte chunk each)
   constexpr int RPS = 256 / LPT;    // rows per workgroup step
@@ -162,17 +169,51 @@ __global__ void __launch_bounds__(256) pa_decode_kernel(
       for (int j = 0; j < 8; ++j) red[(wid * G + h) * D + d0 + j] = acc[h][j];
   }
   __syncthreads();
+  const int nparts = (ctx + PART - 1) / PART;
   for (int i = tid; i < G * D; i += 256) {
     const float o = red[i] + red[G * D + i] + red[2 * G * D + i] + red[3 * G * D + i];
     const int h = i / D, d = i % D;
     const int head = kvh * G + h;
-    if (max_parts == 1) {
+    if (nparts == 1) {  // the whole context in this partition: final output directly
       out[(static_cast<size_t>(seq) * nh + head) * D + d] = from_f32<T>(o / ml[G + h]);
     } else {
       const size_t mi = (static_cast<size_t>(seq) * nh + head) * max_parts + part;
-      tmp_o[mi * D + d] = o;
-      if (d == 0) { tmp_m[mi] = ml[h]; tmp_l[mi] = ml[G + h]; }
+      st_agent(tmp_o + mi * D + d, o);
+      if (d == 0) { st_agent(tmp_m + mi, ml[h]); st_agent(tmp_l + mi, ml[G + h]); }
     }
+  }
+  if (nparts == 1 || counters == nullptr) return;
+  // Split context, fused merge: the last partition of this (sequence, kv-head) to arrive merges
+  // all partials (no second launch).  Partitions run on different XCDs, whose L2s are not
+  // coherent with each other: the partials go out as agent-scope stores (sc1, written through
+  // to the coherent level) and are read back with agent-scope loads, and every store has
+  // completed (vmcnt(0)) before the arrival count, so no L2 writeback / invalidate (the
+  // buffer_wbl2 + buffer_inv of __threadfence(), measured 7x slower decode steps) is needed.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's partial stores are complete
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(ml + 2 * G);
+  if (tid == 0) {
+    unsigned* cp = counters + static_cast<size_t>(seq) * nkv + kvh;
+    const unsigned prev = __hip_atomic_fetch_add(cp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == static_cast<unsigned>(nparts - 1);
+    if (last)  // self-resetting for the next launch (next layer)
+      __hip_atomic_store(cp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  for (int i = tid; i < G * D; i += 256) {
+    const int h = i / D, d = i % D;
+    const size_t base = (static_cast<size_t>(seq) * nh + kvh * G + h) * max_parts;
+    float M = -INFINITY;
+    for (int p = 0; p < nparts; ++p) M = fmaxf(M, ld_agent(tmp_m + base + p));
+    float L = 0.f, o = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      const float w = __expf(ld_agent(tmp_m + base + p) - M);
+      L += ld_agent(tmp_l + base + p) * w;
+      o += ld_agent(tmp_o + (base + p) * D + d) * w;
+    }
+    out[(base / max_parts) * D + d] = from_f32<T>(o / L);
   }
 }
 
@@ -185,6 +226,7 @@ __global__ void __launch_bounds__(256) pa_reduce_kernel(T* __restrict__ out,
                                                         int D, int max_parts, int PART) {
   const int seq = blockIdx.x, head = blockIdx.y;
   const int nparts = (context_lens[seq] + PART - 1) / PART;
+  if (nparts <= 1) return;  // written directly by the decode kernel
   const size_t base = (static_cast<size_t>(seq) * nh + head) * max_parts;
   float M = -INFINITY;
   for (int p = 0; p < nparts; ++p) M = fmaxf(M, tmp_m[base + p]);
@@ -220,15 +262,62 @@ __global__ void __launch_bounds__(256) cache_write_kernel(
       *reinterpret_cast<const uint4*>(v + t * v_stride + static_cast<long long>(h) * D + c * 8);
 }
 
+// RoPE of the q and k heads of the fused token-major QKV rows AND the paged KV-cache write of
+// the rotated k and of v, in one pass (serving: prefill and decode).  Replaces rope_inplace +
+// cache_write: at batch-1 decode each of those was a ~5 us launch per layer for a few KB.
+// Thread = (token, head of q|k|v, 16-element chunk pair i0 / i0 + D/2).
+template <typename T>
+__global__ void __launch_bounds__(256) rope_cache_kernel(
+    T* __restrict__ qkv, long long ld, const int* __restrict__ pos,
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t, T* __restrict__ kc,
+    T* __restrict__ vc, const long long* __restrict__ slots, int ntok, int nh, int nkv, int D,
+    int BS) {
+  const int half = D / 2, chunks = D / 16, H = nh + 2 * nkv;
+  const long long tid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (tid >= static_cast<long long>(ntok) * H * chunks) return;
+  const int c = static_cast<int>(tid % chunks);
+  const int h = static_cast<int>((tid / chunks) % H);
+  const int t = static_cast<int>(tid / (static_cast<long long>(chunks) * H));
+  const int i0 = c * 8;
+  T* row = qkv + static_cast<long long>(t) * ld + static_cast<long long>(h) * D;
+  const long long slot = slots[t];
+  const int hk = h - nh - (h >= nh + nkv ? nkv : 0);  // kv head index for k / v heads
+  const size_t dst = slot >= 0 ? ((static_cast<size_t>(slot / BS) * nkv + hk) * BS + slot % BS) * D
+                               : 0;
+  if (h < nh + nkv) {
+    const int p = pos[t];
+    float cs[8], sn[8], a[8], b[8], oa[8], ob[8];
+    load8(cos_t + static_cast<size_t>(p) * half + i0, cs);
+    load8(sin_t + static_cast<size_t>(p) * half + i0, sn);
+    load8(row + i0, a);
+    load8(row + i0 + half, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      oa[j] = a[j] * cs[j] - b[j] * sn[j];
+      ob[j] = b[j] * cs[j] + a[j] * sn[j];
+    }
+    store8(row + i0, oa);
+    store8(row + i0 + half, ob);
+    if (h >= nh && slot >= 0) {
+      store8(kc + dst + i0, oa);
+      store8(kc + dst + i0 + half, ob);
+    }
+  } else if (slot >= 0) {
+    *reinterpret_cast<uint4*>(vc + dst + i0) = *reinterpret_cast<const uint4*>(row + i0);
+    *reinterpret_cast<uint4*>(vc + dst + i0 + half) =
+        *reinterpret_cast<const uint4*>(row + i0 + half);
+  }
+}
+
 template <typename T, int D>
 static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out, const void* q,
                         const void* kc, const void* vc, const int* bt, const int* cl, int nh,
                         int nkv, int BS, int max_blocks, int max_parts, float scale, float* tm,
-                        float* tl, void* to, int PART) {
+                        float* tl, void* to, int PART, unsigned* cnt) {
 #define LUMEN_PA_G(GG)                                                                         \
   hipLaunchKernelGGL((pa_decode_kernel<T, D, GG>), grid, dim3(256), smem, st, (T*)out,         \
                      (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks,  \
-                     max_parts, scale, tm, tl, (float*)to, PART)
+                     max_parts, scale, tm, tl, (float*)to, PART, cnt)
   if (G == 1) LUMEN_PA_G(1);
   else if (G == 2) LUMEN_PA_G(2);
   else if (G == 4) LUMEN_PA_G(4);
@@ -240,17 +329,17 @@ template <typename T>
 static hipError_t launch_pa(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, const int* cl, int nseq, int nh, int nkv, int D, int BS,
                             int max_blocks, int max_parts, float scale, float* tm, float* tl,
-                            void* to, int PART, hipStream_t st) {
+                            void* to, int PART, unsigned* cnt, hipStream_t st) {
   const int G = nh / nkv;
   if (G != 1 && G != 2 && G != 4 && G != 8) return hipErrorInvalidValue;
   dim3 grid(nseq, nkv, max_parts);
   const size_t smem = (static_cast<size_t>(G) * PART + 4 * G * D + 2 * G + 8) * sizeof(float);
-  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
-  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
-  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
-  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART);
+  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
+  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
+  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
+  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
   else return hipErrorInvalidValue;
-  if (max_parts > 1) {
+  if (max_parts > 1 && cnt == nullptr) {  // unfused merge: second kernel
     dim3 g2(nseq, nh), b2(128);
     hipLaunchKernelGGL(pa_reduce_kernel<T>, g2, b2, 0, st, (T*)out, cl, tm, tl,
                        (const float*)to, nh, D, max_parts, PART);
@@ -267,17 +356,19 @@ extern "C" hipError_t lumen_paged_attention_decode(int dtype, void* out, const v
                                                    int nkv, int D, int BS, int max_blocks,
                                                    int max_parts, float scale, float* tmp_m,
                                                    float* tmp_l, void* tmp_o, int PART,
-                                                   hipStream_t st) {
+                                                   unsigned* counters, hipStream_t st) {
+  // counters: nullptr = merge split contexts in a second kernel; else >= nseq * nkv zeroed
+  // arrival counters (left zeroed again) and the last partition to finish merges in place.
   if (nseq == 0) return hipSuccess;
   if (nh % nkv != 0 || nh / nkv > lumen::kMaxGroup || PART <= 0) return hipErrorInvalidValue;
   if (dtype == lumen::kBF16)
     return lumen::launch_pa<lumen::bf16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, st);
+                                         tmp_o, PART, counters, st);
   if (dtype == lumen::kF16)
     return lumen::launch_pa<lumen::fp16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, st);
+                                         tmp_o, PART, counters, st);
   return hipErrorInvalidValue;
 }
 
@@ -298,6 +389,27 @@ extern "C" hipError_t lumen_reshape_and_cache(int dtype, const void* k, const vo
     hipLaunchKernelGGL(lumen::cache_write_kernel<lumen::fp16>, grid, block, 0, st,
                        (const lumen::fp16*)k, (const lumen::fp16*)v, (lumen::fp16*)kc,
                        (lumen::fp16*)vc, slots, ntok, nkv, D, BS, k_stride, v_stride);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+extern "C" hipError_t lumen_rope_cache(int dtype, void* qkv, long long ld, const int* pos,
+                                       const float* cos_t, const float* sin_t, void* kc, void* vc,
+                                       const long long* slots, int ntok, int nh, int nkv, int D,
+                                       int BS, hipStream_t st) {
+  if (ntok == 0) return hipSuccess;
+  if (D % 16 != 0) return hipErrorInvalidValue;
+  const long long n = static_cast<long long>(ntok) * (nh + 2 * nkv) * (D / 16);
+  dim3 block(256), grid(static_cast<unsigned>((n + 255) / 256));
+  if (dtype == lumen::kBF16)
+    hipLaunchKernelGGL(lumen::rope_cache_kernel<lumen::bf16>, grid, block, 0, st,
+                       (lumen::bf16*)qkv, ld, pos, cos_t, sin_t, (lumen::bf16*)kc,
+                       (lumen::bf16*)vc, slots, ntok, nh, nkv, D, BS);
+  else if (dtype == lumen::kF16)
+    hipLaunchKernelGGL(lumen::rope_cache_kernel<lumen::fp16>, grid, block, 0, st,
+                       (lumen::fp16*)qkv, ld, pos, cos_t, sin_t, (lumen::fp16*)kc,
+                       (lumen::fp16*)vc, slots, ntok, nh, nkv, D, BS);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -143,10 +143,24 @@ __device__ __forceinline__ float sum16(float v) {  // over the 16 lanes of a DPP
 
 constexpr int GU = 8;  // 128-element steps in flight per wave
 
+// SWIGLU: x is the fused gate|up GEMM output [M, 2K] and the operand is act = silu(gate) * up,
+// formed in registers and rounded to T exactly as kernels/swiglu.hip rounds it, so the batch-1
+// down projection needs no separate activation launch.
+template <typename T>
+__device__ __forceinline__ uint4 swiglu8(uint4 g, uint4 u) {
+  const T* ge = reinterpret_cast<const T*>(&g);
+  const T* ue = reinterpret_cast<const T*>(&u);
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = silu(to_f32(ge[j])) * to_f32(ue[j]);
+  return make_uint4(pk2<T>(a[0], a[1]), pk2<T>(a[2], a[3]), pk2<T>(a[4], a[5]),
+                    pk2<T>(a[6], a[7]));
+}
+
 // One workgroup = 4 rows; its 4 waves split K in 128-element steps (weights AND x issued up
 // front for the whole slice) and meet in LDS.  (A variant with one wave per 4 rows over the
 // whole of K, prefetching weights but loading x inside the loop, measured 2.96 vs 3.73 TB/s.)
-template <typename T, int MM>
+template <typename T, int MM, bool SWIGLU = false>
 __global__ void __launch_bounds__(256) gemv_kernel(const T* __restrict__ x,
                                                    const T* __restrict__ W, T* __restrict__ y,
                                                    int M, int N, int K, long long ldx,
@@ -171,8 +185,13 @@ __global__ void __launch_bounds__(256) gemv_kernel(const T* __restrict__ x,
       const bool ok = (s + u < s1) && (k < K);
       wv[u] = ok ? ntload(wp + (s + u) * 128) : z;
 #pragma unroll
-      for (int m = 0; m < MM; ++m)
-        xv[u][m] = (ok && m < M) ? *reinterpret_cast<const uint4*>(xp + m * ldx + (s + u) * 128) : z;
+      for (int m = 0; m < MM; ++m) {
+        const T* xr = xp + m * ldx + (s + u) * 128;
+        xv[u][m] = (ok && m < M) ? *reinterpret_cast<const uint4*>(xr) : z;
+        if constexpr (SWIGLU)  // up half at +K; zero pairs give silu(0) * 0 = 0
+          xv[u][m] = swiglu8<T>(xv[u][m],
+                                (ok && m < M) ? *reinterpret_cast<const uint4*>(xr + K) : z);
+      }
     }
 #pragma unroll
     for (int u = 0; u < GU; ++u)
@@ -199,12 +218,69 @@ __global__ void __launch_bounds__(256) gemv_kernel(const T* __restrict__ x,
   }
 }
 
+// ---- M == 1, rows-per-lane form ---------------------------------------------------------------
+// lane = one 16-byte chunk of K, 4 weight rows per lane: a wave instruction reads 1 KiB of ONE
+// row (fully contiguous), and the x chunk is loaded -- and with SWIGLU activated -- once per 4
+// rows instead of once per row (the form above repeats both for each of its 4 row groups).
+constexpr int GS = 4;  // 512-element steps in flight per wave (x 4 rows = 16 loads per lane)
+
+template <typename T, bool SWIGLU>
+__global__ void __launch_bounds__(256) gemv_r4_kernel(const T* __restrict__ x,
+                                                      const T* __restrict__ W, T* __restrict__ y,
+                                                      int N, int K) {
+  __shared__ float red[4][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 4;
+  const int S = (K + 511) >> 9;  // 512-element steps
+  const int s0 = (wid * S) >> 2, s1 = ((wid + 1) * S) >> 2;
+  const T* wp = W + (long long)n0 * K + 8 * lane;
+  const T* xp = x + 8 * lane;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  for (int s = s0; s < s1; s += GS) {
+    uint4 wv[GS][4], xv[GS];
+#pragma unroll
+    for (int u = 0; u < GS; ++u) {
+      const int k = (s + u) * 512;
+      const bool ok = (s + u < s1) && (k + 8 * lane < K);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wv[u][r] = ok ? ntload(wp + (long long)r * K + k) : z;
+      xv[u] = ok ? *reinterpret_cast<const uint4*>(xp + k) : z;
+      if constexpr (SWIGLU)
+        xv[u] = swiglu8<T>(xv[u], ok ? *reinterpret_cast<const uint4*>(xp + K + k) : z);
+    }
+#pragma unroll
+    for (int u = 0; u < GS; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[r] = dot2<T>(wv[u][r].x, xv[u].x, acc[r]);
+        acc[r] = dot2<T>(wv[u][r].y, xv[u].y, acc[r]);
+        acc[r] = dot2<T>(wv[u][r].z, xv[u].z, acc[r]);
+        acc[r] = dot2<T>(wv[u][r].w, xv[u].w, acc[r]);
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = sum16(acc[r]);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lane == 0) red[wid][r] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int r = threadIdx.x;
+    y[n0 + r] = from_f32<T>(red[0][r] + red[1][r] + red[2][r] + red[3][r]);
+  }
+}
+
 }  // namespace sk
 }  // namespace lumen
 
 // y[M, N] = x[M, K] @ W[N, K]^T with M <= 16, N % 16 == 0, K % 128 == 0; x rows at stride ldx,
 // W contiguous, y rows at stride ldy.
 namespace {
+int g_gemv_form = 1;
+
 template <typename T>
 hipError_t launch_gemv(const void* x, const void* W, void* y, int M, int N, int K, long long ldx,
                        long long ldy, hipStream_t st) {
@@ -212,13 +288,39 @@ hipError_t launch_gemv(const void* x, const void* W, void* y, int M, int N, int 
 #define LUMEN_GEMV(MM)                                                                          \
   hipLaunchKernelGGL((lumen::sk::gemv_kernel<T, MM>), grid, block, 0, st, (const T*)x,        \
                      (const T*)W, (T*)y, M, N, K, ldx, ldy)
-  if (M == 1) LUMEN_GEMV(1);
+  if (M == 1 && g_gemv_form == 1)
+    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<T, false>), grid, block, 0, st, (const T*)x,
+                       (const T*)W, (T*)y, N, K);
+  else if (M == 1) LUMEN_GEMV(1);
   else if (M == 2) LUMEN_GEMV(2);
   else LUMEN_GEMV(4);
 #undef LUMEN_GEMV
   return hipGetLastError();
 }
 }  // namespace
+
+// y[1, N] = (silu(gu[:, :K]) * gu[:, K:]) @ W[N, K]^T: the batch-1 down projection with the
+// SwiGLU activation formed on the fly (gu row stride ldgu >= 2K).
+extern "C" hipError_t lumen_gemv_swiglu(int dtype, const void* gu, const void* W, void* y, int N,
+                                        int K, long long ldgu, long long ldy, hipStream_t st) {
+  if (N % 4 != 0 || K % 8 != 0) return hipErrorInvalidValue;
+  dim3 grid(N / 4), block(256);
+#define LUMEN_GEMV_SW(TT)                                                                       \
+  if (g_gemv_form == 1)                                                                         \
+    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<TT, true>), grid, block, 0, st, (const TT*)gu, \
+                       (const TT*)W, (TT*)y, N, K);                                             \
+  else                                                                                          \
+    hipLaunchKernelGGL((lumen::sk::gemv_kernel<TT, 1, true>), grid, block, 0, st, (const TT*)gu, \
+                       (const TT*)W, (TT*)y, 1, N, K, ldgu, ldy)
+  if (dtype == lumen::kBF16) { LUMEN_GEMV_SW(lumen::bf16); }
+  else if (dtype == lumen::kF16) { LUMEN_GEMV_SW(lumen::fp16); }
+  else return hipErrorInvalidValue;
+#undef LUMEN_GEMV_SW
+  return hipGetLastError();
+}
+
+// M == 1 kernel form: 1 = rows-per-lane (gemv_r4_kernel), 0 = row-group form (gemv_kernel)
+extern "C" void lumen_set_gemv_form(int form) { g_gemv_form = form; }
 
 extern "C" hipError_t lumen_skinny_gemm(int dtype, const void* x, const void* W, void* y, int M,
                                         int N, int K, long long ldx, long long ldy,

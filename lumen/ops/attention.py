@@ -10,6 +10,7 @@ Serving decode uses the paged-KV HIP kernel (``kernels/paged_attention.hip``): s
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -37,13 +38,34 @@ def causal_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
     return o.transpose(1, 2).reshape(B * S, nh * D)
 
 
+_merge_counters: dict = {}
+# Fused split-context merge: measured neutral in decode steps (batch 1: 3.857 vs 3.865 ms ITL,
+# profiles/r02_serve), so the two-kernel merge stays the default.
+PA_FUSED_MERGE = os.environ.get("LUMEN_PA_FUSED_MERGE", "0") == "1"
+
+
+def _pa_counters(device: torch.device, n: int) -> torch.Tensor:
+    """Zeroed int32 arrival counters for the fused split-context merge.  The kernel leaves them
+    zeroed, so one buffer per device serves every layer and step; it is allocated before any
+    HIP-graph capture (the runner's eager warm-up steps reach here first) and only grows."""
+    key = (device.type, device.index)
+    c = _merge_counters.get(key)
+    if c is None or c.numel() < n:
+        c = torch.zeros(max(n, 1 << 16), device=device, dtype=torch.int32)
+        _merge_counters[key] = c
+    return c
+
+
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                  block_tables: torch.Tensor, context_lens: torch.Tensor, max_context: int,
-                 scale: float, partition_size: int = 512) -> torch.Tensor:
+                 scale: float, partition_size: int = 512,
+                 fused_merge: Optional[bool] = None) -> torch.Tensor:
     """Single-token attention over a paged KV cache.
 
     q [num_seqs, nh, D]; caches [num_blocks, nkv, block_size, D]; block_tables [num_seqs,
     max_blocks] int32; context_lens [num_seqs] int32 (number of cached tokens incl. current).
+    Contexts longer than ``partition_size`` are split over workgroups; with ``fused_merge`` the
+    last partition to finish merges the partials (one launch), else a second kernel does.
     """
     num_seqs, nh, D = q.shape
     nb, nkv, bs, _ = k_cache.shape
@@ -57,9 +79,12 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         else:
             tm = torch.empty(1, 1, 1, device=q.device, dtype=torch.float32)
             tl, to = tm, tm
+        fused = PA_FUSED_MERGE if fused_merge is None else fused_merge
+        cnt = (_pa_counters(q.device, num_seqs * nkv) if fused and max_parts > 1
+               else None)
         native().paged_attention_decode(out, q.contiguous(), k_cache, v_cache, block_tables,
                                         context_lens, nkv, bs, block_tables.shape[1], scale, tm,
-                                        tl, to, partition_size)
+                                        tl, to, partition_size, cnt)
         return out
     return paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale)
 
@@ -99,6 +124,28 @@ def write_kv_cache(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor,
     blk, off = sm // bs, sm % bs
     k_cache[blk, :, off] = k[valid].to(k_cache.dtype)
     v_cache[blk, :, off] = v[valid].to(v_cache.dtype)
+
+
+def rope_write_kv(qkv: torch.Tensor, positions: torch.Tensor, nh: int, nkv: int, D: int,
+                  cos_t: torch.Tensor, sin_t: torch.Tensor, k_cache: torch.Tensor,
+                  v_cache: torch.Tensor, slot_mapping: torch.Tensor) -> None:
+    """RoPE on the q and k heads of the fused token-major qkv [T, (nh + 2 nkv) D] in place, then
+    the rotated k and v into the paged cache at ``slot_mapping`` (-1 = skip): one HIP kernel
+    (``rope_cache_kernel``) on GPU, rope_inplace + write_kv_cache elsewhere."""
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    nb, nkv_c, bs, Dc = k_cache.shape
+    if use_native(qkv) and D % 16 == 0 and nkv_c == nkv and Dc == D:
+        native().rope_cache_write(qkv, positions.to(torch.int32), cos_t, sin_t, k_cache, v_cache,
+                                  slot_mapping.to(torch.int64), nh, nkv, D, bs)
+        return
+    from .rope import rope_inplace
+
+    rope_inplace(qkv, positions, nh + nkv, D, cos_t, sin_t)
+    qs, ks = nh * D, nkv * D
+    write_kv_cache(qkv[:, qs:qs + ks].view(T, nkv, D), qkv[:, qs + ks:qs + 2 * ks].view(T, nkv, D),
+                   k_cache, v_cache, slot_mapping)
 
 
 # ------------------------------------------------------------------------------------------------

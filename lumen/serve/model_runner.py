@@ -27,10 +27,10 @@ import torch.nn.functional as F
 from ..models.config import ModelConfig
 from ..ops._native import native, use_native
 from ..ops.activation import swiglu
-from ..ops.attention import flash_attention_qkv, paged_decode, write_kv_cache
-from ..ops.gemm import linear_nt
+from ..ops.attention import flash_attention_qkv, paged_decode, rope_write_kv, write_kv_cache
+from ..ops.gemm import linear_nt, swiglu_linear_nt
 from ..ops.norm import rms_norm
-from ..ops.rope import rope_inplace, rope_tables
+from ..ops.rope import rope_tables
 
 
 @dataclass
@@ -169,11 +169,8 @@ class ModelRunner:
             qkv = linear_nt(y, L.qkv)
             if ml is not None:
                 ml.apply(i, "qkv", y, qkv, masks)
-            rope_inplace(qkv, positions, self.w.nh + self.w.nkv, D, self.cos, self.sin)
-            qs, ks = self.q_size, self.kv_size
-            k = qkv[:, qs:qs + ks].view(T, self.w.nkv, D)
-            v = qkv[:, qs + ks:].view(T, self.w.nkv, D)
-            write_kv_cache(k, v, self.k_cache[i], self.v_cache[i], slots)
+            rope_write_kv(qkv, positions, self.w.nh, self.w.nkv, D, self.cos, self.sin,
+                          self.k_cache[i], self.v_cache[i], slots)
             o = attn_fn(qkv, i)
             a = self._allreduce(linear_nt(o, L.o))
             if ml is not None:
@@ -182,9 +179,11 @@ class ModelRunner:
             gu = linear_nt(y2, L.gate_up)
             if ml is not None:
                 ml.apply(i, "gate_up", y2, gu, masks)
-            act = swiglu(gu)
-            h = self._allreduce(linear_nt(act, L.down))
-            if ml is not None:
+            if ml is None:  # batch 1: SwiGLU formed inside the down-projection weight stream
+                h = self._allreduce(swiglu_linear_nt(gu, L.down))
+            else:
+                act = swiglu(gu)
+                h = self._allreduce(linear_nt(act, L.down))
                 ml.apply(i, "down", act, h, masks, self._allreduce)
         return h, res
 

@@ -224,9 +224,20 @@ def test_paged_decode(nh, nkv, D, ctx_max):
     bt = perm.to(DEV)
     cl = lens.int().to(DEV)
     scale = 1 / math.sqrt(D)
-    o = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale)
     o2 = paged_decode_ref(q, kc, vc, bt, cl, scale)
-    assert rel(o, o2) < 1e-2
+    for part in (512, 64):
+        o = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part)
+        assert rel(o, o2) < 1e-2
+        # fused merge (arrival counters, last partition merges) == two-kernel merge, and the
+        # counters reset themselves: a repeat call gives the same bits
+        o_f = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=True)
+        o_sep = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=False)
+        assert torch.equal(o_f, o_sep)
+        assert torch.equal(
+            paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=True), o_f)
+    from lumen.ops.attention import _merge_counters
+
+    assert all(int(c.abs().sum()) == 0 for c in _merge_counters.values())
 
 
 def test_sampling_greedy_and_topk():
@@ -442,10 +453,13 @@ def test_skinny_gemm(M, N, K):
     from lumen.ops._native import native
 
     y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    native().skinny_gemm(x, w, y)  # both kernel forms (M <= 4 VALU, M > 4 MFMA)
     ref = x.float() @ w.float().t()
-    assert rel(y, ref) < 1e-2
-    assert skinny_ok(x, w) == (M == 1 and N <= 4096)
+    for form in (0, 1):  # M = 1: row-group / rows-per-lane forms; M <= 4 VALU, M > 4 MFMA
+        native().set_gemv_form(form)
+        native().skinny_gemm(x, w, y)
+        assert rel(y, ref) < 1e-2
+    native().set_gemv_form(1)
+    assert skinny_ok(x, w) == (M == 1)
     y = linear_nt(x, w)
     ref = x.float() @ w.float().t()
     assert y.shape == (M, N) and rel(y, ref) < 1e-2
@@ -455,3 +469,64 @@ def test_skinny_gemm(M, N, K):
     yv = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     native().skinny_gemm(xv, w, yv)
     assert rel(yv, xv.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("N,F", [(4096, 11008), (1024, 2752), (4096, 1000)])
+def test_gemv_swiglu(N, F):
+    """Batch-1 down projection with SwiGLU formed inside the weight stream == swiglu kernel +
+    GEMM (the activation rounds to bf16 identically, so only summation order differs)."""
+    from lumen.ops.activation import swiglu
+    from lumen.ops.gemm import swiglu_linear_nt
+    from lumen.ops._native import native
+
+    gu = torch.randn(1, 2 * F, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, F, device=DEV) * 0.02).to(torch.bfloat16)
+    act = swiglu(gu)
+    ref = act.float() @ w.float().t()
+    y = torch.empty(1, N, device=DEV, dtype=torch.bfloat16)
+    # f32 reference of the whole op (silu in f32, product rounded to bf16 as the kernel does)
+    g, u = gu.float().chunk(2, -1)
+    ref32 = (F_silu(g) * u).to(torch.bfloat16).float() @ w.float().t()
+    for form in (0, 1):
+        native().set_gemv_form(form)
+        native().gemv_swiglu(gu, w, y)
+        assert rel(y, ref) < 1e-2
+        assert rel(y, ref32) < 1e-2
+    native().set_gemv_form(1)
+    assert rel(swiglu_linear_nt(gu, w), ref) < 1e-2
+    # row-strided gate|up buffer (a view into a wider allocation)
+    gb = torch.randn(1, 2 * F + 64, device=DEV).to(torch.bfloat16)
+    gv = gb[:, :2 * F]
+    yv = torch.empty(1, N, device=DEV, dtype=torch.bfloat16)
+    native().gemv_swiglu(gv, w, yv)
+    assert rel(yv, swiglu(gv.contiguous()).float() @ w.float().t()) < 1e-2
+
+
+def F_silu(x):
+    return x * torch.sigmoid(x)
+
+
+@pytest.mark.parametrize("nh,nkv", [(32, 32), (8, 2)])
+def test_rope_write_kv_fused(nh, nkv):
+    """Fused RoPE + paged KV-cache write == rope_inplace then write_kv_cache (bit-exact)."""
+    from lumen.ops.attention import rope_write_kv, write_kv_cache
+    from lumen.ops.rope import rope_inplace, rope_tables
+
+    D, T, bs, nb = 128, 37, 16, 64
+    qkv = torch.randn(T, (nh + 2 * nkv) * D + 8, device=DEV).to(torch.bfloat16)[:, :(nh + 2 * nkv) * D]
+    pos = torch.randint(0, 900, (T,), device=DEV, dtype=torch.int32)
+    cos, sin = rope_tables(D, 1024, 10000.0, DEV)
+    slots = torch.randperm(nb * bs, device=DEV)[:T].to(torch.int64)
+    slots[3] = -1  # padding row: no cache write
+    kc = torch.zeros(nb, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    q1 = qkv.clone()
+    rope_write_kv(q1, pos, nh, nkv, D, cos, sin, kc, vc, slots)
+    q2 = qkv.clone()
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    rope_inplace(q2, pos, nh + nkv, D, cos, sin)
+    qs, ks = nh * D, nkv * D
+    write_kv_cache(q2[:, qs:qs + ks].view(T, nkv, D), q2[:, qs + ks:].view(T, nkv, D), kc2, vc2,
+                   slots)
+    assert torch.equal(q1, q2)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
