@@ -58,11 +58,47 @@ def m1_forms():
         del ws
 
 
+def dgemm_sweep():
+    """Decode-batch MFMA GEMM (kernels/decode_gemm.hip) vs hipBLASLt (tuned table) per M."""
+    import torch
+
+    from lumen.ops import gemm as G
+    from lumen.utils.gemm_tuning import load_tuned_gemms
+
+    load_tuned_gemms()
+    dev = "cuda"
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096),
+              "down": (4096, 11008), "lm_head": (32000, 4096)}
+    Ms = (2, 4, 8, 16, 32, 64, 128, 256)
+    if "--splits" in sys.argv:
+        Ms = (2, 8, 16, 32)
+    for M in Ms:
+        row = {"M": M}
+        for name, (N, K) in shapes.items():
+            copies = max(2, int(600e6 // (N * K * 2)))
+            ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            if "--splits" in sys.argv:
+                row[name] = {f"s{sp}": _time(lambda w: G.dgemm(x, w, splits=sp), ws)
+                             for sp in (1, 2, 4, 8, 16)}
+                row[name]["hipblaslt"] = _time(lambda w: torch.matmul(x, w.t()), ws)
+                del ws
+                continue
+            dg = _time(lambda w: G.dgemm(x, w), ws)
+            bl = _time(lambda w: torch.matmul(x, w.t()), ws)
+            row[name] = {"dgemm": dg, "hipblaslt": bl, "splits": G.dgemm_plan(M, N, K)[0],
+                         "dgemm_TBps": round(N * K * 2 / (dg * 1e-6) / 1e12, 2)}
+            del ws
+        print(json.dumps(row), flush=True)
+
+
 def main():
     import torch
 
     if "--m1-forms" in sys.argv:
         return m1_forms()
+    if "--dgemm" in sys.argv:
+        return dgemm_sweep()
 
     from lumen.ops._native import native
     from lumen.utils.gemm_tuning import load_tuned_gemms

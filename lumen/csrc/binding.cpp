@@ -45,6 +45,8 @@ hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int
 hipError_t lumen_gemv_swiglu(int, const void*, const void*, void*, int, int, long long, long long,
                              hipStream_t);
 void lumen_set_gemv_form(int);
+hipError_t lumen_dgemm(int, const void*, const void*, void*, int, int, int, long long, long long, int,
+                       float*, unsigned*, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
                                         float, float*, float*, void*, int, unsigned*, hipStream_t);
@@ -168,6 +170,31 @@ void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
                           static_cast<int>(x.size(0)), static_cast<int>(w.size(0)),
                           static_cast<int>(w.size(1)), x.stride(0), y.stride(0), cur_stream()),
         "skinny_gemm");
+}
+
+// y[M, N] = x[M, K] @ w[N, K]^T on the matrix cores for decode batches (kernels/decode_gemm.hip)
+void dgemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, int64_t splits,
+           const std::optional<at::Tensor>& ws, const std::optional<at::Tensor>& cnt) {
+  if (!x.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: dgemm needs GPU tensors");
+  need_cuda(w, "w");
+  if (x.dim() != 2 || w.dim() != 2 || y.dim() != 2 || x.stride(1) != 1 || y.stride(1) != 1 ||
+      x.size(1) != w.size(1) || y.size(0) != x.size(0) || y.size(1) != w.size(0) ||
+      x.stride(0) % 8 != 0 || y.stride(0) % 4 != 0 || x.scalar_type() != w.scalar_type() ||
+      y.scalar_type() != w.scalar_type())
+    throw std::invalid_argument("lumen: dgemm shape/layout mismatch");
+  float* wsp = nullptr;
+  unsigned* cp = nullptr;
+  if (splits > 1) {
+    if (!ws.has_value() || !cnt.has_value() || ws->scalar_type() != at::kFloat ||
+        cnt->scalar_type() != at::kInt)
+      throw std::invalid_argument("lumen: dgemm split-K needs f32 workspace and int32 counters");
+    wsp = ws->data_ptr<float>();
+    cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+  }
+  check(lumen_dgemm(dcode(w), x.data_ptr(), w.data_ptr(), y.data_ptr(), static_cast<int>(x.size(0)),
+                    static_cast<int>(w.size(0)), static_cast<int>(w.size(1)), x.stride(0),
+                    y.stride(0), static_cast<int>(splits), wsp, cp, cur_stream()),
+        "dgemm");
 }
 
 // y[1, N] = swiglu(gu[1, 2F]) @ w[N, F]^T with the activation formed inside the weight stream
@@ -486,6 +513,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("transpose2d", &transpose2d);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv_swiglu", &gemv_swiglu);
+  m.def("dgemm", &dgemm);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
   m.def("rope_cache_write", &rope_cache_write);
   m.def("paged_attention_decode", &paged_attention_decode);

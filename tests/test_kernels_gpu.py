@@ -471,6 +471,29 @@ def test_skinny_gemm(M, N, K):
     assert rel(yv, xv.float() @ w.float().t()) < 1e-2
 
 
+@pytest.mark.parametrize("M", [2, 5, 16, 32, 33, 64, 96, 128, 200, 256])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (1024, 11008)])
+def test_dgemm(M, N, K):
+    """Decode-batch MFMA GEMM (kernels/decode_gemm.hip) vs an f32 reference: planned split,
+    forced single / split-K (last-arriving split reduces), deterministic, counters left zeroed,
+    row-strided x."""
+    from lumen.ops import gemm as G
+
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    y = G.dgemm(x, w)
+    assert y.shape == (M, N) and rel(y, ref) < 1e-2
+    assert torch.equal(G.dgemm(x, w), y)  # fixed-order split reduction: bitwise repeatable
+    for s in (1, 2, 8):
+        assert rel(G.dgemm(x, w, splits=s), ref) < 1e-2
+    assert all(int(c.abs().sum()) == 0 for c in G._dg_counters.values())
+    xb = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)
+    xv = xb[:, :K]
+    assert rel(G.dgemm(xv, w, splits=2), xv.float() @ w.float().t()) < 1e-2
+    assert G.dgemm_ok(x, w)
+
+
 @pytest.mark.parametrize("N,F", [(4096, 11008), (1024, 2752), (4096, 1000)])
 def test_gemv_swiglu(N, F):
     """Batch-1 down projection with SwiGLU formed inside the weight stream == swiglu kernel +
