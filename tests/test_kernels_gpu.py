@@ -473,7 +473,7 @@ def test_skinny_gemm(M, N, K):
 
 @pytest.mark.parametrize("M", [2, 5, 16, 32, 33, 64, 96, 128, 200, 256])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (1024, 11008)])
-def test_dgemm(M, N, K):
+def test_dgemm(M, N, K, monkeypatch):
     """Decode-batch MFMA GEMM (kernels/decode_gemm.hip) vs an f32 reference: planned split,
     forced single / split-K (last-arriving split reduces), deterministic, counters left zeroed,
     row-strided x."""
@@ -491,7 +491,9 @@ def test_dgemm(M, N, K):
     xb = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)
     xv = xb[:, :K]
     assert rel(G.dgemm(xv, w, splits=2), xv.float() @ w.float().t()) < 1e-2
+    monkeypatch.setattr(G, "DGEMM", True)  # opt-in dispatch (LUMEN_DGEMM=1)
     assert G.dgemm_ok(x, w)
+    assert torch.equal(G.linear_nt(x, w), G.dgemm(x, w))
 
 
 @pytest.mark.parametrize("N,F", [(4096, 11008), (1024, 2752), (4096, 1000)])
