@@ -24,38 +24,41 @@ def _time(fn, ws, reps=20):
 
 
 def m1_forms():
-    """Batch-1 kernel forms: row-group (form 0) vs rows-per-lane (form 1), plain and with the
-    SwiGLU activation fused into the down projection (vs swiglu kernel + GEMV)."""
+    """Decode batches 1..4: row-group (form 0) vs rows-per-lane (form 1) weight-streaming kernels
+    vs hipBLASLt; at M = 1 also the SwiGLU-fused down projection (vs swiglu kernel + GEMV)."""
     import torch
 
     from lumen.ops._native import native
     from lumen.ops.activation import swiglu
+    from lumen.utils.gemm_tuning import load_tuned_gemms
 
+    load_tuned_gemms()
     dev = "cuda"
     shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096),
-              "down": (4096, 11008)}
-    for name, (N, K) in shapes.items():
-        copies = max(2, int(600e6 // (N * K * 2)))
-        ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
-        x = torch.randn(1, K, device=dev).to(torch.bfloat16)
-        y = torch.empty(1, N, device=dev, dtype=torch.bfloat16)
-        row = {"shape": name, "N": N, "K": K}
-        for form in (0, 1):
-            native().set_gemv_form(form)
-            row[f"form{form}_us"] = _time(lambda w: native().skinny_gemm(x, w, y), ws)
-            row[f"form{form}_TBps"] = round(N * K * 2 / (row[f"form{form}_us"] * 1e-6) / 1e12, 2)
-        row["hipblaslt_us"] = _time(lambda w: torch.matmul(x, w.t()), ws)
-        if name == "down":
-            gu = torch.randn(1, 2 * K, device=dev).to(torch.bfloat16)
+              "down": (4096, 11008), "lm_head": (32000, 4096)}
+    for M in (1, 2, 3, 4):
+        for name, (N, K) in shapes.items():
+            copies = max(2, int(600e6 // (N * K * 2)))
+            ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            row = {"M": M, "shape": name, "N": N, "K": K}
             for form in (0, 1):
                 native().set_gemv_form(form)
-                row[f"swiglu_fused_form{form}_us"] = _time(
-                    lambda w: native().gemv_swiglu(gu, w, y), ws)
-                row[f"swiglu_then_gemv_form{form}_us"] = _time(
-                    lambda w: native().skinny_gemm(swiglu(gu), w, y), ws)
-        native().set_gemv_form(1)
-        print(json.dumps(row), flush=True)
-        del ws
+                row[f"form{form}_us"] = _time(lambda w: native().skinny_gemm(x, w, y), ws)
+                row[f"form{form}_TBps"] = round(N * K * 2 / (row[f"form{form}_us"] * 1e-6) / 1e12, 2)
+            row["hipblaslt_us"] = _time(lambda w: torch.matmul(x, w.t()), ws)
+            if name == "down" and M == 1:
+                gu = torch.randn(1, 2 * K, device=dev).to(torch.bfloat16)
+                for form in (0, 1):
+                    native().set_gemv_form(form)
+                    row[f"swiglu_fused_form{form}_us"] = _time(
+                        lambda w: native().gemv_swiglu(gu, w, y), ws)
+                    row[f"swiglu_then_gemv_form{form}_us"] = _time(
+                        lambda w: native().skinny_gemm(swiglu(gu), w, y), ws)
+            native().set_gemv_form(1)
+            print(json.dumps(row), flush=True)
+            del ws
 
 
 def dgemm_sweep():

@@ -224,52 +224,69 @@ __global__ void __launch_bounds__(256) gemv_kernel(const T* __restrict__ x,
 // rows instead of once per row (the form above repeats both for each of its 4 row groups).
 constexpr int GS = 4;  // 512-element steps in flight per wave (x 4 rows = 16 loads per lane)
 
-template <typename T, bool SWIGLU>
+template <typename T, bool SWIGLU, int MM = 1>
 __global__ void __launch_bounds__(256) gemv_r4_kernel(const T* __restrict__ x,
                                                       const T* __restrict__ W, T* __restrict__ y,
-                                                      int N, int K) {
-  __shared__ float red[4][4];
+                                                      int N, int K, int M, long long ldx,
+                                                      long long ldy) {
+  // MM > 1 (decode batches 2..4): the 4 weight rows of a lane meet MM x chunks (one per batch
+  // row, x rows at stride ldx) -- the weight stream is unchanged, x traffic grows to MM : 4
+  __shared__ float red[4][MM][4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 4;
   const int S = (K + 511) >> 9;  // 512-element steps
   const int s0 = (wid * S) >> 2, s1 = ((wid + 1) * S) >> 2;
   const T* wp = W + (long long)n0 * K + 8 * lane;
   const T* xp = x + 8 * lane;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float acc[MM][4];
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[m][r] = 0.f;
   const uint4 z = make_uint4(0, 0, 0, 0);
   for (int s = s0; s < s1; s += GS) {
-    uint4 wv[GS][4], xv[GS];
+    uint4 wv[GS][4], xv[GS][MM];
 #pragma unroll
     for (int u = 0; u < GS; ++u) {
       const int k = (s + u) * 512;
       const bool ok = (s + u < s1) && (k + 8 * lane < K);
 #pragma unroll
       for (int r = 0; r < 4; ++r) wv[u][r] = ok ? ntload(wp + (long long)r * K + k) : z;
-      xv[u] = ok ? *reinterpret_cast<const uint4*>(xp + k) : z;
-      if constexpr (SWIGLU)
-        xv[u] = swiglu8<T>(xv[u], ok ? *reinterpret_cast<const uint4*>(xp + K + k) : z);
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        const T* xr = xp + (long long)m * ldx + k;
+        xv[u][m] = (ok && m < M) ? *reinterpret_cast<const uint4*>(xr) : z;
+        if constexpr (SWIGLU)
+          xv[u][m] = swiglu8<T>(xv[u][m], (ok && m < M) ? *reinterpret_cast<const uint4*>(xr + K) : z);
+      }
     }
 #pragma unroll
     for (int u = 0; u < GS; ++u)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        acc[r] = dot2<T>(wv[u][r].x, xv[u].x, acc[r]);
-        acc[r] = dot2<T>(wv[u][r].y, xv[u].y, acc[r]);
-        acc[r] = dot2<T>(wv[u][r].z, xv[u].z, acc[r]);
-        acc[r] = dot2<T>(wv[u][r].w, xv[u].w, acc[r]);
-      }
+      for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[m][r] = dot2<T>(wv[u][r].x, xv[u][m].x, acc[m][r]);
+          acc[m][r] = dot2<T>(wv[u][r].y, xv[u][m].y, acc[m][r]);
+          acc[m][r] = dot2<T>(wv[u][r].z, xv[u][m].z, acc[m][r]);
+          acc[m][r] = dot2<T>(wv[u][r].w, xv[u][m].w, acc[m][r]);
+        }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float v = sum16(acc[r]);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lane == 0) red[wid][r] = v;
-  }
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = sum16(acc[m][r]);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane == 0) red[wid][m][r] = v;
+    }
   __syncthreads();
-  if (threadIdx.x < 4) {
-    const int r = threadIdx.x;
-    y[n0 + r] = from_f32<T>(red[0][r] + red[1][r] + red[2][r] + red[3][r]);
+  if (threadIdx.x < 4 * MM) {
+    const int m = threadIdx.x >> 2, r = threadIdx.x & 3;
+    if (m < M)
+      y[(long long)m * ldy + n0 + r] =
+          from_f32<T>(red[0][m][r] + red[1][m][r] + red[2][m][r] + red[3][m][r]);
   }
 }
 
@@ -289,8 +306,14 @@ hipError_t launch_gemv(const void* x, const void* W, void* y, int M, int N, int 
   hipLaunchKernelGGL((lumen::sk::gemv_kernel<T, MM>), grid, block, 0, st, (const T*)x,        \
                      (const T*)W, (T*)y, M, N, K, ldx, ldy)
   if (M == 1 && g_gemv_form == 1)
-    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<T, false>), grid, block, 0, st, (const T*)x,
-                       (const T*)W, (T*)y, N, K);
+    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<T, false, 1>), grid, block, 0, st, (const T*)x,
+                       (const T*)W, (T*)y, N, K, 1, ldx, ldy);
+  else if (M == 2 && g_gemv_form == 1)
+    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<T, false, 2>), grid, block, 0, st, (const T*)x,
+                       (const T*)W, (T*)y, N, K, 2, ldx, ldy);
+  else if (M <= 4 && g_gemv_form == 1)
+    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<T, false, 4>), grid, block, 0, st, (const T*)x,
+                       (const T*)W, (T*)y, N, K, M, ldx, ldy);
   else if (M == 1) LUMEN_GEMV(1);
   else if (M == 2) LUMEN_GEMV(2);
   else LUMEN_GEMV(4);
@@ -307,8 +330,8 @@ extern "C" hipError_t lumen_gemv_swiglu(int dtype, const void* gu, const void* W
   dim3 grid(N / 4), block(256);
 #define LUMEN_GEMV_SW(TT)                                                                       \
   if (g_gemv_form == 1)                                                                         \
-    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<TT, true>), grid, block, 0, st, (const TT*)gu, \
-                       (const TT*)W, (TT*)y, N, K);                                             \
+    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<TT, true, 1>), grid, block, 0, st,           \
+                       (const TT*)gu, (const TT*)W, (TT*)y, N, K, 1, ldgu, ldy);                \
   else                                                                                          \
     hipLaunchKernelGGL((lumen::sk::gemv_kernel<TT, 1, true>), grid, block, 0, st, (const TT*)gu, \
                        (const TT*)W, (TT*)y, 1, N, K, ldgu, ldy)

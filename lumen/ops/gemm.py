@@ -14,12 +14,15 @@ import torch
 from ._native import native, use_native
 
 # Measured per shape against hipBLASLt with the tuned table (lumen/bench/skinny_bench.py
-# --m1-forms, profiles/r02_serve/m1_forms.jsonl): at M = 1 the rows-per-lane weight-streaming
-# kernel reaches 4.3-6.5 TB/s and beats hipBLASLt at every Llama-2-7B projection (qkv 17.1 vs
-# 26.0 us, o 7.9 vs 18.1, gate_up 27.7 vs 49.1, down 16.3 vs 37.4); at M > 1 hipBLASLt wins, so
-# those stay library GEMMs.
-SKINNY_MAX_M = int(os.environ.get("LUMEN_SKINNY_MAX_M", "1"))
+# --m1-forms, profiles/r02_serve/m1_forms.jsonl): the rows-per-lane weight-streaming kernel
+# reaches 4.3-6.5 TB/s at M = 1 and beats hipBLASLt at every Llama-2-7B projection (qkv 17.0 vs
+# 22.9 us, o 7.8 vs 22.7, gate_up 27.8 vs 37.3, down 16.5 vs 27.5, lm_head 38.4 vs 60.6); at
+# M = 2 it still wins or ties everywhere (o 10.4 vs 22.6, down 20.7 vs 27.6, lm_head 51.4 vs
+# 59.0); at M = 3-4 only the N = 4096 projections (o, down) stay ahead, and from M = 5 on
+# hipBLASLt wins, so those are library GEMMs.
+SKINNY_MAX_M = int(os.environ.get("LUMEN_SKINNY_MAX_M", "4"))
 SKINNY_MAX_N = int(os.environ.get("LUMEN_SKINNY_MAX_N", str(1 << 30)))
+SKINNY_WIDE_MAX_M = 2  # above this M only N <= 4096 projections take the GEMV
 # SwiGLU formed inside the batch-1 down projection: measured 21.4 us vs 18.5 us for the swiglu
 # kernel + GEMV (every workgroup re-activates the whole gate|up vector), so off by default.
 SWIGLU_GEMV = os.environ.get("LUMEN_SWIGLU_GEMV", "0") == "1"
@@ -27,6 +30,7 @@ SWIGLU_GEMV = os.environ.get("LUMEN_SWIGLU_GEMV", "0") == "1"
 
 def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     return (0 < x.shape[0] <= min(SKINNY_MAX_M, 16) and w.shape[0] <= SKINNY_MAX_N
+            and (x.shape[0] <= SKINNY_WIDE_MAX_M or w.shape[0] <= 4096)
             and use_native(x) and x.dim() == 2
             and w.dim() == 2 and x.dtype == w.dtype and x.dtype in (torch.bfloat16, torch.float16)
             and x.stride(1) == 1 and w.is_contiguous() and x.shape[1] == w.shape[1]

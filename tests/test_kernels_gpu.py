@@ -459,7 +459,7 @@ def test_skinny_gemm(M, N, K):
         native().skinny_gemm(x, w, y)
         assert rel(y, ref) < 1e-2
     native().set_gemv_form(1)
-    assert skinny_ok(x, w) == (M == 1)
+    assert skinny_ok(x, w) == (M <= 2 or (M <= 4 and N <= 4096))
     y = linear_nt(x, w)
     ref = x.float() @ w.float().t()
     assert y.shape == (M, N) and rel(y, ref) < 1e-2
