@@ -57,7 +57,8 @@ hipError_t lumen_sample(int, const void*, const float*, const float*, const int*
 hipError_t lumen_flash_attn(int, int, int, int, const void*, const void*, const void*, long long,
                             long long, long long, void*, long long, float*, const int*, const int*,
                             int, int, int, int, float, const void*, long long, void*, void*, void*,
-                            long long, long long, long long, const float*, hipStream_t);
+                            long long, long long, long long, const float*, const int*, const float*,
+                            const float*, hipStream_t);
 long long lumen_car_signal_bytes();
 int lumen_car_max_blocks();
 int lumen_car_max_ranks();
@@ -406,8 +407,16 @@ void flash_attn(int64_t which, bool causal, int64_t mt, const at::Tensor& q, con
                 const at::Tensor& cu, const at::Tensor& tiles, int64_t nh, int64_t nkv,
                 double scale, const std::optional<at::Tensor>& dout,
                 const std::optional<at::Tensor>& dq, const std::optional<at::Tensor>& dk,
-                const std::optional<at::Tensor>& dv, const std::optional<at::Tensor>& delta) {
+                const std::optional<at::Tensor>& dv, const std::optional<at::Tensor>& delta,
+                const std::optional<at::Tensor>& rope_pos, const std::optional<at::Tensor>& rope_cos,
+                const std::optional<at::Tensor>& rope_sin) {
   if (!q.is_cuda()) throw std::invalid_argument("lumen: flash_attn needs GPU tensors");
+  if (rope_pos.has_value() &&
+      (!rope_cos.has_value() || !rope_sin.has_value() || rope_pos->scalar_type() != at::kInt ||
+       rope_cos->scalar_type() != at::kFloat || rope_sin->scalar_type() != at::kFloat ||
+       !rope_pos->is_contiguous() || !rope_cos->is_contiguous() || !rope_sin->is_contiguous() ||
+       rope_cos->size(-1) != 64 || rope_pos->numel() < q.size(0)))
+    throw std::invalid_argument("lumen: flash_attn rope needs int32 pos [T] and f32 cos/sin [*, 64]");
   auto st = [](const std::optional<at::Tensor>& t) -> long long { return t.has_value() ? t->stride(0) : 0; };
   const int T = static_cast<int>(q.size(0));
   const int ntiles = static_cast<int>(tiles.numel() / 2);
@@ -417,7 +426,8 @@ void flash_attn(int64_t which, bool causal, int64_t mt, const at::Tensor& q, con
                          cu.data_ptr<int>(), tiles.data_ptr<int>(), ntiles, static_cast<int>(nh),
                          static_cast<int>(nkv), T, static_cast<float>(scale), ptr(dout), st(dout),
                          ptr(dq), ptr(dk), ptr(dv), st(dq), st(dk), st(dv), ptr<const float>(delta),
-                         cur_stream()),
+                         ptr<const int>(rope_pos), ptr<const float>(rope_cos),
+                         ptr<const float>(rope_sin), cur_stream()),
         "flash_attn");
 }
 

@@ -194,7 +194,21 @@ struct Args {
   const void* dout; long long lddo;
   void* dq; void* dk; void* dv; long long lddq, lddk, lddv;
   const float* delta;                             // [nh][T]
+  // optional (backward dQ / dK epilogues): undo the rotary embedding the forward applied to q / k
+  // -- write d(pre-RoPE) directly, so no separate inverse-rotation pass over dQKV is needed.
+  // rope_pos [T] (token positions), rope_cos / rope_sin [max_pos][64]; nullptr = off
+  const int* rope_pos;
+  const float* rope_cos;
+  const float* rope_sin;
 };
+
+// Inverse rotary embedding of one (x, x ^ 64) column pair: the forward rotation
+// y1 = x1 c - x2 s, y2 = x2 c + x1 s has the transpose dx1 = dy1 c + dy2 s, dx2 = dy2 c - dy1 s.
+__device__ __forceinline__ void rope_inv_pair(float& lo, float& hi, float c, float s) {
+  const float l = lo, h = hi;
+  lo = l * c + h * s;
+  hi = h * c - l * s;
+}
 
 // =============================================================================================
 // forward
@@ -658,9 +672,18 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   for (int r = 0; r < 4; ++r) {
     const int kr = wk0 + 4 * lg + r;
     if (kr >= L) continue;
+    float kv[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
+    if (a.rope_pos != nullptr) {  // column 16n + lr pairs with 16(n + 4) + lr: same lane
+      const long long pb = (long long)a.rope_pos[s0 + kr] * 64 + lr;
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        rope_inv_pair(kv[n], kv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
+    }
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
-      dK[(long long)kr * a.lddk + n * 16 + lr] = from_f32<T>(dk[n][r] * a.scale);
+      dK[(long long)kr * a.lddk + n * 16 + lr] = from_f32<T>(kv[n]);
       dV[(long long)kr * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
     }
   }
@@ -1301,10 +1324,34 @@ __global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
+      for (int r = 0; r < 16; ++r) dq[n][r] *= a.scale;
+    if (a.rope_pos != nullptr) {
+      // column 32n + 8jj + 4hi + i pairs with n ^ 2 (64 columns on): same lane and register
+      const float* cb = a.rope_cos + (long long)a.rope_pos[s0 + qrow] * 64 + 4 * hi;
+      const float* sb = a.rope_sin + (long long)a.rope_pos[s0 + qrow] * 64 + 4 * hi;
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float4 c4 = *reinterpret_cast<const float4*>(cb + 32 * n + 8 * jj);
+          const float4 s4 = *reinterpret_cast<const float4*>(sb + 32 * n + 8 * jj);
+          const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float lo = dq[n][4 * jj + i], hi2 = dq[n + 2][4 * jj + i];
+            rope_inv_pair(lo, hi2, cs[i], sn[i]);
+            dq[n][4 * jj + i] = lo;
+            dq[n + 2][4 * jj + i] = hi2;
+          }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         struct alignas(8) O4 { T v[4]; } q4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) q4.v[i] = from_f32<T>(dq[n][4 * jj + i] * a.scale);
+        for (int i = 0; i < 4; ++i) q4.v[i] = from_f32<T>(dq[n][4 * jj + i]);
         *reinterpret_cast<O4*>(dQ + 32 * n + 8 * jj + 4 * hi) = q4;
       }
   }
@@ -1373,8 +1420,12 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
                                        const int* tiles, int ntiles, int nh, int nkv, int T,
                                        float scale, const void* dout, long long lddo, void* dq,
                                        void* dk, void* dv, long long lddq, long long lddk,
-                                       long long lddv, const float* delta, hipStream_t st) {
+                                       long long lddv, const float* delta, const int* rope_pos,
+                                       const float* rope_cos, const float* rope_sin,
+                                       hipStream_t st) {
   if (nkv <= 0 || nh % nkv != 0) return hipErrorInvalidValue;
+  // the fused inverse RoPE exists in the dK/dV kernel (which 2) and the 32x32 dQ kernel (which 5)
+  if (rope_pos != nullptr && which != 2 && which != 5) return hipErrorInvalidValue;
   if (which != 1 && ntiles == 0) return hipSuccess;
   lumen::fa::Args a;
   a.q = q; a.k = k; a.v = v; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.o = o; a.ldo = ldo;
@@ -1382,6 +1433,7 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
   a.dout = dout; a.lddo = lddo; a.dq = dq; a.dk = dk; a.dv = dv; a.lddq = lddq; a.lddk = lddk;
   a.lddv = lddv; a.delta = delta;
+  a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
   return hipErrorInvalidValue;

@@ -53,7 +53,9 @@ class LlamaAttention(nn.Module):
                 qkv = self.qkv_proj(x2d, rope=(pos, cos, sin, (nh + nkv) * D))
             else:
                 qkv = rope_qkv_(self.qkv_proj(x2d), pos, nh, nkv, D, cos, sin)
-            o = flash_attention_qkv(qkv, tuple(range(0, B * S + 1, S)), nh, nkv, D, True)
+            # the FA backward undoes the rotation in its dQ / dK epilogues (FUSED_ROPE_BWD)
+            o = flash_attention_qkv(qkv, tuple(range(0, B * S + 1, S)), nh, nkv, D, True,
+                                    rope=(pos, cos, sin) if FUSED_ROPE_BWD else None)
             return self.o_proj(o)
         qkv = self.qkv_proj(x2d)
         q, k, v = qkv_rope_split(qkv, B, S, nh, nkv, D, cos, sin, pos)
@@ -63,6 +65,7 @@ class LlamaAttention(nn.Module):
 
 USE_FLASH = True
 FUSED_ROPE = True  # RoPE inside the q|k|v adapter write-back (lora_v2 UP kernel)
+FUSED_ROPE_BWD = True  # inverse RoPE inside the flash-attention dQ / dK epilogues
 _POS = {}
 
 

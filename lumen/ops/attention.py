@@ -204,7 +204,7 @@ FA_BWD = _os.environ.get("LUMEN_FA_BWD", "mix")
 
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cu, nh, nkv, D, causal):
+    def forward(ctx, qkv, cu, nh, nkv, D, causal, rope=None):
         C = native()
         T = qkv.shape[0]
         q = qkv[:, :nh * D]
@@ -216,9 +216,10 @@ class _FlashAttn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(D)
         C.flash_attn(0, causal, FA_FWD_MT, q, k, v, o, lse, cut,
                      _tiles(cu, FA_FWD_ROWS, qkv.device), nh, nkv, scale, None, None, None, None,
-                     None)
+                     None, None, None, None)
         ctx.save_for_backward(qkv, o, lse)
         ctx.meta = (cu, nh, nkv, D, causal, scale)
+        ctx.rope = rope
         return o
 
     @staticmethod
@@ -239,25 +240,35 @@ class _FlashAttn(torch.autograd.Function):
         delta = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
         cut = _cu_tensor(cu, qkv.device)
         C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
-                     scale, do, None, None, None, delta)
+                     scale, do, None, None, None, delta, None, None, None)
         # dK/dV and dQ kernels per FA_BWD: "v16" both 16x16x32 (64-row tiles), "v32" both
         # 32x32x16 (128-row tiles), "mix" = 16x16x32 dK/dV + 32x32x16 dQ
         wkv, rkv = (4, 128) if FA_BWD == "v32" else (2, 64)
         wq, rq = (5, 128) if FA_BWD in ("v32", "mix") else (3, 64)
+        # the mix kernels undo the forward's RoPE in their dQ / dK epilogues (d(pre-rotation)
+        # written directly): the producer of q|k then skips its own inverse-rotation pass
+        rp = ctx.rope if (ctx.rope is not None and wkv == 2 and wq == 5) else None
+        pos, cos, sin = rp if rp is not None else (None, None, None)
         C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh, nkv,
-                     scale, do, dq, dk, dv, delta)
+                     scale, do, dq, dk, dv, delta, pos, cos, sin)
         C.flash_attn(wq, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rq, qkv.device), nh, nkv,
-                     scale, do, dq, dk, dv, delta)
-        return dqkv, None, None, None, None, None
+                     scale, do, dq, dk, dv, delta, pos, cos, sin)
+        if rp is not None:
+            dqkv._lumen_rope_undone = True
+        return dqkv, None, None, None, None, None, None
 
 
 def flash_attention_qkv(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int,
-                        causal: bool = True) -> torch.Tensor:
+                        causal: bool = True, rope=None) -> torch.Tensor:
     """Causal attention straight from the fused token-major QKV buffer [T, (nh+2nkv)*D]
-    (q/k already rotated); returns O token-major [T, nh*D].  ``cu_seqlens``: sequence offsets."""
+    (q/k already rotated); returns O token-major [T, nh*D].  ``cu_seqlens``: sequence offsets.
+
+    ``rope`` = (pos int32 [T], cos, sin) of the rotation the q/k producer applied: the backward
+    then returns the gradient w.r.t. the PRE-rotation q/k (marked ``_lumen_rope_undone`` on the
+    dQKV tensor so the producer's backward skips its inverse pass)."""
     cu = tuple(int(c) for c in cu_seqlens)
     if use_native(qkv) and D == 128:
-        return _FlashAttn.apply(qkv, cu, nh, nkv, D, causal)
+        return _FlashAttn.apply(qkv, cu, nh, nkv, D, causal, rope)
     return flash_attention_ref(qkv, cu, nh, nkv, D, causal)
 
 

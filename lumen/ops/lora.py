@@ -328,8 +328,9 @@ class _LoraLinear(torch.autograd.Function):
         x2d, A, B, Z = ctx.saved_tensors
         segs, r, scale, p, seed = ctx.meta
         dy = dy.contiguous()
-        if ctx.rope is not None:
-            # y was rotated in the forward: d(pre-rope) = inverse rotation of the incoming grad.
+        if ctx.rope is not None and not getattr(dy, "_lumen_rope_undone", False):
+            # y was rotated in the forward: d(pre-rope) = inverse rotation of the incoming grad
+            # (already done when the flash-attention backward produced it, _lumen_rope_undone).
             # In place when the grad is a scratch buffer nothing else reads (the flash-attention
             # backward's fresh dQKV, marked), otherwise on a copy.
             if not getattr(dy, "_lumen_scratch", False):

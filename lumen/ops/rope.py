@@ -139,6 +139,8 @@ class _RopeQKV(torch.autograd.Function):
         nqk, D, cos_t, sin_t = ctx.meta
         # g is the flash-attention backward's fresh dQKV buffer (sole consumer): rotate it in
         # place instead of copying 3*T*H*2 bytes
+        if getattr(g, "_lumen_rope_undone", False):  # the flash-attention backward did it
+            return g, None, None, None, None, None
         g = g if g.is_contiguous() else g.contiguous()
         native().rope_inplace(g, pos, cos_t, _neg(sin_t), g.shape[0], g.stride(0), nqk, D)
         return g, None, None, None, None, None

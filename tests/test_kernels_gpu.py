@@ -309,6 +309,73 @@ def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch):
     assert rel(g[:, qs + ks:], g2[:, qs + ks:]) < 3e-2, "dv"
 
 
+@pytest.mark.parametrize("nh,nkv", [(8, 8), (8, 2)])
+def test_flash_backward_fused_inverse_rope(nh, nkv):
+    """dQ / dK epilogues with the inverse RoPE (FA backward given the rotation) == plain FA
+    backward followed by the separate inverse-rotation pass; dV untouched.  (The skip of the
+    producer's own inverse pass is checked end to end by test_llama_fused_rope_backward_matches.)"""
+    from lumen.ops.attention import flash_attention_qkv
+    from lumen.ops.rope import _neg, rope_tables
+
+    D = 128
+    cu = [0, 300, 812, 1000]
+    T = cu[-1]
+    cos, sin = rope_tables(D, 4096, 10000.0, DEV)
+    pos = torch.randint(0, 4096, (T,), device=DEV, dtype=torch.int32)
+    qkv = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(torch.bfloat16)
+    do = torch.randn(T, nh * D, device=DEV).to(torch.bfloat16)
+    grads = []
+    for fused in (True, False):
+        x = qkv.clone().requires_grad_(True)
+        o = flash_attention_qkv(x, cu, nh, nkv, D, True, rope=(pos, cos, sin) if fused else None)
+        (g,) = torch.autograd.grad(o, x, do)
+        if not fused:
+            g = g.clone()
+            from lumen.ops._native import native
+
+            native().rope_inplace(g, pos, cos, _neg(sin), T, g.stride(0), nh + nkv, D)
+        grads.append(g.float())
+    qk = (nh + nkv) * D
+    assert rel(grads[0][:, :qk], grads[1][:, :qk]) < 1e-2
+    assert torch.equal(grads[0][:, qk:], grads[1][:, qk:])
+
+
+def test_llama_fused_rope_backward_matches():
+    """Full model step: inverse RoPE in the flash-attention epilogues vs in the q|k|v adapter
+    backward -- same loss, same adapter gradients."""
+    import lumen.models.llama as L
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+
+    torch.manual_seed(0)
+    m = build_model("llama2-7b", dtype=torch.bfloat16, device="meta")  # config only
+    cfg = m.config
+    cfg.num_hidden_layers = 2
+    cfg.vocab_size = 1024
+    model = L.LlamaForCausalLM(cfg, dtype=torch.bfloat16, device=DEV)
+    model.init_weights(seed=1)
+    apply_lora(model, LoraConfig(r=8, lora_dropout=0.0))
+    for p in model.parameters():
+        if p.requires_grad:
+            p.data.normal_(0, 0.02)
+    ids = torch.randint(3, 1024, (2, 256), device=DEV)
+    labels = torch.full_like(ids, -100)
+    labels[:, :-1] = ids[:, 1:]
+    res = {}
+    try:
+        for fused in (True, False):
+            L.FUSED_ROPE_BWD = fused
+            model.zero_grad(set_to_none=True)
+            loss = model(ids, labels, int((labels != -100).sum()))
+            loss.backward()
+            res[fused] = (loss.item(), [p.grad.clone() for p in model.parameters() if p.requires_grad])
+    finally:
+        L.FUSED_ROPE_BWD = True
+    assert abs(res[True][0] - res[False][0]) < 1e-3  # LoRA split-K atomics: order-dependent
+    for a, b in zip(res[True][1], res[False][1]):
+        assert rel(a, b) < 1e-2
+
+
 def test_llama_layer_flash_vs_sdpa_path():
     import lumen.models.llama as L
     from lumen.lora import LoraConfig, apply_lora
