@@ -49,7 +49,7 @@ hipError_t lumen_dgemm(int, const void*, const void*, void*, int, int, int, long
                        float*, unsigned*, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
-                                        float, float*, float*, void*, int, unsigned*, hipStream_t);
+                                        float, float*, float*, void*, int, unsigned*, int, hipStream_t);
 hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, const long long*,
                                    int, int, int, int, long long, long long, int, hipStream_t);
 hipError_t lumen_sample(int, const void*, const float*, const float*, const int*,
@@ -327,7 +327,7 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                             const at::Tensor& context_lens, int64_t num_kv_heads, int64_t block_size,
                             int64_t max_blocks_per_seq, double scale, at::Tensor& tmp_m,
                             at::Tensor& tmp_l, at::Tensor& tmp_o, int64_t partition_size,
-                            const std::optional<at::Tensor>& counters) {
+                            const std::optional<at::Tensor>& counters, bool one_pass) {
   need_cuda(q, "q"); need_cuda(out, "out");
   const int num_seqs = static_cast<int>(q.size(0));
   const int nh = static_cast<int>(q.size(1));
@@ -348,7 +348,7 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                                      static_cast<int>(tmp_m.size(-1)), static_cast<float>(scale),
                                      tmp_m.data_ptr<float>(), tmp_l.data_ptr<float>(),
                                      tmp_o.data_ptr(), static_cast<int>(partition_size), cnt,
-                                     cur_stream()),
+                                     one_pass ? 1 : 0, cur_stream()),
         "paged_attention_decode");
 }
 

@@ -217,6 +217,138 @@ __global__ void __launch_bounds__(256) pa_decode_kernel(
   }
 }
 
+// ---- single-pass variant (online softmax per row group) ------------------------------------
+// The two-pass kernel above streams K, stops the memory pipe for a block-wide softmax, then
+// streams V.  Here each 16-lane row group streams K AND V rows together (U of each in flight
+// per lane) and keeps its own running (max, sum, P.V) state per head -- flash-decoding inside
+// the workgroup -- so HBM traffic never pauses and no score buffer lives in LDS.  The 16 groups
+// merge at the end: xor-16/32 exchanges inside a wave, then the 4 waves through LDS.  Output
+// (and split partials for the merge kernel) have exactly the two-pass kernel's semantics.
+__device__ __forceinline__ void pa_merge(float& m, float& l, float (&acc)[8], float m2, float l2,
+                                         const float (&acc2)[8]) {
+  const float M = fmaxf(m, m2);
+  const float a1 = m == -INFINITY ? 0.f : __expf(m - M);
+  const float a2 = m2 == -INFINITY ? 0.f : __expf(m2 - M);
+  l = l * a1 + l2 * a2;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = acc[j] * a1 + acc2[j] * a2;
+  m = M;
+}
+
+template <typename T, int D, int G>
+__global__ void __launch_bounds__(256) pa_decode1_kernel(
+    T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
+    const T* __restrict__ vc, const int* __restrict__ block_tables,
+    const int* __restrict__ context_lens, int nh, int nkv, int BS, int max_blocks, int max_parts,
+    float scale, float* __restrict__ tmp_m, float* __restrict__ tmp_l, float* __restrict__ tmp_o,
+    int PART) {
+  constexpr int LPT = D / 8;        // lanes per cache row (16-byte chunk each)
+  constexpr int NGR = 256 / LPT;    // row groups per workgroup
+  constexpr int U = 4;              // K and V rows in flight per lane
+  __shared__ float wst[4][G][D + 2];  // per-wave merged state: acc[D], m, l
+  const int seq = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
+  const int ctx = context_lens[seq];
+  const int start = part * PART;
+  if (start >= ctx) return;
+  const int end = min(ctx, start + PART);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = tid / LPT, d0 = (tid % LPT) * 8;
+  float qv[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    load8(q + (static_cast<size_t>(seq) * nh + kvh * G + h) * D + d0, qv[h]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[h][j] *= scale;
+  }
+  const int* bt = block_tables + static_cast<size_t>(seq) * max_blocks;
+  const size_t head_off = static_cast<size_t>(kvh) * BS * D;
+  const size_t blk_stride = static_cast<size_t>(nkv) * BS * D;
+  float m[G], l[G], acc[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    m[h] = -INFINITY;
+    l[h] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
+  }
+  for (int t0 = start + grp; t0 < end; t0 += NGR * U) {
+    float kr[U][8], vr[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * NGR;
+      if (t < end) {
+        const size_t off = bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
+        load8(kc + off, kr[u]);
+        load8(vc + off, vr[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * NGR;
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += kr[u][j] * qv[h][j];
+        s = LPT == 16 ? pa_red16(s) : wave_sum_width<LPT>(s);
+        if (t < end) {  // uniform within the row group
+          const float mn = fmaxf(m[h], s);
+          const float al = __expf(m[h] - mn);  // m = -inf on the first row: al = 0
+          const float p = __expf(s - mn);
+          l[h] = l[h] * al + p;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[h][j] = acc[h][j] * al + p * vr[u][j];
+          m[h] = mn;
+        }
+      }
+    }
+  }
+  // merge the 64 / LPT row groups of each wave (lanes d0-aligned at xor 16, 32, ...)
+#pragma unroll
+  for (int o = LPT; o < 64; o <<= 1) {
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      float a2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a2[j] = __shfl_xor(acc[h][j], o, 64);
+      const float m2 = __shfl_xor(m[h], o, 64), l2 = __shfl_xor(l[h], o, 64);
+      pa_merge(m[h], l[h], acc[h], m2, l2, a2);
+    }
+  }
+  if (lane < LPT) {
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wst[wid][h][d0 + j] = acc[h][j];
+      if (lane == 0) { wst[wid][h][D] = m[h]; wst[wid][h][D + 1] = l[h]; }
+    }
+  }
+  __syncthreads();
+  const int nparts = (ctx + PART - 1) / PART;
+  for (int i = tid; i < G * D; i += 256) {
+    const int h = i / D, d = i % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, wst[w][h][D]);
+    float L = 0.f, o = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float mw = wst[w][h][D];
+      const float a = mw == -INFINITY ? 0.f : __expf(mw - M);
+      L += wst[w][h][D + 1] * a;
+      o += wst[w][h][d] * a;
+    }
+    const int head = kvh * G + h;
+    if (nparts == 1) {
+      out[(static_cast<size_t>(seq) * nh + head) * D + d] = from_f32<T>(o / L);
+    } else {
+      const size_t mi = (static_cast<size_t>(seq) * nh + head) * max_parts + part;
+      tmp_o[mi * D + d] = o;
+      if (d == 0) { tmp_m[mi] = M; tmp_l[mi] = L; }
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) pa_reduce_kernel(T* __restrict__ out,
                                                         const int* __restrict__ context_lens,
@@ -313,11 +445,16 @@ template <typename T, int D>
 static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out, const void* q,
                         const void* kc, const void* vc, const int* bt, const int* cl, int nh,
                         int nkv, int BS, int max_blocks, int max_parts, float scale, float* tm,
-                        float* tl, void* to, int PART, unsigned* cnt) {
+                        float* tl, void* to, int PART, unsigned* cnt, bool one_pass) {
 #define LUMEN_PA_G(GG)                                                                         \
-  hipLaunchKernelGGL((pa_decode_kernel<T, D, GG>), grid, dim3(256), smem, st, (T*)out,         \
-                     (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks,  \
-                     max_parts, scale, tm, tl, (float*)to, PART, cnt)
+  if (one_pass)                                                                                 \
+    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG>), grid, dim3(256), 0, st, (T*)out,          \
+                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, \
+                       max_parts, scale, tm, tl, (float*)to, PART);                             \
+  else                                                                                          \
+    hipLaunchKernelGGL((pa_decode_kernel<T, D, GG>), grid, dim3(256), smem, st, (T*)out,       \
+                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, \
+                       max_parts, scale, tm, tl, (float*)to, PART, cnt)
   if (G == 1) LUMEN_PA_G(1);
   else if (G == 2) LUMEN_PA_G(2);
   else if (G == 4) LUMEN_PA_G(4);
@@ -329,17 +466,17 @@ template <typename T>
 static hipError_t launch_pa(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, const int* cl, int nseq, int nh, int nkv, int D, int BS,
                             int max_blocks, int max_parts, float scale, float* tm, float* tl,
-                            void* to, int PART, unsigned* cnt, hipStream_t st) {
+                            void* to, int PART, unsigned* cnt, int one_pass, hipStream_t st) {
   const int G = nh / nkv;
   if (G != 1 && G != 2 && G != 4 && G != 8) return hipErrorInvalidValue;
   dim3 grid(nseq, nkv, max_parts);
   const size_t smem = (static_cast<size_t>(G) * PART + 4 * G * D + 2 * G + 8) * sizeof(float);
-  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
-  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
-  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
-  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt);
+  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
+  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
+  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
+  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
   else return hipErrorInvalidValue;
-  if (max_parts > 1 && cnt == nullptr) {  // unfused merge: second kernel
+  if (max_parts > 1 && (cnt == nullptr || one_pass)) {  // unfused merge: second kernel
     dim3 g2(nseq, nh), b2(128);
     hipLaunchKernelGGL(pa_reduce_kernel<T>, g2, b2, 0, st, (T*)out, cl, tm, tl,
                        (const float*)to, nh, D, max_parts, PART);
@@ -356,7 +493,8 @@ extern "C" hipError_t lumen_paged_attention_decode(int dtype, void* out, const v
                                                    int nkv, int D, int BS, int max_blocks,
                                                    int max_parts, float scale, float* tmp_m,
                                                    float* tmp_l, void* tmp_o, int PART,
-                                                   unsigned* counters, hipStream_t st) {
+                                                   unsigned* counters, int one_pass,
+                                                   hipStream_t st) {
   // counters: nullptr = merge split contexts in a second kernel; else >= nseq * nkv zeroed
   // arrival counters (left zeroed again) and the last partition to finish merges in place.
   if (nseq == 0) return hipSuccess;
@@ -364,11 +502,11 @@ extern "C" hipError_t lumen_paged_attention_decode(int dtype, void* out, const v
   if (dtype == lumen::kBF16)
     return lumen::launch_pa<lumen::bf16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, counters, st);
+                                         tmp_o, PART, counters, one_pass, st);
   if (dtype == lumen::kF16)
     return lumen::launch_pa<lumen::fp16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, counters, st);
+                                         tmp_o, PART, counters, one_pass, st);
   return hipErrorInvalidValue;
 }
 

@@ -42,6 +42,8 @@ _merge_counters: dict = {}
 # Fused split-context merge: measured neutral in decode steps (batch 1: 3.857 vs 3.865 ms ITL,
 # profiles/r02_serve), so the two-kernel merge stays the default.
 PA_FUSED_MERGE = os.environ.get("LUMEN_PA_FUSED_MERGE", "0") == "1"
+# single-pass decode kernel (K and V streamed together, online softmax per row group)
+PA_ONE_PASS = os.environ.get("LUMEN_PA_1PASS", "1") == "1"
 
 
 def _pa_counters(device: torch.device, n: int) -> torch.Tensor:
@@ -59,7 +61,7 @@ def _pa_counters(device: torch.device, n: int) -> torch.Tensor:
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                  block_tables: torch.Tensor, context_lens: torch.Tensor, max_context: int,
                  scale: float, partition_size: int = 512,
-                 fused_merge: Optional[bool] = None) -> torch.Tensor:
+                 fused_merge: Optional[bool] = None, one_pass: Optional[bool] = None) -> torch.Tensor:
     """Single-token attention over a paged KV cache.
 
     q [num_seqs, nh, D]; caches [num_blocks, nkv, block_size, D]; block_tables [num_seqs,
@@ -79,12 +81,13 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         else:
             tm = torch.empty(1, 1, 1, device=q.device, dtype=torch.float32)
             tl, to = tm, tm
-        fused = PA_FUSED_MERGE if fused_merge is None else fused_merge
+        one = PA_ONE_PASS if one_pass is None else one_pass
+        fused = (PA_FUSED_MERGE if fused_merge is None else fused_merge) and not one
         cnt = (_pa_counters(q.device, num_seqs * nkv) if fused and max_parts > 1
                else None)
         native().paged_attention_decode(out, q.contiguous(), k_cache, v_cache, block_tables,
                                         context_lens, nkv, bs, block_tables.shape[1], scale, tm,
-                                        tl, to, partition_size, cnt)
+                                        tl, to, partition_size, cnt, one)
         return out
     return paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale)
 

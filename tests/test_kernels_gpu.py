@@ -228,13 +228,18 @@ def test_paged_decode(nh, nkv, D, ctx_max):
     for part in (512, 64):
         o = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part)
         assert rel(o, o2) < 1e-2
+        for one in (True, False):  # single-pass (online softmax) and two-pass kernels
+            assert rel(paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part,
+                                    one_pass=one), o2) < 1e-2
         # fused merge (arrival counters, last partition merges) == two-kernel merge, and the
         # counters reset themselves: a repeat call gives the same bits
-        o_f = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=True)
-        o_sep = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=False)
+        o_f = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=True,
+                           one_pass=False)
+        o_sep = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=False,
+                             one_pass=False)
         assert torch.equal(o_f, o_sep)
-        assert torch.equal(
-            paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=True), o_f)
+        assert torch.equal(paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part,
+                                        fused_merge=True, one_pass=False), o_f)
     from lumen.ops.attention import _merge_counters
 
     assert all(int(c.abs().sum()) == 0 for c in _merge_counters.values())
