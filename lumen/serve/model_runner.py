@@ -17,6 +17,7 @@ removes the per-kernel launch cost that otherwise dominates small-batch decode.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence as Seq
 
@@ -145,7 +146,11 @@ class ModelRunner:
             <= self.car.max_bytes)
         self._graphs: Dict[int, tuple] = {}
         self._graph_pool = None
-        self.partition = 512  # context tokens per decode workgroup at full batch
+        # context tokens per decode workgroup at full batch (LUMEN_PA_PARTITION): 2048 measured
+        # 20.15 vs 20.87 ms ITL at 256 requests (one partition per sequence: no partials, no
+        # merge kernel); the single-pass kernel keeps no per-token scores, so long partitions
+        # cost no LDS
+        self.partition = int(os.environ.get("LUMEN_PA_PARTITION", "2048"))
         self.lora = None  # serve.multi_lora.MultiLoRA when adapters are served un-merged
 
     # ------------------------------------------------------------------------------------------
@@ -262,10 +267,11 @@ class ModelRunner:
         return self._vocab_gather(logits) if gather else logits
 
     def decode_partition(self, n_seqs: int) -> int:
-        """Context tokens per paged-decode workgroup for a batch of ``n_seqs``: 512 once
-        sequences x kv heads alone give >= 2048 workgroups (8 per CU), shorter partitions (down
-        to 64) below that, so a small batch still spreads its KV read over the chip (batch 1 at
-        576 tokens of context: 64 -> 288 workgroups; the kernel went from 53 to a few us)."""
+        """Context tokens per paged-decode workgroup for a batch of ``n_seqs``: the full-batch
+        partition (2048) once sequences x kv heads x partitions give >= 2048 workgroups (8 per
+        CU), shorter partitions (down to 64) below that, so a small batch still spreads its KV
+        read over the chip (batch 1 at 576 tokens of context: 64 -> 288 workgroups; the kernel
+        went from 53 to a few us)."""
         pairs = max(1, n_seqs * self.w.nkv)
         part = self.partition
         while part > 64 and pairs * (self.partition // part) < 2048:
