@@ -564,6 +564,7 @@ def test_dgemm(M, N, K, monkeypatch):
     xv = xb[:, :K]
     assert rel(G.dgemm(xv, w, splits=2), xv.float() @ w.float().t()) < 1e-2
     monkeypatch.setattr(G, "DGEMM", True)  # opt-in dispatch (LUMEN_DGEMM=1)
+    monkeypatch.setattr(G, "SKINNY_MAX_M", 0)  # (the batch <= 4 GEMV would take M = 2..4)
     assert G.dgemm_ok(x, w)
     assert torch.equal(G.linear_nt(x, w), G.dgemm(x, w))
 
