@@ -81,7 +81,10 @@ __device__ __forceinline__ void load_big(uint4 (&v)[4], const T* base, long long
   }
 }
 
-// write the big tile into a swizzled image, applying dropout (index t * ld + dcol0 + col)
+// write the big tile into a swizzled image, applying the dropout MASK (index t * ld + dcol0 +
+// col) as a bit mask on the packed 16-bit values; the 1 / (1 - p) keep-scale is linear and is
+// applied once to the kernel's f32 output (drop_alpha) instead of per element -- the per-element
+// unpack / multiply / repack made these stages VALU-bound (PMC: 0.4 VALU per wave-cycle)
 template <typename T, bool DROP>
 __device__ __forceinline__ void store_big(char* img, uint4 (&v)[4], int r0, int c0, const Drop& d,
                                           long long dcol0) {
@@ -91,17 +94,24 @@ __device__ __forceinline__ void store_big(char* img, uint4 (&v)[4], int r0, int 
     const int row = idx >> 4, ch = idx & 15;
     uint4 u = v[i];
     if (DROP) {
-      float f[8];
-      unpack8<T>(u, f);
       const unsigned long long i0 =
           static_cast<unsigned long long>(r0 + row) * d.ld + dcol0 + c0 + ch * 8;
       const uint32_t keep = dropout_keep8(d.seed, i0, d.thresh);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = (keep >> e) & 1u ? f[e] * d.scale : 0.f;
-      u = pack8<T>(f);
+      // element 2w + h sits in 16-bit half h of word w
+      const auto wmask = [keep](int w) {
+        return ((keep >> (2 * w)) & 1u ? 0x0000FFFFu : 0u) |
+               ((keep >> (2 * w + 1)) & 1u ? 0xFFFF0000u : 0u);
+      };
+      u = make_uint4(u.x & wmask(0), u.y & wmask(1), u.z & wmask(2), u.w & wmask(3));
     }
     *reinterpret_cast<uint4*>(img + img_off(row, ch)) = u;
   }
+}
+
+// output scale of a kernel whose big operand went through store_big<DROP>
+template <bool DROP>
+__device__ __forceinline__ float drop_alpha(const Args& a) {
+  return DROP ? a.alpha * a.drop.scale : a.alpha;
 }
 
 constexpr int kSmallRegs = 8;  // float4 per thread for the small tile (J <= 64)
@@ -206,7 +216,7 @@ __global__ void __launch_bounds__(256) down_kernel(Args a) {
     for (int r = 0; r < 4; ++r) {
       const int t = t0 + wid * 16 + g * 4 + r;
       if (t < a.T) atomicAdd(out + (long long)t * a.cs0 + (long long)(jt * 16 + L) * a.cs1,
-                             a.alpha * acc[jt][r]);
+                             drop_alpha<DROP>(a) * acc[jt][r]);
     }
   }
 }
@@ -310,7 +320,8 @@ __global__ void __launch_bounds__(256) wgrad_kernel(Args a) {
         // accumulator lane holds row 4g + r, column L of the 16x16 tile
         const int m = m0 + wid * 32 + mt * 16 + (SWAP ? L : g * 4 + r);
         const int j = jt * 16 + (SWAP ? g * 4 + r : L);
-        if (m < M) atomicAdd(out + (long long)m * a.cs0 + (long long)j * a.cs1, a.alpha * acc[mt][jt][r]);
+        if (m < M)
+          atomicAdd(out + (long long)m * a.cs0 + (long long)j * a.cs1, drop_alpha<DROP>(a) * acc[mt][jt][r]);
       }
     }
 }
