@@ -123,24 +123,28 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_row_kernel(
   }
 }
 
-template <typename T, int VPL>
+template <typename T, int VPL, int WPR>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ s, const T* __restrict__ w,
     const float* __restrict__ rstd, const T* __restrict__ ds_res, T* __restrict__ dx,
     float* __restrict__ dw, int rows, int H) {
   // All row loads (dy, s and the residual-stream gradient) are issued up front and kept packed
   // (16-bit) in registers, so the reduction and the write-back never wait on a second round of
-  // HBM latency and the VGPR budget leaves room for 3-4 waves per SIMD.
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const size_t base = static_cast<size_t>(row) * H;
-  const float rs = rstd[row];
+  // HBM latency.  WPR waves share a row (WPR = 2 at H = 4096: 48 instead of 96 VGPRs of row
+  // data per lane, twice the waves in flight -- one wave per row measured 4.3 TB/s against the
+  // forward's 5.4); their partial dot products meet in LDS.
+  __shared__ float part[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ws = wid % WPR;
+  const int row = blockIdx.x * (4 / WPR) + wid / WPR;
+  const bool rok = row < rows;  // no early return: the waves of a block meet at a barrier
+  const size_t base = static_cast<size_t>(rok ? row : 0) * H;
+  const float rs = rok ? rstd[row] : 0.f;
   uint4 dyr[VPL], sr[VPL], rr[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const int c = (lane + i * 64) * 8;
-    const bool ok = c < H;
+    const int c = ((i * WPR + ws) * 64 + lane) * 8;
+    const bool ok = rok && c < H;
     dyr[i] = ok ? *reinterpret_cast<const uint4*>(dy + base + c) : make_uint4(0, 0, 0, 0);
     sr[i] = ok ? *reinterpret_cast<const uint4*>(s + base + c) : make_uint4(0, 0, 0, 0);
     rr[i] = (ok && ds_res) ? *reinterpret_cast<const uint4*>(ds_res + base + c) : make_uint4(0, 0, 0, 0);
@@ -148,8 +152,8 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
   float dot = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const int c = (lane + i * 64) * 8;
-    if (c < H) {
+    const int c = ((i * WPR + ws) * 64 + lane) * 8;
+    if (rok && c < H) {
       const T* dyv = reinterpret_cast<const T*>(&dyr[i]);
       const T* sv = reinterpret_cast<const T*>(&sr[i]);
       float wv[8];
@@ -162,11 +166,19 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
       }
     }
   }
-  dot = wave_sum(dot) / static_cast<float>(H);
+  dot = wave_sum(dot);
+  if (WPR > 1) {
+    if (lane == 0) part[wid] = dot;
+    __syncthreads();
+    dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < WPR; ++k) dot += part[(wid / WPR) * WPR + k];
+  }
+  dot /= static_cast<float>(H);
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const int c = (lane + i * 64) * 8;
-    if (c < H) {
+    const int c = ((i * WPR + ws) * 64 + lane) * 8;
+    if (rok && c < H) {
       const T* dyv = reinterpret_cast<const T*>(&dyr[i]);
       const T* sv = reinterpret_cast<const T*>(&sr[i]);
       const T* rv = reinterpret_cast<const T*>(&rr[i]);
@@ -217,17 +229,24 @@ template <typename T>
 static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const float* rstd,
                              const void* ds_res, void* dx, float* dw, int rows, int H,
                              hipStream_t st) {
-  dim3 grid((rows + 3) / 4), block(256);
-  const int vpl = (H + 511) / 512;
-#define LUMEN_RMS_BWD(V)                                                                        \
-  hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, V>), grid, block, 0, st, (const T*)dy, (const T*)s, \
-                     (const T*)w, rstd, (const T*)ds_res, (T*)dx, dw, rows, H)
-  if (vpl <= 1) LUMEN_RMS_BWD(1);
-  else if (vpl <= 2) LUMEN_RMS_BWD(2);
-  else if (vpl <= 4) LUMEN_RMS_BWD(4);
-  else if (vpl <= 8) LUMEN_RMS_BWD(8);
-  else if (vpl <= 16) LUMEN_RMS_BWD(16);
-  else return hipErrorInvalidValue;
+  dim3 block(256);
+  // two waves per row once a row needs more than 4 vectors per lane (H > 2048)
+  const int wpr = H > 2048 ? 2 : 1;
+  dim3 grid((rows + 4 / wpr - 1) / (4 / wpr));
+  const int vpl = (H + 512 * wpr - 1) / (512 * wpr);
+#define LUMEN_RMS_BWD(V, W)                                                                     \
+  hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, V, W>), grid, block, 0, st, (const T*)dy,          \
+                     (const T*)s, (const T*)w, rstd, (const T*)ds_res, (T*)dx, dw, rows, H)
+  if (wpr == 1) {
+    if (vpl <= 1) LUMEN_RMS_BWD(1, 1);
+    else if (vpl <= 2) LUMEN_RMS_BWD(2, 1);
+    else LUMEN_RMS_BWD(4, 1);
+  } else {
+    if (vpl <= 4) LUMEN_RMS_BWD(4, 2);
+    else if (vpl <= 8) LUMEN_RMS_BWD(8, 2);
+    else if (vpl <= 16) LUMEN_RMS_BWD(16, 2);
+    else return hipErrorInvalidValue;
+  }
 #undef LUMEN_RMS_BWD
   return hipGetLastError();
 }
