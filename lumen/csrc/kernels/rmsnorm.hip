@@ -17,23 +17,29 @@
 //       dw (optional) += sum_rows(dy * s * rstd)  (f32, per-block partials then atomics)
 #include "common.h"
 
+#include <cstdlib>
+
 namespace lumen {
 
-template <typename T, int VPL>
+template <typename T, int VPL, int WPR = 1>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
     const T* __restrict__ x, const T* __restrict__ residual, const T* __restrict__ w,
     T* __restrict__ y, T* __restrict__ s_out, float* __restrict__ rstd_out, int rows, int H,
     float eps) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const size_t base = static_cast<size_t>(row) * H;
+  // WPR waves per row (2 at H > 2048: half the row registers per lane, more waves in flight);
+  // their partial sums of squares meet in LDS
+  __shared__ float part[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ws = wid % WPR;
+  const int row = blockIdx.x * (4 / WPR) + wid / WPR;
+  const bool rok = row < rows;  // no early return: the waves of a block meet at a barrier
+  const size_t base = static_cast<size_t>(rok ? row : 0) * H;
   float v[VPL][8];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const int c = (lane + i * 64) * 8;
-    if (c < H) {
+    const int c = ((i * WPR + ws) * 64 + lane) * 8;
+    if (rok && c < H) {
       load8(x + base + c, v[i]);
       if (residual) {
         float r[8];
@@ -46,12 +52,19 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
     }
   }
   ss = wave_sum(ss);
+  if (WPR > 1) {
+    if (lane == 0) part[wid] = ss;
+    __syncthreads();
+    ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < WPR; ++k) ss += part[(wid / WPR) * WPR + k];
+  }
   const float rs = rsqrtf(ss / static_cast<float>(H) + eps);
-  if (lane == 0 && rstd_out) rstd_out[row] = rs;
+  if (rok && lane == 0 && ws == 0 && rstd_out) rstd_out[row] = rs;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const int c = (lane + i * 64) * 8;
-    if (c < H) {
+    const int c = ((i * WPR + ws) * 64 + lane) * 8;
+    if (rok && c < H) {
       if (s_out) {
         // round the residual stream to the activation dtype first: the normalisation below
         // must see exactly the value the next layer reads back.
@@ -210,17 +223,29 @@ static hipError_t launch_fwd(const void* x, const void* res, const void* w, void
 #undef LUMEN_RMS_ROW
     return hipGetLastError();
   }
-  dim3 grid((rows + 3) / 4);
-  const int vpl = (H + 511) / 512;
-#define LUMEN_RMS_FWD(V)                                                                          \
-  hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, V>), grid, block, 0, st, (const T*)x, (const T*)res, \
-                     (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps)
-  if (vpl <= 1) LUMEN_RMS_FWD(1);
-  else if (vpl <= 2) LUMEN_RMS_FWD(2);
-  else if (vpl <= 4) LUMEN_RMS_FWD(4);
-  else if (vpl <= 8) LUMEN_RMS_FWD(8);
-  else if (vpl <= 16) LUMEN_RMS_FWD(16);
-  else return hipErrorInvalidValue;
+  // two waves per row above H = 2048 (LUMEN_RMS_FWD_WPR=1: one)
+  static const int env_wpr = [] {
+    const char* e = getenv("LUMEN_RMS_FWD_WPR");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  const int wpr = H > 2048 ? env_wpr : 1;
+  dim3 grid((rows + 4 / wpr - 1) / (4 / wpr));
+  const int vpl = (H + 512 * wpr - 1) / (512 * wpr);
+#define LUMEN_RMS_FWD(V, W)                                                                       \
+  hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, V, W>), grid, block, 0, st, (const T*)x,             \
+                     (const T*)res, (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps)
+  if (wpr == 1) {
+    if (vpl <= 1) LUMEN_RMS_FWD(1, 1);
+    else if (vpl <= 2) LUMEN_RMS_FWD(2, 1);
+    else if (vpl <= 4) LUMEN_RMS_FWD(4, 1);
+    else if (vpl <= 8) LUMEN_RMS_FWD(8, 1);
+    else if (vpl <= 16) LUMEN_RMS_FWD(16, 1);
+    else return hipErrorInvalidValue;
+  } else {
+    if (vpl <= 4) LUMEN_RMS_FWD(4, 2);
+    else if (vpl <= 8) LUMEN_RMS_FWD(8, 2);
+    else return hipErrorInvalidValue;
+  }
 #undef LUMEN_RMS_FWD
   return hipGetLastError();
 }
