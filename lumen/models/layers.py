@@ -158,6 +158,15 @@ class Linear(nn.Module):
 GATHERED_TN = ("q_proj", "down_proj", "fc2")
 
 
+def _gathered_tn() -> tuple:
+    """Linears whose ZeRO-3-gathered weights get a per-step W^T (env ``LUMEN_GATHERED_TN``:
+    comma list of first-segment names, overriding ``GATHERED_TN``)."""
+    import os
+
+    e = os.environ.get("LUMEN_GATHERED_TN")
+    return GATHERED_TN if e is None else tuple(x for x in e.split(",") if x)
+
+
 def configure_backward_layout(model: nn.Module, policy=None) -> int:
     """Enable the transposed-weight (TN) input-gradient GEMM on the linears whose first segment
     name is in ``policy`` (env ``LUMEN_BWD_WT``: comma list, ``all`` or ``none``; default
@@ -173,6 +182,7 @@ def configure_backward_layout(model: nn.Module, policy=None) -> int:
     else:
         names = set(policy)
     budget = _transpose_budget(model)
+    gathered_tn = _gathered_tn()
     n = 0
     for name, m in model.named_modules():
         if isinstance(m, Linear):
@@ -185,7 +195,7 @@ def configure_backward_layout(model: nn.Module, policy=None) -> int:
             m.transpose_bwd = on
             # per-step transposes of gathered weights pay off where the NN GEMM is slowest
             # relative to the transpose's traffic (q|k|v: 299 -> 188 us, down: 277 -> 200 us)
-            m.transpose_gathered = on and m.seg_names[0] in GATHERED_TN
+            m.transpose_gathered = on and m.seg_names[0] in gathered_tn
             m.invalidate_weight_cache()
             n += int(on)
     return n
