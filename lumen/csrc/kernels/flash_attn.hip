@@ -1259,7 +1259,10 @@ __device__ __forceinline__ void dq32_tile(const char* kimg, const char* vimg, co
 
 // ---- backward dQ: 32 queries per wave, 128 per workgroup ------------------------------------
 // S^T = K Q^T, dP^T = V dO^T (keys on rows, lane = query); dQ^T += K^T dS^T.
-template <typename T, bool CAUSAL>
+// FUSE_DELTA: the kernel also forms delta = rowsum(dO * O) for its own 128 queries (from L2-warm
+// rows it is loading anyway) and writes it for the dK/dV kernel, which then runs after it --
+// this replaces the separate delta pass over O and dO.
+template <typename T, bool CAUSAL, bool FUSE_DELTA = false>
 __global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
   constexpr int BM = 128;
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
@@ -1274,20 +1277,38 @@ __global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
   const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
   const int wq0 = q0 + wid * 32;
   const int qrow = wq0 + lq;
-  uint4 qf[8], of[8];
+  uint4 qf[8], of[8], ob[8];
+  // FUSE_DELTA: this lane's O fragments, issued with the Q / dO loads so one latency covers all
+  const T* orow = reinterpret_cast<const T*>(a.o) + (long long)(s0 + qrow) * a.ldo + head * D;
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) {
     qf[ks] = gload16(Q + (long long)qrow * a.ldq + 16 * ks + 8 * hi, qrow < L);
     of[ks] = gload16(dO + (long long)qrow * a.lddo + 16 * ks + 8 * hi, qrow < L);
+    if constexpr (FUSE_DELTA) ob[ks] = gload16(orow + 16 * ks + 8 * hi, qrow < L);
   }
   const float lse_q = qrow < L ? a.lse[(long long)head * a.T + s0 + qrow] : INFINITY;
-  const float del_q = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
+  float del_q = 0.f;
+  if constexpr (!FUSE_DELTA) del_q = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
   f32x16 dq[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) dq[n] = zero16();
   const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
   const int w_end = CAUSAL ? min(kv_end, wq0 + 32) : kv_end;
   wait_vm_all();
+  if constexpr (FUSE_DELTA) {
+    // delta = rowsum(dO * O): lanes q and q + 32 hold the two halves of every 16-column chunk
+    float sd = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const T* x = reinterpret_cast<const T*>(&of[ks]);
+      const T* y = reinterpret_cast<const T*>(&ob[ks]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sd += to_f32(x[e]) * to_f32(y[e]);
+    }
+    sd += __shfl_xor(sd, 32, 64);
+    del_q = sd;  // 0 for rows past the end (their fragments were zero-filled)
+    if (hi == 0 && qrow < L) const_cast<float*>(a.delta)[(long long)head * a.T + s0 + qrow] = sd;
+  }
   if (kv_end > 0) {
     stage64_async(smem, K, a.ldk, 0, L);
     stage64_async(smem + IMG, V, a.ldv, 0, L);
@@ -1396,10 +1417,16 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     dim3 grid(ntiles, a.nkv);
     if (causal) hipLaunchKernelGGL((bwd_dkdv32_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dkdv32_kernel<T, false>), grid, block, 0, st, a);
-  } else if (which == 5) {  // dQ, 32x32x16 kernel, 128-query tiles
+  } else if (which == 5) {  // dQ, 32x32x16 kernel, 128-query tiles (mt == 2: + delta)
     dim3 grid(ntiles, a.nh);
-    if (causal) hipLaunchKernelGGL((bwd_dq32_kernel<T, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((bwd_dq32_kernel<T, false>), grid, block, 0, st, a);
+    if (mt == 2) {
+      if (causal) hipLaunchKernelGGL((bwd_dq32_kernel<T, true, true>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((bwd_dq32_kernel<T, false, true>), grid, block, 0, st, a);
+    } else if (causal) {
+      hipLaunchKernelGGL((bwd_dq32_kernel<T, true>), grid, block, 0, st, a);
+    } else {
+      hipLaunchKernelGGL((bwd_dq32_kernel<T, false>), grid, block, 0, st, a);
+    }
   } else {
     return hipErrorInvalidValue;
   }
@@ -1412,7 +1439,8 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 // which: 0 = forward (tiles of 64*mt query rows; mt >= 10 selects the transposed-formulation
 //        kernel with 64*(mt-10)-row tiles; mt == 20 the 32x32x16 kernel, 128-row tiles),
 //        1 = delta, 2 = dK/dV (64-key tiles), 3 = dQ (64-query tiles),
-//        4 = dK/dV (32x32x16, 128-key tiles), 5 = dQ (32x32x16, 128-query tiles)
+//        4 = dK/dV (32x32x16, 128-key tiles), 5 = dQ (32x32x16, 128-query tiles; mt == 2: it
+//        also writes delta, so it runs before dK/dV and replaces which 1)
 extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
                                        const void* q, const void* k, const void* v,
                                        long long ldq, long long ldk, long long ldv, void* o,

@@ -203,6 +203,9 @@ FA_FWD_ROWS = _fwd_rows(FA_FWD_MT)
 # backward kernels: "v16" = 16x16x32 dK/dV (64-key tiles) + dQ (64-query tiles);
 # "v32" = 32x32x16 kernels with 128-row tiles; "mix" = 16x16x32 dK/dV + 32x32x16 dQ
 FA_BWD = _os.environ.get("LUMEN_FA_BWD", "mix")
+# LUMEN_FA_DQ_DELTA=1: the 32x32 dQ kernel forms delta itself and runs before dK/dV (opt-in:
+# measured neutral end to end and +0.22 ms/step of kernel time, profiles/r04_train)
+FA_DQ_DELTA = _os.environ.get("LUMEN_FA_DQ_DELTA", "0") == "1"
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -242,8 +245,6 @@ class _FlashAttn(torch.autograd.Function):
         dv = dqkv[:, (nh + nkv) * D:]
         delta = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
         cut = _cu_tensor(cu, qkv.device)
-        C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
-                     scale, do, None, None, None, delta, None, None, None)
         # dK/dV and dQ kernels per FA_BWD: "v16" both 16x16x32 (64-row tiles), "v32" both
         # 32x32x16 (128-row tiles), "mix" = 16x16x32 dK/dV + 32x32x16 dQ
         wkv, rkv = (4, 128) if FA_BWD == "v32" else (2, 64)
@@ -252,10 +253,20 @@ class _FlashAttn(torch.autograd.Function):
         # written directly): the producer of q|k then skips its own inverse-rotation pass
         rp = ctx.rope if (ctx.rope is not None and wkv == 2 and wq == 5) else None
         pos, cos, sin = rp if rp is not None else (None, None, None)
-        C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh, nkv,
-                     scale, do, dq, dk, dv, delta, pos, cos, sin)
-        C.flash_attn(wq, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rq, qkv.device), nh, nkv,
-                     scale, do, dq, dk, dv, delta, pos, cos, sin)
+        qtiles = _tiles(cu, rq, qkv.device)
+        if wq == 5 and FA_DQ_DELTA:
+            # the 32x32 dQ kernel forms delta = rowsum(dO * O) itself and runs first
+            C.flash_attn(wq, causal, 2, q, k, v, o, lse, cut, qtiles, nh, nkv,
+                         scale, do, dq, dk, dv, delta, pos, cos, sin)
+            C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh,
+                         nkv, scale, do, dq, dk, dv, delta, pos, cos, sin)
+        else:
+            C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
+                         scale, do, None, None, None, delta, None, None, None)
+            C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh,
+                         nkv, scale, do, dq, dk, dv, delta, pos, cos, sin)
+            C.flash_attn(wq, causal, 1, q, k, v, o, lse, cut, qtiles, nh, nkv,
+                         scale, do, dq, dk, dv, delta, pos, cos, sin)
         if rp is not None:
             dqkv._lumen_rope_undone = True
         return dqkv, None, None, None, None, None, None

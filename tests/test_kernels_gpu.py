@@ -283,15 +283,17 @@ def test_sampling_greedy_and_topk():
 @pytest.mark.parametrize("nh,nkv,lens", [(8, 8, [512, 512]), (8, 2, [512, 300, 77]),
                                          (4, 4, [1000, 64, 129])])
 @pytest.mark.parametrize("fwd,bwd", [("t1", "v16"), ("t2", "v16"), ("old", "v16"),
-                                     ("v32", "v32"), ("v32", "mix")])
+                                     ("v32", "v32"), ("v32", "mix"), ("v32", "mix-sep")])
 def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch):
+    """bwd "mix-sep": mix kernels with the separate delta pass instead of the dQ kernel's own."""
     import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
 
     mt = {"t1": 11, "t2": 12, "old": 1, "v32": 20}[fwd]
     monkeypatch.setattr(att, "FA_FWD_MT", mt)
     monkeypatch.setattr(att, "FA_FWD_ROWS", att._fwd_rows(mt))
-    monkeypatch.setattr(att, "FA_BWD", bwd)
+    monkeypatch.setattr(att, "FA_DQ_DELTA", bwd != "mix-sep")
+    monkeypatch.setattr(att, "FA_BWD", "mix" if bwd == "mix-sep" else bwd)
 
     D = 128
     cu = [0]
