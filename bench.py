@@ -23,6 +23,8 @@ import os
 import sys
 import time
 
+T_START = time.time()
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -72,6 +74,8 @@ def main():
     from lumen.train.config import load_ds_config
     from lumen.train.engine import ZeroEngine
 
+    # a hung collective must end the run (non-zero exit), not eat the driver's time budget
+    os.environ.setdefault("LUMEN_DIST_TIMEOUT", "300")
     env = init()
     world = env.world_size
     from lumen.utils.gemm_tuning import load_tuned_gemms, start_gemm_tuning, tuned_entries
@@ -86,7 +90,7 @@ def main():
     ds = load_ds_config(args.config, args.micro_batch, args.grad_accum, world, 2e-4)
     torch.manual_seed(1234)
     cfg = get_config(args.model)
-    t0 = time.time()
+    t_build = time.time()
     model = build_model(args.model, dtype=ds.torch_dtype, device=env.device, init="random", seed=0)
     apply_lora(model, LoraConfig(r=args.lora_r, lora_dropout=0.05))
     model.gradient_checkpointing = args.gradient_checkpointing
@@ -96,7 +100,21 @@ def main():
     on_gpu = env.device.type == "cuda"
     if on_gpu:
         torch.cuda.synchronize()
-    setup_s = time.time() - t0
+    build_s = time.time() - t_build
+    setup_s = time.time() - T_START  # process start -> engine ready (imports, init, build)
+    coord = engine.coordinator
+    # what RCCL itself sees: an all-reduce of ones over the default (gradient) group, and over
+    # the ZeRO-3 weight-gather group when it is a separate communicator
+    rccl_world = world
+    gather_world = None
+    if dist.is_initialized():
+        one = torch.ones(1, device=env.device)
+        dist.all_reduce(one)
+        rccl_world = int(one.item())
+        if engine.gather_group is not None:
+            one = torch.ones(1, device=env.device)
+            dist.all_reduce(one, group=engine.gather_group)
+            gather_world = int(one.item())
 
     B, S = ds.micro_batch, args.seq_len
     n_batches = (args.warmup + args.steps) * ds.grad_accum
@@ -140,8 +158,10 @@ def main():
 
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
-    coord = engine.coordinator
     gb0 = coord.gathered_bytes if coord else 0
+    if coord is not None:
+        coord.pop_exposed_wait_ms()
+        coord.track_waits = True  # timing events around every gather wait (exposed comm)
     t1 = time.perf_counter()
     loss = run_steps(args.steps, args.warmup)
     sync()
@@ -152,14 +172,24 @@ def main():
         prof.export_chrome_trace(os.path.join(args.profile_dir, "bench_trace.json"))
         with open(os.path.join(args.profile_dir, "bench_ops.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
-    t = torch.tensor([dt], device=env.device)
+    exposed_ms = coord.pop_exposed_wait_ms() if coord is not None else 0.0
+    peak_gb = torch.cuda.max_memory_allocated() / 1e9 if on_gpu else 0.0
+    # max over ranks of: timed region, exposed gather wait, peak HBM
+    t = torch.tensor([dt, exposed_ms, peak_gb], dtype=torch.float64 if not on_gpu
+                     else torch.float32, device=env.device)
     if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+    dt, exposed_ms, peak_gb = (float(x) for x in t.tolist())
     final_loss = float(loss.item())
     tokens = world * B * ds.grad_accum * S * args.steps
     value = tokens / dt
-    peak_gb = torch.cuda.max_memory_allocated() / 1e9 if on_gpu else 0.0
+    if coord is None:
+        par = f"dp{world}-zero{ds.stage}"
+    elif coord.identity:
+        par = f"dp{world}-zero{ds.stage}(world-1 partition = whole model: no gathers)"
+    else:
+        par = f"dp{world}-zero{ds.stage}"
+    gathered_mb = ((coord.gathered_bytes - gb0) / 1e6 / args.steps) if coord else 0.0
     if env.is_main:
         from lumen.train.trainer import model_flops_per_token
 
@@ -183,7 +213,7 @@ def main():
                 "micro_batch": B,
                 "grad_accum": ds.grad_accum,
                 "seq_len": S,
-                "parallelism": f"dp{world}-zero{ds.stage}",
+                "parallelism": par,
                 "lora": f"r={args.lora_r} alpha={2 * args.lora_r} dropout=0.05 q,k,v,o",
                 "trainable_params": n_tr,
                 "total_params": n_all,
@@ -191,18 +221,24 @@ def main():
             "extra": {
                 "tflops_per_gpu": round(tflops, 1),
                 "samples_per_second": round(B * ds.grad_accum * world * args.steps / dt, 2),
-                "peak_mem_gb_rank0": round(peak_gb, 2),
+                "peak_hbm_gb_max_rank": round(peak_gb, 2),
                 "final_loss": round(final_loss, 4),
-                "setup_s": round(setup_s, 1),
-                "zero3_schedule": coord.schedule if coord else None,
-                "zero3_gathered_mb_per_step": (round((coord.gathered_bytes - gb0) / 1e6
-                                                     / args.steps, 1) if coord else 0.0),
+                "setup_s": round(setup_s, 2),
+                "model_build_s": round(build_s, 3),
+                "rccl_world": rccl_world,
+                "gather_group_world": gather_world,
+                "backend": env.backend,
+                "zero3": coord.stats() if coord else None,
+                "zero3_gathered_mb_per_step": round(gathered_mb, 1),
+                "zero3_received_mb_per_step_per_rank": round(gathered_mb * (world - 1) / world, 1),
+                "zero3_exposed_wait_ms_per_step_max_rank": round(exposed_ms / args.steps, 2),
                 "baseline_tok_s": BASELINE_TOK_S,
                 "gemm_algos": gemm_table,
                 "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,
             },
         }
         print(json.dumps(out), flush=True)
+    engine.close()  # drain in-flight (next-step) gathers before teardown
     if dist.is_initialized():
         from lumen.parallel.dist import barrier
 

@@ -27,7 +27,8 @@ hipError_t lumen_cross_entropy(int, void*, const int64_t*, float*, float*, int, 
                                int, hipStream_t);
 hipError_t lumen_grad_norm_sq(int, const void*, long long, float*, hipStream_t);
 hipError_t lumen_adamw(float*, int, const void*, float*, float*, int, void*, long long, float, float,
-                       float, float, float, float, float, float, const float*, float, hipStream_t);
+                       float, float, float, float, float, float, const float*, float, float*,
+                       hipStream_t);
 hipError_t lumen_lora_gemm(int, int, int, const void*, const void*, void*, long long, long long,
                            long long, long long, float, int, unsigned long long, unsigned int, float,
                            long long, int, const long long*, const long long*, const long long*,
@@ -70,9 +71,11 @@ hipError_t lumen_car_open_handle(const void*, void**);
 hipError_t lumen_car_close_handle(void*);
 hipError_t lumen_car_read_err(void*, unsigned int*);
 hipError_t lumen_car_allreduce(int, const long long*, const long long*, int, int, const void*,
-                               void*, long long, int, int, double, hipStream_t);
+                               void*, long long, int, int, double, void*, hipStream_t);
 hipError_t lumen_car_allgather(int, const long long*, const long long*, int, int, const void*,
-                               void*, long long, long long, int, double, hipStream_t);
+                               void*, long long, long long, int, double, void*, hipStream_t);
+hipError_t lumen_car_host_flag_alloc(void**, void**);
+hipError_t lumen_car_host_flag_free(void*);
 void lumen_cpu_adamw(float*, const float*, float*, float*, long long, float, float, float, float,
                      float, float, float, float);
 int lumen_cpu_has_avx512();
@@ -237,8 +240,11 @@ void grad_norm_sq(const at::Tensor& g, at::Tensor& out) {
 void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
            const std::optional<at::Tensor>& out_copy, double lr, double b1, double b2, double eps,
            double wd, double bc1, double bc2, double inv_scale,
-           const std::optional<at::Tensor>& norm_sq, double max_norm) {
+           const std::optional<at::Tensor>& norm_sq, double max_norm,
+           const std::optional<at::Tensor>& step_state) {
   need_cuda(p, "param"); need_cuda(g, "grad"); need_cuda(m, "exp_avg"); need_cuda(v, "exp_avg_sq");
+  if (step_state.has_value() && (step_state->scalar_type() != at::kFloat || step_state->numel() < 2))
+    throw std::invalid_argument("lumen: adamw step_state must be f32[2] (applied, skipped)");
   if (p.scalar_type() != at::kFloat) throw std::invalid_argument("lumen: adamw master must be f32");
   const int od = out_copy.has_value() ? dcode(*out_copy) : 0;
   check(lumen_adamw(p.data_ptr<float>(), dcode(g), g.data_ptr(), m.data_ptr<float>(),
@@ -246,7 +252,7 @@ void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                     static_cast<float>(b1), static_cast<float>(b2), static_cast<float>(eps),
                     static_cast<float>(wd), static_cast<float>(bc1), static_cast<float>(bc2),
                     static_cast<float>(inv_scale), ptr<const float>(norm_sq),
-                    static_cast<float>(max_norm), cur_stream()),
+                    static_cast<float>(max_norm), ptr<float>(step_state), cur_stream()),
         "adamw");
 }
 
@@ -469,8 +475,27 @@ int64_t car_open(const py::bytes& handle) {
 
 void car_close(int64_t p) { check(lumen_car_close_handle(reinterpret_cast<void*>(p)), "car_close"); }
 
+// pinned host-mapped error word: (host address, device address); read with car_host_flag_read
+std::vector<int64_t> car_host_flag_alloc() {
+  void *h = nullptr, *d = nullptr;
+  check(lumen_car_host_flag_alloc(&h, &d), "car_host_flag_alloc");
+  return {reinterpret_cast<int64_t>(h), reinterpret_cast<int64_t>(d)};
+}
+
+void car_host_flag_free(int64_t h) {
+  check(lumen_car_host_flag_free(reinterpret_cast<void*>(h)), "car_host_flag_free");
+}
+
+// a plain load of the host word: no device sync (the kernel writes it system-coherently)
+int64_t car_host_flag_read(int64_t h) {
+  return static_cast<int64_t>(*reinterpret_cast<volatile uint32_t*>(h));
+}
+
+void car_host_flag_clear(int64_t h) { *reinterpret_cast<volatile uint32_t*>(h) = 0; }
+
 void car_allgather(const std::vector<int64_t>& data, const std::vector<int64_t>& sig, int rank,
-                   const at::Tensor& in, at::Tensor& out, int blocks, double timeout_s) {
+                   const at::Tensor& in, at::Tensor& out, int blocks, double timeout_s,
+                   int64_t host_err) {
   need_cuda(in, "in");
   need_cuda(out, "out");
   const int world = (int)data.size();
@@ -481,7 +506,8 @@ void car_allgather(const std::vector<int64_t>& data, const std::vector<int64_t>&
     throw std::invalid_argument("lumen: car_allgather shapes: in [R, Vs], out [R, W*Vs], Vs % 8 == 0");
   std::vector<long long> d(data.begin(), data.end()), s(sig.begin(), sig.end());
   check(lumen_car_allgather(dcode(in), d.data(), s.data(), rank, world, in.data_ptr(),
-                            out.data_ptr(), in.size(0), in.size(1), blocks, timeout_s, cur_stream()),
+                            out.data_ptr(), in.size(0), in.size(1), blocks, timeout_s,
+                            reinterpret_cast<void*>(host_err), cur_stream()),
         "car_allgather");
 }
 
@@ -493,7 +519,7 @@ int64_t car_err(int64_t sig) {
 
 void car_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>& sig, int rank,
                    const at::Tensor& in, at::Tensor& out, bool two_shot, int blocks,
-                   double timeout_s) {
+                   double timeout_s, int64_t host_err) {
   need_cuda(in, "in");
   need_cuda(out, "out");
   const int world = (int)data.size();
@@ -504,7 +530,7 @@ void car_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>&
   std::vector<long long> d(data.begin(), data.end()), s(sig.begin(), sig.end());
   check(lumen_car_allreduce(dcode(in), d.data(), s.data(), rank, world, in.data_ptr(),
                             out.data_ptr(), in.numel(), two_shot ? 1 : 0, blocks, timeout_s,
-                            cur_stream()),
+                            reinterpret_cast<void*>(host_err), cur_stream()),
         "car_allreduce");
 }
 
@@ -536,6 +562,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("car_open", &car_open);
   m.def("car_close", &car_close);
   m.def("car_err", &car_err);
+  m.def("car_host_flag_alloc", &car_host_flag_alloc);
+  m.def("car_host_flag_free", &car_host_flag_free);
+  m.def("car_host_flag_read", &car_host_flag_read);
+  m.def("car_host_flag_clear", &car_host_flag_clear);
   m.def("car_allreduce", &car_allreduce);
   m.def("car_allgather", &car_allgather);
   m.def("car_signal_bytes", &lumen_car_signal_bytes);

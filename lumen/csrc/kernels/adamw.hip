@@ -45,8 +45,16 @@ template <typename G, typename O>
 __global__ void __launch_bounds__(256) adamw_kernel(
     float* __restrict__ p, const G* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     O* __restrict__ out_copy, long long n, float lr, float beta1, float beta2, float eps, float wd,
-    float bc1, float bc2, float inv_scale, const float* __restrict__ norm_sq, float max_norm) {
+    float bc1, float bc2, float inv_scale, const float* __restrict__ norm_sq, float max_norm,
+    const float* __restrict__ step_state) {
   float coef = inv_scale;
+  if (step_state) {
+    // device-side Adam step counter: t = applied updates so far + 1, so a skipped (non-finite)
+    // step never advances the bias correction (adamw_commit_kernel counts it afterwards)
+    const float t = step_state[0] + 1.f;
+    bc1 = 1.f - powf(beta1, t);
+    bc2 = 1.f - powf(beta2, t);
+  }
   if (norm_sq) {
     const float nsq = *norm_sq;
     if (!isfinite(nsq)) return;  // overflow: skip the step (loss scaler backs off on the host)
@@ -93,6 +101,14 @@ __global__ void __launch_bounds__(256) adamw_kernel(
   }
 }
 
+// after adamw_kernel: count the step as applied (state[0]) or skipped (state[1])
+__global__ void adamw_commit_kernel(float* __restrict__ state, const float* __restrict__ norm_sq) {
+  if (threadIdx.x == 0) {
+    const bool ok = norm_sq == nullptr || isfinite(*norm_sq);
+    state[ok ? 0 : 1] += 1.f;
+  }
+}
+
 static inline unsigned grid_for(long long n) {
   long long blocks = (n + 256 * 8 - 1) / (256 * 8);
   if (blocks > 2048) blocks = 2048;  // grid-stride the rest
@@ -124,13 +140,13 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
                                   int out_dtype, void* out_copy, long long n, float lr,
                                   float beta1, float beta2, float eps, float wd, float bc1,
                                   float bc2, float inv_scale, const float* norm_sq, float max_norm,
-                                  hipStream_t st) {
+                                  float* step_state, hipStream_t st) {
   if (n == 0) return hipSuccess;
   dim3 grid(lumen::grid_for(n)), block(256);
 #define LUMEN_ADAMW(G, O)                                                                    \
   hipLaunchKernelGGL((lumen::adamw_kernel<G, O>), grid, block, 0, st, p, (const G*)g, m, v, \
                      (O*)out_copy, n, lr, beta1, beta2, eps, wd, bc1, bc2, inv_scale, norm_sq,  \
-                     max_norm)
+                     max_norm, step_state)
   if (gdtype == lumen::kF32) {
     if (out_copy == nullptr || out_dtype == lumen::kF32) LUMEN_ADAMW(float, float);
     else if (out_dtype == lumen::kBF16) LUMEN_ADAMW(float, lumen::bf16);
@@ -147,5 +163,8 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
     return hipErrorInvalidValue;
   }
 #undef LUMEN_ADAMW
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || step_state == nullptr) return e;
+  hipLaunchKernelGGL(lumen::adamw_commit_kernel, dim3(1), dim3(64), 0, st, step_state, norm_sq);
   return hipGetLastError();
 }

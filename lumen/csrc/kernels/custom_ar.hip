@@ -28,6 +28,9 @@
 //
 // Every spin has a deadline (s_memrealtime, 100 MHz). A rank whose peer never arrives sets
 // `err` and leaves, so a missing peer turns into a host-visible error instead of a hung GPU.
+// The same timeout also sets a word in pinned, host-mapped memory (`host_err`), so the host
+// can poll it after every step with a plain load -- no device sync, no copy -- and stop before
+// it hands out tokens computed from a half-reduced tensor.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -52,6 +55,7 @@ struct Signal {
 struct Peers {
   void* data[kMaxRanks];
   Signal* sig[kMaxRanks];
+  uint32_t* host_err;  // pinned host-mapped error word (device view), or null
 };
 
 __device__ __forceinline__ void block_barrier(const Peers& P, Signal* self, int slot, int rank,
@@ -71,6 +75,8 @@ __device__ __forceinline__ void block_barrier(const Peers& P, Signal* self, int 
     while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > deadline_ticks) {
         __hip_atomic_fetch_or(&self->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (P.host_err)
+          __hip_atomic_store(P.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -256,6 +262,16 @@ hipError_t lumen_car_open_handle(const void* handle, void** ptr) {
 
 hipError_t lumen_car_close_handle(void* ptr) { return hipIpcCloseMemHandle(ptr); }
 
+// pinned host word the kernels raise on a barrier timeout; *dev is its device-side address
+hipError_t lumen_car_host_flag_alloc(void** host, void** dev) {
+  hipError_t e = hipHostMalloc(host, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return e;
+  memset(*host, 0, 64);
+  return hipHostGetDevicePointer(dev, *host, 0);
+}
+
+hipError_t lumen_car_host_flag_free(void* host) { return hipHostFree(host); }
+
 hipError_t lumen_car_read_err(void* sig, unsigned int* err) {
   return hipMemcpy(err, &reinterpret_cast<Signal*>(sig)->err, sizeof(unsigned int),
                    hipMemcpyDeviceToHost);
@@ -264,10 +280,11 @@ hipError_t lumen_car_read_err(void* sig, unsigned int* err) {
 // data[i] / sig[i]: rank i's staging buffer and signal as mapped in THIS process
 hipError_t lumen_car_allreduce(int dtype, const long long* data, const long long* sig, int rank,
                                int world, const void* in, void* out, long long numel, int two_shot,
-                               int blocks, double timeout_s, hipStream_t st) {
+                               int blocks, double timeout_s, void* host_err, hipStream_t st) {
   if (world < 1 || world > kMaxRanks || blocks < 1 || blocks > kMaxBlocks || (numel & 7))
     return hipErrorInvalidValue;
   Peers P{};
+  P.host_err = reinterpret_cast<uint32_t*>(host_err);
   for (int i = 0; i < world; ++i) {
     P.data[i] = reinterpret_cast<void*>(data[i]);
     P.sig[i] = reinterpret_cast<Signal*>(sig[i]);
@@ -282,10 +299,12 @@ hipError_t lumen_car_allreduce(int dtype, const long long* data, const long long
 
 hipError_t lumen_car_allgather(int dtype, const long long* data, const long long* sig, int rank,
                                int world, const void* in, void* out, long long rows,
-                               long long shard_cols, int blocks, double timeout_s, hipStream_t st) {
+                               long long shard_cols, int blocks, double timeout_s, void* host_err,
+                               hipStream_t st) {
   if (world < 1 || world > kMaxRanks || blocks < 1 || blocks > kMaxBlocks || (shard_cols & 7))
     return hipErrorInvalidValue;
   Peers P{};
+  P.host_err = reinterpret_cast<uint32_t*>(host_err);
   for (int i = 0; i < world; ++i) {
     P.data[i] = reinterpret_cast<void*>(data[i]);
     P.sig[i] = reinterpret_cast<Signal*>(sig[i]);

@@ -127,6 +127,10 @@ PRESETS = {
     "tiny-llama": dict(arch="llama", vocab_size=512, hidden_size=256, intermediate_size=688,
                        num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=4,
                        max_position_embeddings=512, name="tiny-llama"),
+    # deeper toy model: 8 ZeRO-3 units, so the release ring / prefetch / turn-reuse logic has room
+    "tiny-llama-deep": dict(arch="llama", vocab_size=512, hidden_size=128, intermediate_size=344,
+                            num_hidden_layers=6, num_attention_heads=4, num_key_value_heads=2,
+                            max_position_embeddings=512, name="tiny-llama-deep"),
     # head_dim 128 like Llama-2: exercises the HIP flash-attention / fused-RoPE path at toy size
     "small-llama": dict(arch="llama", vocab_size=1024, hidden_size=512, intermediate_size=1376,
                         num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,

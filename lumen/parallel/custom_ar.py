@@ -38,6 +38,10 @@ from ..ops._native import native
 _DTYPES = (torch.float32, torch.float16, torch.bfloat16)
 
 
+class CollectiveTimeout(RuntimeError):
+    """A custom all-reduce / all-gather barrier gave up waiting for a peer."""
+
+
 def _default_one_shot_max(world: int) -> int:
     # one-shot reads (W-1)·n over the links vs 2(W-1)/W·n for two-shot plus one more barrier;
     # the crossover moves down as W grows
@@ -71,6 +75,7 @@ class CustomAllReduce:
         # every step below is collective; a rank that fails still takes part in both
         # exchanges, so either all ranks end up with the custom path or all raise
         self._buf = self._sig = None
+        self._flag_host = self._flag_dev = 0
         self._opened: List[int] = []
         self.data: List[int] = []
         self.sig: List[int] = []
@@ -107,6 +112,9 @@ class CustomAllReduce:
         if not all(oks):
             self.close()
             raise RuntimeError(f"custom all-reduce setup failed: {err or 'on a peer rank'}")
+        # pinned host-mapped word every kernel raises on a barrier timeout: ``poll()`` reads it
+        # with a plain host load after each step (no device sync)
+        self._flag_host, self._flag_dev = C.car_host_flag_alloc()
         self.calls = 0
 
     # ------------------------------------------------------------------------------------------
@@ -135,7 +143,8 @@ class CustomAllReduce:
         p_two, p_blocks = self.plan(t.numel() * t.element_size(), t.numel())
         two = p_two if two_shot is None else bool(two_shot)
         nb = p_blocks if blocks is None else int(blocks)
-        self.C.car_allreduce(self.data, self.sig, self.rank, t, out, two, nb, self.timeout_s)
+        self.C.car_allreduce(self.data, self.sig, self.rank, t, out, two, nb, self.timeout_s,
+                             self._flag_dev)
         self.calls += 1
         return out
 
@@ -153,9 +162,20 @@ class CustomAllReduce:
             out = torch.empty(R, Vs * self.world, dtype=t.dtype, device=t.device)
         units = t.numel() // 8
         nb = blocks if blocks is not None else max(1, min(self.max_blocks, -(-units // 512)))
-        self.C.car_allgather(self.data, self.sig, self.rank, t, out, int(nb), self.timeout_s)
+        self.C.car_allgather(self.data, self.sig, self.rank, t, out, int(nb), self.timeout_s,
+                             self._flag_dev)
         self.calls += 1
         return out
+
+    def poll(self) -> None:
+        """Raise if a kernel launched so far and already finished hit a barrier timeout.  A plain
+        read of the pinned host word: call it after each step's host sync (the serving engine
+        does, right after reading the sampled tokens) so a step whose reduction went wrong never
+        returns its tokens."""
+        if self._flag_host and self.C.car_host_flag_read(self._flag_host):
+            raise CollectiveTimeout(
+                f"custom all-reduce rank {self.rank}: a barrier timed out (a peer did not "
+                f"arrive within {self.timeout_s:.0f} s); this step's TP reduction is invalid")
 
     def check(self) -> None:
         """Raise if any barrier of this rank timed out (a peer never arrived).  Syncs."""
@@ -174,6 +194,9 @@ class CustomAllReduce:
         self._buf = self._sig = None
         self._opened = []
         self.data, self.sig = [], []
+        if getattr(self, "_flag_host", 0):
+            self.C.car_host_flag_free(self._flag_host)
+            self._flag_host = self._flag_dev = 0
 
 
 def maybe_custom_allreduce(group, device, max_bytes: int) -> Optional[CustomAllReduce]:

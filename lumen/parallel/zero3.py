@@ -1,0 +1,653 @@
+"""ZeRO-3 parameter coordinator: partitioned frozen weights, gathered around each model unit.
+
+Reference behaviour: DeepSpeed stage 3 as configured by configs/ds_config_zero3.json:16-37
+(``stage3_max_live_parameters``, ``stage3_max_reuse_distance``, ``stage3_prefetch_bucket_size``,
+``stage3_param_persistence_threshold``, ``offload_param``) and exercised by the notebook's
+ZeRO-3 matrix (training/train.ipynb:900-960).
+
+MI355X-first design (not a DeepSpeed translation):
+
+* One flat 16-bit shard per unit (embedding, each decoder layer, final norm + head) per rank and
+  ONE ``all_gather_into_tensor`` per unit.  A Llama-2-7B layer is 386 MiB per collective: large
+  enough for RCCL to drive all 7 xGMI links of an MI355X at full rate (DeepSpeed's 5e7-element
+  buckets are latency-bound there).
+* Weight gathers run on their OWN process group (a separate RCCL communicator, hence a separate
+  RCCL stream).  Gradient reduce-scatters, the grad-norm all-reduce and the adapter publish
+  all-gather stay on the default group, so a backward's reduce-scatter never queues behind the
+  next micro-step's 6-12 GB of weight traffic.
+* Schedules, picked from the live-parameter budget (``stage3_max_live_parameters``; ``"auto"``
+  sizes it from free HBM):
+
+  ``pipelined`` (budget >= 2x model: Llama-2-7B on 288 GB).  Two buffers per unit; the NEXT
+      micro-step's gathers are issued, in forward order, when the current one starts.  One step
+      of compute hides one step of xGMI traffic: at 2 GPUs each rank receives 6.75 GB per step
+      over ONE ~77 GB/s link (~90 ms), against a ~96 ms step.
+  ``keep`` (model <= budget < 2x model: Llama-2-70B on 8 GPUs).  One buffer per unit, kept from
+      the forward to the backward; re-gathered for the next micro-step right after the unit's
+      backward.  The next forward waits for whatever of those gathers did not fit in the
+      backward, so at N=2 it exposes ~comm - backward; pipelined exposes only comm - step.
+  ``release`` (budget < model: the reference's ``stage3_max_live_parameters: 1e9``).  A
+      preallocated ring of ``P = budget / unit`` gather buffers (no allocator churn); prefetch
+      depth from ``stage3_prefetch_bucket_size``; the last units of the forward stay live across
+      the forward->backward turn when they fall within ``stage3_max_reuse_distance`` (DeepSpeed's
+      reuse semantics), everything else is gathered twice per micro-step.
+  ``identity`` (world size 1).  The one-rank partition IS the unit: parameters view the shard
+      permanently and no gather runs.  ``LUMEN_ZERO3_SINGLE=1`` instead forces real per-step
+      materialisation (a side-stream copy with RCCL's stream semantics) so the three schedules
+      above run on a one-GPU box.
+
+* ``offload_param``: pinned host shards are copied H2D on a dedicated copy stream into a ring of
+  device staging buffers and the all-gather is issued from that stream, so neither the copy nor
+  the collective waits on -- or stalls -- the compute stream.
+* Observability: bytes gathered / received per step and the EXPOSED wait (GPU time the compute
+  stream spent blocked on a gather, from timing events around ``work.wait()``) when
+  ``track_waits`` is on (bench.py reports both).
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .dist import DistEnv
+
+ALIGN = 64  # elements: every rank slice stays 16-byte aligned
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class _LocalGather:
+    """World-1 stand-in for an async ``all_gather_into_tensor`` (the shard IS the whole unit):
+    a copy on a side stream ordered after the issuing stream; ``wait()`` makes the current stream
+    wait on it -- the stream semantics ProcessGroupNCCL gives."""
+
+    _streams: Dict[str, torch.cuda.Stream] = {}
+
+    def __init__(self, out: torch.Tensor, shard: torch.Tensor):
+        if out.is_cuda:
+            key = str(out.device)
+            s = _LocalGather._streams.get(key)
+            if s is None:
+                s = _LocalGather._streams[key] = torch.cuda.Stream(device=out.device)
+            s.wait_stream(torch.cuda.current_stream(out.device))
+            with torch.cuda.stream(s):
+                out[:shard.numel()].copy_(shard, non_blocking=True)
+                self.ev = torch.cuda.Event()
+                self.ev.record(s)
+        else:
+            out[:shard.numel()].copy_(shard)
+            self.ev = None
+
+    def wait(self):
+        if self.ev is not None:
+            torch.cuda.current_stream().wait_event(self.ev)
+
+
+class _EventWork:
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+class _Unit:
+    def __init__(self, idx):
+        self.idx = idx
+        self.params: List[nn.Parameter] = []
+        self.deps: List[int] = []
+        self.numel = 0
+        self.padded = 0
+        self.shard: Optional[torch.Tensor] = None      # [padded / W] (device, or pinned host)
+        self.bufs: List[Optional[torch.Tensor]] = []   # per slot: [>= padded] gathered (device)
+        self.works: List[Optional[object]] = []
+        self.states: List[str] = []                    # per slot: empty | inflight | ready
+        self.bound = -1                                # slot the params currently view, or -1
+        self.dtype = None
+        # W^T copies made off the critical path (keep / pipelined): (param idx, off, wt_off)
+        self.tn: List[tuple] = []
+        self.wt_numel = 0
+        self.wt_bufs: List[Optional[torch.Tensor]] = []
+        self.wt_events: List[Optional[object]] = []
+
+
+class ParamCoordinator:
+    """Gathers / releases ZeRO-3 partitioned units around the model's unit loop.
+
+    The model calls ``pre_forward(i)`` / ``post_forward(i, out)``; gradient hooks on unit outputs
+    call ``pre_backward(i)`` (before unit i's backward runs); the engine calls
+    ``end_micro_step()`` after ``loss.backward()``.  See the module docstring for schedules."""
+
+    SCHEDULES = ("release", "keep", "pipelined", "identity")
+
+    def __init__(self, model: nn.Module, env: DistEnv, persistence_threshold: int,
+                 max_live: int, prefetch_numel: int, offload_param: bool = False,
+                 pin_memory: bool = True, schedule: Optional[str] = None,
+                 group=None, max_reuse_distance: int = int(1e9), force_partition: bool = False):
+        self.env = env
+        self.model = model
+        self.offload = offload_param
+        W = env.world_size
+        self.world = W
+        self.group = group
+        self.dist = dist.is_available() and dist.is_initialized() and W > 1
+        self.local = not self.dist
+        if W == 1 and not (force_partition or offload_param):
+            schedule = "identity"
+        elif schedule == "identity":
+            raise ValueError("the identity schedule needs world size 1 and no param offload")
+        mark_zero_shapes(model)
+        owner: Dict[int, int] = {}
+        self.units: List[_Unit] = []
+        self.persistent: List[nn.Parameter] = []
+        for i, mods in enumerate(model.zero_units()):
+            u = _Unit(i)
+            for m in mods:
+                for p in m.parameters():
+                    if p.requires_grad:
+                        continue  # trainable params are handled by FlatTrainable (persistent)
+                    if p.numel() < persistence_threshold:
+                        if id(p) not in owner:
+                            owner[id(p)] = -1
+                            self.persistent.append(p)
+                        continue
+                    if id(p) in owner:
+                        if owner[id(p)] >= 0 and owner[id(p)] != i and owner[id(p)] not in u.deps:
+                            u.deps.append(owner[id(p)])
+                        continue
+                    owner[id(p)] = i
+                    u.params.append(p)
+            self.units.append(u)
+        total = 0
+        for u in self.units:
+            if not u.params:
+                continue
+            u.dtype = u.params[0].dtype
+            assert all(p.dtype == u.dtype for p in u.params), "a unit must have one dtype"
+            u.numel = sum(p.numel() for p in u.params)
+            u.padded = _round_up(u.numel, W * ALIGN)
+            total += u.padded
+            s = u.padded // W
+            r0 = env.rank * s
+            flat = torch.cat([p.data.reshape(-1) for p in u.params])
+            if flat.numel() < u.padded:
+                flat = torch.cat([flat, flat.new_zeros(u.padded - flat.numel())])
+            shard = flat[r0:r0 + s].clone() if W > 1 else flat
+            if offload_param:
+                shard = shard.cpu()
+                if pin_memory and torch.cuda.is_available():
+                    shard = shard.pin_memory()
+            u.shard = shard
+            del flat
+            if schedule == "identity":
+                self._bind_views(u, shard)       # the one-rank partition is the unit
+            else:
+                for p in u.params:
+                    p.data = torch.empty(0, dtype=u.dtype, device=p.device)
+                    p._lumen_gathered = True     # storage swapped per gather: no derived caches
+        self.total_numel = total
+        self.elem_bytes = units_dtype_bytes(self.units)
+        self.max_live = max_live if max_live >= 0 else self._hbm_live_budget(self.elem_bytes)
+        if schedule is None:
+            schedule = ("pipelined" if 2 * total <= self.max_live else
+                        "keep" if total <= self.max_live else "release")
+        assert schedule in self.SCHEDULES, schedule
+        self.schedule = schedule
+        self.identity = schedule == "identity"
+        self.keep = schedule in ("keep", "pipelined")
+        n_slots = 2 if schedule == "pipelined" else 1
+        for u in self.units:
+            u.bufs = [None] * n_slots
+            u.works = [None] * n_slots
+            u.states = ["empty"] * n_slots
+            u.wt_bufs = [None] * n_slots
+            u.wt_events = [None] * n_slots
+        self._tstream = None
+        self._cstream = None
+        self.transposed_numel = 0
+        self.slot = 0
+        self.last = len(self.units) - 1
+        self.device = env.device
+        sizes = [u.padded for u in self.units if u.padded]
+        self.max_unit = max(sizes) if sizes else 0
+        avg = (sum(sizes) / len(sizes)) if sizes else 1
+        # prefetch depth: upcoming units whose gathered size fits the prefetch bucket
+        self.depth = max(1, int(prefetch_numel // max(avg, 1)))
+        # release: ring of P gather buffers sized from the live budget; units kept across the
+        # forward->backward turn (those within the reuse distance that the ring can hold)
+        self.pool_size = 0
+        self.turn_keep = 0
+        self._pool: Dict[torch.dtype, List[torch.Tensor]] = {}
+        self._pool_alloc = 0
+        self.pool_overflows = 0
+        if schedule == "release":
+            n_units = len(sizes)
+            P = int(self.max_live // max(self.max_unit, 1))
+            P = max(2, min(P, n_units))
+            self.pool_size = P
+            # DeepSpeed reuse distance: elements accessed between two uses of a unit.  Unit
+            # last-k is reused after ~2k units (k more forward, k backward).  Reuse saves xGMI
+            # bytes, prefetch depth only hides latency: the ring serves reuse first, then depth
+            reuse_units = int(max_reuse_distance // max(2 * avg, 1))
+            self.turn_keep = max(0, min(P - 2, reuse_units))
+            self.depth = max(1, min(self.depth, P - 1 - self.turn_keep))
+        elif self.keep:
+            self.depth = max(self.depth, 2)
+        # staging ring for offloaded shards (device side of the H2D copy)
+        self._staging: List[Optional[torch.Tensor]] = []
+        self._staging_work: List[Optional[object]] = []
+        self._staging_i = 0
+        self._bwd_seen = set()
+        self._in_step = False
+        self.gathered_bytes = 0    # bytes materialised by gathers (all ranks' shards)
+        self.gathers = 0
+        self.track_waits = False
+        self._wait_events: List[tuple] = []
+        self._wait_host_s = 0.0
+        from ..utils.debug import zero3_poison_enabled
+
+        self.poison = zero3_poison_enabled() and not self.identity
+
+    # ---- sizing -----------------------------------------------------------------------------
+    def _hbm_live_budget(self, elem_bytes: int) -> int:
+        """``stage3_max_live_parameters: "auto"``: elements of gathered weights that fit in the
+        free HBM left after the shards, minus an activation reserve (max(48 GiB, 25% of the
+        device)).  On MI355X (288 GB) that is both buffers of the pipelined schedule for
+        Llama-2-7B and one full copy (keep) for Llama-2-70B.  Unlimited off-GPU."""
+        if self.env.device.type != "cuda":
+            return 1 << 62
+        free, total = torch.cuda.mem_get_info(self.env.device)
+        # blocks the caching allocator holds but no tensor uses (the full weights just sharded)
+        free += torch.cuda.memory_reserved(self.env.device) - torch.cuda.memory_allocated(
+            self.env.device)
+        reserve = float(os.environ.get("LUMEN_ZERO3_RESERVE_GB", "0")) * 2**30 or max(
+            48 * 2**30, 0.25 * total)
+        return max(0, int((free - reserve) // max(elem_bytes, 1)))
+
+    def stats(self) -> Dict:
+        return dict(schedule=self.schedule, world=self.world, units=len(self.units),
+                    total_numel=self.total_numel, max_live=self.max_live, depth=self.depth,
+                    pool_size=self.pool_size, turn_keep=self.turn_keep,
+                    pool_overflows=self.pool_overflows, separate_group=self.group is not None,
+                    offload=self.offload)
+
+    # ---- buffers ----------------------------------------------------------------------------
+    def _buffer(self, u: _Unit, slot: int) -> torch.Tensor:
+        if self.schedule != "release":
+            if u.bufs[slot] is None:
+                u.bufs[slot] = torch.empty(u.padded, dtype=u.dtype, device=self.device)
+            return u.bufs[slot]
+        free = self._pool.setdefault(u.dtype, [])
+        if free:
+            buf = free.pop()
+        else:
+            if self._pool_alloc >= self.pool_size:
+                self.pool_overflows += 1  # schedule bug or a model whose units re-enter
+            self._pool_alloc += 1
+            buf = torch.empty(self.max_unit, dtype=u.dtype, device=self.device)
+        u.bufs[slot] = buf
+        return buf
+
+    def _pool_free(self, dtype) -> bool:
+        return bool(self._pool.get(dtype)) or self._pool_alloc < self.pool_size
+
+    def _copy_stream(self):
+        if self._cstream is None:
+            self._cstream = torch.cuda.Stream(device=self.device)
+        return self._cstream
+
+    def _stage(self, shard: torch.Tensor) -> tuple:
+        """Next device staging buffer of the offload ring (depth + 1 entries)."""
+        n = self.depth + 1
+        if not self._staging:
+            self._staging = [None] * n
+            self._staging_work = [None] * n
+        k = self._staging_i % n
+        self._staging_i += 1
+        st = self._staging[k]
+        if st is None or st.numel() < shard.numel():
+            st = self._staging[k] = torch.empty(max(shard.numel(), self.max_unit // self.world),
+                                                dtype=shard.dtype, device=self.device)
+        return k, st[:shard.numel()]
+
+    # ---- gather / bind / release ------------------------------------------------------------
+    def _issue(self, i: int, slot: Optional[int] = None):
+        if self.identity or i < 0 or i > self.last:
+            return
+        slot = self.slot if slot is None else slot
+        u = self.units[i]
+        for d in u.deps:
+            self._issue(d, slot)
+        if not u.params or u.states[slot] != "empty":
+            return
+        buf = self._buffer(u, slot)
+        if self.poison:  # race detector: stale reads of this buffer now see NaN
+            buf.fill_(float("nan"))
+        if self.offload and buf.is_cuda:
+            u.works[slot] = self._issue_offloaded(u, buf)
+        elif self.local:
+            u.works[slot] = _LocalGather(buf, u.shard)
+        else:
+            u.works[slot] = dist.all_gather_into_tensor(buf[:u.padded], u.shard,
+                                                        group=self.group, async_op=True)
+        self.gathered_bytes += u.padded * buf.element_size()
+        self.gathers += 1
+        u.states[slot] = "inflight"
+        if u.tn:
+            self._transpose_after_gather(u, slot)
+
+    def _issue_offloaded(self, u: _Unit, buf: torch.Tensor):
+        """H2D copy of the pinned shard and the gather, both on the copy stream: ordered after
+        the compute that last read ``buf`` (wait_stream at issue), never blocking compute."""
+        cs = self._copy_stream()
+        cs.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(cs):
+            if self.local:
+                buf[:u.shard.numel()].copy_(u.shard, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                return _EventWork(ev)
+            k, st = self._stage(u.shard)
+            prev = self._staging_work[k]
+            if prev is not None:
+                prev.wait()   # the gather that last read this staging buffer is done
+            st.copy_(u.shard, non_blocking=True)
+            work = dist.all_gather_into_tensor(buf[:u.padded], st, group=self.group,
+                                               async_op=True)
+            self._staging_work[k] = work
+            return work
+
+    def _transpose_after_gather(self, u: _Unit, slot: int):
+        """On a side stream: wait for the gather, write W^T of the unit's projections (for the
+        backward's TN input-gradient GEMMs).  The compute stream waits on the event only when it
+        binds the unit."""
+        from ..ops.transpose import transpose_2d
+
+        cur = torch.cuda.current_stream(self.device)
+        if self._tstream is None:
+            self._tstream = torch.cuda.Stream(device=self.device)
+        side = self._tstream
+        if u.wt_bufs[slot] is None:
+            u.wt_bufs[slot] = torch.empty(u.wt_numel, dtype=u.dtype, device=self.device)
+        side.wait_stream(cur)      # earlier readers of this slot's W^T are done
+        with torch.cuda.stream(side):
+            u.works[slot].wait()   # side stream waits on the collective
+            full, wt = u.bufs[slot], u.wt_bufs[slot]
+            for k, off, wt_off in u.tn:
+                rows, cols = u.params[k]._zero_shape
+                transpose_2d(full[off:off + rows * cols].view(rows, cols),
+                             out=wt[wt_off:wt_off + rows * cols].view(cols, rows))
+            ev = torch.cuda.Event()
+            ev.record(side)
+        u.wt_events[slot] = ev
+
+    def enable_transposes(self, params: Sequence[nn.Parameter]) -> int:
+        """Keep W^T of these gathered weights next to the gathered buffer (keep / pipelined
+        schedules, when HBM allows: one more copy of the projections per slot).  Returns the
+        number of weights covered."""
+        if not self.keep or self.device.type != "cuda":
+            return 0
+        want = {id(p) for p in params}
+        need = 0
+        plan = []
+        for u in self.units:
+            tn, o, wo = [], 0, 0
+            for k, p in enumerate(u.params):
+                shape = p._zero_shape
+                n = math.prod(shape)
+                if (id(p) in want and len(shape) == 2 and shape[0] % 8 == 0
+                        and shape[1] % 8 == 0 and p.dtype in (torch.bfloat16, torch.float16)):
+                    tn.append((k, o, wo))
+                    wo += n
+                o += n
+            plan.append((u, tn, wo))
+            need += wo * (u.dtype.itemsize if u.dtype is not None else 2) * len(u.bufs)
+        free, total = torch.cuda.mem_get_info(self.device)
+        gathered = sum(u.padded * u.dtype.itemsize for u in self.units if u.params) * len(
+            self.units[0].bufs)
+        if need + gathered > free - max(48 * 2**30, 0.25 * total):
+            return 0
+        n = 0
+        for u, tn, wo in plan:
+            u.tn, u.wt_numel = tn, wo
+            n += len(tn)
+            self.transposed_numel += wo
+        return n
+
+    @staticmethod
+    def _bind_views(u: _Unit, full: torch.Tensor):
+        o = 0
+        for p in u.params:
+            shape = p._zero_shape
+            n = math.prod(shape)
+            p.data = full[o:o + n].view(shape)
+            o += n
+
+    def _wait_work(self, work):
+        if not self.track_waits:
+            work.wait()
+            return
+        if self.device.type == "cuda":
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            work.wait()
+            e1.record()
+            self._wait_events.append((e0, e1))
+        else:
+            t = time.perf_counter()
+            work.wait()
+            self._wait_host_s += time.perf_counter() - t
+
+    def pop_exposed_wait_ms(self) -> float:
+        """GPU time the compute stream spent blocked on gathers since the last call (call after
+        a device synchronize)."""
+        ms = sum(a.elapsed_time(b) for a, b in self._wait_events) + self._wait_host_s * 1e3
+        self._wait_events.clear()
+        self._wait_host_s = 0.0
+        return ms
+
+    def _wait(self, i: int):
+        """Make unit i's params view the current slot's gathered buffer."""
+        if self.identity:
+            return
+        u = self.units[i]
+        for d in u.deps:
+            self._wait(d)
+        if not u.params:
+            return
+        s = self.slot
+        if u.states[s] == "empty":
+            self._issue(i, s)
+        if u.states[s] == "inflight":
+            self._wait_work(u.works[s])
+            u.works[s] = None
+            u.states[s] = "ready"
+        if u.bound != s:
+            self._bind_views(u, u.bufs[s])
+            if u.tn:
+                if u.wt_events[s] is not None:
+                    torch.cuda.current_stream(self.device).wait_event(u.wt_events[s])
+                    u.wt_events[s] = None
+                wt = u.wt_bufs[s]
+                for k, off, wt_off in u.tn:
+                    rows, cols = u.params[k]._zero_shape
+                    u.params[k]._lumen_wt = wt[wt_off:wt_off + rows * cols].view(cols, rows)
+            u.bound = s
+
+    def _unbind(self, u: _Unit):
+        if u.bound >= 0:
+            for p in u.params:
+                p.data = torch.empty(0, dtype=u.dtype, device=p.device)
+                p._lumen_wt = None
+            u.bound = -1
+
+    def _release(self, i: int):
+        """Drop unit i's current-slot contents (release schedule: the buffer returns to the ring;
+        reuse is stream-ordered because the next gather is issued after this point)."""
+        if self.identity or i < 0 or i > self.last:
+            return
+        u = self.units[i]
+        if not u.params:
+            return
+        s = self.slot
+        if u.states[s] == "inflight":
+            u.works[s].wait()
+            u.works[s] = None
+        self._unbind(u)
+        if self.schedule == "release" and u.bufs[s] is not None:
+            self._pool.setdefault(u.dtype, []).append(u.bufs[s])
+            u.bufs[s] = None
+        u.states[s] = "empty"
+
+    def _prefetch(self, i: int):
+        """release: gather unit i ahead of use if a ring buffer is free (never grows the ring)."""
+        if i < 0 or i > self.last:
+            return
+        u = self.units[i]
+        if not u.params or u.states[self.slot] != "empty":
+            return
+        if self.schedule == "release" and not self._pool_free(u.dtype):
+            return
+        self._issue(i)
+
+    def _refresh(self, i: int):
+        """keep: unit i is done for this micro-step -> re-gather it for the next one into the
+        same buffer (issued after the compute that read it)."""
+        if i < 1 or i > self.last:
+            return
+        u = self.units[i]
+        if not u.params or u.states[self.slot] != "ready":
+            return
+        self._release(i)
+        self._issue(i)
+
+    # ---- model hooks ------------------------------------------------------------------------
+    def begin_micro_step(self):
+        self._bwd_seen.clear()
+        self._in_step = True
+        if self.identity:
+            return
+        if self.schedule == "pipelined":
+            for i in range(self.last + 1):
+                self._issue(i, self.slot)
+            for i in range(self.last + 1):
+                self._issue(i, 1 - self.slot)  # next micro-step, behind this one's
+        else:
+            for i in range(min(self.depth, self.last + 1)):
+                self._prefetch(i)
+
+    def pre_forward(self, i: int):
+        if i == 0 and not self._in_step:
+            self.begin_micro_step()
+        if self.identity:
+            return
+        self._wait(i)
+        if self.schedule != "pipelined":
+            for j in range(i + 1, min(i + 1 + self.depth, self.last + 1)):
+                self._prefetch(j)
+
+    def post_forward(self, i: int, out):
+        # release: the head (last) and the ``turn_keep`` units before it are consumed by the
+        # backward right after the turn and stay live; everything else is freed
+        if self.schedule == "release" and i < self.last - self.turn_keep:
+            self._release(i)
+        if torch.is_grad_enabled():
+            tensors = out if isinstance(out, (tuple, list)) else (out,)
+            for t in tensors:
+                if isinstance(t, torch.Tensor) and t.requires_grad:
+                    t.register_hook(self._make_bwd_hook(i))
+        elif i == self.last:
+            self.end_micro_step()
+        return out
+
+    def _make_bwd_hook(self, i):
+        def hook(grad):
+            self.pre_backward(i)
+            return grad
+        return hook
+
+    def pre_backward(self, i: int):
+        """Runs when the gradient of unit i's output is complete, i.e. after unit i+1's backward
+        and before unit i's."""
+        if i in self._bwd_seen:
+            return
+        if not self._bwd_seen:
+            # first hook of this backward: close the micro-step when the whole pass is done
+            torch.autograd.Variable._execution_engine.queue_callback(self.end_micro_step)
+        self._bwd_seen.add(i)
+        if self.identity:
+            return
+        if self.schedule == "release":
+            self._release(i + 1)
+        elif self.schedule == "keep":
+            self._refresh(i + 1)
+        self._wait(i)
+        if self.schedule == "release":
+            for j in range(i - 1, max(i - 1 - self.depth, 0), -1):
+                self._prefetch(j)  # unit 0 (embedding) has no backward
+
+    def end_micro_step(self):
+        """After the backward (or a no-grad forward): nothing of this micro-step is read any
+        more.  Idempotent (the autograd callback and the engine both call it)."""
+        if not self._in_step:
+            return
+        self._in_step = False
+        if self.identity:
+            return
+        if self.schedule == "keep":
+            for i in range(self.last + 1):  # units without a backward, then unit 1
+                u = self.units[i]
+                if u.params and u.states[self.slot] == "ready":
+                    self._release(i)
+                    self._issue(i)
+        elif self.schedule == "pipelined":
+            for u in self.units:
+                self._unbind(u)
+                u.states[self.slot] = "empty"   # re-gathered (for micro-step t+2) at t+1's start
+            self.slot = 1 - self.slot
+        else:
+            for i in range(self.last + 1):
+                self._release(i)
+
+    def gather_all_full(self) -> None:
+        """Materialise every unit (checkpoint save with gather_16bit_weights_on_model_save).
+        The release ring grows for this (the save is outside the step loop)."""
+        for i in range(self.last + 1):
+            self._issue(i)
+            self._wait(i)
+
+    def release_all(self):
+        for i in range(self.last + 1):
+            self._release(i)
+        self._in_step = False
+        for free in self._pool.values():  # gather_all_full grew the ring: shrink it back
+            while self._pool_alloc > self.pool_size and free:
+                free.pop()
+                self._pool_alloc -= 1
+
+    def drain(self):
+        """Complete every in-flight gather (all slots): before process-group teardown."""
+        for u in self.units:
+            for s, w in enumerate(u.works):
+                if w is not None:
+                    w.wait()
+                    u.works[s] = None
+                    u.states[s] = "ready"
+
+
+def units_dtype_bytes(units: Sequence[_Unit]) -> int:
+    return max((u.dtype.itemsize for u in units if u.params), default=2)
+
+
+def mark_zero_shapes(model: nn.Module):
+    for p in model.parameters():
+        if not hasattr(p, "_zero_shape"):
+            p._zero_shape = tuple(p.shape)

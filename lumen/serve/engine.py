@@ -260,6 +260,7 @@ class LLMEngine:
                                        self.step_count, want_logprobs=True)
         toks = toks.tolist()
         lps = lps.tolist() if lps is not None else [None] * len(toks)
+        self.runner.check_collectives()  # a timed-out TP reduction never returns its tokens
         for s, t, lp in zip(batch.seqs, toks, lps):
             s.num_cached = s.length
             s.append(int(t), lp, self.eos_id)

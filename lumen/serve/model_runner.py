@@ -154,6 +154,12 @@ class ModelRunner:
         self.lora = None  # serve.multi_lora.MultiLoRA when adapters are served un-merged
 
     # ------------------------------------------------------------------------------------------
+    def check_collectives(self) -> None:
+        """Raise if a TP custom all-reduce / all-gather timed out waiting for a peer (reads a
+        pinned host word: call after the step's host sync)."""
+        if self.car is not None:
+            self.car.poll()
+
     def _allreduce(self, x):
         if self.tp > 1:
             if self.car is not None and self.car.eligible(x):

@@ -67,7 +67,8 @@ def recv_step(device) -> Optional[StepInput]:
 def worker_loop(runner) -> None:
     """Ranks 1..TP-1: execute broadcast steps until shutdown."""
     while True:
-        inp = recv_step(runner.device)
+        inp = recv_step(runner.device)   # host-syncs: the previous step has completed
+        runner.check_collectives()
         if inp is None:
             return
         if inp.kind == "prefill":

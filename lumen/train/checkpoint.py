@@ -21,7 +21,16 @@ Resume is resolved on EVERY rank (fixes reference quirk 7: rank-0-only discovery
 thread and writes the files on a side thread; ranks signal completion with marker files, and
 rank 0 writes ``trainer_state.json`` -- the completeness marker ``latest_checkpoint`` looks
 for -- only after every rank's shard is on disk, so a crash mid-save never yields a checkpoint
-that resume would pick.  No collective runs off the training thread.
+that resume would pick.  Every save carries a nonce (broadcast from rank 0 on the training
+thread): a marker counts only if it holds the current nonce, and rank 0 removes a re-saved
+directory's old ``trainer_state.json`` / ``latest`` before any rank writes, so stale markers of
+a crashed earlier save at the same step can never complete a half-written checkpoint.  No
+collective runs off the training thread.
+
+World-size portability: every shard file carries the flat-buffer layout (bucket offsets, per-
+parameter offsets, world size), so ``load_checkpoint`` reshards a checkpoint saved at world N
+into world M (``lumen.train.reshard``), and ``scripts/zero_to_fp32.py`` consolidates the f32
+master weights (DeepSpeed's ``zero_to_fp32.py`` equivalent).
 """
 from __future__ import annotations
 
@@ -96,10 +105,12 @@ def load_checkpoint(path: str, engine, model, env) -> Dict:
     with open(os.path.join(path, "latest")) as f:
         tag = f.read().strip()
     load_adapter(model, path, apply=False)
-    shard = os.path.join(path, tag, f"zero_pp_rank_{env.rank}_mp_rank_00_optim_states.pt")
-    sd = torch.load(shard, map_location="cpu", weights_only=True)
-    engine.load_state_dict(sd)
+    from .reshard import load_engine_state
+
+    load_engine_state(os.path.join(path, tag), engine, env.rank)
     rng = os.path.join(path, f"rng_state_{env.rank}.pth")
+    if not os.path.exists(rng):  # resumed at a larger world size: new ranks take rank 0's
+        rng = os.path.join(path, "rng_state_0.pth")
     if os.path.exists(rng):
         st = torch.load(rng, map_location="cpu", weights_only=True)
         torch.set_rng_state(st["cpu"])
@@ -107,6 +118,14 @@ def load_checkpoint(path: str, engine, model, env) -> Dict:
             torch.cuda.set_rng_state(st["cuda"])
     with open(os.path.join(path, "trainer_state.json")) as f:
         return json.load(f)
+
+
+def _marker(gs: str, rank: int) -> Optional[str]:
+    try:
+        with open(os.path.join(gs, f".done_{rank}")) as f:
+            return f.read()
+    except OSError:
+        return None
 
 
 def _to_host(obj):
@@ -142,6 +161,19 @@ class AsyncCheckpointer:
         path = os.path.join(output_dir, f"checkpoint-{step}")
         gs = os.path.join(path, f"global_step{step}")
         os.makedirs(gs, exist_ok=True)
+        # invalidate a previous (possibly crashed) save into this directory BEFORE any rank
+        # writes, then agree on this save's nonce (the collective orders the two)
+        mine = os.path.join(gs, f".done_{env.rank}")
+        if os.path.exists(mine):
+            os.remove(mine)
+        if env.rank == 0:
+            for f in ("trainer_state.json", "latest"):
+                if os.path.exists(os.path.join(path, f)):
+                    os.remove(os.path.join(path, f))
+        from ..parallel.dist import broadcast_object
+
+        nonce = broadcast_object(f"{os.getpid()}-{time.time_ns()}-{step}" if env.rank == 0
+                                 else None)
         sd = _to_host(engine.state_dict())        # device -> host snapshot on this thread
         rng = _rng_state()
         adapter = {k: v.to("cpu", copy=True) for k, v in adapter_state_dict(model).items()} \
@@ -153,12 +185,14 @@ class AsyncCheckpointer:
             try:
                 torch.save(sd, os.path.join(gs, f"zero_pp_rank_{rank}_mp_rank_00_optim_states.pt"))
                 torch.save(rng, os.path.join(path, f"rng_state_{rank}.pth"))
-                with open(os.path.join(gs, f".done_{rank}"), "w") as f:
-                    f.write("ok")
+                tmp = os.path.join(gs, f".done_{rank}.tmp")
+                with open(tmp, "w") as f:
+                    f.write(nonce)
+                os.replace(tmp, os.path.join(gs, f".done_{rank}"))  # atomic: never half a nonce
                 if rank != 0:
                     return
                 deadline = time.time() + self.timeout_s
-                while not all(os.path.exists(os.path.join(gs, f".done_{r}")) for r in range(world)):
+                while not all(_marker(gs, r) == nonce for r in range(world)):
                     if time.time() > deadline:
                         raise TimeoutError(f"ranks did not finish writing {path}")
                     time.sleep(0.05)

@@ -153,15 +153,19 @@ def zero_stage_from_config(path: str) -> int:
 
 
 def warmup_lr(step: int, c: DSConfig) -> float:
-    """DeepSpeed WarmupLR (log warm-up by default) as used by every reference config."""
-    n = c.warmup_num_steps
-    if n <= 0 or step >= n:
+    """DeepSpeed WarmupLR (log warm-up by default) as used by every reference config.
+
+    DeepSpeed clamps the warm-up length to ``max(2, warmup_num_steps)`` and the first optimizer
+    step runs at iteration 0, i.e. at ``warmup_min_lr`` (gamma = log(1) = 0); with the "auto"
+    configs (HF fills ``warmup_num_steps`` = 0) every later step runs at ``warmup_max_lr``."""
+    n = max(2, c.warmup_num_steps)
+    if step >= n:
         return c.warmup_max_lr
     if c.warmup_type == "linear":
         gamma = step / n
     else:
         import math
-        gamma = math.log(step + 1) / math.log(max(n, 2))
+        gamma = math.log(step + 1) / math.log(n)
     return c.warmup_min_lr + (c.warmup_max_lr - c.warmup_min_lr) * gamma
 
 

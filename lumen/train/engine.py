@@ -65,24 +65,33 @@ class ZeroEngine:
         self.sharded = W > 1 and self.stage >= 1
         self.micro_step = 0
         self.global_step = 0
-        self.skipped_steps = 0
+        self._scaler_skipped = 0
         self.last_grad_norm: Optional[torch.Tensor] = None
         self.timers = Timers(cfg.wall_clock_breakdown, self.device)
 
         trainable = [p for p in model.parameters() if p.requires_grad]
         if not trainable:
             raise ValueError("model has no trainable parameters")
-        # ZeRO-3: partition frozen weights first (trainable adapters stay persistent)
+        # ZeRO-3: partition frozen weights first (trainable adapters stay persistent).  At world
+        # size 1 the one-rank partition is the whole unit ("identity" schedule: no gathers);
+        # LUMEN_ZERO3_SINGLE=1 forces per-step materialisation there (a side-stream copy with
+        # RCCL's stream semantics) to run the gather schedules on a single-GPU box.
         self.coordinator: Optional[ParamCoordinator] = None
-        # LUMEN_ZERO3_SINGLE=1 partitions at world size 1 too (a one-rank "gather" is a copy on
-        # a side stream): runs the coordinator's schedules on a single-GPU box
+        self.gather_group = None
         single = os.environ.get("LUMEN_ZERO3_SINGLE", "0") == "1"
-        if self.stage >= 3 and (W > 1 or single):
+        if self.stage >= 3:
+            if W > 1 and dist.is_initialized() and os.environ.get(
+                    "LUMEN_ZERO3_SHARED_GROUP", "0") != "1":
+                # weight gathers on their own communicator (own RCCL stream): gradient
+                # reduce-scatters / norm / publish on the default group never queue behind them
+                self.gather_group = dist.new_group(ranks=list(range(W)))
             self.coordinator = ParamCoordinator(
                 model, env, cfg.stage3_param_persistence_threshold,
                 cfg.stage3_max_live_parameters, cfg.stage3_prefetch_bucket_size,
                 offload_param=cfg.offload_param == "cpu", pin_memory=cfg.offload_param_pin,
-                schedule=os.environ.get("LUMEN_ZERO3_SCHEDULE") or None)
+                schedule=os.environ.get("LUMEN_ZERO3_SCHEDULE") or None,
+                group=self.gather_group, max_reuse_distance=cfg.stage3_max_reuse_distance,
+                force_partition=single)
             model.coordinator = self.coordinator
         if self.device.type == "cuda":
             from ..models.layers import configure_backward_layout
@@ -224,7 +233,7 @@ class ZeroEngine:
             overflow = not math.isfinite(nsq)
             self.scaler.update(overflow)
         if overflow:
-            self.skipped_steps += 1
+            self._scaler_skipped += 1
         else:
             self.opt.step(grad, lr, inv_scale, self._norm_buf, self.cfg.gradient_clipping)
             self._publish_params()
@@ -249,21 +258,36 @@ class ZeroEngine:
             dist.all_gather_into_tensor(self.flat.param[b.off:b.off + b.size],
                                         self.flat.shard_view(master, b))
 
+    @property
+    def skipped_steps(self) -> int:
+        """Steps skipped for a non-finite gradient: fp16 overflows seen by the loss scaler plus
+        bf16 NaN/Inf steps the fused AdamW kernel skipped on the device (reading that syncs)."""
+        return self._scaler_skipped + self.opt.skipped
+
+    def close(self):
+        """Complete in-flight ZeRO-3 gathers (the pipelined schedule keeps the next micro-step's
+        in flight) so the process groups can be torn down cleanly."""
+        if self.coordinator is not None:
+            self.coordinator.drain()
+
     # ---- checkpoint state ----------------------------------------------------------------------
     def state_dict(self) -> Dict:
+        from .reshard import engine_layout
+
         return dict(optimizer=self.opt.state_dict(), global_step=self.global_step,
                     micro_step=self.micro_step, skipped_steps=self.skipped_steps,
                     scaler=self.scaler.state_dict() if self.scaler else None,
                     stage=self.stage, world_size=self.env.world_size,
-                    shard_numel=self.opt.master.numel())
+                    shard_numel=self.opt.master.numel(), layout=engine_layout(self))
 
     def load_state_dict(self, d: Dict):
         if d["shard_numel"] != self.opt.master.numel():
-            raise ValueError("checkpoint shard layout does not match (world size / stage changed)")
+            raise ValueError("checkpoint shard layout does not match (world size / stage changed): "
+                             "load it through lumen.train.reshard.load_engine_state")
         self.opt.load_state_dict(d["optimizer"])
         self.global_step = d["global_step"]
         self.micro_step = d["micro_step"]
-        self.skipped_steps = d.get("skipped_steps", 0)
+        self._scaler_skipped = d.get("skipped_steps", 0)
         if self.scaler and d.get("scaler"):
             self.scaler.load_state_dict(d["scaler"])
         with torch.no_grad():

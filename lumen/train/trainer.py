@@ -131,6 +131,13 @@ class Trainer:
                 self.log_history = st.get("log_history", [])
                 start_epoch = int(st.get("epoch_int", 0))
                 skip = int(st.get("samples_in_epoch", 0))
+                old_world = int(st.get("world_size", env.world_size))
+                if old_world != env.world_size:
+                    # per-rank position -> same GLOBAL position: step k covers the contiguous
+                    # permutation block [k*G, (k+1)*G) at any world size (ShardedSampler)
+                    skip = skip * old_world // env.world_size
+                    self.print(f"[lumen] resharded checkpoint: world {old_world} -> "
+                               f"{env.world_size}")
                 self.print(f"[lumen] resumed from {ck} (step {eng.global_step})")
             else:
                 self.print("[lumen] no checkpoint found; starting fresh")
@@ -201,6 +208,7 @@ class Trainer:
                 self._save(epoch + 1, 0)
             epoch += 1
         prof.close()
+        eng.close()  # no ZeRO-3 gather left in flight past the loop
         if self.ckpt is not None:
             self.ckpt.wait()  # the last periodic checkpoint is complete before we report / exit
         if env.device.type == "cuda":

@@ -30,11 +30,21 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
            "bf16": {"enabled": False}}
     if extra and extra.get("offload"):
         raw["zero_optimization"]["offload_optimizer"] = {"device": "cpu", "pin_memory": False}
+    if extra and extra.get("offload_param"):
+        raw["zero_optimization"]["offload_param"] = {"device": "cpu", "pin_memory": False}
+    if extra and extra.get("prefetch") is not None:
+        raw["zero_optimization"]["stage3_prefetch_bucket_size"] = extra["prefetch"]
+    if extra and extra.get("reuse") is not None:
+        raw["zero_optimization"]["stage3_max_reuse_distance"] = extra["reuse"]
     ds = load_ds_config(raw, micro, accum, world, 1e-2, dtype_override="fp32")
+    ex = extra or {}
     a = TrainArgs(model_name=model, synthetic=True, synthetic_samples=64, max_length=16,
                   per_device_train_batch_size=micro, gradient_accumulation_steps=accum,
                   max_steps=steps, logging_steps=1, lora_r=4, lora_dropout=0.0,
-                  save_strategy="no", save_final=False, output_dir=os.path.join(outdir, "ck"),
+                  save_strategy="steps" if ex.get("save_steps") else "no",
+                  save_steps=ex.get("save_steps", 100), resume_from_checkpoint=ex.get(
+                      "resume", False), save_final=False,
+                  output_dir=ex.get("ckdir") or os.path.join(outdir, "ck"),
                   seed=7, gradient_checkpointing=bool((extra or {}).get("gc", False)))
     try:
         t = Trainer(a, ds, env, printer=lambda *x, **k: None)
@@ -49,7 +59,12 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
                 os.environ[k] = v
     if rank == 0:
         sd = adapter_state_dict(t.model)
-        torch.save({"sd": sd, "losses": [r["loss"] for r in t.log_history], "res": res},
+        co = t.engine.coordinator
+        stats = dict(co.stats(), gathers=co.gathers) if co is not None else None
+        if stats is not None:
+            stats["gather_group_separate"] = t.engine.gather_group is not None
+        torch.save({"sd": sd, "losses": [r["loss"] for r in t.log_history], "res": res,
+                    "zero3": stats},
                    os.path.join(outdir, f"result_stage{stage}_w{world}.pt"))
     shutdown()
 
@@ -294,4 +309,43 @@ def car_gather_worker(rank, world, port, outdir):
     if rank == 0:
         with open(os.path.join(outdir, "gather.json"), "w") as f:
             json.dump({"mismatches": bad}, f)
+    dist.destroy_process_group()
+
+
+def car_timeout_worker(rank, world, port, outdir):
+    """Rank 1 skips a custom all-reduce: rank 0's barrier must give up after its deadline, set
+    the pinned host error word, and ``poll()`` must raise (no silent half-reduced result)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import json
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lumen.parallel.custom_ar import CollectiveTimeout, CustomAllReduce
+
+    dev = torch.device("cuda", 0)
+    car = CustomAllReduce(dist.group.WORLD, dev, max_bytes=1 << 20, timeout_s=2.0)
+    x = torch.ones(4096, dtype=torch.bfloat16, device=dev)
+    car.all_reduce(x)          # a good call first: both ranks take part
+    torch.cuda.synchronize()
+    car.poll()
+    res = {"first": float(x[0])}
+    dist.barrier()
+    if rank == 0:
+        car.all_reduce(x)      # rank 1 never joins this one
+        torch.cuda.synchronize()
+        try:
+            car.poll()
+            res["raised"] = False
+        except CollectiveTimeout:
+            res["raised"] = True
+        res["err_word"] = int(car.C.car_err(car._sig))
+    dist.barrier()
+    car.close()
+    if rank == 0:
+        with open(os.path.join(outdir, "car_timeout.json"), "w") as f:
+            json.dump(res, f)
     dist.destroy_process_group()

@@ -90,6 +90,20 @@ def test_warmup_lr_log():
     assert warmup_lr(10, c) == 1.0 and warmup_lr(100, c) == 1.0
 
 
+def test_warmup_lr_auto_matches_deepspeed():
+    """The reference configs' "auto" warm-up (HF fills warmup_num_steps = 0): DeepSpeed clamps
+    to 2 steps, so optimizer step 0 runs at warmup_min_lr and step 1 on at the full LR."""
+    raw = {"scheduler": {"type": "WarmupLR", "params": {"warmup_min_lr": 0,
+                                                         "warmup_max_lr": "auto",
+                                                         "warmup_num_steps": "auto"}}}
+    c = load_ds_config(raw, 1, 1, 1, 2e-4)
+    assert warmup_lr(0, c) == 0.0
+    assert warmup_lr(1, c) == 2e-4 and warmup_lr(5, c) == 2e-4
+    lin = load_ds_config({"scheduler": {"params": {"warmup_num_steps": 1,
+                                                   "warmup_type": "linear"}}}, 1, 1, 1, 1.0)
+    assert warmup_lr(0, lin) == 0.0 and warmup_lr(1, lin) == 0.5 and warmup_lr(2, lin) == 1.0
+
+
 def test_loss_scaler_deepspeed_semantics():
     s = DynamicLossScaler(2 ** 16, window=3, hysteresis=2)
     s.update(True)  # first overflow absorbed by hysteresis

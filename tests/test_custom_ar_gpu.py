@@ -69,3 +69,19 @@ def test_tp2_serving_on_one_gpu_matches_single_process(tmp_path):
         agree += sum(int(a == b) for a, b in zip(pred, out))
         total += 8
     assert agree / total >= 0.85, (agree, total)
+
+
+def test_custom_allreduce_peer_timeout_raises(tmp_path):
+    """A peer that never arrives: the barrier deadline (2 s) ends the kernel, the pinned host
+    error word is raised and ``poll()`` -- what the serving engine calls after each step --
+    raises instead of returning a half-reduced tensor."""
+    from tests._dist_worker import car_timeout_worker
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(car_timeout_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    res = json.loads((tmp_path / "car_timeout.json").read_text())
+    assert res["first"] == 2.0
+    assert res["raised"] is True and res["err_word"] == 1

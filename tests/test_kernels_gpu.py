@@ -142,7 +142,7 @@ def test_grad_norm_and_adamw():
     lr, b1, b2, eps, wd, inv = 1e-3, 0.9, 0.999, 1e-8, 0.01, 0.5
     maxn = 1.0
     copy = torch.empty(n, device=DEV, dtype=torch.bfloat16)
-    C.adamw(p, g, m, v, copy, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, inv, ns, maxn)
+    C.adamw(p, g, m, v, copy, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, inv, ns, maxn, None)
     gn = math.sqrt(ns.item()) * inv
     coef = inv * (maxn / (gn + 1e-6) if gn > maxn else 1.0)
     _adamw_torch(p2, g, m2, v2, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, coef)
@@ -152,8 +152,37 @@ def test_grad_norm_and_adamw():
     # overflow -> no update
     p3 = p.clone()
     bad = torch.tensor([float("inf")], device=DEV)
-    C.adamw(p, g, m, v, None, lr, b1, b2, eps, wd, 0.1, 0.1, 1.0, bad, 1.0)
+    C.adamw(p, g, m, v, None, lr, b1, b2, eps, wd, 0.1, 0.1, 1.0, bad, 1.0, None)
     assert torch.equal(p, p3)
+
+
+def test_adamw_device_step_counter():
+    """Device Adam step counter: bias corrections from [applied, skipped]; a non-finite norm
+    skips the update and counts as skipped without advancing t (bf16 NaN steps)."""
+    from lumen.ops._native import native
+    from lumen.parallel.zero import _adamw_torch
+
+    C = native()
+    n = 4096 * 3 + 5
+    p = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    st = torch.zeros(2, device=DEV)
+    lr, b1, b2 = 1e-2, 0.9, 0.999
+    g = torch.randn(n, device=DEV)
+    good = torch.zeros(1, device=DEV)
+    C.grad_norm_sq(g, good)
+    bad = torch.tensor([float("nan")], device=DEV)
+    t = 0
+    for norm in (good, bad, good, good, bad):
+        C.adamw(p, g, m, v, None, lr, b1, b2, 1e-8, 0.0, 1.0, 1.0, 1.0, norm, 0.0, st)
+        if norm is good:
+            t += 1
+            _adamw_torch(p2, g, m2, v2, lr, b1, b2, 1e-8, 0.0, 1 - b1 ** t, 1 - b2 ** t, 1.0)
+    assert st.tolist() == [3.0, 2.0]
+    assert (p - p2).abs().max().item() < 1e-5
+    assert (v - v2).abs().max().item() < 1e-6
 
 
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])

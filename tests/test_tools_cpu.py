@@ -213,9 +213,12 @@ def test_profiler_and_debug_guards(tmp_path, monkeypatch):
         check_finite("x", torch.tensor([1.0, float("nan")]))
 
 
-def test_bench_contract_torchrun_world2():
-    """bench.py under torch.distributed.run (2 ranks, gloo, tiny model): one JSON line from
-    rank 0 with the driver's fields, whole-job tokens/s, ZeRO-3 partitioning active."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_contract_torchrun(world):
+    """bench.py under torch.distributed.run (2 / 4 ranks, gloo, tiny model): one JSON line from
+    rank 0 with the driver's fields, whole-job tokens/s, ZeRO-3 partitioning active on its own
+    gather communicator, and the comm diagnostics (collective-observed world size, gathered /
+    received bytes, exposed gather wait, peak memory over ranks)."""
     import json
     import socket
 
@@ -224,10 +227,10 @@ def test_bench_contract_torchrun_world2():
     port = s.getsockname()[1]
     s.close()
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
-                          str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-                          "--warmup", "1", "--model", "tiny-llama", "--seq_len", "32",
-                          "--micro_batch", "2"], capture_output=True, text=True, timeout=600,
+                          "--nproc-per-node", str(world), "--master-addr", "127.0.0.1", "--master-port",
+                          str(port), os.path.join(ROOT, "bench.py"), "--gpus", str(world),
+                          "--steps", "2", "--warmup", "1", "--model", "tiny-llama", "--seq_len",
+                          "32", "--micro_batch", "2"], capture_output=True, text=True, timeout=600,
                          env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -236,8 +239,16 @@ def test_bench_contract_torchrun_world2():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in j, k
-    assert j["n_gpus"] == 2 and j["steps"] == 2 and j["scaling"] == "weak"
-    assert j["config"]["global_batch"] == 4 and j["config"]["parallelism"] == "dp2-zero3"
-    assert j["extra"]["zero3_schedule"] == "pipelined"
-    assert j["extra"]["zero3_gathered_mb_per_step"] > 0
-    assert abs(j["value"] - 4 * 32 * 2 / (j["ms_per_step"] * 2 / 1000)) / j["value"] < 0.02
+    assert j["n_gpus"] == world and j["steps"] == 2 and j["scaling"] == "weak"
+    assert j["config"]["global_batch"] == 2 * world
+    assert j["config"]["parallelism"] == f"dp{world}-zero3"
+    x = j["extra"]
+    assert x["zero3"]["schedule"] == "pipelined" and x["zero3"]["separate_group"]
+    assert x["rccl_world"] == world and x["gather_group_world"] == world
+    assert x["zero3_gathered_mb_per_step"] > 0
+    assert abs(x["zero3_received_mb_per_step_per_rank"]
+               - x["zero3_gathered_mb_per_step"] * (world - 1) / world) < 0.2
+    assert x["zero3_exposed_wait_ms_per_step_max_rank"] >= 0
+    assert "peak_hbm_gb_max_rank" in x and x["setup_s"] > 0
+    tokens = 2 * world * 32 * 2
+    assert abs(j["value"] - tokens / (j["ms_per_step"] * 2 / 1000)) / j["value"] < 0.02

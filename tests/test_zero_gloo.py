@@ -101,3 +101,124 @@ def test_zero2_cpu_offload_optimizer(tmp_path):
              extra={"offload": True})
     # C++ AVX-512 AdamW vs torch AdamW: same math, different rounding order
     _close(r["sd"], ref["sd"], tol=3e-4)
+
+
+# ---- world size 4: every ZeRO-3 schedule on split communicators -----------------------------
+
+def _layer_numel(model="tiny-llama-deep"):
+    from lumen.models import get_config
+
+    c = get_config(model)
+    H, D = c.hidden_size, c.head_dim
+    return (H * (c.num_attention_heads + 2 * c.num_key_value_heads) * D
+            + c.num_attention_heads * D * H + 3 * H * c.intermediate_size + 2 * H)
+
+
+@pytest.fixture(scope="module")
+def deep_reference(tmp_path_factory):
+    d = tmp_path_factory.mktemp("deepref")
+    return _run(1, 0, str(d), model="tiny-llama-deep", micro=4, accum=2, steps=2)
+
+
+@pytest.mark.parametrize("case", [
+    dict(schedule="pipelined"),
+    dict(schedule="keep", gc=True),
+    # release, ring of 2 buffers: depth 1, nothing kept across the fwd->bwd turn
+    dict(schedule="release", live_units=2),
+    # release, ring of 5: depth 2 (prefetch bucket = 2 layers), 2 units reused at the turn
+    dict(schedule="release", live_units=5, prefetch_units=2, reuse_units=2, gc=True),
+    # release, ring of 5, default reuse distance: the ring serves reuse first (3 units kept)
+    dict(schedule="release", live_units=5, prefetch_units=2),
+    # release + reuse distance 0: every unit gathered twice
+    dict(schedule="release", live_units=5, prefetch_units=1, reuse=0),
+    # offloaded (host) shards: H2D + gather issued off the compute stream
+    dict(schedule="pipelined", offload_param=True),
+])
+def test_zero3_world4_split_groups(case, deep_reference, tmp_path):
+    """World 4 over gloo: every schedule, on a separate weight-gather process group, with
+    gradient accumulation (and checkpointing where marked) == single-process stage 0."""
+    L = _layer_numel()
+    extra = {"schedule": case["schedule"], "gc": case.get("gc", False)}
+    if "live_units" in case:
+        extra["max_live"] = int(case["live_units"] * L * 1.02)
+    if "prefetch_units" in case:
+        extra["prefetch"] = int(case["prefetch_units"] * L * 1.02)
+    if "reuse" in case:
+        extra["reuse"] = case["reuse"]
+    if "reuse_units" in case:
+        extra["reuse"] = int(2 * case["reuse_units"] * L * 1.1)
+    if case.get("offload_param"):
+        extra["offload_param"] = True
+    r = _run(4, 3, str(tmp_path), model="tiny-llama-deep", micro=1, accum=2, steps=2,
+             extra=extra)
+    _close(r["sd"], deep_reference["sd"])
+    z = r["zero3"]
+    assert z["schedule"] == case["schedule"] and z["world"] == 4
+    assert z["gather_group_separate"]
+    assert z["pool_overflows"] == 0
+    n_units = 8
+    if case["schedule"] == "release":
+        assert z["pool_size"] == case["live_units"]
+        if case.get("reuse") == 0:
+            assert z["turn_keep"] == 0
+            # 2 steps x 2 micro-steps x (8 fwd + 6 bwd: every layer re-gathered, the head is
+            # consumed at the turn)
+            assert z["gathers"] == 2 * 2 * (n_units + n_units - 2)
+        elif case["live_units"] == 5:
+            keep = 2 if "reuse_units" in case else 3
+            assert z["turn_keep"] == keep
+            assert z["depth"] == 4 - keep
+            assert z["gathers"] == 2 * 2 * (n_units + n_units - 2 - keep)
+    else:
+        assert z["gathers"] >= 2 * 2 * n_units
+
+
+def test_zero3_world1_identity(tmp_path):
+    """World size 1 without forced partitioning: the one-rank partition is the whole unit, the
+    coordinator binds parameters to it once and never gathers; == stage 0."""
+    ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama", micro=2, accum=2, steps=2)
+    r = _run(1, 3, str(tmp_path / "b"), model="tiny-llama", micro=2, accum=2, steps=2)
+    _close(r["sd"], ref["sd"], tol=0)
+    assert r["zero3"]["schedule"] == "identity" and r["zero3"]["gathers"] == 0
+
+
+# ---- checkpoint resharding across world sizes ------------------------------------------------
+
+@pytest.mark.parametrize("stage,w_save,w_load", [(2, 2, 1), (1, 1, 2), (3, 2, 4), (2, 4, 2)])
+def test_resume_at_different_world_size(stage, w_save, w_load, tmp_path):
+    """Save at world N after 2 steps, resume at world M (same global batch of 4) to step 4:
+    the adapters match an uninterrupted world-N run (optimizer shards resharded by name)."""
+    gb = 4
+    ref = _run(w_save, stage, str(tmp_path / "ref"), model="tiny-llama", micro=gb // w_save,
+               accum=1, steps=4)
+    ck = str(tmp_path / "ck")
+    _run(w_save, stage, str(tmp_path / "a"), model="tiny-llama", micro=gb // w_save, accum=1,
+         steps=2, extra={"save_steps": 2, "ckdir": ck})
+    r = _run(w_load, stage, str(tmp_path / "b"), model="tiny-llama", micro=gb // w_load,
+             accum=1, steps=4, extra={"save_steps": 100, "ckdir": ck, "resume": True})
+    _close(r["sd"], ref["sd"], tol=3e-5)
+    assert r["res"]["global_step"] == 4
+
+
+def test_zero_to_fp32_consolidation(tmp_path):
+    """scripts/zero_to_fp32.py: world-2 ZeRO-2 shards -> one f32 PEFT adapter equal to the
+    trained adapters."""
+    import subprocess
+    import sys
+
+    from safetensors.torch import load_file
+
+    ck = str(tmp_path / "ck")
+    r = _run(2, 2, str(tmp_path / "a"), model="tiny-llama", micro=2, accum=1, steps=2,
+             extra={"save_steps": 2, "ckdir": ck})
+    out = str(tmp_path / "fp32")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run([sys.executable, os.path.join(root, "scripts", "zero_to_fp32.py"),
+                    os.path.join(ck, "checkpoint-2"), out], check=True, cwd=root)
+    got = load_file(os.path.join(out, "adapter_model.safetensors"))
+    assert got.keys() == r["sd"].keys()
+    for k in got:
+        assert got[k].dtype == torch.float32
+        assert torch.equal(got[k], r["sd"][k]), k
+    st = torch.load(os.path.join(out, "optimizer_fp32.pt"), weights_only=True)
+    assert all(set(v) == {"exp_avg", "exp_avg_sq"} for v in st.values())
