@@ -28,7 +28,7 @@ hipError_t lumen_cross_entropy(int, void*, const int64_t*, float*, float*, int, 
 hipError_t lumen_grad_norm_sq(int, const void*, long long, float*, hipStream_t);
 hipError_t lumen_adamw(float*, int, const void*, float*, float*, int, void*, long long, float, float,
                        float, float, float, float, float, float, const float*, float, float*,
-                       hipStream_t);
+                       const double*, hipStream_t);
 hipError_t lumen_lora_gemm(int, int, int, const void*, const void*, void*, long long, long long,
                            long long, long long, float, int, unsigned long long, unsigned int, float,
                            long long, int, const long long*, const long long*, const long long*,
@@ -241,10 +241,14 @@ void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
            const std::optional<at::Tensor>& out_copy, double lr, double b1, double b2, double eps,
            double wd, double bc1, double bc2, double inv_scale,
            const std::optional<at::Tensor>& norm_sq, double max_norm,
-           const std::optional<at::Tensor>& step_state) {
+           const std::optional<at::Tensor>& step_state, const std::vector<double>& sched) {
   need_cuda(p, "param"); need_cuda(g, "grad"); need_cuda(m, "exp_avg"); need_cuda(v, "exp_avg_sq");
   if (step_state.has_value() && (step_state->scalar_type() != at::kFloat || step_state->numel() < 2))
     throw std::invalid_argument("lumen: adamw step_state must be f32[2] (applied, skipped)");
+  if (step_state.has_value() && (step_state->numel() < 8 || sched.size() < 9))
+    throw std::invalid_argument("lumen: adamw step_state needs 8 words and 9 schedule values "
+                                "(lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, "
+                                "window, hysteresis, min_scale)");
   if (p.scalar_type() != at::kFloat) throw std::invalid_argument("lumen: adamw master must be f32");
   const int od = out_copy.has_value() ? dcode(*out_copy) : 0;
   check(lumen_adamw(p.data_ptr<float>(), dcode(g), g.data_ptr(), m.data_ptr<float>(),
@@ -252,7 +256,8 @@ void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                     static_cast<float>(b1), static_cast<float>(b2), static_cast<float>(eps),
                     static_cast<float>(wd), static_cast<float>(bc1), static_cast<float>(bc2),
                     static_cast<float>(inv_scale), ptr<const float>(norm_sq),
-                    static_cast<float>(max_norm), ptr<float>(step_state), cur_stream()),
+                    static_cast<float>(max_norm), ptr<float>(step_state),
+                    sched.empty() ? nullptr : sched.data(), cur_stream()),
         "adamw");
 }
 

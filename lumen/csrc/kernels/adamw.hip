@@ -17,6 +17,31 @@
 
 namespace lumen {
 
+// Device-side optimizer schedule (optional).  ``state`` (f32, 8 words):
+//   [0] applied updates  [1] skipped steps  [2] loss scale  [3] current hysteresis
+//   [4] scaler iteration [5] last overflow iteration
+// When present, the Adam bias corrections, the WarmupLR learning rate (DeepSpeed semantics: the
+// scheduler advances only on applied steps, warm-up length clamped to >= 2) and the loss-scale
+// unscale all come from device memory, and adamw_commit_kernel advances the counters and the
+// DynamicLossScaler after the update -- so neither a bf16 nor an fp16 step syncs the host.
+struct OptSched {
+  float* state;
+  float lr_min, lr_max;
+  int warm_n, warm_linear;
+  float inv_world;
+  int dynamic_scale;
+  float scale_window;
+  int hysteresis;
+  float min_scale;
+};
+
+__device__ __forceinline__ float sched_lr(const OptSched& s, float it) {
+  const float n = (float)(s.warm_n > 2 ? s.warm_n : 2);
+  if (it >= n) return s.lr_max;
+  const float gamma = s.warm_linear ? it / n : logf(it + 1.f) / logf(n);
+  return s.lr_min + (s.lr_max - s.lr_min) * gamma;
+}
+
 template <typename G>
 __global__ void __launch_bounds__(256) norm_sq_kernel(const G* __restrict__ g, long long n,
                                                       float* __restrict__ out) {
@@ -46,15 +71,18 @@ __global__ void __launch_bounds__(256) adamw_kernel(
     float* __restrict__ p, const G* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     O* __restrict__ out_copy, long long n, float lr, float beta1, float beta2, float eps, float wd,
     float bc1, float bc2, float inv_scale, const float* __restrict__ norm_sq, float max_norm,
-    const float* __restrict__ step_state) {
-  float coef = inv_scale;
-  if (step_state) {
-    // device-side Adam step counter: t = applied updates so far + 1, so a skipped (non-finite)
-    // step never advances the bias correction (adamw_commit_kernel counts it afterwards)
-    const float t = step_state[0] + 1.f;
+    OptSched sc) {
+  if (sc.state) {
+    // device-side step counter: t = applied updates so far + 1, so a skipped (non-finite) step
+    // never advances the bias correction or the LR schedule (adamw_commit_kernel counts it)
+    const float applied = sc.state[0];
+    const float t = applied + 1.f;
     bc1 = 1.f - powf(beta1, t);
     bc2 = 1.f - powf(beta2, t);
+    lr = sched_lr(sc, applied);
+    inv_scale = sc.inv_world / sc.state[2];
   }
+  float coef = inv_scale;
   if (norm_sq) {
     const float nsq = *norm_sq;
     if (!isfinite(nsq)) return;  // overflow: skip the step (loss scaler backs off on the host)
@@ -101,12 +129,24 @@ __global__ void __launch_bounds__(256) adamw_kernel(
   }
 }
 
-// after adamw_kernel: count the step as applied (state[0]) or skipped (state[1])
-__global__ void adamw_commit_kernel(float* __restrict__ state, const float* __restrict__ norm_sq) {
-  if (threadIdx.x == 0) {
-    const bool ok = norm_sq == nullptr || isfinite(*norm_sq);
-    state[ok ? 0 : 1] += 1.f;
+// after adamw_kernel: count the step as applied (state[0]) or skipped (state[1]) and advance the
+// dynamic loss scaler (DeepSpeed DynamicLossScaler, consecutive_hysteresis = false)
+__global__ void adamw_commit_kernel(OptSched sc, const float* __restrict__ norm_sq) {
+  if (threadIdx.x != 0) return;
+  float* st = sc.state;
+  const bool overflow = norm_sq != nullptr && !isfinite(*norm_sq);
+  st[overflow ? 1 : 0] += 1.f;
+  if (!sc.dynamic_scale) return;
+  const float it = st[4];
+  if (overflow) {
+    if (sc.hysteresis == 1 || st[3] <= 1.f) st[2] = fmaxf(st[2] * 0.5f, sc.min_scale);
+    else st[3] -= 1.f;
+    st[5] = it;
+  } else if (fmodf(it - st[5], sc.scale_window) == 0.f) {
+    st[2] *= 2.f;
+    st[3] = (float)sc.hysteresis;
   }
+  st[4] = it + 1.f;
 }
 
 static inline unsigned grid_for(long long n) {
@@ -140,13 +180,27 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
                                   int out_dtype, void* out_copy, long long n, float lr,
                                   float beta1, float beta2, float eps, float wd, float bc1,
                                   float bc2, float inv_scale, const float* norm_sq, float max_norm,
-                                  float* step_state, hipStream_t st) {
+                                  float* step_state, const double* sched, hipStream_t st) {
+  lumen::OptSched sc{};
+  sc.state = step_state;
+  if (step_state) {
+    // sched: lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, window, hysteresis, min
+    sc.lr_min = (float)sched[0];
+    sc.lr_max = (float)sched[1];
+    sc.warm_n = (int)sched[2];
+    sc.warm_linear = (int)sched[3];
+    sc.inv_world = (float)sched[4];
+    sc.dynamic_scale = (int)sched[5];
+    sc.scale_window = (float)sched[6];
+    sc.hysteresis = (int)sched[7];
+    sc.min_scale = (float)sched[8];
+  }
   if (n == 0) return hipSuccess;
   dim3 grid(lumen::grid_for(n)), block(256);
 #define LUMEN_ADAMW(G, O)                                                                    \
   hipLaunchKernelGGL((lumen::adamw_kernel<G, O>), grid, block, 0, st, p, (const G*)g, m, v, \
                      (O*)out_copy, n, lr, beta1, beta2, eps, wd, bc1, bc2, inv_scale, norm_sq,  \
-                     max_norm, step_state)
+                     max_norm, sc)
   if (gdtype == lumen::kF32) {
     if (out_copy == nullptr || out_dtype == lumen::kF32) LUMEN_ADAMW(float, float);
     else if (out_dtype == lumen::kBF16) LUMEN_ADAMW(float, lumen::bf16);
@@ -165,6 +219,6 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
 #undef LUMEN_ADAMW
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || step_state == nullptr) return e;
-  hipLaunchKernelGGL(lumen::adamw_commit_kernel, dim3(1), dim3(64), 0, st, step_state, norm_sq);
+  hipLaunchKernelGGL(lumen::adamw_commit_kernel, dim3(1), dim3(64), 0, st, sc, norm_sq);
   return hipGetLastError();
 }

@@ -185,8 +185,33 @@ class ShardAdamW:
             self.master, self.m, self.v = (t.pin_memory() for t in (self.master, self.m, self.v))
         self._host_step = 0
         self._host_skipped = 0
-        self.state = (torch.zeros(2, dtype=torch.float32, device=device)
-                      if not offload and device.type == "cuda" else None)
+        # device schedule state (see kernels/adamw.hip OptSched): [applied, skipped, loss scale,
+        # cur hysteresis, scaler iter, last overflow iter, -, -]
+        self.state = None
+        self.sched: Optional[List[float]] = None
+        if not offload and device.type == "cuda":
+            self.state = torch.zeros(8, dtype=torch.float32, device=device)
+            self.state[2] = 1.0
+
+    def configure_schedule(self, lr_min: float, lr_max: float, warm_n: int, warm_linear: bool,
+                           world: int, scaler=None) -> bool:
+        """Move the WarmupLR schedule and (fp16) the dynamic loss scaler onto the device.
+        Returns True when the device path is active (GPU, fused kernel available)."""
+        if self.state is None or not use_native(self.master):
+            return False
+        dyn = scaler is not None and not scaler.static
+        self.sched = [lr_min, lr_max, float(warm_n), 1.0 if warm_linear else 0.0, 1.0 / world,
+                      1.0 if dyn else 0.0, float(scaler.window if scaler else 1000),
+                      float(scaler.hysteresis if scaler else 2),
+                      float(scaler.min_scale if scaler else 1.0)]
+        st = [0.0, 0.0, float(scaler.scale) if scaler else 1.0,
+              float(scaler.cur_hysteresis if scaler else 2), 0.0, -1.0, 0.0, 0.0]
+        self.state.copy_(torch.tensor(st, dtype=torch.float32))
+        return True
+
+    @property
+    def device_sched(self) -> bool:
+        return self.sched is not None
 
     @property
     def step_count(self) -> int:
@@ -204,9 +229,15 @@ class ShardAdamW:
     def step(self, grad: torch.Tensor, lr: float, inv_scale: float,
              norm_sq: Optional[torch.Tensor], max_norm: float) -> None:
         if self.state is not None and use_native(self.master):
-            # bias corrections come from the device counter (bc arguments unused)
+            # bias corrections from the device counter; with a device schedule also the LR and
+            # the loss-scale unscale (then ``lr`` / ``inv_scale`` are ignored)
+            sched = self.sched if self.sched is not None else [
+                lr, lr, 0.0, 0.0, inv_scale, 0.0, 1000.0, 2.0, 1.0]
+            if self.sched is None:
+                self.state[2] = 1.0
             native().adamw(self.master, grad, self.m, self.v, None, lr, self.b1, self.b2,
-                           self.eps, self.wd, 1.0, 1.0, inv_scale, norm_sq, max_norm, self.state)
+                           self.eps, self.wd, 1.0, 1.0, inv_scale, norm_sq, max_norm, self.state,
+                           sched)
             return
         coef = inv_scale
         if norm_sq is not None:
@@ -241,10 +272,14 @@ class ShardAdamW:
         self.master.copy_(d["master"])
         self.m.copy_(d["exp_avg"])
         self.v.copy_(d["exp_avg_sq"])
-        self._host_step = int(d["step"])
         self._host_skipped = 0
-        if self.state is not None:
-            self.state.zero_()
+        if self.state is not None and use_native(self.master):
+            # the device counter drives bias correction (and the LR schedule): restore it there
+            self._host_step = 0
+            self.state[0] = float(d["step"])
+            self.state[1] = 0.0
+        else:
+            self._host_step = int(d["step"])
 
 
 def _adamw_torch(p, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, coef):

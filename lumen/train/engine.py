@@ -129,6 +129,11 @@ class ZeroEngine:
         if cfg.dtype == "fp16":
             self.scaler = DynamicLossScaler(2.0 ** cfg.initial_scale_power, cfg.loss_scale_window,
                                             cfg.hysteresis, cfg.min_loss_scale, cfg.loss_scale)
+        # GPU: LR warm-up, Adam bias correction and the fp16 loss scaler run on the device from
+        # the applied-step counter (no host sync per step, bf16 or fp16); host logic otherwise
+        self.device_sched = self.opt.configure_schedule(
+            cfg.warmup_min_lr, cfg.warmup_max_lr, cfg.warmup_num_steps,
+            cfg.warmup_type == "linear", W, self.scaler)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._works: List = []
         for prm in trainable:  # .grad is a view of flat.grad: kernels may accumulate into it
@@ -139,13 +144,24 @@ class ZeroEngine:
     # ----------------------------------------------------------------------------------------
     @property
     def loss_scale(self) -> float:
+        """Current loss scale (device path: reads the device state, syncs)."""
+        if self.device_sched and self.scaler is not None:
+            return float(self.opt.state[2].item())
         return self.scaler.scale if self.scaler else 1.0
+
+    @property
+    def last_lr(self) -> float:
+        """LR of the last optimizer step: DeepSpeed WarmupLR indexed by APPLIED steps (an
+        overflow-skipped step does not advance the scheduler)."""
+        applied = self.opt.step_count
+        return warmup_lr(max(applied - 1, 0), self.cfg) if applied else warmup_lr(0, self.cfg)
 
     def is_boundary(self) -> bool:
         return (self.micro_step + 1) % self.cfg.grad_accum == 0
 
     def lr(self) -> float:
-        return warmup_lr(self.global_step, self.cfg)
+        """LR for the next update (host path): WarmupLR at the applied-step count."""
+        return warmup_lr(self.opt.step_count, self.cfg)
 
     # ---- stage 2/3: reduce-scatter buckets as soon as backward finished them ----------------
     def _install_bucket_hooks(self):
@@ -181,8 +197,12 @@ class ZeroEngine:
 
     def backward(self, loss: torch.Tensor):
         self.timers.start("bwd")
-        scale = self.loss_scale / self.cfg.grad_accum
-        (loss * scale if scale != 1.0 else loss).backward()
+        if self.device_sched and self.scaler is not None:
+            # fp16: scale by the device loss scale (no host read of it)
+            (loss * (self.opt.state[2] / self.cfg.grad_accum)).backward()
+        else:
+            scale = self.loss_scale / self.cfg.grad_accum
+            (loss * scale if scale != 1.0 else loss).backward()
         if self.coordinator is not None:
             self.coordinator.end_micro_step()
         if self.sharded and self.stage >= 2:
@@ -225,20 +245,26 @@ class ZeroEngine:
         if self.sharded:
             dist.all_reduce(self._norm_buf)
         # grads are sums over ranks of (loss * scale / accum) gradients
-        inv_scale = 1.0 / (self.loss_scale * W)
-        lr = self.lr()
-        overflow = False
-        if self.scaler is not None:
-            nsq = float(self._norm_buf.item())
-            overflow = not math.isfinite(nsq)
-            self.scaler.update(overflow)
-        if overflow:
-            self._scaler_skipped += 1
+        if self.device_sched:
+            # one kernel: unscale, clip, skip-on-overflow, bias correction, WarmupLR and the
+            # loss-scaler update all read / advance device state -- no host sync
+            self.last_grad_norm = self._norm_buf.sqrt() / (self.opt.state[2] * W)
+            self.opt.step(grad, 0.0, 0.0, self._norm_buf, self.cfg.gradient_clipping)
+            self._publish_params()   # a skipped step publishes unchanged values
         else:
-            self.opt.step(grad, lr, inv_scale, self._norm_buf, self.cfg.gradient_clipping)
-            self._publish_params()
-        self.last_grad_norm = self._norm_buf.sqrt() * inv_scale
-        self.last_lr = lr
+            inv_scale = 1.0 / (self.loss_scale * W)
+            lr = self.lr()
+            overflow = False
+            if self.scaler is not None:
+                nsq = float(self._norm_buf.item())
+                overflow = not math.isfinite(nsq)
+                self.scaler.update(overflow)
+            if overflow:
+                self._scaler_skipped += 1
+            else:
+                self.opt.step(grad, lr, inv_scale, self._norm_buf, self.cfg.gradient_clipping)
+                self._publish_params()
+            self.last_grad_norm = self._norm_buf.sqrt() * inv_scale
         self.flat.grad.zero_()
         if self.grad_shard is not None:
             self.grad_shard.zero_()
@@ -258,6 +284,14 @@ class ZeroEngine:
             dist.all_gather_into_tensor(self.flat.param[b.off:b.off + b.size],
                                         self.flat.shard_view(master, b))
 
+    def _scaler_state(self):
+        if self.scaler is None:
+            return None
+        if self.device_sched:
+            sc, hy, it, lo = self.opt.state[2:6].tolist()
+            return dict(scale=sc, cur_hysteresis=int(hy), iter=int(it), last_overflow_iter=int(lo))
+        return self.scaler.state_dict()
+
     @property
     def skipped_steps(self) -> int:
         """Steps skipped for a non-finite gradient: fp16 overflows seen by the loss scaler plus
@@ -276,7 +310,7 @@ class ZeroEngine:
 
         return dict(optimizer=self.opt.state_dict(), global_step=self.global_step,
                     micro_step=self.micro_step, skipped_steps=self.skipped_steps,
-                    scaler=self.scaler.state_dict() if self.scaler else None,
+                    scaler=self._scaler_state(),
                     stage=self.stage, world_size=self.env.world_size,
                     shard_numel=self.opt.master.numel(), layout=engine_layout(self))
 
@@ -290,5 +324,10 @@ class ZeroEngine:
         self._scaler_skipped = d.get("skipped_steps", 0)
         if self.scaler and d.get("scaler"):
             self.scaler.load_state_dict(d["scaler"])
+            if self.device_sched:
+                sc = d["scaler"]
+                self.opt.state[2:6] = torch.tensor(
+                    [sc["scale"], sc["cur_hysteresis"], sc["iter"], sc["last_overflow_iter"]],
+                    dtype=torch.float32)
         with torch.no_grad():
             self._publish_params()

@@ -54,12 +54,13 @@ def test_rmsnorm_fwd_bwd(dtype, H):
 
 
 @pytest.mark.parametrize("nh,nkv", [(32, 32), (8, 2)])
-def test_qkv_rope_split(nh, nkv):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_qkv_rope_split(nh, nkv, dtype):
     from lumen.ops.rope import qkv_rope_split, qkv_rope_split_ref, rope_tables
 
     B, S, D = 2, 64, 128
     cos, sin = rope_tables(D, 4096, 10000.0, DEV)
-    qkv = torch.randn(B * S, (nh + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16,
+    qkv = torch.randn(B * S, (nh + 2 * nkv) * D, device=DEV, dtype=dtype,
                       requires_grad=True)
     q, k, v = qkv_rope_split(qkv, B, S, nh, nkv, D, cos, sin)
     qkv2 = qkv.detach().float().requires_grad_(True)
@@ -77,12 +78,13 @@ def test_qkv_rope_split(nh, nkv):
     assert rel(qp, qr) < 1e-2 and rel(kp, kr) < 1e-2
 
 
-def test_rope_inplace():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_rope_inplace(dtype):
     from lumen.ops.rope import rope_inplace, rope_tables, _rotate_ref
 
     T, nh, D = 37, 4, 128
     cos, sin = rope_tables(D, 4096, 10000.0, DEV)
-    x = torch.randn(T, 3 * nh * D, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(T, 3 * nh * D, device=DEV, dtype=dtype)
     pos = torch.randint(0, 2000, (T,), device=DEV)
     ref = x.clone().float()
     view = ref[:, nh * D: 2 * nh * D].view(T, nh, D)
@@ -91,10 +93,11 @@ def test_rope_inplace():
     assert rel(x, ref) < 1e-2
 
 
-def test_swiglu():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_swiglu(dtype):
     from lumen.ops.activation import swiglu, swiglu_ref
 
-    gu = torch.randn(333, 2 * 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    gu = torch.randn(333, 2 * 1024, device=DEV, dtype=dtype, requires_grad=True)
     y = swiglu(gu)
     gu2 = gu.detach().float().requires_grad_(True)
     y2 = swiglu_ref(gu2)
@@ -106,12 +109,13 @@ def test_swiglu():
 
 
 @pytest.mark.parametrize("V", [32000, 50272])
-def test_lm_head_cross_entropy(V):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_lm_head_cross_entropy(V, dtype):
     from lumen.ops.loss import lm_head_cross_entropy
 
     T, H = 257, 256
-    h = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    W = (torch.randn(V, H, device=DEV) * 0.05).to(torch.bfloat16)
+    h = torch.randn(T, H, device=DEV, dtype=dtype, requires_grad=True)
+    W = (torch.randn(V, H, device=DEV) * 0.05).to(dtype)
     labels = torch.randint(0, V, (T,), device=DEV)
     labels[::7] = -100
     n_valid = int((labels != -100).sum())
@@ -188,7 +192,8 @@ def test_adamw_device_step_counter():
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
 @pytest.mark.parametrize("impl", ["v2", "f32"])
-def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch, dtype):
     """impl v2: 16-bit MFMA kernels (lora_v2.hip); f32: exact-f32 MFMA kernel (lora.hip)."""
     import lumen.ops.lora as lora_mod
     from lumen.ops.lora import lora_linear, lora_linear_ref
@@ -208,8 +213,8 @@ def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch):
     N = sum(sizes)
     R = r * len(segs)
     nb = sum(s[1] for s in segs)
-    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=dtype, requires_grad=True)
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(dtype)
     A = (torch.randn(R, K, device=DEV) / math.sqrt(K)).requires_grad_(True)
     B = (torch.randn(nb, r, device=DEV) * 0.1).requires_grad_(True)
     seed = 1234567
@@ -217,7 +222,7 @@ def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch):
     x2 = x.detach().float().requires_grad_(True)
     A2 = A.detach().clone().requires_grad_(True)
     B2 = B.detach().clone().requires_grad_(True)
-    y2 = lora_linear_ref(x2.to(torch.bfloat16).float(), W.float(), None, A2, B2, segs, r, 2.0,
+    y2 = lora_linear_ref(x2.to(dtype).float(), W.float(), None, A2, B2, segs, r, 2.0,
                          p_drop, seed)
     assert rel(y, y2) < 1e-2
     dy = torch.randn_like(y)
@@ -313,7 +318,8 @@ def test_sampling_greedy_and_topk():
                                          (4, 4, [1000, 64, 129])])
 @pytest.mark.parametrize("fwd,bwd", [("t1", "v16"), ("t2", "v16"), ("old", "v16"),
                                      ("v32", "v32"), ("v32", "mix"), ("v32", "mix-sep")])
-def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch, dtype):
     """bwd "mix-sep": mix kernels with the separate delta pass instead of the dQ kernel's own."""
     import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
@@ -329,7 +335,7 @@ def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch):
     for L in lens:
         cu.append(cu[-1] + L)
     T = cu[-1]
-    qkv = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(torch.bfloat16)
+    qkv = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(dtype)
     qkv.requires_grad_(True)
     o = flash_attention_qkv(qkv, cu, nh, nkv, D, True)
     q2 = qkv.detach().float().requires_grad_(True)
@@ -346,7 +352,8 @@ def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch):
 
 
 @pytest.mark.parametrize("nh,nkv", [(8, 8), (8, 2)])
-def test_flash_backward_fused_inverse_rope(nh, nkv):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_flash_backward_fused_inverse_rope(nh, nkv, dtype):
     """dQ / dK epilogues with the inverse RoPE (FA backward given the rotation) == plain FA
     backward followed by the separate inverse-rotation pass; dV untouched.  (The skip of the
     producer's own inverse pass is checked end to end by test_llama_fused_rope_backward_matches.)"""
@@ -358,8 +365,8 @@ def test_flash_backward_fused_inverse_rope(nh, nkv):
     T = cu[-1]
     cos, sin = rope_tables(D, 4096, 10000.0, DEV)
     pos = torch.randint(0, 4096, (T,), device=DEV, dtype=torch.int32)
-    qkv = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(torch.bfloat16)
-    do = torch.randn(T, nh * D, device=DEV).to(torch.bfloat16)
+    qkv = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(dtype)
+    do = torch.randn(T, nh * D, device=DEV).to(dtype)
     grads = []
     for fused in (True, False):
         x = qkv.clone().requires_grad_(True)
@@ -518,7 +525,8 @@ def test_engine_lora_grad_paths_match(direct, arena, ckpt, monkeypatch):
 
 
 @pytest.mark.parametrize("nh,nkv", [(8, 8), (8, 2)])
-def test_lora_linear_fused_rope(nh, nkv):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_lora_linear_fused_rope(nh, nkv, dtype):
     """RoPE fused into the q|k adapter write-back == lora_linear followed by RoPE (fwd + grads)."""
     from lumen.ops.lora import lora_linear
     from lumen.ops.rope import rope_qkv_, rope_tables
@@ -527,8 +535,8 @@ def test_lora_linear_fused_rope(nh, nkv):
     N = (nh + 2 * nkv) * D
     segs = [(0, nh * D, 0, 0), (nh * D, nkv * D, 16, nh * D), ((nh + nkv) * D, nkv * D, 32, (nh + nkv) * D)]
     torch.manual_seed(0)
-    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=dtype, requires_grad=True)
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(dtype)
     A = (torch.randn(48, K, device=DEV) / math.sqrt(K)).requires_grad_(True)
     B = (torch.randn(N, r, device=DEV) * 0.1).requires_grad_(True)
     cos, sin = rope_tables(D, 4096, 10000.0, DEV)

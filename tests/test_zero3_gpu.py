@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_wt="none",
-           config=None):
+           config=None, max_live=None):
     from lumen.lora import LoraConfig, adapter_state_dict, apply_lora
     from lumen.models import build_model
     from lumen.parallel.dist import init
@@ -35,9 +35,10 @@ def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_
         ds = load_ds_config(config, 2, accum, 1, 1e-3, dtype_override="bf16")
         ds.stage3_param_persistence_threshold = int(1e4)
     else:
-        ds = load_ds_config({"zero_optimization": {"stage": stage,
-                                                   "stage3_param_persistence_threshold": 1e4}},
-                            2, accum, 1, 1e-3)
+        z = {"stage": stage, "stage3_param_persistence_threshold": 1e4}
+        if max_live is not None:
+            z["stage3_max_live_parameters"] = max_live
+        ds = load_ds_config({"zero_optimization": z}, 2, accum, 1, 1e-3)
     eng = ZeroEngine(m, ds, env)
     g = torch.Generator(device="cpu").manual_seed(5)
     losses = []
@@ -57,14 +58,21 @@ def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_
                                            ("pipelined", True), ("release", True)])
 def test_zero3_schedules_match_stage0_on_gpu(schedule, ckpt, monkeypatch):
     ref, ref_losses, _ = _train(monkeypatch, 0, ckpt=ckpt)
-    got, losses, coord = _train(monkeypatch, 3, schedule, ckpt=ckpt)
+    # release: a live budget of one unit -> a ring of 2 buffers, nothing kept across the turn,
+    # every layer gathered twice per micro-step
+    got, losses, coord = _train(monkeypatch, 3, schedule, ckpt=ckpt,
+                                max_live=1 if schedule == "release" else None)
     assert coord is not None and coord.schedule == schedule
     n_units = sum(1 for u in coord.units if u.params)
-    per_step = 2 if schedule == "release" else 1
-    # every micro-step re-gathers every unit (the shards are the only persistent copy);
-    # pipelined has the next micro-step's gathers issued already
-    extra = n_units if schedule == "pipelined" else 0
-    assert coord.gathers >= per_step * 8 * (n_units - 1) + extra
+    if schedule == "release":
+        assert coord.pool_size == 2 and coord.turn_keep == 0 and coord.pool_overflows == 0
+        # forward: every unit; backward: every layer (the head is consumed at the turn)
+        assert coord.gathers == 8 * (n_units + n_units - 2)
+    else:
+        # every micro-step re-gathers every unit (the shards are the only persistent copy);
+        # pipelined has the next micro-step's gathers issued already
+        extra = n_units if schedule == "pipelined" else 0
+        assert coord.gathers >= 8 * (n_units - 1) + extra
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 2e-2 * max(1.0, abs(b))
     for k in ref:
@@ -114,9 +122,10 @@ def test_zero3_schedules_race_free_under_nan_poison(schedule, monkeypatch):
     """Race detector: with LUMEN_ZERO3_POISON every buffer is NaN-filled right before each
     (re-)gather.  A read outside a buffer's live window would make the loss NaN; the run must
     match the unpoisoned one."""
-    ref, ref_losses, _ = _train(monkeypatch, 3, schedule, ckpt=True, steps=3)
+    ml = 1 if schedule == "release" else None   # release: a 2-buffer ring, re-used every unit
+    ref, ref_losses, _ = _train(monkeypatch, 3, schedule, ckpt=True, steps=3, max_live=ml)
     monkeypatch.setenv("LUMEN_ZERO3_POISON", "1")
-    got, losses, coord = _train(monkeypatch, 3, schedule, ckpt=True, steps=3)
+    got, losses, coord = _train(monkeypatch, 3, schedule, ckpt=True, steps=3, max_live=ml)
     assert coord.poison
     assert all(math.isfinite(x) for x in losses)
     # (not bitwise: the LoRA kernels' split-K f32 atomics make run-to-run rounding differ)
