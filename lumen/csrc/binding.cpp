@@ -24,7 +24,7 @@ hipError_t lumen_rope_inplace(int, void*, const int*, const float*, const float*
                               int, hipStream_t);
 hipError_t lumen_swiglu(int, int, const void*, const void*, void*, int, int, hipStream_t);
 hipError_t lumen_cross_entropy(int, void*, const int64_t*, float*, float*, int, int, int, float,
-                               int, hipStream_t);
+                               int, const float*, hipStream_t);
 hipError_t lumen_grad_norm_sq(int, const void*, long long, float*, hipStream_t);
 hipError_t lumen_adamw(float*, int, const void*, float*, float*, int, void*, long long, float, float,
                        float, float, float, float, float, float, const float*, float, float*,
@@ -219,7 +219,7 @@ void gemv_swiglu(const at::Tensor& gu, const at::Tensor& w, at::Tensor& y) {
 
 void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
                    const std::optional<at::Tensor>& row_loss, int64_t ignore_index, double scale,
-                   bool write_grad) {
+                   bool write_grad, const std::optional<at::Tensor>& gscale) {
   need_cuda(logits, "logits"); need_cuda(labels, "labels");
   if (labels.scalar_type() != at::kLong) throw std::invalid_argument("lumen: labels must be int64");
   const int V = static_cast<int>(logits.size(-1));
@@ -227,7 +227,7 @@ void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::opti
   check(lumen_cross_entropy(dcode(logits), logits.data_ptr(), labels.data_ptr<int64_t>(),
                             ptr<float>(loss_sum), ptr<float>(row_loss), rows, V,
                             static_cast<int>(ignore_index), static_cast<float>(scale),
-                            write_grad ? 1 : 0, cur_stream()),
+                            write_grad ? 1 : 0, ptr<const float>(gscale), cur_stream()),
         "cross_entropy");
 }
 

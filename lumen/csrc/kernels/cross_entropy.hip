@@ -10,6 +10,9 @@
 // the [T, V] f32 copy and the separate backward launch disappear.  `scale` is 1/num_valid_tokens
 // (known on the host from the collated labels); the upstream grad scalar is applied later to the
 // [T, H] result of the LM-head dX GEMM, which is 8x smaller than the logits.
+// fp16 with dynamic loss scaling: `gscale` (device f32, optional) multiplies the written gradient
+// by the CURRENT loss scale, as the reference's upcast-logits graph does ((p - y) * S / n reaches
+// the fp16 LM-head GEMM already scaled); without it p / n underflows fp16 for most of the vocab.
 #include "common.h"
 
 namespace lumen {
@@ -18,7 +21,8 @@ template <typename T, int NT>
 __global__ void __launch_bounds__(NT) xent_kernel(T* __restrict__ logits, const int64_t* labels,
                                                   float* __restrict__ loss_sum,
                                                   float* __restrict__ row_loss, int V,
-                                                  int ignore_index, float scale, int write_grad) {
+                                                  int ignore_index, float scale, int write_grad,
+                                                  const float* __restrict__ gscale) {
   __shared__ float red[NT / 64];
   const int row = blockIdx.x;
   T* lr = logits + static_cast<size_t>(row) * V;
@@ -50,7 +54,7 @@ __global__ void __launch_bounds__(NT) xent_kernel(T* __restrict__ logits, const 
   }
   if (!write_grad) return;
   __syncthreads();  // everyone has read lr[lab] before it is overwritten
-  const float sc = valid ? scale : 0.f;
+  const float sc = valid ? scale * (gscale ? *gscale : 1.f) : 0.f;
   for (int i = threadIdx.x; i < nvec; i += NT) {
     float x[8];
     load8(lr + i * 8, x);
@@ -69,21 +73,21 @@ __global__ void __launch_bounds__(NT) xent_kernel(T* __restrict__ logits, const 
 extern "C" hipError_t lumen_cross_entropy(int dtype, void* logits, const int64_t* labels,
                                           float* loss_sum, float* row_loss, int rows, int V,
                                           int ignore_index, float scale, int write_grad,
-                                          hipStream_t st) {
+                                          const float* gscale, hipStream_t st) {
   if (V % 8 != 0) return hipErrorInvalidValue;
   if (rows == 0) return hipSuccess;
   dim3 grid(rows), block(512);
   if (dtype == lumen::kBF16)
     hipLaunchKernelGGL((lumen::xent_kernel<lumen::bf16, 512>), grid, block, 0, st,
                        (lumen::bf16*)logits, labels, loss_sum, row_loss, V, ignore_index, scale,
-                       write_grad);
+                       write_grad, gscale);
   else if (dtype == lumen::kF16)
     hipLaunchKernelGGL((lumen::xent_kernel<lumen::fp16, 512>), grid, block, 0, st,
                        (lumen::fp16*)logits, labels, loss_sum, row_loss, V, ignore_index, scale,
-                       write_grad);
+                       write_grad, gscale);
   else if (dtype == lumen::kF32)
     hipLaunchKernelGGL((lumen::xent_kernel<float, 512>), grid, block, 0, st, (float*)logits,
-                       labels, loss_sum, row_loss, V, ignore_index, scale, write_grad);
+                       labels, loss_sum, row_loss, V, ignore_index, scale, write_grad, gscale);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

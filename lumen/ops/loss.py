@@ -18,6 +18,12 @@ from ._native import native, use_native
 
 IGNORE_INDEX = -100
 
+# fp16 dynamic loss scaling: the engine points this at the device scalar it will multiply the
+# loss by (loss scale / grad accum) before each forward, so the CE kernel writes dlogits already
+# scaled -- (p - y) * S / n, like the reference's upcast-logits graph -- instead of the
+# unscaled p / n that underflows fp16.  None in bf16 / fp32.
+GRAD_SCALE_HINT = [None]
+
 
 class _LMHeadCE(torch.autograd.Function):
     @staticmethod
@@ -25,8 +31,10 @@ class _LMHeadCE(torch.autograd.Function):
         W = weight_fn()
         logits = torch.matmul(h, W.t())
         loss_sum = torch.zeros(1, dtype=torch.float32, device=h.device)
+        hint = GRAD_SCALE_HINT[0]
+        ctx.hint = hint
         native().cross_entropy(logits, labels, loss_sum, None, IGNORE_INDEX,
-                               1.0 / max(n_valid, 1), True)
+                               1.0 / max(n_valid, 1), True, hint)
         ctx.weight_fn = weight_fn
         ctx.w_grad = dummy_w is not None and dummy_w.requires_grad
         ctx.save_for_backward(logits, h if ctx.w_grad else torch.empty(0))
@@ -37,10 +45,14 @@ class _LMHeadCE(torch.autograd.Function):
         dlogits, h = ctx.saved_tensors
         W = ctx.weight_fn()
         dh = torch.matmul(dlogits, W)
-        dh.mul_(g.to(dh.dtype))
+        # upstream grad (a 0-dim f32 tensor): multiplied in f32 math, never cast to 16 bits
+        # first (2^16, the initial fp16 loss scale, is not representable in fp16); dlogits that
+        # already carry the hinted scale are divided by it (ratio 1 on the engine's path)
+        dh.mul_(g / ctx.hint if ctx.hint is not None else g)
         dw = None
         if ctx.w_grad:
-            dw = torch.matmul(dlogits.t(), h) * g.to(h.dtype)
+            dw = torch.matmul(dlogits.t(), h)
+            dw.mul_(g / ctx.hint if ctx.hint is not None else g)
         return dh, None, None, None, dw
 
 
@@ -64,6 +76,6 @@ def cross_entropy_rows(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tens
     if use_native(logits):
         out = torch.empty(logits.shape[0], dtype=torch.float32, device=logits.device)
         native().cross_entropy(logits.contiguous(), labels.contiguous(), None, out, IGNORE_INDEX,
-                               1.0, False)
+                               1.0, False, None)
         return out
     return F.cross_entropy(logits.float(), labels, ignore_index=IGNORE_INDEX, reduction="none")

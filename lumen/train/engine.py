@@ -135,6 +135,7 @@ class ZeroEngine:
             cfg.warmup_min_lr, cfg.warmup_max_lr, cfg.warmup_num_steps,
             cfg.warmup_type == "linear", W, self.scaler)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._gscale = torch.ones(1, dtype=torch.float32, device=self.device)
         self._works: List = []
         for prm in trainable:  # .grad is a view of flat.grad: kernels may accumulate into it
             prm._lumen_direct_grad = True
@@ -188,8 +189,20 @@ class ZeroEngine:
     # ----------------------------------------------------------------------------------------
     def forward(self, batch: Dict) -> torch.Tensor:
         self.timers.start("fwd")
-        loss = self.model(batch["input_ids"], batch["labels"], batch.get("n_valid"),
-                          batch.get("pos"))
+        fp16_dev = self.device_sched and self.scaler is not None
+        if fp16_dev:
+            # the fused LM-head CE writes dlogits already multiplied by the scale the backward
+            # will apply (device scalar: no host read of the loss scale)
+            from ..ops import loss as loss_ops
+
+            torch.div(self.opt.state[2:3], self.cfg.grad_accum, out=self._gscale)
+            loss_ops.GRAD_SCALE_HINT[0] = self._gscale
+        try:
+            loss = self.model(batch["input_ids"], batch["labels"], batch.get("n_valid"),
+                              batch.get("pos"))
+        finally:
+            if fp16_dev:
+                loss_ops.GRAD_SCALE_HINT[0] = None
         self.timers.stop("fwd")
         return loss
 
@@ -198,8 +211,9 @@ class ZeroEngine:
     def backward(self, loss: torch.Tensor):
         self.timers.start("bwd")
         if self.device_sched and self.scaler is not None:
-            # fp16: scale by the device loss scale (no host read of it)
-            (loss * (self.opt.state[2] / self.cfg.grad_accum)).backward()
+            # fp16: scale by the device loss scale / accum (no host read of it); the same tensor
+            # the forward handed the CE kernel as its gradient-scale hint
+            (loss * self._gscale[0]).backward()
         else:
             scale = self.loss_scale / self.cfg.grad_accum
             (loss * scale if scale != 1.0 else loss).backward()

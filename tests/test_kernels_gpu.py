@@ -146,7 +146,8 @@ def test_grad_norm_and_adamw():
     lr, b1, b2, eps, wd, inv = 1e-3, 0.9, 0.999, 1e-8, 0.01, 0.5
     maxn = 1.0
     copy = torch.empty(n, device=DEV, dtype=torch.bfloat16)
-    C.adamw(p, g, m, v, copy, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, inv, ns, maxn, None)
+    C.adamw(p, g, m, v, copy, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, inv, ns, maxn, None,
+            [])
     gn = math.sqrt(ns.item()) * inv
     coef = inv * (maxn / (gn + 1e-6) if gn > maxn else 1.0)
     _adamw_torch(p2, g, m2, v2, lr, b1, b2, eps, wd, 1 - b1 ** 3, 1 - b2 ** 3, coef)
@@ -156,7 +157,7 @@ def test_grad_norm_and_adamw():
     # overflow -> no update
     p3 = p.clone()
     bad = torch.tensor([float("inf")], device=DEV)
-    C.adamw(p, g, m, v, None, lr, b1, b2, eps, wd, 0.1, 0.1, 1.0, bad, 1.0, None)
+    C.adamw(p, g, m, v, None, lr, b1, b2, eps, wd, 0.1, 0.1, 1.0, bad, 1.0, None, [])
     assert torch.equal(p, p3)
 
 
@@ -172,19 +173,22 @@ def test_adamw_device_step_counter():
     m = torch.zeros(n, device=DEV)
     v = torch.zeros(n, device=DEV)
     p2, m2, v2 = p.clone(), m.clone(), v.clone()
-    st = torch.zeros(2, device=DEV)
+    st = torch.zeros(8, device=DEV)
+    st[2] = 1.0                      # loss scale
     lr, b1, b2 = 1e-2, 0.9, 0.999
+    # lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, window, hysteresis, min_scale
+    sched = [lr, lr, 0, 0, 1.0, 0, 1000, 2, 1.0]
     g = torch.randn(n, device=DEV)
     good = torch.zeros(1, device=DEV)
     C.grad_norm_sq(g, good)
     bad = torch.tensor([float("nan")], device=DEV)
     t = 0
     for norm in (good, bad, good, good, bad):
-        C.adamw(p, g, m, v, None, lr, b1, b2, 1e-8, 0.0, 1.0, 1.0, 1.0, norm, 0.0, st)
+        C.adamw(p, g, m, v, None, 0.0, b1, b2, 1e-8, 0.0, 1.0, 1.0, 0.0, norm, 0.0, st, sched)
         if norm is good:
             t += 1
             _adamw_torch(p2, g, m2, v2, lr, b1, b2, 1e-8, 0.0, 1 - b1 ** t, 1 - b2 ** t, 1.0)
-    assert st.tolist() == [3.0, 2.0]
+    assert st[:2].tolist() == [3.0, 2.0]
     assert (p - p2).abs().max().item() < 1e-5
     assert (v - v2).abs().max().item() < 1e-6
 
