@@ -85,6 +85,7 @@ def bench_engine(a) -> dict:
             "itl_p50_ms": round(1000 * _pct(itl, 0.5), 3),
             "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
             "kv_blocks": eng.blocks.num_blocks, "preemptions": eng.scheduler.num_preemptions,
+            "max_batched_tokens": a.max_batched_tokens, "steps": eng.stats["steps"],
             "setup_s": round(setup, 1), "graphs": sorted(eng.runner._graphs)}
 
 
@@ -97,7 +98,8 @@ def bench_http(a) -> dict:
     s.close()
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "serve.py"), "--model", a.model,
            "--port", str(port), "--max-model-len", str(a.max_model_len),
-           "--max-num-seqs", str(a.max_num_seqs)]
+           "--max-num-seqs", str(a.max_num_seqs),
+           "--max-num-batched-tokens", str(a.max_batched_tokens)]
     if a.no_graphs:
         cmd.append("--no-graphs")
     proc = subprocess.Popen(cmd, env=dict(os.environ, PYTHONPATH=ROOT))
@@ -143,7 +145,7 @@ def main():
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-num-seqs", type=int, default=256)
-    ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
     a = ap.parse_args()
     res = bench_engine(a) if a.mode == "engine" else bench_http(a)

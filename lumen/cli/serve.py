@@ -27,7 +27,8 @@ def build_parser():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-num-seqs", type=int, default=256)
-    ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=2048,
+                    help="tokens per engine step (running decodes + prefill chunks)")
     ap.add_argument("--block-size", type=int, default=16)
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
     ap.add_argument("--no-graphs", action="store_true")

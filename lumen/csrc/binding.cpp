@@ -55,6 +55,9 @@ hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, 
                                    int, int, int, int, long long, long long, int, hipStream_t);
 hipError_t lumen_sample(int, const void*, const float*, const float*, const int*,
                         unsigned long long, long long, long long*, float*, int, int, hipStream_t);
+hipError_t lumen_flash_attn_paged(int, int, const void*, long long, const void*, const void*, void*,
+                                  long long, const int*, const int*, const int*, int, const int*,
+                                  int, int, int, int, int, float, hipStream_t);
 hipError_t lumen_flash_attn(int, int, int, int, const void*, const void*, const void*, long long,
                             long long, long long, void*, long long, float*, const int*, const int*,
                             int, int, int, int, float, const void*, long long, void*, void*, void*,
@@ -442,6 +445,38 @@ void flash_attn(int64_t which, bool causal, int64_t mt, const at::Tensor& q, con
         "flash_attn");
 }
 
+// q [T, >= nh*D] token-major rows (any row stride), caches [nblocks, nkv, bs, D], o [T, nh*D]
+void flash_attn_paged(bool causal, const at::Tensor& q, const at::Tensor& k_cache,
+                      const at::Tensor& v_cache, at::Tensor& o, const at::Tensor& cu_q,
+                      const at::Tensor& kv_lens, const at::Tensor& tiles,
+                      const at::Tensor& block_tables, int64_t nh, int64_t nkv, double scale) {
+  need_cuda(q, "q"); need_cuda(k_cache, "k_cache"); need_cuda(v_cache, "v_cache");
+  need_cuda(o, "o");
+  if (k_cache.dim() != 4 || k_cache.size(3) != 128 || k_cache.size(1) != nkv ||
+      !k_cache.is_contiguous() || !v_cache.is_contiguous() ||
+      v_cache.sizes() != k_cache.sizes() || q.scalar_type() != k_cache.scalar_type() ||
+      o.scalar_type() != q.scalar_type() || q.stride(1) != 1 || o.stride(1) != 1)
+    throw std::invalid_argument("lumen: flash_attn_paged needs [nblocks, nkv, bs, 128] caches "
+                                "of the query dtype and row-major q / o");
+  for (const at::Tensor* t : {&cu_q, &kv_lens, &tiles, &block_tables})
+    if (t->scalar_type() != at::kInt || !t->is_contiguous() || !t->is_cuda())
+      throw std::invalid_argument("lumen: flash_attn_paged index tensors must be int32 on GPU");
+  if (block_tables.dim() != 2 || block_tables.size(0) < kv_lens.numel() ||
+      cu_q.numel() != kv_lens.numel() + 1)
+    throw std::invalid_argument("lumen: flash_attn_paged: cu_q [nseq+1], kv_lens [nseq], "
+                                "block_tables [nseq, max_blocks]");
+  check(lumen_flash_attn_paged(dcode(q), causal ? 1 : 0, q.data_ptr(), q.stride(0),
+                               k_cache.data_ptr(), v_cache.data_ptr(), o.data_ptr(), o.stride(0),
+                               cu_q.data_ptr<int>(), kv_lens.data_ptr<int>(),
+                               tiles.data_ptr<int>(), static_cast<int>(tiles.numel() / 2),
+                               block_tables.data_ptr<int>(),
+                               static_cast<int>(block_tables.stride(0)),
+                               static_cast<int>(k_cache.size(2)), static_cast<int>(nh),
+                               static_cast<int>(nkv), static_cast<int>(q.size(0)),
+                               static_cast<float>(scale), cur_stream()),
+        "flash_attn_paged");
+}
+
 void cpu_adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, double lr, double b1,
                double b2, double eps, double wd, double bc1, double bc2, double grad_scale) {
   if (p.is_cuda() || g.is_cuda()) throw std::invalid_argument("lumen: cpu_adamw takes host tensors");
@@ -561,6 +596,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("reshape_and_cache", &reshape_and_cache);
   m.def("sample", &sample);
   m.def("flash_attn", &flash_attn);
+  m.def("flash_attn_paged", &flash_attn_paged);
   m.def("car_alloc", &car_alloc);
   m.def("car_free", &car_free);
   m.def("car_handle", &car_handle);

@@ -90,6 +90,28 @@ __device__ __forceinline__ void stage64_async(char* img, const T* base, long lon
   }
 }
 
+// stage64_async for the paged KV cache: row r of the tile is key kv0 + r of the sequence, found
+// in block bt[key / bs] at offset key % bs ([block][nkv][bs][D] layout: every (block, kv head)
+// is one contiguous bs x D run, so a 64-key tile is 64 / bs contiguous runs).  Same LDS image
+// and lane mapping as stage64_async.
+template <typename T>
+__device__ __forceinline__ void stage64_paged(char* img, const T* cache, int kvh, int nkv,
+                                              const int* bt, int bs, int r0, int rmax) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ swz(row);
+    int gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;
+    const long long blk = bt[gr / bs];
+    const T* src = cache + ((blk * nkv + kvh) * bs + gr % bs) * D + ch * 8;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)src, (__attribute__((address_space(3))) void*)(img + (wid * 4 + i) * 1024),
+        16, 0, 0);
+  }
+}
+
 // vmcnt waits as the s_waitcnt builtin (gfx9 simm16: vmcnt bits [3:0], expcnt [6:4] = 7,
 // lgkmcnt [11:8] = 15 i.e. "don't care"), NOT inline asm: the compiler's wait-insertion pass
 // sees the builtin, knows that every LDS-DMA older than the newest N has landed, and does not add
@@ -200,6 +222,14 @@ struct Args {
   const int* rope_pos;
   const float* rope_cos;
   const float* rope_sin;
+  // optional (forward, PAGED): keys / values come from the serving KV cache
+  // [num_blocks][nkv][block_size][D] (k / v point at the caches) through per-sequence block
+  // tables; kv_lens[seq] = keys visible to the sequence (cached context + this chunk), and the
+  // chunk's queries sit at positions kv_lens - q_len .. kv_lens - 1 (chunked / mixed prefill)
+  const int* kv_lens;
+  const int* block_tables;
+  int bt_stride;
+  int block_size;
 };
 
 // Inverse rotary embedding of one (x, x ^ 64) column pair: the forward rotation
@@ -997,7 +1027,7 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
   }
 }
 
-template <typename T, bool CAUSAL>
+template <typename T, bool CAUSAL, bool PAGED = false>
 __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   constexpr int BM = 128;
   // Two SEPARATE LDS objects for the ping-pong K|V buffers, with the loop unrolled by two so
@@ -1011,12 +1041,18 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   const int lq = lane & 31, hi = lane >> 5;
   const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
   const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
-  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;  // L = this sequence's query rows
+  // keys: self-attention over the same rows, or (PAGED) the cached context + this chunk, the
+  // chunk's queries sitting at key positions qoff .. qoff + L - 1
+  const int Lk = PAGED ? a.kv_lens[seq] : L;
+  const int qoff = Lk - L;
   const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
-  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
-  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
+  const T* K = reinterpret_cast<const T*>(a.k) + (PAGED ? 0 : (long long)s0 * a.ldk + kvh * D);
+  const T* V = reinterpret_cast<const T*>(a.v) + (PAGED ? 0 : (long long)s0 * a.ldv + kvh * D);
+  const int* bt = PAGED ? a.block_tables + (long long)seq * a.bt_stride : nullptr;
   const int wq0 = q0 + wid * 32;
   const int qrow = wq0 + lq;
+  const int qpos = qrow + qoff;  // key position of this lane's query (causal limit)
   Off32 off;
   make_off32(off, lane);
   uint4 qf[8];  // B operand of S^T: Q[qrow][16ks + 8hi .. +7]
@@ -1027,30 +1063,35 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
 #pragma unroll
   for (int n = 0; n < 4; ++n) acc[n] = zero16();
   float m_i = -INFINITY, l_i = 0.f;
-  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
-  const int w_end = CAUSAL ? min(kv_end, wq0 + 32) : kv_end;  // keys this wave can see
+  const int kv_end = CAUSAL ? min(Lk, q0 + qoff + BM) : Lk;
+  const int w_end = CAUSAL ? min(kv_end, wq0 + qoff + 32) : kv_end;  // keys this wave can see
+  auto stage = [&](char* img, int r0) {
+    if constexpr (PAGED) {
+      stage64_paged(img, K, kvh, a.nkv, bt, a.block_size, r0, Lk);
+      stage64_paged(img + IMG, V, kvh, a.nkv, bt, a.block_size, r0, Lk);
+    } else {
+      stage64_async(img, K, a.ldk, r0, L);
+      stage64_async(img + IMG, V, a.ldv, r0, L);
+    }
+  };
   wait_vm_all();  // Q fragments in registers before the DMA ring starts (exact vmcnt below)
-  if (kv_end > 0) {
-    stage64_async(bufA, K, a.ldk, 0, L);
-    stage64_async(bufA + IMG, V, a.ldv, 0, L);
-  }
+  if (kv_end > 0) stage(bufA, 0);
   // one K/V tile: prefetch the next into `nxt`, wait for `cur`, compute, release `cur`
   auto tile = [&](char* cur, char* nxt, int kv0) {
     if (kv0 + BN < kv_end) {
-      stage64_async(nxt, K, a.ldk, kv0 + BN, L);
-      stage64_async(nxt + IMG, V, a.ldv, kv0 + BN, L);
+      stage(nxt, kv0 + BN);
       wait_vm_8();
     } else {
       wait_vm_all();
     }
     lds_fence_barrier();
     if (kv0 < w_end) {  // (causal: tiles entirely above this wave's rows are skipped)
-      const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
+      const bool need_mask = (kv0 + BN > Lk) || (CAUSAL && kv0 + BN - 1 > wq0 + qoff);
       if (need_mask)
-        fwd32_tile<T, CAUSAL, true>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
+        fwd32_tile<T, CAUSAL, true>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos, hi,
                                     a.scale_log2);
       else
-        fwd32_tile<T, CAUSAL, false>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
+        fwd32_tile<T, CAUSAL, false>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos, hi,
                                      a.scale_log2);
     }
     lds_fence_barrier();  // every wave is done with `cur` before it is refilled
@@ -1427,6 +1468,10 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     } else {
       hipLaunchKernelGGL((bwd_dq32_kernel<T, false>), grid, block, 0, st, a);
     }
+  } else if (which == 6) {  // forward over the paged KV cache (32x32x16, 128-row tiles)
+    dim3 grid(ntiles, a.nh);
+    if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((fwd32_kernel<T, false, true>), grid, block, 0, st, a);
   } else {
     return hipErrorInvalidValue;
   }
@@ -1462,7 +1507,33 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.dout = dout; a.lddo = lddo; a.dq = dq; a.dk = dk; a.dv = dv; a.lddq = lddq; a.lddk = lddk;
   a.lddv = lddv; a.delta = delta;
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
+  a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
+  if (which == 6) return hipErrorInvalidValue;  // paged: lumen_flash_attn_paged
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
+  return hipErrorInvalidValue;
+}
+
+// Serving prefill (whole prompts, chunks of long prompts, or the prefill part of a mixed step):
+// queries from the token-major q rows (cu_q: per-sequence row offsets), keys / values from the
+// paged KV cache (this chunk's K/V already written there), kv_lens[s] = cached context + chunk.
+extern "C" hipError_t lumen_flash_attn_paged(int dtype, int causal, const void* q, long long ldq,
+                                             const void* k_cache, const void* v_cache, void* o,
+                                             long long ldo, const int* cu_q, const int* kv_lens,
+                                             const int* tiles, int ntiles,
+                                             const int* block_tables, int bt_stride,
+                                             int block_size, int nh, int nkv, int T, float scale,
+                                             hipStream_t st) {
+  if (nkv <= 0 || nh % nkv != 0 || block_size <= 0) return hipErrorInvalidValue;
+  if (ntiles == 0) return hipSuccess;
+  lumen::fa::Args a{};
+  a.q = q; a.ldq = ldq; a.k = k_cache; a.v = v_cache; a.ldk = a.ldv = 0;
+  a.o = o; a.ldo = ldo; a.lse = nullptr; a.cu = cu_q; a.tiles = tiles;
+  a.nh = nh; a.nkv = nkv; a.T = T;
+  a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
+  a.kv_lens = kv_lens; a.block_tables = block_tables; a.bt_stride = bt_stride;
+  a.block_size = block_size;
+  if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(6, causal, 20, ntiles, a, st);
+  if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(6, causal, 20, ntiles, a, st);
   return hipErrorInvalidValue;
 }

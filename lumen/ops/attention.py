@@ -1,11 +1,12 @@
-"""Causal self-attention for training / prefill.
+"""Attention ops for training and serving.
 
-Training uses PyTorch-ROCm's fused scaled-dot-product attention (flash kernels on gfx950) over
-head-major q/k/v produced by ``qkv_rope_split``; GQA is handled natively (no K/V repeat).  The
-output is returned token-major [B*S, nh*D] ready for the o_proj GEMM.
-
-Serving decode uses the paged-KV HIP kernel (``kernels/paged_attention.hip``): see
-``paged_decode`` below; prefill reuses the SDPA path per sequence then writes K/V to the cache.
+* Training (head_dim 128): the HIP flash-attention kernels (``kernels/flash_attn.hip``) read q/k/v
+  straight from the fused token-major QKV buffer (``flash_attention_qkv``); other head dims use
+  torch SDPA over head-major q/k/v (``causal_attention``).
+* Serving decode: the paged-KV HIP kernel (``kernels/paged_attention.hip``, ``paged_decode``).
+* Serving prefill -- whole prompts, chunks of long prompts and the prefill part of mixed
+  prefill+decode steps: ``flash_attention_paged``, the 32x32x16 flash forward reading keys /
+  values from the paged cache through block tables, queries offset by the cached context.
 """
 from __future__ import annotations
 
@@ -108,6 +109,62 @@ def paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale):
         p = torch.softmax(s, -1)
         out[i] = torch.einsum("hgl,hld->hgd", p, vv).reshape(nh, D).to(q.dtype)
     return out
+
+
+def flash_attention_paged(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                          cu_q, kv_lens, block_tables: torch.Tensor, nh: int, nkv: int,
+                          D: int, scale: Optional[float] = None,
+                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Causal attention of prefill chunks over the paged KV cache.
+
+    q: token-major rows [T, >= nh*D] (e.g. the q part of the fused qkv buffer, already rotated);
+    sequence s owns rows cu_q[s]..cu_q[s+1] and sees kv_lens[s] keys (its cached context plus
+    this chunk, whose K/V are already in the cache); query row j of s sits at key position
+    kv_lens[s] - (cu_q[s+1]-cu_q[s]) + j.  cu_q / kv_lens: int sequences (host) or int32 device
+    tensors; block_tables [nseq, max_blocks] int32.  Returns / fills out [T, nh*D]."""
+    T = q.shape[0]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if out is None:
+        out = torch.empty(T, nh * D, device=q.device, dtype=q.dtype)
+    if use_native(q) and D == 128 and k_cache.shape[-1] == 128:
+        cu = tuple(int(c) for c in cu_q)
+        dev = q.device
+        cut = _cu_tensor(cu, dev)
+        kl = (kv_lens if isinstance(kv_lens, torch.Tensor)
+              else torch.tensor(list(kv_lens), dtype=torch.int32, device=dev))
+        native().flash_attn_paged(True, q, k_cache, v_cache, out, cut, kl.to(torch.int32),
+                                  _tiles(cu, 128, dev), block_tables.to(torch.int32), nh, nkv,
+                                  scale)
+        return out
+    out.copy_(flash_attention_paged_ref(q, k_cache, v_cache, cu_q, kv_lens, block_tables, nh,
+                                        nkv, D, scale))
+    return out
+
+
+def flash_attention_paged_ref(q, k_cache, v_cache, cu_q, kv_lens, block_tables, nh, nkv, D,
+                              scale=None):
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    cu = [int(c) for c in cu_q]
+    kl = [int(x) for x in kv_lens]
+    bs = k_cache.shape[2]
+    g = nh // nkv
+    outs = []
+    for s in range(len(kl)):
+        a, b = cu[s], cu[s + 1]
+        n, L = b - a, kl[s]
+        nblk = (L + bs - 1) // bs
+        blks = block_tables[s, :nblk].long()
+        kk = k_cache[blks].permute(1, 0, 2, 3).reshape(nkv, nblk * bs, D)[:, :L].float()
+        vv = v_cache[blks].permute(1, 0, 2, 3).reshape(nkv, nblk * bs, D)[:, :L].float()
+        qq = q[a:b, :nh * D].float().view(n, nkv, g, D)
+        sc = torch.einsum("nhgd,hld->hgnl", qq, kk) * scale
+        qpos = torch.arange(L - n, L, device=q.device)[:, None]
+        kpos = torch.arange(L, device=q.device)[None, :]
+        sc = sc.masked_fill(kpos > qpos, float("-inf"))
+        p = torch.softmax(sc, -1)
+        o = torch.einsum("hgnl,hld->nhgd", p, vv).reshape(n, nh * D)
+        outs.append(o.to(q.dtype))
+    return torch.cat(outs, 0) if outs else q.new_zeros(0, nh * D)
 
 
 def write_kv_cache(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor,

@@ -2,13 +2,16 @@
 
 The reference declares "vLLM ... OpenAI-compatible API" (README.md:10,16): this serves the same
 surface -- ``GET /v1/models``, ``POST /v1/completions``, ``POST /v1/chat/completions`` (both with
-``stream: true`` Server-Sent Events ending in ``data: [DONE]``), ``GET /health`` and a
+``stream: true`` Server-Sent Events ending in ``data: [DONE]``; ``stop`` strings, ``n`` /
+``best_of``, ``presence_penalty`` / ``frequency_penalty`` and vLLM's ``repetition_penalty``,
+``stop_token_ids``, ``ignore_eos``, ``seed``), ``GET /health`` and a
 Prometheus-format ``GET /metrics`` (requests, tokens, TTFT / inter-token latency summaries,
 KV-cache usage).  Chat requests use the Llama-2 chat template the reference trains with
 (``<s>[INST] {user} [/INST]``, scripts/prepare_dataset.py:12-25).
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import time
 import uuid
@@ -77,7 +80,65 @@ def _params(body: Dict[str, Any], eos: Optional[int]) -> SamplingParams:
                           temperature=float(body.get("temperature", 1.0)),
                           top_p=float(body.get("top_p", 1.0)), top_k=int(body.get("top_k", 0) or 0),
                           stop_token_ids=list(stop_ids), ignore_eos=bool(body.get("ignore_eos", False)),
-                          seed=body.get("seed"), logprobs=bool(body.get("logprobs", False)))
+                          seed=body.get("seed"), logprobs=bool(body.get("logprobs", False)),
+                          presence_penalty=float(body.get("presence_penalty") or 0.0),
+                          frequency_penalty=float(body.get("frequency_penalty") or 0.0),
+                          repetition_penalty=float(body.get("repetition_penalty") or 1.0))
+
+
+def _stops(body: Dict[str, Any]) -> List[str]:
+    st = body.get("stop")
+    if st is None:
+        return []
+    if isinstance(st, str):
+        st = [st]
+    if not isinstance(st, list) or not all(isinstance(x, str) for x in st) or len(st) > 16:
+        raise ValueError("stop must be a string or a list of up to 16 strings")
+    return [x for x in st if x]
+
+
+def _n_best_of(body: Dict[str, Any], stream: bool):
+    n = int(body.get("n") or 1)
+    best_of = int(body.get("best_of") or n)
+    if n < 1 or best_of < n or best_of > 16:
+        raise ValueError("need 1 <= n <= best_of <= 16")
+    if stream and best_of != n:
+        raise ValueError("best_of != n cannot be streamed")
+    return n, best_of
+
+
+class StopChecker:
+    """OpenAI ``stop`` strings over the streamed text: text that could still be the start of a
+    stop string is held back (len(longest stop) - 1 characters); when one appears the output is
+    cut before it (vLLM ``include_stop_str_in_output`` keeps it) and the request finishes with
+    ``finish_reason: "stop"`` -- the caller then leaves the engine stream, which aborts the
+    request and frees its KV blocks."""
+
+    def __init__(self, stops: List[str], include: bool = False):
+        self.stops = stops
+        self.include = include
+        self.hold = max((len(x) for x in stops), default=1) - 1
+        self.text = ""
+        self.emitted = 0
+        self.stopped = False
+
+    def feed(self, delta: str, final: bool = False) -> str:
+        """Add decoded text; returns what may be sent now."""
+        if self.stopped:
+            return ""
+        start = max(0, len(self.text) - self.hold)
+        self.text += delta
+        if self.stops:
+            hits = [(i, x) for x in self.stops for i in [self.text.find(x, start)] if i >= 0]
+            if hits:
+                i, x = min(hits)
+                self.text = self.text[:i + (len(x) if self.include else 0)]
+                self.stopped = True
+                final = True
+        end = len(self.text) if final else max(self.emitted, len(self.text) - self.hold)
+        out = self.text[self.emitted:end]
+        self.emitted = end
+        return out
 
 
 class IncrementalDetokenizer:
@@ -150,73 +211,129 @@ def create_app(aengine, served_model_name: Optional[str] = None):
         ]
         return PlainTextResponse("\n".join(lines) + "\n")
 
-    async def _run(prompt, params, chat: bool, stream: bool, model: str):
+    async def _one(prompt, params, rid, lora, stops, include_stop, on_delta=None):
+        """Drive one engine stream through the detokenizer and the stop-string check.  Calls
+        ``on_delta(text, finish_reason, seq)`` per engine step (streaming); returns
+        (text, seq, finish_reason)."""
+        detok = IncrementalDetokenizer(tok)
+        stop = StopChecker(stops, include_stop)
+        last, fin = None, None
+        async for seq in aengine.stream(prompt, params, rid, lora):
+            last = seq
+            fin = seq.finish_reason if seq.finished else None
+            d = detok.step(seq.output_ids)
+            if fin:
+                d += detok.flush(seq.output_ids)
+            out = stop.feed(d, final=fin is not None)
+            if stop.stopped:
+                fin = "stop"
+            if on_delta is not None:
+                await on_delta(out, fin, seq)
+            if fin is not None:
+                break   # a stop string ends the stream early: the engine request is aborted
+        if last is not None:
+            stats.observe(last)
+        return stop.text, last, fin
+
+    async def _run(prompt, params, chat: bool, stream: bool, model: str, body: Dict[str, Any]):
         rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex
         lora = model if model in loras else None  # OpenAI "model" selects a served adapter
         created = int(time.time())
         stats.requests += 1
         obj = "chat.completion" if chat else "text_completion"
+        try:
+            stops = _stops(body)
+            n, best_of = _n_best_of(body, stream)
+        except ValueError as e:
+            raise HTTPException(status_code=400, detail=str(e))
+        include_stop = bool(body.get("include_stop_str_in_output", False))
 
-        def chunk(delta_text, finish, seq=None):
+        def sub_params(i):
+            p = SamplingParams(**vars(params))
+            if p.seed is not None:
+                p.seed = p.seed + i     # distinct choices under a fixed seed
+            return p
+
+        def chunk(delta_text, finish, index=0):
             if chat:
                 d = {"content": delta_text} if delta_text else {}
-                ch = {"index": 0, "delta": d, "finish_reason": finish}
+                ch = {"index": index, "delta": d, "finish_reason": finish}
                 o = "chat.completion.chunk"
             else:
-                ch = {"index": 0, "text": delta_text, "logprobs": None, "finish_reason": finish}
+                ch = {"index": index, "text": delta_text, "logprobs": None,
+                      "finish_reason": finish}
                 o = "text_completion"
             return {"id": rid, "object": o, "created": created, "model": model, "choices": [ch]}
 
         if stream:
             async def gen():
-                last = None
-                detok = IncrementalDetokenizer(tok)
-                try:
-                    if chat:
-                        first = {"id": rid, "object": "chat.completion.chunk", "created": created,
-                                 "model": model, "choices": [{"index": 0, "delta": {"role": "assistant"},
-                                                              "finish_reason": None}]}
-                        yield f"data: {json.dumps(first)}\n\n"
-                    async for seq in aengine.stream(prompt, params, rid, lora):
-                        last = seq
-                        fin = seq.finish_reason if seq.finished else None
-                        delta = detok.step(seq.output_ids)
-                        if fin:
-                            delta += detok.flush(seq.output_ids)
+                q: asyncio.Queue = asyncio.Queue()
+
+                async def run_choice(i):
+                    async def on_delta(text, fin, seq):
                         # one event per engine step that produced tokens, even when the text
-                        # delta is still empty (incomplete UTF-8 / special ids): clients see
-                        # token timing (TTFT, inter-token latency) as OpenAI streams show it
-                        yield f"data: {json.dumps(chunk(delta, fin))}\n\n"
-                    if last is not None:
-                        stats.observe(last)
-                except ValueError as e:
-                    stats.errors += 1
-                    yield f"data: {json.dumps({'error': {'message': str(e)}})}\n\n"
+                        # delta is still empty (incomplete UTF-8 / held-back stop prefix):
+                        # clients see token timing (TTFT, inter-token latency)
+                        await q.put(f"data: {json.dumps(chunk(text, fin, i))}\n\n")
+                    try:
+                        await _one(prompt, sub_params(i), f"{rid}-{i}" if n > 1 else rid, lora,
+                                   stops, include_stop, on_delta)
+                    except ValueError as e:
+                        stats.errors += 1
+                        await q.put(f"data: {json.dumps({'error': {'message': str(e)}})}\n\n")
+                    finally:
+                        await q.put(None)
+
+                if chat:
+                    for i in range(n):
+                        first = {"id": rid, "object": "chat.completion.chunk",
+                                 "created": created, "model": model,
+                                 "choices": [{"index": i, "delta": {"role": "assistant"},
+                                              "finish_reason": None}]}
+                        yield f"data: {json.dumps(first)}\n\n"
+                tasks = [asyncio.ensure_future(run_choice(i)) for i in range(n)]
+                live = n
+                try:
+                    while live:
+                        item = await q.get()
+                        if item is None:
+                            live -= 1
+                            continue
+                        yield item
+                finally:
+                    for t in tasks:
+                        if not t.done():
+                            t.cancel()
                 yield "data: [DONE]\n\n"
             return StreamingResponse(gen(), media_type="text/event-stream")
 
-        last = None
         try:
-            async for seq in aengine.stream(prompt, params, rid, lora):
-                last = seq
+            res = await asyncio.gather(*[
+                _one(prompt, sub_params(i), f"{rid}-{i}" if best_of > 1 else rid, lora, stops,
+                     include_stop) for i in range(best_of)])
         except ValueError as e:
             stats.errors += 1
             raise HTTPException(status_code=400, detail=str(e))
-        stats.observe(last)
-        text = decode(last.output_ids)
-        usage = {"prompt_tokens": len(last.prompt_ids), "completion_tokens": len(last.output_ids),
-                 "total_tokens": last.length}
-        if chat:
-            choice = {"index": 0, "message": {"role": "assistant", "content": text},
-                      "finish_reason": last.finish_reason}
-        else:
-            lp = None
-            if params.logprobs:
-                lp = {"tokens": [decode([t]) for t in last.output_ids],
-                      "token_logprobs": list(last.output_logprobs)}
-            choice = {"index": 0, "text": text, "logprobs": lp, "finish_reason": last.finish_reason}
+        if best_of > n:  # OpenAI best_of: the n choices with the highest total log probability
+            res = sorted(res, key=lambda r: -sum(r[1].output_logprobs))[:n]
+        choices = []
+        n_out = 0
+        for i, (text, seq, fin) in enumerate(res):
+            n_out += len(seq.output_ids)
+            if chat:
+                choices.append({"index": i, "message": {"role": "assistant", "content": text},
+                                "finish_reason": fin})
+            else:
+                lp = None
+                if params.logprobs:
+                    lp = {"tokens": [decode([t]) for t in seq.output_ids],
+                          "token_logprobs": list(seq.output_logprobs)}
+                choices.append({"index": i, "text": text, "logprobs": lp, "finish_reason": fin})
+        p_tok = len(res[0][1].prompt_ids)
+        usage = {"prompt_tokens": p_tok, "completion_tokens": n_out,
+                 "total_tokens": p_tok + n_out}
         return JSONResponse({"id": rid, "object": obj, "created": created, "model": model,
-                             "choices": [choice], "usage": usage})
+                             "choices": choices, "usage": usage})
 
     @app.post("/v1/completions")
     async def completions(req: Request):
@@ -231,7 +348,7 @@ def create_app(aengine, served_model_name: Optional[str] = None):
         except ValueError as e:
             raise HTTPException(status_code=400, detail=str(e))
         return await _run(prompt, params, False, bool(body.get("stream", False)),
-                          body.get("model", name))
+                          body.get("model", name), body)
 
     @app.post("/v1/chat/completions")
     async def chat(req: Request):
@@ -244,7 +361,7 @@ def create_app(aengine, served_model_name: Optional[str] = None):
         except ValueError as e:
             raise HTTPException(status_code=400, detail=str(e))
         return await _run(llama2_chat_prompt(msgs), params, True, bool(body.get("stream", False)),
-                          body.get("model", name))
+                          body.get("model", name), body)
 
     app.state.stats = stats
     return app

@@ -38,9 +38,9 @@ class EngineConfig:
     gpu_memory_utilization: float = 0.90
     num_blocks: Optional[int] = None
     max_num_seqs: int = 256
-    # prefill chunk budget: 8192 tokens keeps the GEMMs at full rate (M >= 8192) while cutting
-    # the burst p50 TTFT vs 16384 (740 vs 824 ms at 256 x 512-token prompts, profiles/r02_serve)
-    max_num_batched_tokens: int = 8192
+    # tokens per engine step (decode rows + prefill chunks): bounds the time a prefill can add
+    # to a step, i.e. the inter-token latency of the running streams (chunked prefill)
+    max_num_batched_tokens: int = 2048
     tp_size: int = 1
     seed: int = 0
     use_graphs: bool = True
@@ -52,6 +52,41 @@ class EngineConfig:
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
+
+
+def apply_penalties(logits: torch.Tensor, seqs: List[Sequence]) -> torch.Tensor:
+    """Presence / frequency / repetition penalties on the rows of ``logits`` (f32 result), one
+    scatter-add of the rows' token ids into a [rows, V] count table on the device."""
+    out = logits.float().clone()
+    rows = [i for i, s in enumerate(seqs) if s.params.has_penalties]
+    V = out.shape[1]
+    dev = out.device
+
+    def counts(id_lists):
+        L = max((len(x) for x in id_lists), default=0)
+        c = torch.zeros(len(id_lists), V + 1, dtype=torch.float32, device=dev)
+        if L:
+            ids = torch.full((len(id_lists), L), V, dtype=torch.long)
+            for j, x in enumerate(id_lists):
+                if x:
+                    ids[j, :len(x)] = torch.tensor(x, dtype=torch.long)
+            ids = ids.to(dev)
+            c.scatter_add_(1, ids, torch.ones_like(ids, dtype=torch.float32))
+        return c[:, :V]
+
+    sel = [seqs[i] for i in rows]
+    ridx = torch.tensor(rows, dtype=torch.long, device=dev)
+    lg = out[ridx]
+    out_c = counts([s.output_ids for s in sel])
+    fp = torch.tensor([s.params.frequency_penalty for s in sel], device=dev)[:, None]
+    pp = torch.tensor([s.params.presence_penalty for s in sel], device=dev)[:, None]
+    lg -= fp * out_c + pp * (out_c > 0).float()
+    rp = torch.tensor([s.params.repetition_penalty for s in sel], device=dev)[:, None]
+    if bool((rp != 1.0).any()):
+        seen = (counts([s.all_ids for s in sel]) > 0) & (rp != 1.0)
+        lg = torch.where(seen, torch.where(lg > 0, lg / rp, lg * rp), lg)
+    out[ridx] = lg
+    return out
 
 
 class LLMEngine:
@@ -173,49 +208,86 @@ class LLMEngine:
     def _build_input(self, batch: Batch) -> StepInput:
         """Host-side step metadata, vectorised with numpy and shipped in ONE host-to-device copy
         (a Python/torch loop per sequence cost ~10 ms per 256-sequence decode step, a third of
-        the step)."""
+        the step).  Rows: prefill chunks first, then decode tokens."""
         bm = self.blocks
         bs = bm.block_size
-        if batch.kind == "prefill":
-            toks, pos, slots, cu = [], [], [], [0]
-            for s in batch.seqs:
-                ids = s.all_ids
-                n = len(ids)
-                toks.append(np.asarray(ids, dtype=np.int64))
-                p = np.arange(n, dtype=np.int64)
-                pos.append(p)
-                tbl = np.asarray(bm.tables[s.seq_id], dtype=np.int64)
-                slots.append(tbl[p // bs] * bs + p % bs)
-                cu.append(cu[-1] + n)
-            T = cu[-1]
-            extra = []
-            if self.runner.lora is not None:
-                extra = [np.repeat(np.array([s.lora_slot for s in batch.seqs], dtype=np.int64),
-                                   np.diff(np.asarray(cu)))]
-            host = np.concatenate(toks + pos + slots + extra)
-            dev = self._to_device(host)
-            return StepInput("prefill", dev[:T], dev[T:2 * T].int(), dev[2 * T:3 * T], cu,
-                             lora_ids=dev[3 * T:4 * T].int() if extra else None)
-        N = len(batch.seqs)
-        tables = [bm.tables[s.seq_id] for s in batch.seqs]
-        lens = np.fromiter((s.length for s in batch.seqs), dtype=np.int64, count=N)
-        toks = np.fromiter((s.last_token for s in batch.seqs), dtype=np.int64, count=N)
-        maxb = max(len(t) for t in tables)
-        bt = np.zeros((N, maxb), dtype=np.int64)
-        for i, t in enumerate(tables):
-            bt[i, :len(t)] = t
-        pos = lens - 1
-        slots = bt[np.arange(N), pos // bs] * bs + pos % bs
-        parts = [toks, pos, slots, lens, bt.reshape(-1)]
-        if self.runner.lora is not None:
-            parts.append(np.fromiter((s.lora_slot for s in batch.seqs), dtype=np.int64, count=N))
-        host = np.concatenate(parts)
+        use_lora = self.runner.lora is not None
+        toks, pos, slots, lora = [], [], [], []
+        cu, kv_lens, ptables = [0], [], []
+        for s, c in batch.prefills:
+            a = s.num_cached
+            ids = s.all_ids
+            toks.append(np.asarray(ids[a:a + c], dtype=np.int64))
+            p = np.arange(a, a + c, dtype=np.int64)
+            pos.append(p)
+            tbl = np.asarray(bm.tables[s.seq_id], dtype=np.int64)
+            slots.append(tbl[p // bs] * bs + p % bs)
+            cu.append(cu[-1] + c)
+            kv_lens.append(a + c)
+            ptables.append(tbl)
+            if use_lora:
+                lora.append(np.full(c, s.lora_slot, dtype=np.int64))
+        Tp = cu[-1]
+        N = len(batch.decodes)
+        parts = toks + pos + slots
+        dec_bt = None
+        maxb_d = 0
+        if N:
+            tables = [bm.tables[s.seq_id] for s in batch.decodes]
+            lens = np.fromiter((s.length for s in batch.decodes), dtype=np.int64, count=N)
+            dtok = np.fromiter((s.last_token for s in batch.decodes), dtype=np.int64, count=N)
+            maxb_d = max(len(t) for t in tables)
+            dec_bt = np.zeros((N, maxb_d), dtype=np.int64)
+            for i, t in enumerate(tables):
+                dec_bt[i, :len(t)] = t
+            dpos = lens - 1
+            dslots = dec_bt[np.arange(N), dpos // bs] * bs + dpos % bs
+            # decode rows go after the prefill rows in each of tokens / positions / slots
+            parts = toks + [dtok] + pos + [dpos] + slots + [dslots]
+            if use_lora:
+                lora.append(np.fromiter((s.lora_slot for s in batch.decodes), dtype=np.int64,
+                                        count=N))
+        T = Tp + N
+        P = len(batch.prefills)
+        maxb_p = max((len(t) for t in ptables), default=0)
+        extra = []
+        if P:
+            pt = np.zeros((P, maxb_p), dtype=np.int64)
+            for i, t in enumerate(ptables):
+                pt[i, :len(t)] = t
+            extra += [pt.reshape(-1), np.asarray(kv_lens, dtype=np.int64)]
+        if N:
+            extra += [dec_bt.reshape(-1), lens]
+        n_done = len(batch.completing())
+        done_rows = [cu[i + 1] - 1 for i, (s, c) in enumerate(batch.prefills)
+                     if s.num_cached + c == s.length]
+        assert len(done_rows) == n_done
+        rows = np.concatenate([np.asarray(done_rows, dtype=np.int64),
+                               np.arange(Tp, T, dtype=np.int64)])
+        extra.append(rows)
+        if use_lora:
+            extra.append(np.concatenate(lora))
+        host = np.concatenate([np.concatenate(parts)] + extra)
         dev = self._to_device(host)
-        e = 4 * N + N * maxb
-        return StepInput("decode", dev[:N], dev[N:2 * N].int(), dev[2 * N:3 * N], [],
-                         dev[4 * N:e].view(N, maxb).int(), dev[3 * N:4 * N].int(),
-                         int(lens.max()),
-                         lora_ids=dev[e:e + N].int() if self.runner.lora is not None else None)
+        o = 3 * T
+        inp = StepInput(batch.kind, dev[:T], dev[T:2 * T].int(), dev[2 * T:3 * T], cu)
+        if P:
+            inp.prefill_tables = dev[o:o + P * maxb_p].view(P, maxb_p).int()
+            o += P * maxb_p
+            inp.kv_lens = kv_lens
+            inp.kv_lens_t = dev[o:o + P].int()
+            o += P
+        if N:
+            inp.block_tables = dev[o:o + N * maxb_d].view(N, maxb_d).int()
+            o += N * maxb_d
+            inp.context_lens = dev[o:o + N].int()
+            o += N
+            inp.max_context = int(lens.max())
+        inp.sample_rows = dev[o:o + len(rows)]
+        o += len(rows)
+        if use_lora:
+            inp.lora_ids = dev[o:o + T].int()
+        return inp
 
     def _to_device(self, host: "np.ndarray") -> torch.Tensor:
         t = torch.from_numpy(host)
@@ -244,31 +316,43 @@ class LLMEngine:
         batch = self.scheduler.schedule()
         if batch is None:
             return []
+        return self._run_batch(batch)
+
+    def _run_batch(self, batch: Batch) -> List[Sequence]:
         inp = self._build_input(batch)
         if self.tp > 1:
             self._broadcast(inp)
-        if batch.kind == "prefill":
-            logits = self.runner.prefill(inp)
-            self.stats["prefill_tokens"] += len(inp.tokens)
-        else:
+        sampled = batch.sampled   # before the cache bookkeeping below changes num_cached
+        if batch.kind == "decode":
             logits = self.runner.decode(inp)
-            self.stats["decode_tokens"] += len(batch.seqs)
-        ps = [s.params for s in batch.seqs]
-        seed = self.cfg.seed if ps[0].seed is None else ps[0].seed
-        toks, lps = self.runner.sample(logits, [p.temperature for p in ps],
+        else:
+            logits = self.runner.execute(inp)
+        self.stats["prefill_tokens"] += inp.num_prefill_rows
+        self.stats["decode_tokens"] += len(batch.decodes)
+        toks, lps = [], []
+        if sampled:
+            ps = [s.params for s in sampled]
+            seed = self.cfg.seed if ps[0].seed is None else ps[0].seed
+            if any(p.has_penalties for p in ps):
+                logits = apply_penalties(logits, sampled)
+            t, lp = self.runner.sample(logits, [p.temperature for p in ps],
                                        [p.top_p for p in ps], [p.top_k for p in ps], seed,
                                        self.step_count, want_logprobs=True)
-        toks = toks.tolist()
-        lps = lps.tolist() if lps is not None else [None] * len(toks)
+            toks = t.tolist()
+            lps = lp.tolist() if lp is not None else [None] * len(toks)
         self.runner.check_collectives()  # a timed-out TP reduction never returns its tokens
-        for s, t, lp in zip(batch.seqs, toks, lps):
+        for s, c in batch.prefills:
+            s.num_cached += c
+        for s in batch.decodes:
             s.num_cached = s.length
+        for s, t, lp in zip(sampled, toks, lps):
+            s.prefilled = True
             s.append(int(t), lp, self.eos_id)
         done = self.scheduler.finish(batch)
         self.stats["finished"] += len(done)
         self.stats["steps"] += 1
         self.step_count += 1
-        return list(batch.seqs)
+        return sampled
 
     def generate(self, prompts: Iterable[Union[str, List[int]]],
                  params: Optional[SamplingParams] = None) -> List[Sequence]:

@@ -1,11 +1,14 @@
-"""Serving model runner: paged-KV prefill / decode of Llama-family models on MI355X.
+"""Serving model runner: paged-KV mixed prefill / decode of Llama-family models on MI355X.
 
 Per layer (token-major activations, no autograd):
-    fused add+RMSNorm (HIP) -> q|k|v GEMM (hipBLASLt) -> in-place RoPE on q,k at each token's
-    position (HIP) -> K/V scattered into the paged cache by slot (HIP) -> attention
-    [prefill: PyTorch-ROCm fused SDPA per sequence (causal, GQA); decode: HIP paged-attention]
-    -> o GEMM (+ RCCL all-reduce under TP) -> fused add+RMSNorm -> gate|up GEMM -> SwiGLU (HIP)
+    fused add+RMSNorm (HIP) -> q|k|v GEMM (hipBLASLt) -> RoPE on q,k at each token's position +
+    K/V scattered into the paged cache by slot (one HIP kernel) -> attention
+    [prefill chunks: 32x32x16 flash forward over the paged cache, queries offset by the cached
+    context (whole prompts, chunks of long prompts); decode rows: HIP paged decode]
+    -> o GEMM (+ all-reduce under TP) -> fused add+RMSNorm -> gate|up GEMM -> SwiGLU (HIP)
     -> down GEMM (+ all-reduce) ; final norm on the sampled rows only -> LM head -> HIP sampler.
+A "mixed" step packs [prefill chunk tokens | decode tokens] into one forward (every GEMM sees
+all of them); a pure decode step replays a hipGraph.
 
 Tensor parallelism: Megatron-style column split of q|k|v and gate|up by
 heads / FFN columns, row split of o and down followed by an all-reduce over the TP group.
@@ -28,7 +31,7 @@ import torch.nn.functional as F
 from ..models.config import ModelConfig
 from ..ops._native import native, use_native
 from ..ops.activation import swiglu
-from ..ops.attention import flash_attention_qkv, paged_decode, rope_write_kv, write_kv_cache
+from ..ops.attention import flash_attention_paged, paged_decode, rope_write_kv
 from ..ops.gemm import linear_nt, swiglu_linear_nt
 from ..ops.norm import rms_norm
 from ..ops.rope import rope_tables
@@ -87,15 +90,23 @@ class ServeWeights:
 
 @dataclass
 class StepInput:
-    kind: str                          # prefill | decode
-    tokens: torch.Tensor               # [T] int64 (device)
+    kind: str                          # mixed | decode
+    tokens: torch.Tensor               # [T] int64 (device): prefill chunk rows, then decode rows
     positions: torch.Tensor            # [T] int32
     slots: torch.Tensor                # [T] int64
-    cu_seqlens: List[int]              # prefill: per-sequence token offsets (host)
-    block_tables: Optional[torch.Tensor] = None  # decode [N, maxb] int32
-    context_lens: Optional[torch.Tensor] = None  # decode [N] int32
+    cu_seqlens: List[int]              # prefill chunks: per-sequence row offsets (host), [0] if none
+    block_tables: Optional[torch.Tensor] = None  # decode rows [N, maxb] int32
+    context_lens: Optional[torch.Tensor] = None  # decode rows [N] int32
     max_context: int = 0
     lora_ids: Optional[torch.Tensor] = None      # [T] int32 adapter slot per token (multi-LoRA)
+    kv_lens: Optional[List[int]] = None          # prefill chunks: cached context + chunk (host)
+    kv_lens_t: Optional[torch.Tensor] = None     # ... on the device, int32 [P]
+    prefill_tables: Optional[torch.Tensor] = None  # prefill chunks [P, maxb] int32
+    sample_rows: Optional[torch.Tensor] = None   # rows whose logits are sampled, int64 [R]
+
+    @property
+    def num_prefill_rows(self) -> int:
+        return self.cu_seqlens[-1] if self.cu_seqlens else 0
 
 
 def kv_bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2, tp_size: int = 1) -> int:
@@ -218,42 +229,36 @@ class ModelRunner:
         y, _ = rms_norm(h[rows], self.w.norm, self.cfg.rms_norm_eps, res[rows])
         return self._vocab_gather(torch.matmul(y, self.w.lm_head.t()))
 
-    # ---- prefill: whole prompts, packed ----------------------------------------------------
+    # ---- mixed step: prefill chunks (whole prompts or pieces of long ones) + decode rows -----
     @torch.no_grad()
-    def prefill(self, inp: StepInput) -> torch.Tensor:
+    def execute(self, inp: StepInput) -> torch.Tensor:
+        """Logits [len(sample_rows), V] of one mixed step (see StepInput)."""
         h = F.embedding(inp.tokens, self.w.embed)
+        T = inp.tokens.shape[0]
+        Tp = inp.num_prefill_rows
+        N = T - Tp
         cu = inp.cu_seqlens
         nh, nkv, D = self.w.nh, self.w.nkv, self.cfg.head_dim
-        qs, ks = self.q_size, self.kv_size
 
         def attn(qkv, i):
-            if qkv.is_cuda and D == 128:
-                # packed varlen causal flash attention straight from the QKV buffer (HIP)
-                return flash_attention_qkv(qkv, cu, nh, nkv, D, True)
-            outs = []
-            for s in range(len(cu) - 1):
-                a, b = cu[s], cu[s + 1]
-                n = b - a
-                q = qkv[a:b, :qs].view(n, nh, D).transpose(0, 1)[None]
-                k = qkv[a:b, qs:qs + ks].view(n, nkv, D).transpose(0, 1)[None]
-                v = qkv[a:b, qs + ks:].view(n, nkv, D).transpose(0, 1)[None]
-                if nkv != nh:
-                    if q.is_cuda:
-                        o = F.scaled_dot_product_attention(q, k, v, is_causal=True,
-                                                           enable_gqa=True)
-                    else:
-                        rep = nh // nkv
-                        o = F.scaled_dot_product_attention(q, k.repeat_interleave(rep, 1),
-                                                           v.repeat_interleave(rep, 1),
-                                                           is_causal=True)
-                else:
-                    o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-                outs.append(o[0].transpose(0, 1).reshape(n, nh * D))
-            return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
+            o = torch.empty(T, nh * D, device=qkv.device, dtype=qkv.dtype)
+            if Tp:
+                # this chunk's K/V are already in the cache (rope_write_kv): read everything the
+                # chunk may see -- cached context + chunk -- from there
+                flash_attention_paged(qkv[:Tp], self.k_cache[i], self.v_cache[i], cu,
+                                      inp.kv_lens_t if qkv.is_cuda else inp.kv_lens,
+                                      inp.prefill_tables, nh, nkv, D, self.scale, out=o[:Tp])
+            if N:
+                q = qkv[Tp:, :self.q_size].reshape(N, nh, D)
+                o[Tp:] = paged_decode(q, self.k_cache[i], self.v_cache[i], inp.block_tables,
+                                      inp.context_lens, inp.max_context, self.scale,
+                                      self.decode_partition(N)).view(N, nh * D)
+            return o
 
         h, res = self._layers(h, inp.positions, inp.slots, attn, inp.lora_ids)
-        last = torch.tensor([c - 1 for c in cu[1:]], device=h.device)
-        return self._logits(h, res, last)
+        return self._logits(h, res, inp.sample_rows)
+
+    prefill = execute  # a whole-prompt step is a mixed step without decode rows
 
     # ---- decode: one token per sequence ----------------------------------------------------
     def _decode_eager(self, tokens, positions, slots, block_tables, context_lens, max_context,

@@ -1,17 +1,29 @@
-"""Continuous-batching scheduler (vLLM 0.6 semantics, re-designed).
+"""Continuous-batching scheduler with chunked prefill and mixed prefill + decode steps
+(the vLLM 0.6 engine the reference declares, README.md:10,16; re-designed).
 
-Every engine step is either a PREFILL step (admit waiting requests while the token budget and
-free KV blocks allow; their whole prompts run as one packed batch) or a DECODE step (one token
-for every running sequence).  Prefill has priority, as in vLLM's default policy, which keeps
-TTFT low under load; decode batches grow and shrink every step as requests join and finish.
-When a decode step cannot get a new KV block the youngest running sequence is preempted
-(blocks freed, sequence requeued at the front, recomputed on re-admission).
+Every engine step spends a TOKEN BUDGET (``max_num_batched_tokens``):
+
+1. every running sequence that is past its prompt decodes one token (always: a prefill never
+   stalls the running streams, which is what bounds inter-token latency under load);
+2. the rest of the budget goes to prefill CHUNKS, first to sequences whose prompt is already
+   partly in the cache, then to waiting requests in arrival order.  A prompt longer than what
+   is left is split: its first chunk runs now, the next chunks in later steps (its queries
+   attend to the cached earlier chunks through the paged-prefill kernel).
+
+The step is one forward over [prefill chunk tokens | decode tokens] (GEMMs see every token at
+once); a sequence gets a sampled token only when the chunk that completes its prompt runs.
+A step without prefill work is a pure decode step (hipGraph-captured in the runner).
+
+KV blocks for a whole prompt are reserved when the request is admitted, so a chunked prefill
+never runs out of blocks halfway; decodes grow their tables a block at a time, and when none is
+left the youngest running sequence is preempted (blocks freed, requeued at the front, its prompt
+plus the tokens generated so far recomputed on re-admission: vLLM's recompute preemption).
 """
 from __future__ import annotations
 
 from collections import deque
 from dataclasses import dataclass, field
-from typing import Deque, List, Optional
+from typing import Deque, List, Optional, Tuple
 
 from .block_manager import BlockManager
 from .sequence import Sequence, Status
@@ -20,20 +32,32 @@ from .sequence import Sequence, Status
 @dataclass
 class SchedulerConfig:
     max_num_seqs: int = 256
-    max_num_batched_tokens: int = 16384
+    max_num_batched_tokens: int = 2048
     max_model_len: int = 4096
 
 
 @dataclass
 class Batch:
-    kind: str                       # "prefill" | "decode"
-    seqs: List[Sequence] = field(default_factory=list)
+    kind: str                                                    # "mixed" | "decode"
+    prefills: List[Tuple[Sequence, int]] = field(default_factory=list)  # (seq, chunk length)
+    decodes: List[Sequence] = field(default_factory=list)
+
+    @property
+    def seqs(self) -> List[Sequence]:
+        return [s for s, _ in self.prefills] + self.decodes
 
     @property
     def num_tokens(self) -> int:
-        if self.kind == "decode":
-            return len(self.seqs)
-        return sum(s.length - s.num_cached for s in self.seqs)
+        return sum(c for _, c in self.prefills) + len(self.decodes)
+
+    def completing(self) -> List[Sequence]:
+        """Prefill sequences whose prompt this step finishes (they get a sampled token)."""
+        return [s for s, c in self.prefills if s.num_cached + c == s.length]
+
+    @property
+    def sampled(self) -> List[Sequence]:
+        """Rows of the step's logits, in order: completing prefills, then decodes."""
+        return self.completing() + self.decodes
 
 
 class Scheduler:
@@ -63,56 +87,61 @@ class Scheduler:
         return bool(self.waiting or self.running)
 
     def schedule(self) -> Optional[Batch]:
-        # 1) prefill: admit in FCFS order while budget / blocks / seq slots allow
-        if self.waiting:
-            batch = Batch("prefill")
-            budget = self.cfg.max_num_batched_tokens
-            while self.waiting and len(self.running) + len(batch.seqs) < self.cfg.max_num_seqs:
-                s = self.waiting[0]
-                n = s.length
-                if batch.seqs and n > budget:
-                    break
-                if not self.blocks.can_allocate(n + 1):
-                    break
-                self.waiting.popleft()
-                self.blocks.allocate(s.seq_id, n + 1)
-                s.num_cached = 0
-                s.status = Status.RUNNING
-                batch.seqs.append(s)
-                budget -= n
-            if batch.seqs:
-                self.running.extend(batch.seqs)
-                return batch
-        # 2) decode every running sequence (grow block tables; preempt on exhaustion)
-        if not self.running:
-            return None
-        ready: List[Sequence] = []
+        budget = self.cfg.max_num_batched_tokens
+        batch = Batch("mixed")
+        # 1) one token for every sequence past its prompt (grow block tables; preempt the
+        #    youngest running sequence when the cache is exhausted)
         preempted = set()
         for s in list(self.running):
-            if s.seq_id in preempted:
+            if s.seq_id in preempted or not s.prefilled:
                 continue
             while True:
                 try:
                     self.blocks.ensure(s.seq_id, s.length + 1)
-                    ready.append(s)
+                    batch.decodes.append(s)
                     break
                 except RuntimeError:
                     victim = self.running[-1]
                     self._preempt(victim)
                     preempted.add(victim.seq_id)
+                    if victim in batch.decodes:
+                        batch.decodes.remove(victim)
                     if victim is s:
                         break
-                    if victim in ready:
-                        ready.remove(victim)
-        if not ready:
+        budget -= len(batch.decodes)
+        # 2) continue partially cached prompts, then admit waiting requests (FCFS)
+        for s in self.running:
+            if budget <= 0:
+                break
+            if not s.prefilled and s.seq_id not in preempted:
+                c = min(s.length - s.num_cached, budget)
+                batch.prefills.append((s, c))
+                budget -= c
+        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
+            s = self.waiting[0]
+            if not self.blocks.can_allocate(s.length + 1):
+                break
+            self.waiting.popleft()
+            self.blocks.allocate(s.seq_id, s.length + 1)
+            s.num_cached = 0
+            s.prefilled = False
+            s.status = Status.RUNNING
+            self.running.append(s)
+            c = min(s.length, budget)
+            batch.prefills.append((s, c))
+            budget -= c
+        if not batch.prefills and not batch.decodes:
             return None
-        return Batch("decode", ready)
+        if not batch.prefills:
+            batch.kind = "decode"
+        return batch
 
     def _preempt(self, s: Sequence) -> None:
         self.running.remove(s)
         self.blocks.free_seq(s.seq_id)
         s.status = Status.WAITING
         s.num_cached = 0
+        s.prefilled = False
         s.preemptions += 1
         self.num_preemptions += 1
         # recompute: re-admission prefills prompt + tokens generated so far (outputs kept, so

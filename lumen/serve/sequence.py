@@ -18,10 +18,25 @@ class SamplingParams:
     ignore_eos: bool = False
     seed: Optional[int] = None
     logprobs: bool = False
+    # OpenAI penalties (logit -= frequency * count + presence * [count > 0], over the generated
+    # tokens) and vLLM's repetition penalty (prompt + generated tokens: positive logits divided,
+    # negative multiplied)
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    repetition_penalty: float = 1.0
+
+    @property
+    def has_penalties(self) -> bool:
+        return (self.presence_penalty != 0.0 or self.frequency_penalty != 0.0
+                or self.repetition_penalty != 1.0)
 
     def __post_init__(self):
         if self.max_tokens < 1:
             raise ValueError("max_tokens must be >= 1")
+        if not -2.0 <= self.presence_penalty <= 2.0 or not -2.0 <= self.frequency_penalty <= 2.0:
+            raise ValueError("presence_penalty / frequency_penalty must be in [-2, 2]")
+        if self.repetition_penalty <= 0:
+            raise ValueError("repetition_penalty must be > 0")
         if self.temperature < 0:
             raise ValueError("temperature must be >= 0")
         if not 0.0 < self.top_p <= 1.0:
@@ -52,6 +67,7 @@ class Sequence:
     last_token_time: Optional[float] = None
     token_times: List[float] = field(default_factory=list)
     num_cached: int = 0          # tokens whose K/V are in the cache
+    prefilled: bool = False      # prompt (incl. recomputed outputs) fully in the cache
     preemptions: int = 0
     lora_slot: int = 0           # multi-LoRA serving: adapter slot (0 = base model)
 

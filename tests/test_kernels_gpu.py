@@ -671,3 +671,35 @@ def test_rope_write_kv_fused(nh, nkv):
                    slots)
     assert torch.equal(q1, q2)
     assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+
+
+@pytest.mark.parametrize("nh,nkv", [(32, 32), (16, 4)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_flash_attention_paged_prefill(nh, nkv, dtype):
+    """Chunked / mixed prefill: queries of each chunk attend (causally, offset by the cached
+    context) over K/V read from the paged cache through a shuffled block table."""
+    from lumen.ops.attention import flash_attention_paged, flash_attention_paged_ref
+
+    torch.manual_seed(0)
+    D, bs = 128, 16
+    # (cached context, chunk length): whole prompts, chunks after long contexts, 1-row chunks
+    shapes = [(0, 512), (37, 100), (600, 200), (128, 1), (0, 7), (1000, 129)]
+    nblocks = sum((c + n + bs - 1) // bs for c, n in shapes) + 8
+    perm = torch.randperm(nblocks).tolist()
+    kc = (torch.randn(nblocks, nkv, bs, D, device=DEV) * 0.5).to(dtype)
+    vc = torch.randn(nblocks, nkv, bs, D, device=DEV).to(dtype)
+    maxb = max((c + n + bs - 1) // bs for c, n in shapes)
+    bt = torch.zeros(len(shapes), maxb, dtype=torch.int32, device=DEV)
+    cu, kl, used = [0], [], 0
+    for i, (c, n) in enumerate(shapes):
+        nb = (c + n + bs - 1) // bs
+        bt[i, :nb] = torch.tensor(perm[used:used + nb], dtype=torch.int32)
+        used += nb
+        cu.append(cu[-1] + n)
+        kl.append(c + n)
+    T = cu[-1]
+    q = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(dtype)  # fused qkv rows
+    got = flash_attention_paged(q, kc, vc, cu, kl, bt, nh, nkv, D)
+    ref = flash_attention_paged_ref(q.float(), kc.float(), vc.float(), cu, kl, bt, nh, nkv, D)
+    assert torch.isfinite(got.float()).all()
+    assert rel(got, ref) < 1e-2
