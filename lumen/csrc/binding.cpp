@@ -38,6 +38,17 @@ hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long
                        float, long long, long long, int, const long long*, const long long*,
                        const long long*, const int*, const float*, const float*, const int*, int,
                        hipStream_t);
+hipError_t lumen_lora3_down(int, const void*, long long, const float*, long long, float*, long long,
+                            int, int, int, float, unsigned long long, unsigned int, float, long long,
+                            long long, hipStream_t);
+hipError_t lumen_lora3_up(int, int, void*, long long, const float*, long long, const float*,
+                          long long, int, int, float, unsigned long long, unsigned int, float,
+                          long long, long long, int, const long long*, const long long*,
+                          const long long*, const int*, const float*, const float*, const int*,
+                          int, hipStream_t);
+hipError_t lumen_lora3_dy(int, const void*, long long, const float*, int, const float*, long long,
+                          float*, long long, float*, int, int, float, int, const long long*,
+                          const long long*, const long long*, const int*, hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, const float*, void*,
                             void*, const long long*, int, int, int, int, int, hipStream_t);
@@ -326,6 +337,82 @@ void lora2(int64_t dtype, int64_t kind, int64_t flag, const at::Tensor& big, int
         "lora2");
 }
 
+void need_cuda_f32(const at::Tensor& t, const char* what) {
+  if (!t.is_cuda() || t.scalar_type() != at::kFloat)
+    throw std::invalid_argument(std::string("lumen: ") + what + " must be an f32 GPU tensor");
+}
+
+// Z[t, :R] += alpha * drop(x) A^T   (x [T, K] 16-bit, row stride ldx; A [R, K] f32; Z f32)
+void lora3_down(const at::Tensor& x, int64_t ldx, const at::Tensor& A, at::Tensor& Z, int64_t ldz,
+                int64_t T, int64_t K, int64_t R, double alpha, int64_t seed, int64_t thresh,
+                double drop_scale, int64_t drop_ld, int64_t drop_col0) {
+  if (!x.is_cuda()) throw std::invalid_argument("lumen: lora3_down needs GPU tensors");
+  need_cuda_f32(A, "lora3_down A");
+  need_cuda_f32(Z, "lora3_down Z");
+  if (A.stride(1) != 1 || A.size(0) < R || A.size(1) < K || x.size(0) < T || Z.size(0) < T)
+    throw std::invalid_argument("lumen: lora3_down shape mismatch");
+  check(lumen_lora3_down(dcode(x), x.data_ptr(), ldx, A.data_ptr<float>(), A.stride(0),
+                         Z.data_ptr<float>(), ldz, static_cast<int>(T), static_cast<int>(K),
+                         static_cast<int>(R), static_cast<float>(alpha),
+                         static_cast<unsigned long long>(seed), static_cast<unsigned int>(thresh),
+                         static_cast<float>(drop_scale), drop_ld, drop_col0, cur_stream()),
+        "lora3_down");
+}
+
+// segs: (out_off, s1_off, s2_off, ncols)
+void lora3_up(int64_t fwd, at::Tensor& out, int64_t ldo, const at::Tensor& s1, int64_t ld1,
+              const at::Tensor& s2, int64_t ld2, int64_t T, int64_t J, double alpha, int64_t seed,
+              int64_t thresh, double drop_scale, int64_t drop_ld, int64_t drop_col0,
+              const std::vector<std::vector<int64_t>>& segs, const c10::optional<at::Tensor>& rope_cos,
+              const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& rope_pos,
+              int64_t rope_mask) {
+  if (!out.is_cuda()) throw std::invalid_argument("lumen: lora3_up needs GPU tensors");
+  need_cuda_f32(s1, "lora3_up s1");
+  need_cuda_f32(s2, "lora3_up s2");
+  const int nseg = static_cast<int>(segs.size());
+  if (nseg < 1 || nseg > 4) throw std::invalid_argument("lumen: lora3_up needs 1..4 segments");
+  long long oo[4] = {0}, so1[4] = {0}, so2[4] = {0};
+  int nc[4] = {0};
+  for (int i = 0; i < nseg; ++i) {
+    if (segs[i].size() != 4) throw std::invalid_argument("lumen: lora3_up segment = (out_off, s1_off, s2_off, ncols)");
+    oo[i] = segs[i][0]; so1[i] = segs[i][1]; so2[i] = segs[i][2]; nc[i] = static_cast<int>(segs[i][3]);
+  }
+  check(lumen_lora3_up(dcode(out), static_cast<int>(fwd), out.data_ptr(), ldo, s1.data_ptr<float>(),
+                       ld1, s2.data_ptr<float>(), ld2, static_cast<int>(T), static_cast<int>(J),
+                       static_cast<float>(alpha), static_cast<unsigned long long>(seed),
+                       static_cast<unsigned int>(thresh), static_cast<float>(drop_scale), drop_ld,
+                       drop_col0, nseg, oo, so1, so2, nc,
+                       rope_cos ? rope_cos->data_ptr<float>() : nullptr,
+                       rope_sin ? rope_sin->data_ptr<float>() : nullptr,
+                       rope_pos ? rope_pos->data_ptr<int>() : nullptr, static_cast<int>(rope_mask),
+                       cur_stream()),
+        "lora3_up");
+}
+
+// segs: (n_off, r_off, b_off, n_len)
+void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r, const at::Tensor& Z,
+              int64_t ldz, at::Tensor& dZ, int64_t lddz, at::Tensor& dB, int64_t T, int64_t tw,
+              double alpha, const std::vector<std::vector<int64_t>>& segs) {
+  if (!dy.is_cuda()) throw std::invalid_argument("lumen: lora3_dy needs GPU tensors");
+  need_cuda_f32(B, "lora3_dy B");
+  need_cuda_f32(Z, "lora3_dy Z");
+  need_cuda_f32(dZ, "lora3_dy dZ");
+  need_cuda_f32(dB, "lora3_dy dB");
+  const int nseg = static_cast<int>(segs.size());
+  if (nseg < 1 || nseg > 4) throw std::invalid_argument("lumen: lora3_dy needs 1..4 segments");
+  long long no[4] = {0}, ro[4] = {0}, bo[4] = {0};
+  int nl[4] = {0};
+  for (int i = 0; i < nseg; ++i) {
+    if (segs[i].size() != 4) throw std::invalid_argument("lumen: lora3_dy segment = (n_off, r_off, b_off, n_len)");
+    no[i] = segs[i][0]; ro[i] = segs[i][1]; bo[i] = segs[i][2]; nl[i] = static_cast<int>(segs[i][3]);
+  }
+  check(lumen_lora3_dy(dcode(dy), dy.data_ptr(), ldy, B.data_ptr<float>(), static_cast<int>(r),
+                       Z.data_ptr<float>(), ldz, dZ.data_ptr<float>(), lddz, dB.data_ptr<float>(),
+                       static_cast<int>(T), static_cast<int>(tw), static_cast<float>(alpha), nseg,
+                       no, ro, bo, nl, cur_stream()),
+        "lora3_dy");
+}
+
 void transpose2d(const at::Tensor& in, at::Tensor& out) {
   if (!in.is_cuda() || !out.is_cuda() || in.dim() != 2 || out.dim() != 2)
     throw std::invalid_argument("lumen: transpose2d needs 2-D GPU tensors");
@@ -577,6 +664,9 @@ void car_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>&
 PYBIND11_MODULE(_C, m) {
   m.doc() = "lumen native ops for MI355X (gfx950)";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("lora3_down", &lora3_down);
+  m.def("lora3_up", &lora3_up);
+  m.def("lora3_dy", &lora3_dy);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("qkv_rope", &qkv_rope);
   m.def("rope_inplace", &rope_inplace);

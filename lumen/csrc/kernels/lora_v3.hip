@@ -1,0 +1,627 @@
+// LoRA adapter passes, third generation (gfx950, v_mfma_f32_16x16x32 on bf16/fp16).
+//
+// Reference behaviour: PEFT LoraLayer under fp16 autocast (training/train_baseline.py:131-141,
+// r=16, alpha=32, dropout 0.05 on q/k/v/o).  The adapter products are memory-bound streams over
+// the [T, K] activation and the [T, N] output / output-gradient; lora_v2.hip ran them at ~50% of
+// HBM speed (profiles/r03_lora).  This file restructures them around bytes in flight and the
+// number of passes instead of around LDS images:
+//
+//   down3  Z  = drop(x) A^T           one shot per wave: 64 rows x 128 k loaded straight into the
+//                                     MFMA A-operand registers (no LDS image), the 8 waves of a
+//                                     block cover 1024 k and meet in an LDS tile (ds_add_f32);
+//                                     one global f32 atomic per (row, j) per 1024 k.
+//   up3    y  += s Z B^T  (+RoPE)     swapped-operand MFMA whose row map puts 32 consecutive output
+//          dx += drop(dZ A)           columns of one row in each lane: the read-modify-write of the
+//                                     output is lane-local 16-byte vectors (no f32 LDS scratch) and
+//                                     the rotate_half partner (column ^ 64) is in the same lane.
+//   dy3    dZ = s dY B,  dB = s dY^T Z   ONE pass over dY for both backward products (v2 read dY
+//                                     twice): the staged [64 x 128] dY tile feeds the dZ MFMAs with
+//                                     row reads and the dB MFMAs with ds_read_b64_tr_b16 reads.
+//
+// Dropout is the same counter hash as lora_v2 (common.h dropout_keep8), so masks regenerate
+// bit-identically across kernels and against lumen.ops.lora.dropout_mask_ref.
+#include "tile128.h"
+
+namespace lumen {
+namespace lv3 {
+
+using namespace tile;
+
+struct Drop {
+  unsigned int seed, thresh;
+  float scale;      // 1 / (1 - p)
+  long long ld;     // logical row length of the dropout index (t * ld + col0 + col)
+  long long col0;
+};
+
+__device__ __forceinline__ uint4 mask8(uint4 u, uint32_t keep) {
+  const auto wm = [keep](int w) {
+    return ((keep >> (2 * w)) & 1u ? 0x0000FFFFu : 0u) | ((keep >> (2 * w + 1)) & 1u ? 0xFFFF0000u : 0u);
+  };
+  return make_uint4(u.x & wm(0), u.y & wm(1), u.z & wm(2), u.w & wm(3));
+}
+
+// 8 consecutive f32 -> packed 16-bit MFMA operand (zeros when !ok)
+template <typename T>
+__device__ __forceinline__ uint4 ld_f32x8(const float* p, bool ok) {
+  if (!ok) return make_uint4(0, 0, 0, 0);
+  const float4 u = *reinterpret_cast<const float4*>(p);
+  const float4 v = *reinterpret_cast<const float4*>(p + 4);
+  return make_uint4(pk2<T>(u.x, u.y), pk2<T>(u.z, u.w), pk2<T>(v.x, v.y), pk2<T>(v.z, v.w));
+}
+
+// ------------------------------------------------------------------------------------------
+// down3:  Z[t, j] += alpha * sum_k drop(x)[t, k] * A[j, k]      j < R = 16 * NJ
+// grid (ceil(T / 64), ceil(K / 1024)), block 512 (8 waves x 128 k)
+// ------------------------------------------------------------------------------------------
+struct DownArgs {
+  const void* x; long long ldx;
+  const float* A; long long lda;
+  float* Z; long long ldz;
+  int T, K;
+  float alpha;
+  Drop drop;
+  int probe;   // cost probes (0 in production): 1 no dropout hash, 2 no A loads, 4 no reduction,
+               // 8 no global atomics
+};
+
+template <typename T, bool DROP, int NJ>
+__global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
+  constexpr int J = NJ * 16, JP = J + 4;   // padded LDS row: the 4 g-rows of a store hit
+  __shared__ float red[4][64 * JP];        // distinct bank groups
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, L = lane & 15, g = lane >> 4;
+  const int t0 = blockIdx.x * 64;
+  const int k0 = (blockIdx.y * 8 + wid) * 128;
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int jt = 0; jt < NJ; ++jt) acc[rt][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (k0 < a.K) {
+    const T* x = reinterpret_cast<const T*>(a.x);
+    uint4 xv[4][4];
+    // every load of the wave's 64 x 128 tile is in flight before the first MFMA
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = t0 + rt * 16 + L, c = k0 + 32 * i + 8 * g;
+        xv[rt][i] = (t < a.T && c < a.K)
+                        ? *reinterpret_cast<const uint4*>(x + (long long)t * a.ldx + c)
+                        : make_uint4(0, 0, 0, 0);
+      }
+    if (DROP && !(a.probe & 1)) {
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const long long t = t0 + rt * 16 + L;
+          const int c = k0 + 32 * i + 8 * g;
+          xv[rt][i] = mask8(xv[rt][i], dropout_keep8(a.drop.seed,
+                                                     (unsigned long long)(t * a.drop.ld + a.drop.col0 + c),
+                                                     a.drop.thresh));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = k0 + 32 * i + 8 * g;
+      uint4 bop[NJ];
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt)
+        bop[jt] = (a.probe & 2) ? xv[jt & 3][i] : ld_f32x8<T>(a.A + (long long)(jt * 16 + L) * a.lda + c, c < a.K);
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int jt = 0; jt < NJ; ++jt) acc[rt][jt] = Mfma<T>::run(xv[rt][i], bop[jt], acc[rt][jt]);
+    }
+  }
+  if (a.probe & 4) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt) sacc += acc[rt][jt][0] + acc[rt][jt][3];
+    if (sacc == 1234.5f) a.Z[threadIdx.x] = sacc;
+    return;
+  }
+  // two-phase LDS reduction of the 8 waves' [64 x J] partials with plain stores / loads:
+  // waves 4..7 park theirs in slots 0..3, waves 0..3 add their own in place, then every thread
+  // sums the 4 slots of its output elements.  Accumulator lane (L, g), element r = row
+  // 16 rt + 4 g + r, column 16 jt + L.
+  float* slot = red[wid & 3];
+  if (wid >= 4) {
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slot[(rt * 16 + g * 4 + r) * JP + jt * 16 + L] = acc[rt][jt][r];
+  }
+  __syncthreads();
+  if (wid < 4) {
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slot[(rt * 16 + g * 4 + r) * JP + jt * 16 + L] += acc[rt][jt][r];
+  }
+  __syncthreads();
+  const float alpha = DROP ? a.alpha * a.drop.scale : a.alpha;
+  for (int i = threadIdx.x; i < 64 * J; i += 512) {
+    const int row = i / J, j = i % J, t = t0 + row;
+    const int o = row * JP + j;
+    const float v = alpha * (red[0][o] + red[1][o] + red[2][o] + red[3][o]);
+    if (t < a.T) {
+      if (a.probe & 8) { if (v == 1234.5f) a.Z[i] = v; }
+      else atomicAdd(a.Z + (long long)t * a.ldz + j, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// up3:  out[t, c] += alpha * sum_j S1[t, j] * S2(c, j)   (16-bit read-modify-write)
+//   FWD (mode 6):  y  += s Z_seg B_seg^T   S2(c, j) = B[c][j];   optional RoPE on the result
+//   !FWD (mode 5): dx += drop'(dZ A)       S2(c, j) = A[j][c];   dropout mask on the delta
+// Block: 128 output columns of one segment x 4 waves x RT row tiles of 16.
+// Swapped MFMA: A-operand = S2 rows (output columns via cmap), B-operand = S1^T (k = j), so the
+// accumulator of n-tile n holds out^T[m = 4g + r][t = L] and column cmap(n, 4g + r) =
+// 32 (n >> 1) + 8 g + 4 (n & 1) + r: lane (L, g) owns columns 32 i + 8 g + [0, 8) of row t0 + L
+// for i = 0..3 -- four 16-byte vectors, each wave instruction covering 64 contiguous bytes of 16
+// rows; RoPE's rotate_half partner (column ^ 64) is i ^ 2 in the same lane.
+// ------------------------------------------------------------------------------------------
+struct UpSeg {
+  long long out_off[4];  // first output column of the segment
+  long long s1_off[4];   // first S1 column
+  long long s2_off[4];   // FWD: first B row; !FWD: first A column
+  int ncols[4];
+  int nseg;
+};
+
+struct UpArgs {
+  void* out; long long ldo;
+  const float* s1; long long ld1;
+  const float* s2; long long ld2;
+  int T, J;
+  float alpha;
+  Drop drop;
+  UpSeg seg;
+  const float* rope_cos; const float* rope_sin; const int* rope_pos;
+  int rope_mask;
+};
+
+constexpr int kUpRT = 4;
+
+__device__ __forceinline__ int up_cmap(int n, int L) {
+  return 32 * (n >> 1) + 8 * (L >> 2) + 4 * (n & 1) + (L & 3);
+}
+
+template <typename T, bool FWD, bool DROP, int KJ>
+__global__ void __launch_bounds__(256) up3_kernel(UpArgs a) {
+  constexpr int NKS = KJ / 32, SP = KJ + 8;   // k-steps; LDS row stride (16-bit elements)
+  __shared__ __attribute__((aligned(16))) T s2[128 * SP];
+  const int seg = blockIdx.z;
+  const int NC = a.seg.ncols[seg];
+  const int c0 = blockIdx.x * 128;
+  if (c0 >= NC) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, L = lane & 15, g = lane >> 4;
+  const int J = a.J;
+  // stage S2(c, j) for c in [c0, c0 + 128), j < KJ as 16-bit [c][j] (zeros beyond J / NC)
+  if (FWD) {
+    const float* B = a.s2 + a.seg.s2_off[seg] * a.ld2;
+    for (int idx = threadIdx.x; idx < 128 * (KJ / 4); idx += 256) {
+      const int c = idx / (KJ / 4), j = (idx % (KJ / 4)) * 4;
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c0 + c < NC && j < J) f = *reinterpret_cast<const float4*>(B + (long long)(c0 + c) * a.ld2 + j);
+      *reinterpret_cast<uint2*>(s2 + c * SP + j) = pack4<T>(f.x, f.y, f.z, f.w);
+    }
+  } else {
+    const float* A = a.s2 + a.seg.s2_off[seg];
+    for (int idx = threadIdx.x; idx < 32 * KJ; idx += 256) {
+      const int j = idx / 32, c = (idx % 32) * 4;
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (j < J && c0 + c < NC) f = *reinterpret_cast<const float4*>(A + (long long)j * a.ld2 + c0 + c);
+      s2[(c + 0) * SP + j] = from_f32<T>(f.x);
+      s2[(c + 1) * SP + j] = from_f32<T>(f.y);
+      s2[(c + 2) * SP + j] = from_f32<T>(f.z);
+      s2[(c + 3) * SP + j] = from_f32<T>(f.w);
+    }
+  }
+  __syncthreads();
+  uint4 aop[8][NKS];
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      aop[n][ks] = *reinterpret_cast<const uint4*>(s2 + up_cmap(n, L) * SP + ks * 32 + g * 8);
+
+  T* out = reinterpret_cast<T*>(a.out) + a.seg.out_off[seg];
+  const float* s1 = a.s1 + a.seg.s1_off[seg];
+  const bool rope = FWD && ((a.rope_mask >> seg) & 1);
+  const int tw0 = (blockIdx.y * 4 + wid) * kUpRT * 16;
+
+  // double-buffered per-row-tile operands: S1 row (B-operand), 4 output vectors
+  uint4 bcur[NKS], bnxt[NKS], ycur[4], ynxt[4];
+  const auto load_tile = [&](int t0, uint4 (&bop)[NKS], uint4 (&yv)[4]) {
+    const int t = t0 + L;
+    const bool tok = t < a.T;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int j = ks * 32 + g * 8;
+      bop[ks] = ld_f32x8<T>(s1 + (long long)t * a.ld1 + j, tok && j < J);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + 32 * i + 8 * g;
+      yv[i] = (tok && c < NC) ? *reinterpret_cast<const uint4*>(out + (long long)t * a.ldo + c)
+                              : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (tw0 >= a.T) return;
+  load_tile(tw0, bcur, ycur);
+#pragma unroll
+  for (int rt = 0; rt < kUpRT; ++rt) {
+    const int t0 = tw0 + rt * 16;
+    if (t0 >= a.T) break;
+    if (rt + 1 < kUpRT && t0 + 16 < a.T) load_tile(t0 + 16, bnxt, ynxt);
+    f32x4 acc[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int n = 0; n < 8; ++n) acc[n] = Mfma<T>::run(aop[n][ks], bcur[ks], acc[n]);
+    const int t = t0 + L;
+    float y[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      unpack8<T>(ycur[i], y[i]);
+      const int c = c0 + 32 * i + 8 * g;
+      const uint32_t keep = DROP ? dropout_keep8(a.drop.seed,
+                                                 (unsigned long long)((long long)t * a.drop.ld + a.drop.col0 + a.seg.out_off[seg] + c),
+                                                 a.drop.thresh)
+                                 : 0xFFu;
+      const float sc = DROP ? a.alpha * a.drop.scale : a.alpha;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = acc[2 * i + (e >> 2)][e & 3];
+        y[i][e] += ((keep >> e) & 1u) ? sc * d : 0.f;
+      }
+    }
+    if (rope && t < a.T) {
+      // block-uniform: c0 is a head boundary, the block's 128 columns are one head
+      const long long p = (long long)a.rope_pos[t] * 64;
+      float cs[2][8], sn[2][8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float* cp = a.rope_cos + p + 32 * h + 8 * g;
+        const float* sp = a.rope_sin + p + 32 * h + 8 * g;
+        const float4 c_lo = *reinterpret_cast<const float4*>(cp), c_hi = *reinterpret_cast<const float4*>(cp + 4);
+        const float4 s_lo = *reinterpret_cast<const float4*>(sp), s_hi = *reinterpret_cast<const float4*>(sp + 4);
+        cs[h][0] = c_lo.x; cs[h][1] = c_lo.y; cs[h][2] = c_lo.z; cs[h][3] = c_lo.w;
+        cs[h][4] = c_hi.x; cs[h][5] = c_hi.y; cs[h][6] = c_hi.z; cs[h][7] = c_hi.w;
+        sn[h][0] = s_lo.x; sn[h][1] = s_lo.y; sn[h][2] = s_lo.z; sn[h][3] = s_lo.w;
+        sn[h][4] = s_hi.x; sn[h][5] = s_hi.y; sn[h][6] = s_hi.z; sn[h][7] = s_hi.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float lo = y[i][e], hi = y[i + 2][e];   // columns h and h + 64 of the head
+          y[i][e] = lo * cs[i][e] - hi * sn[i][e];
+          y[i + 2][e] = hi * cs[i][e] + lo * sn[i][e];
+        }
+    }
+    if (t < a.T) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 + 32 * i + 8 * g;
+        if (c < NC) store8(out + (long long)t * a.ldo + c, y[i]);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) bcur[ks] = bnxt[ks];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ycur[i] = ynxt[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// dy3: per segment (dY columns [n_off, n_off + n_len), adapter columns [r_off, r_off + r)):
+//   dZ[t, r_off + j] += alpha * sum_c dY[t, n_off + c] * B[b_off + c, j]
+//   dB[b_off + c, j] += alpha * sum_t dY[t, n_off + c] * Z[t, r_off + j]
+// Block (4 waves) = 256 columns (2 chunks of 128) x TW rows (64-row sub-tiles); the staged dY
+// sub-tile [64][128] is read row-wise for dZ (wave w: rows 16w..16w+15) and transposed for dB
+// (wave w: columns 32w..32w+31 of the chunk).  dZ partials are flushed per sub-tile, dB partials
+// stay in registers for the whole row range and are flushed once.
+// grid (ceil(maxlen / 256), ceil(T / TW), nseg)
+// ------------------------------------------------------------------------------------------
+struct DySeg {
+  long long n_off[4], r_off[4], b_off[4];
+  int n_len[4];
+  int nseg;
+};
+
+struct DyArgs {
+  const void* dy; long long ldy;
+  const float* B; int r;        // B [*, r]
+  const float* Z; long long ldz;
+  float* dZ; long long lddz;
+  float* dB;                    // [*, r]
+  int T, TW;
+  float alpha;
+  DySeg seg;
+};
+
+constexpr int kDyCC = 2;
+
+template <typename T>
+__device__ __forceinline__ void dy_load(uint4 (&v)[4], const T* base, long long ld, int r0, int rmax,
+                                        int c0, int cmax) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + i * 256;
+    const int r = r0 + (idx >> 4), c = c0 + (idx & 15) * 8;
+    v[i] = (r < rmax && c < cmax) ? *reinterpret_cast<const uint4*>(base + (long long)r * ld + c)
+                                  : make_uint4(0, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void dy_store(char* img, const uint4 (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + i * 256;
+    *reinterpret_cast<uint4*>(img + img_off(idx >> 4, idx & 15)) = v[i];
+  }
+}
+
+template <typename T, int NJ>
+__global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
+  __shared__ __attribute__((aligned(16))) char img[2][64 * 256];
+  const int seg = blockIdx.z;
+  const int NL = a.seg.n_len[seg];
+  const int cb = blockIdx.x * 128 * kDyCC;
+  const int tb = blockIdx.y * a.TW, te = min(a.T, tb + a.TW);
+  if (cb >= NL || tb >= a.T) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, L = lane & 15, g = lane >> 4;
+  const T* dy = reinterpret_cast<const T*>(a.dy) + a.seg.n_off[seg];
+  const float* B = a.B + a.seg.b_off[seg] * a.r;
+  const float* Z = a.Z + a.seg.r_off[seg];
+  float* dZ = a.dZ + a.seg.r_off[seg];
+  float* dB = a.dB + a.seg.b_off[seg] * a.r;
+  const int nch = min(kDyCC, (NL - cb + 127) / 128);
+
+  // dZ B-operand for every chunk: lane (L, g) <- B[cb + 128 cc + 32 i + 8 g + e][16 jt + L]
+  uint4 bop[kDyCC][4][NJ];
+#pragma unroll
+  for (int cc = 0; cc < kDyCC; ++cc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt) {
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = cb + cc * 128 + 32 * i + 8 * g + e;
+          f[e] = c < NL ? B[(long long)c * a.r + jt * 16 + L] : 0.f;
+        }
+        bop[cc][i][jt] = pack8<T>(f);
+      }
+  f32x4 dbacc[kDyCC][2][NJ];
+#pragma unroll
+  for (int cc = 0; cc < kDyCC; ++cc)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt) dbacc[cc][m][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsub = (te - tb + 63) / 64;
+  const int nstage = nsub * nch;
+  uint4 v[4];
+  dy_load<T>(v, dy, a.ldy, tb, te, cb, NL);
+  int buf = 0;
+  f32x4 dzacc[NJ];
+  uint4 zop[2][NJ];
+  for (int s = 0; s < nstage; ++s, buf ^= 1) {
+    const int ts = s / nch, cc = s % nch;
+    const int t0 = tb + ts * 64, cbase = cb + cc * 128;
+    dy_store(img[buf], v);
+    __syncthreads();
+    if (s + 1 < nstage) {
+      const int ts1 = (s + 1) / nch, cc1 = (s + 1) % nch;
+      dy_load<T>(v, dy, a.ldy, tb + ts1 * 64, te, cb + cc1 * 128, NL);
+    }
+    if (cc == 0) {
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt) dzacc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // dB B-operand: lane (L, g) <- Z[t0 + 32 ks + 8 g + e][16 jt + L]
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int jt = 0; jt < NJ; ++jt) {
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int t = t0 + 32 * ks + 8 * g + e;
+            f[e] = t < te ? Z[(long long)t * a.ldz + jt * 16 + L] : 0.f;
+          }
+          zop[ks][jt] = pack8<T>(f);
+        }
+    }
+    const char* im = img[buf];
+    // dZ: rows 16 wid + L, k = chunk columns
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 av = row_read(im, wid * 16 + L, i * 4 + g);
+#pragma unroll
+      for (int c2 = 0; c2 < kDyCC; ++c2)
+        if (c2 == cc) {
+#pragma unroll
+          for (int jt = 0; jt < NJ; ++jt) dzacc[jt] = Mfma<T>::run(av, bop[c2][i][jt], dzacc[jt]);
+        }
+    }
+    // dB: columns 32 wid + 16 m + (4 g + r), k = sub-tile rows
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const uint4 tv = tr_read_img(im, ks * 32, wid * 32 + m * 16, lane);
+#pragma unroll
+        for (int c2 = 0; c2 < kDyCC; ++c2)
+          if (c2 == cc) {
+#pragma unroll
+            for (int jt = 0; jt < NJ; ++jt) dbacc[c2][m][jt] = Mfma<T>::run(tv, zop[ks][jt], dbacc[c2][m][jt]);
+          }
+      }
+    if (cc == nch - 1) {
+      // flush this sub-tile's dZ rows: accumulator row 4 g + r, column 16 jt + L
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = t0 + wid * 16 + g * 4 + r;
+          if (t < te) atomicAdd(dZ + (long long)t * a.lddz + jt * 16 + L, a.alpha * dzacc[jt][r]);
+        }
+    }
+  }
+#pragma unroll
+  for (int cc = 0; cc < kDyCC; ++cc) {
+    if (cc >= nch) break;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb + cc * 128 + wid * 32 + m * 16 + g * 4 + r;
+          if (c < NL) atomicAdd(dB + (long long)c * a.r + jt * 16 + L, a.alpha * dbacc[cc][m][jt][r]);
+        }
+  }
+}
+
+}  // namespace lv3
+}  // namespace lumen
+
+using namespace lumen;
+
+#include <cstdlib>
+static int lv3_probe() {
+  static int v = [] { const char* e = std::getenv("LUMEN_LV3_PROBE"); return e ? std::atoi(e) : 0; }();
+  return v;
+}
+
+// Z[t, j] += alpha * sum_k drop(x)[t, k] A[j, k]; R = 16 * nj (nj 1..4); K, ldx multiples of 8
+extern "C" hipError_t lumen_lora3_down(int dtype, const void* x, long long ldx, const float* A,
+                                       long long lda, float* Z, long long ldz, int T, int K, int R,
+                                       float alpha, unsigned long long seed, unsigned int thresh,
+                                       float drop_scale, long long drop_ld, long long drop_col0,
+                                       hipStream_t st) {
+  if (T <= 0 || K <= 0 || R < 16 || R > 64 || (R & 15) || (K & 7) || (ldx & 7) || (lda & 3))
+    return hipErrorInvalidValue;
+  lv3::DownArgs a{x, ldx, A, lda, Z, ldz, T, K, alpha,
+                  {static_cast<unsigned>(seed) ^ static_cast<unsigned>(seed >> 32), thresh, drop_scale,
+                   drop_ld, drop_col0}, lv3_probe()};
+  const dim3 grid((T + 63) / 64, (K + 1023) / 1024), block(512);
+  const bool drop = thresh != 0;
+#define LV3_DOWN(TT, NJ)                                                                           \
+  do {                                                                                           \
+    if (drop) hipLaunchKernelGGL((lv3::down3_kernel<TT, true, NJ>), grid, block, 0, st, a);     \
+    else hipLaunchKernelGGL((lv3::down3_kernel<TT, false, NJ>), grid, block, 0, st, a);         \
+  } while (0)
+#define LV3_DOWN_NJ(TT)                                                                            \
+  switch (R / 16) {                                                                              \
+    case 1: LV3_DOWN(TT, 1); break;                                                              \
+    case 2: LV3_DOWN(TT, 2); break;                                                              \
+    case 3: LV3_DOWN(TT, 3); break;                                                              \
+    default: LV3_DOWN(TT, 4); break;                                                             \
+  }
+  if (dtype == kBF16) { LV3_DOWN_NJ(bf16) }
+  else if (dtype == kF16) { LV3_DOWN_NJ(fp16) }
+  else return hipErrorInvalidValue;
+#undef LV3_DOWN_NJ
+#undef LV3_DOWN
+  return hipGetLastError();
+}
+
+// fwd != 0: out[t, out_off + c] += alpha * sum_j s1[t, s1_off + j] * s2[s2_off + c][j]  (+RoPE)
+// fwd == 0: out[t, out_off + c] += drop(alpha * sum_j s1[t, s1_off + j] * s2[j][s2_off + c])
+// J <= 64; segment widths, out_off, ldo multiples of 8; RoPE segments start on 128-col heads
+extern "C" hipError_t lumen_lora3_up(int dtype, int fwd, void* out, long long ldo, const float* s1,
+                                     long long ld1, const float* s2, long long ld2, int T, int J,
+                                     float alpha, unsigned long long seed, unsigned int thresh,
+                                     float drop_scale, long long drop_ld, long long drop_col0,
+                                     int nseg, const long long* out_off, const long long* s1_off,
+                                     const long long* s2_off, const int* ncols,
+                                     const float* rope_cos, const float* rope_sin,
+                                     const int* rope_pos, int rope_mask, hipStream_t st) {
+  if (T <= 0 || J < 1 || J > 64 || nseg < 1 || nseg > 4 || (ldo & 7) || (ld1 & 3) || (ld2 & 3))
+    return hipErrorInvalidValue;
+  lv3::UpArgs a;
+  a.out = out; a.ldo = ldo; a.s1 = s1; a.ld1 = ld1; a.s2 = s2; a.ld2 = ld2; a.T = T; a.J = J;
+  a.alpha = alpha;
+  a.drop = {static_cast<unsigned>(seed) ^ static_cast<unsigned>(seed >> 32), thresh, drop_scale,
+            drop_ld, drop_col0};
+  a.seg.nseg = nseg;
+  int maxc = 0;
+  for (int i = 0; i < 4; ++i) {
+    const bool v = i < nseg;
+    a.seg.out_off[i] = v ? out_off[i] : 0; a.seg.s1_off[i] = v ? s1_off[i] : 0;
+    a.seg.s2_off[i] = v ? s2_off[i] : 0; a.seg.ncols[i] = v ? ncols[i] : 0;
+    if (v && ((ncols[i] & 7) || (out_off[i] & 7) || (s1_off[i] & 3))) return hipErrorInvalidValue;
+    if (v && ncols[i] > maxc) maxc = ncols[i];
+  }
+  a.rope_cos = rope_cos; a.rope_sin = rope_sin; a.rope_pos = rope_pos;
+  a.rope_mask = (fwd && rope_cos && rope_sin && rope_pos) ? rope_mask : 0;
+  for (int i = 0; i < nseg; ++i)
+    if (((a.rope_mask >> i) & 1) && ((out_off[i] & 127) || (ncols[i] & 127))) return hipErrorInvalidValue;
+  if (maxc == 0) return hipSuccess;
+  const dim3 grid((maxc + 127) / 128, (T + 64 * lv3::kUpRT - 1) / (64 * lv3::kUpRT), nseg), block(256);
+  const bool drop = !fwd && thresh != 0;
+#define LV3_UP(TT, KJ)                                                                             \
+  do {                                                                                           \
+    if (fwd) hipLaunchKernelGGL((lv3::up3_kernel<TT, true, false, KJ>), grid, block, 0, st, a);   \
+    else if (drop) hipLaunchKernelGGL((lv3::up3_kernel<TT, false, true, KJ>), grid, block, 0, st, a); \
+    else hipLaunchKernelGGL((lv3::up3_kernel<TT, false, false, KJ>), grid, block, 0, st, a);     \
+  } while (0)
+  if (dtype == kBF16) { if (J <= 32) LV3_UP(bf16, 32); else LV3_UP(bf16, 64); }
+  else if (dtype == kF16) { if (J <= 32) LV3_UP(fp16, 32); else LV3_UP(fp16, 64); }
+  else return hipErrorInvalidValue;
+#undef LV3_UP
+  return hipGetLastError();
+}
+
+// fused dZ / dB over one pass of dY (see dy3_kernel); r in {16, 32, 64}; tw multiple of 64
+extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, const float* B, int r,
+                                     const float* Z, long long ldz, float* dZ, long long lddz,
+                                     float* dB, int T, int tw, float alpha, int nseg,
+                                     const long long* n_off, const long long* r_off,
+                                     const long long* b_off, const int* n_len, hipStream_t st) {
+  if (T <= 0 || nseg < 1 || nseg > 4 || (r != 16 && r != 32 && r != 64) || tw < 64 || (tw & 63) ||
+      (ldy & 7))
+    return hipErrorInvalidValue;
+  lv3::DyArgs a;
+  a.dy = dy; a.ldy = ldy; a.B = B; a.r = r; a.Z = Z; a.ldz = ldz; a.dZ = dZ; a.lddz = lddz;
+  a.dB = dB; a.T = T; a.TW = tw; a.alpha = alpha;
+  a.seg.nseg = nseg;
+  int maxl = 0;
+  for (int i = 0; i < 4; ++i) {
+    const bool v = i < nseg;
+    a.seg.n_off[i] = v ? n_off[i] : 0; a.seg.r_off[i] = v ? r_off[i] : 0;
+    a.seg.b_off[i] = v ? b_off[i] : 0; a.seg.n_len[i] = v ? n_len[i] : 0;
+    if (v && ((n_len[i] & 7) || (n_off[i] & 7))) return hipErrorInvalidValue;
+    if (v && n_len[i] > maxl) maxl = n_len[i];
+  }
+  if (maxl == 0) return hipSuccess;
+  const dim3 grid((maxl + 128 * lv3::kDyCC - 1) / (128 * lv3::kDyCC), (T + tw - 1) / tw, nseg), block(256);
+#define LV3_DY(TT)                                                                                 \
+  switch (r) {                                                                                   \
+    case 16: hipLaunchKernelGGL((lv3::dy3_kernel<TT, 1>), grid, block, 0, st, a); break;          \
+    case 32: hipLaunchKernelGGL((lv3::dy3_kernel<TT, 2>), grid, block, 0, st, a); break;          \
+    default: hipLaunchKernelGGL((lv3::dy3_kernel<TT, 4>), grid, block, 0, st, a); break;          \
+  }
+  if (dtype == kBF16) { LV3_DY(bf16) }
+  else if (dtype == kF16) { LV3_DY(fp16) }
+  else return hipErrorInvalidValue;
+#undef LV3_DY
+  return hipGetLastError();
+}

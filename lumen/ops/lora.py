@@ -175,6 +175,53 @@ def _zeros(*shape, device, train: bool = False):
     return torch.zeros(*shape, device=device, dtype=torch.float32)
 
 
+USE_V3 = _os.environ.get("LUMEN_LORA_V3", "1") != "0"
+DY_TW = int(_os.environ.get("LUMEN_LORA_DY_TW", "0"))  # dY rows per block of lora3_dy (0 = auto)
+# per-call A/B (scripts/probes/lora_kernels.py, us): the v3 UP write-back is on par with v2
+# without RoPE (o_proj 15.0 vs 14.3) and slower with it (q|k|v 55.7 vs 45.6), so v2 stays the
+# forward UP; v3's DOWN (17.3 vs 21.9), fused dY pass (32.5 vs 53.3) and dx update win
+UP_V3 = _os.environ.get("LUMEN_LORA_UP_V3", "0") == "1"
+
+
+def _v3_ok(r: int, R: int, segs, *mats) -> bool:
+    """kernels/lora_v3.hip: ranks 16/32/64, up to 64 stacked adapter rows, 8-element aligned
+    rows and segments, contiguous f32 adapter weights (checked by the caller)."""
+    return (USE_V3 and r in (16, 32, 64) and R % 16 == 0 and R <= 64
+            and all(s[0] % 8 == 0 and s[1] % 8 == 0 for s in segs)
+            and all(m.stride(1) == 1 and m.stride(0) % 8 == 0 for m in mats))
+
+
+def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope):
+    T, K = x2d.shape
+    R = A.shape[0]
+    nat = native()
+    nat.lora3_down(x2d, x2d.stride(0), A, Z, R, T, K, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
+                   drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0)
+    fuse = rope is not None and len(segs) <= 4 and _rope_covered(segs, rope[3])
+    for i in range(0, len(segs), 4):
+        ch = segs[i:i + 4]
+        mask = sum(1 << j for j, sg in enumerate(ch) if sg[0] + sg[1] <= rope[3]) if fuse else 0
+        if UP_V3:
+            rp = (rope[1], rope[2], rope[0]) if fuse else (None, None, None)
+            nat.lora3_up(1, y, y.stride(0), Z, R, B, r, T, r, scale, 0, 0, 1.0, 0, 0,
+                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
+                         *rp, mask)
+        else:  # v2 UP: its write-back issues the RoPE table loads with the output loads
+            _lora2(2, 1, B, Z, y, y.stride(0), 1, scale, T, r, 1,
+                   [(b_off * r, r_off, n_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
+                   rope=(rope[1], rope[2], rope[0], mask) if fuse else None)
+    return fuse
+
+
+def _dy_tw(segs, T: int) -> int:
+    """dY rows per block of lora3_dy: 256 unless that leaves fewer than 512 blocks (dZ / dB
+    atomics grow as the tile shrinks: 128 only for narrow outputs such as o_proj)."""
+    if DY_TW:
+        return DY_TW
+    cols = sum(math.ceil(s[1] / 256) for s in segs)
+    return 256 if cols * math.ceil(T / 256) >= 512 else 128
+
+
 def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train: bool = False,
                     rope=None):
     """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place).
@@ -187,6 +234,9 @@ def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train:
     Ntot = y.shape[1]
     act = DTYPE_CODE[x2d.dtype]
     Z = _zeros(T, R, device=x2d.device, train=train)
+    if (_v3_ok(r, R, segs, x2d, y) and K % 8 == 0 and A.is_contiguous() and B.is_contiguous()
+            and A.dtype == B.dtype == torch.float32):
+        return Z, _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope)
     if _v2_ok(r, R, x2d):
         _lora2(0, 1, x2d, A, Z, R, 1, 1.0, T, R, _split(math.ceil(T / 64), K, 256),
                [(0, 0, 0, K)], seed, p, K)
@@ -231,9 +281,14 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
     act = DTYPE_CODE[dy.dtype]
     dev = dy.device
     v2 = _v2_ok(r, R, x2d, dy)
+    v3 = (v2 and _v3_ok(r, R, segs, x2d, dy) and K % 8 == 0 and A.is_contiguous()
+          and B.is_contiguous() and A.dtype == B.dtype == torch.float32
+          and (dx is None or _v3_ok(r, R, segs, dx)))
     # dA / dB accumulate straight into the parameters' .grad (views of the engine's flat f32
     # gradient buffer) when they exist: no zero-filled temporaries and no autograd add kernels
     direct = v2 and DIRECT_GRAD and _direct_ok(A) and _direct_ok(B)
+    if v3:
+        return _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, direct)
     nA = R * K if need_dA and not direct else 0
     nB = B.shape[0] * r if need_dB and not direct else 0
     ws = _zeros(T * R + nA + nB, device=dev)
@@ -285,6 +340,40 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
                 cb(prm)
         return None, None
     return dA, dB
+
+
+def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, direct):
+    """v3 backward: ONE pass over dY for dZ and dB (lora3_dy), dA from the dropped-out input
+    (v2 WGRAD), dx += drop'(dZ A) lane-local (lora3_up mode 5)."""
+    T, K = x2d.shape
+    R = A.shape[0]
+    dev = dy.device
+    nat = native()
+    nA = R * K if need_dA and not direct else 0
+    nB = B.shape[0] * r if not direct or not need_dB else 0  # dB target even when unused
+    ws = _zeros(T * R + nA + nB, device=dev)
+    dZ = ws[:T * R].view(T, R)
+    dB = B.grad if (direct and need_dB) else ws[T * R + nA:].view(B.shape[0], r)
+    for i in range(0, len(segs), 4):
+        ch = segs[i:i + 4]
+        nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
+                     [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+    dA = None
+    if need_dA:
+        dA = A.grad if direct else ws[T * R:T * R + nA].view(R, K)
+        _lora2(1, 1, x2d, dZ, dA, 1, K, 1.0, T, R, _split(math.ceil(K / 128), T, 128),
+               [(0, 0, 0, K)], seed, p, K)
+    if dx is not None:
+        nat.lora3_up(0, dx, dx.stride(0), dZ, R, A, K, T, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
+                     drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, [(0, 0, 0, K)],
+                     None, None, None, 0)
+    if direct:
+        for prm, need in ((A, need_dA), (B, need_dB)):
+            cb = getattr(prm, "_lumen_grad_ready", None)
+            if need and cb is not None:
+                cb(prm)
+        return None, None
+    return dA, (dB if need_dB else None)
 
 
 DIRECT_GRAD = _os.environ.get("LUMEN_LORA_DIRECT_GRAD", "1") != "0"

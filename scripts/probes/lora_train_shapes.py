@@ -29,7 +29,7 @@ dev = torch.device("cuda")
 T, K, r, D = 4096, 4096, 16, 128
 cos, sin = rope_tables(D, 4096, 10000.0, dev)
 pos = (torch.arange(T, device=dev) % 512).to(torch.int32)
-out = {"up_rt": os.environ.get("LUMEN_LORA_UP_RT", "default")}
+out = {"v3": L.USE_V3, "dy_tw": L.DY_TW}
 for name, segs, rope_cols in (("qkv", [(0, 4096, 0, 0), (4096, 4096, 16, 1), (8192, 4096, 32, 2)], 8192),
                               ("o", [(0, 4096, 0, 0)], 0)):
     N = segs[-1][0] + segs[-1][1]
