@@ -57,6 +57,14 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     # lumen extensions
     ap.add_argument("--synthetic", action="store_true", help="random-token dataset (offline)")
     ap.add_argument("--synthetic_samples", type=int, default=1024)
+    ap.add_argument("--synthetic_min_len", type=int, default=None,
+                    help="variable-length synthetic rows: lengths uniform in [min, max_length]")
+    ap.add_argument("--no_packing", action="store_true",
+                    help="pad to the longest row (reference collation) instead of packing")
+    ap.add_argument("--prefetch", type=int, default=2, help="batches collated ahead (0 = inline)")
+    ap.add_argument("--pack_tokens", type=int, default=0,
+                    help="token-budget batching: pack whole sequences up to N tokens per "
+                         "micro-step (packing only; the micro-batch size is then variable)")
     ap.add_argument("--max_steps", type=int, default=-1)
     ap.add_argument("--max_length", type=int, default=512)
     ap.add_argument("--init", default="auto", choices=["auto", "random", "pretrained"])
@@ -130,7 +138,9 @@ def main(variant: str, argv=None) -> dict:
         gradient_checkpointing=not args.no_gradient_checkpointing,
         resume_from_checkpoint=args.resume_from_checkpoint, max_steps=args.max_steps,
         warmup_steps=args.warmup_steps, synthetic=args.synthetic,
-        synthetic_samples=args.synthetic_samples, init=args.init, experiment=experiment)
+        synthetic_samples=args.synthetic_samples, init=args.init, experiment=experiment,
+        synthetic_min_len=args.synthetic_min_len, pack_sequences=not args.no_packing,
+        prefetch=args.prefetch, pack_tokens=args.pack_tokens)
     t0 = time.time()
     trainer = Trainer(targs, ds, env)
     result = trainer.train()

@@ -60,3 +60,63 @@ class CausalLMCollator:
         n_tokens = int(attn.sum())
         return {"input_ids": input_ids, "labels": shifted, "attention_mask": attn,
                 "n_valid": n_valid, "n_tokens": n_tokens}
+
+
+class PackedCollator:
+    """Sequence packing for the varlen flash-attention path (no padding compute).
+
+    The micro-batch's sequences are laid back to back in ONE row of T = sum(len) tokens;
+    ``cu_seqlens`` marks their boundaries so attention stays within each sequence, and
+    ``pos`` restarts RoPE positions at 0 per sequence.  Labels are shifted WITHIN each sequence
+    (the last token of a sequence predicts nothing), and -- as in the padded collator / the
+    reference's DataCollatorForLanguageModeling with pad = eos -- a token equal to the pad id
+    is never a target.  The loss over the packed row therefore equals the padded batch's
+    (mean over the same valid labels), at sum(len) instead of B * max(len) tokens.
+
+    T is rounded up to ``pad_to_multiple_of`` (default 256) so the frozen-weight GEMMs meet a
+    small set of M values that the tuned hipBLASLt table covers; the filler tokens form one
+    extra sequence of their own (attends only to itself, no labels)."""
+
+    def __init__(self, pad_id: int, max_length: Optional[int] = None, pad_to_multiple_of: int = 256,
+                 mask_pad_equal_eos: bool = True):
+        self.pad_id = pad_id
+        self.max_length = max_length
+        self.mult = max(1, pad_to_multiple_of)
+        self.mask_pad = mask_pad_equal_eos
+
+    def __call__(self, examples: Sequence) -> Dict:
+        import numpy as np
+
+        seqs = []
+        for e in examples:
+            ids = e["input_ids"] if isinstance(e, dict) else e
+            ids = np.asarray(ids, dtype=np.int64)
+            if self.max_length:
+                ids = ids[: self.max_length]
+            if ids.size:
+                seqs.append(ids)
+        T = int(sum(s.size for s in seqs))
+        Tp = max(self.mult, (T + self.mult - 1) // self.mult * self.mult)
+        ids = np.full(Tp, self.pad_id, dtype=np.int64)
+        labels = np.full(Tp, IGNORE, dtype=np.int64)
+        pos = np.zeros(Tp, dtype=np.int32)
+        cu = [0]
+        o = 0
+        for s in seqs:
+            n = s.size
+            ids[o:o + n] = s
+            pos[o:o + n] = np.arange(n, dtype=np.int32)
+            tgt = s[1:].copy()
+            if self.mask_pad:
+                tgt[tgt == self.pad_id] = IGNORE
+            labels[o:o + n - 1] = tgt
+            o += n
+            cu.append(o)
+        if Tp > T:
+            pos[T:] = np.arange(Tp - T, dtype=np.int32)
+            cu.append(Tp)
+        n_valid = int((labels != IGNORE).sum())
+        return {"input_ids": torch.from_numpy(ids).view(1, Tp),
+                "labels": torch.from_numpy(labels).view(1, Tp),
+                "pos": torch.from_numpy(pos), "cu_seqlens": tuple(cu),
+                "n_valid": n_valid, "n_tokens": T, "n_padded": Tp, "n_seqs": len(seqs)}

@@ -21,7 +21,7 @@ import torch.utils.checkpoint as cp
 
 from ..ops.lora import arena_reset
 from ..ops.activation import swiglu
-from ..ops.attention import causal_attention, flash_attention_qkv
+from ..ops.attention import causal_attention, flash_attention_qkv, prepare_varlen
 from ..ops.loss import lm_head_cross_entropy
 from ..ops.rope import qkv_rope_split, rope_qkv_, rope_tables
 from .config import ModelConfig
@@ -38,7 +38,10 @@ class LlamaAttention(nn.Module):
                                seg_names=["q_proj", "k_proj", "v_proj"])
         self.o_proj = Linear(nh * D, H, dtype=dtype, device=device, seg_names=["o_proj"])
 
-    def forward(self, x2d: torch.Tensor, B: int, S: int, pos: Optional[torch.Tensor] = None):
+    def forward(self, x2d: torch.Tensor, B: int, S: int, pos: Optional[torch.Tensor] = None,
+                cu: Optional[tuple] = None):
+        """``cu`` (packed batches): sequence offsets into the B*S token rows; attention stays
+        within each sequence and ``pos`` holds the per-sequence positions."""
         c = self.cfg
         nh, nkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
         cos, sin = rope_tables(D, c.max_position_embeddings, c.rope_theta, x2d.device)
@@ -54,10 +57,18 @@ class LlamaAttention(nn.Module):
             else:
                 qkv = rope_qkv_(self.qkv_proj(x2d), pos, nh, nkv, D, cos, sin)
             # the FA backward undoes the rotation in its dQ / dK epilogues (FUSED_ROPE_BWD)
-            o = flash_attention_qkv(qkv, tuple(range(0, B * S + 1, S)), nh, nkv, D, True,
+            o = flash_attention_qkv(qkv, cu if cu is not None else tuple(range(0, B * S + 1, S)),
+                                    nh, nkv, D, True,
                                     rope=(pos, cos, sin) if FUSED_ROPE_BWD else None)
             return self.o_proj(o)
         qkv = self.qkv_proj(x2d)
+        if cu is not None:  # packed rows, portable path: one causal block per sequence
+            outs = []
+            for s0, s1 in zip(cu[:-1], cu[1:]):
+                q, k, v = qkv_rope_split(qkv[s0:s1], 1, s1 - s0, nh, nkv, D, cos, sin,
+                                         pos[s0:s1] if pos is not None else None)
+                outs.append(causal_attention(q, k, v))
+            return self.o_proj(torch.cat(outs, 0))
         q, k, v = qkv_rope_split(qkv, B, S, nh, nkv, D, cos, sin, pos)
         o = causal_attention(q, k, v)
         return self.o_proj(o)
@@ -98,9 +109,9 @@ class LlamaDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device)
         self.mlp = LlamaMLP(cfg, dtype, device)
 
-    def forward(self, h, res, B: int, S: int, pos=None):
+    def forward(self, h, res, B: int, S: int, pos=None, cu=None):
         y, s = self.input_layernorm(h, res)
-        a = self.self_attn(y, B, S, pos)
+        a = self.self_attn(y, B, S, pos, cu)
         y2, s2 = self.post_attention_layernorm(a, s)
         return self.mlp(y2), s2
 
@@ -145,24 +156,41 @@ class LlamaForCausalLM(nn.Module):
         out = fn(*args)
         return c.post_forward(idx, out)
 
-    def hidden_states(self, input_ids: torch.Tensor, pos: Optional[torch.Tensor] = None):
+    supports_packing = True  # forward(..., cu_seqlens=...) runs packed varlen rows
+
+    def hidden_states(self, input_ids: torch.Tensor, pos: Optional[torch.Tensor] = None,
+                      cu: Optional[tuple] = None):
+        if input_ids.dim() == 1:
+            input_ids = input_ids.view(1, -1)
         B, S = input_ids.shape
+        if cu is not None:
+            cu = tuple(int(c) for c in cu)
+            if cu[0] != 0 or cu[-1] != B * S:
+                raise ValueError(f"cu_seqlens must span the {B * S} packed tokens, got {cu}")
+            if pos is None:
+                pos = torch.cat([torch.arange(b - a, dtype=torch.int32) for a, b in
+                                 zip(cu[:-1], cu[1:])]).to(input_ids.device)
+            if input_ids.is_cuda:
+                prepare_varlen(cu, input_ids.device)  # tile lists: one async copy per step
         h = self._run_unit(0, lambda ids: F.embedding(ids, self.embed_tokens.weight),
                            input_ids.reshape(-1))
         res = None
         for i, layer in enumerate(self.layers):
             if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
-                fn = lambda h_, r_, L=layer: cp.checkpoint(L, h_, r_, B, S, pos, use_reentrant=False)  # noqa: E731
+                fn = lambda h_, r_, L=layer: cp.checkpoint(L, h_, r_, B, S, pos, cu, use_reentrant=False)  # noqa: E731
             else:
-                fn = lambda h_, r_, L=layer: L(h_, r_, B, S, pos)  # noqa: E731
+                fn = lambda h_, r_, L=layer: L(h_, r_, B, S, pos, cu)  # noqa: E731
             h, res = self._run_unit(i + 1, fn, h, res)
         return h, res
 
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
-                n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None):
+                n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None,
+                cu_seqlens: Optional[tuple] = None):
+        """``cu_seqlens``: the rows of ``input_ids`` are packed sequences with these offsets
+        (lumen.data.PackedCollator); ``pos`` then holds per-sequence positions."""
         if self.training and torch.is_grad_enabled():
             arena_reset(input_ids.device)  # adapter scratch of the previous micro-step is dead
-        h, res = self.hidden_states(input_ids, pos)
+        h, res = self.hidden_states(input_ids, pos, cu_seqlens)
         last = len(self.layers) + 1
 
         def head(h_, r_):

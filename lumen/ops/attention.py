@@ -243,6 +243,34 @@ def _cu_tensor(cu: tuple, device) -> torch.Tensor:
     return t
 
 
+def prepare_varlen(cu: tuple, device) -> None:
+    """Seed the tile / offset caches for a packed batch's ``cu`` with ONE pinned, non-blocking
+    host-to-device copy, before the layer loop: every layer's forward and backward then hits
+    the cache instead of building (and synchronously uploading) its tile lists."""
+    rows_set = (FA_FWD_ROWS, 64, 128)
+    keys = [("cu", cu, str(device))] + [(cu, r, str(device), True) for r in rows_set]
+    if all(k in _TILE_CACHE for k in keys):
+        return
+    parts = [list(cu)]
+    for rows in rows_set:
+        lst = []
+        for s in range(len(cu) - 1):
+            lst += [(s, r) for r in range(0, cu[s + 1] - cu[s], rows)]
+        lst.sort(key=lambda x: -x[1])
+        parts.append([v for t in lst for v in t])
+    flat = torch.tensor([v for p in parts for v in p], dtype=torch.int32)
+    if torch.cuda.is_available():
+        flat = flat.pin_memory()
+    dev = flat.to(device, non_blocking=True)
+    if len(_TILE_CACHE) > 256:
+        _TILE_CACHE.clear()
+    o = 0
+    for k, p in zip(keys, parts):
+        _TILE_CACHE[k] = dev[o:o + len(p)]
+        o += len(p)
+    _TILE_CACHE[("pin", cu, str(device))] = flat  # host buffer outlives the async copy
+
+
 import os as _os
 FA_MT = int(_os.environ.get("LUMEN_FA_MT", "1"))  # query m-tiles (16 rows) per wave (old fwd)
 # forward kernel: "v32" = 32x32x16 MFMA, 32 queries per wave, 128-row tiles (default: 56 vs 71

@@ -198,8 +198,9 @@ class ZeroEngine:
             torch.div(self.opt.state[2:3], self.cfg.grad_accum, out=self._gscale)
             loss_ops.GRAD_SCALE_HINT[0] = self._gscale
         try:
+            kw = {"cu_seqlens": batch["cu_seqlens"]} if batch.get("cu_seqlens") is not None else {}
             loss = self.model(batch["input_ids"], batch["labels"], batch.get("n_valid"),
-                              batch.get("pos"))
+                              batch.get("pos"), **kw)
         finally:
             if fp16_dev:
                 loss_ops.GRAD_SCALE_HINT[0] = None

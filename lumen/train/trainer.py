@@ -17,7 +17,8 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ..data import CausalLMCollator, ShardedSampler, build_dataset, load_tokenizer
+from ..data import (CausalLMCollator, PackedCollator, PrefetchLoader, ShardedSampler,
+                    build_dataset, load_tokenizer)
 from ..lora import LoraConfig, apply_lora, print_trainable_parameters, save_adapter
 from ..models import build_model, get_config
 from ..parallel.dist import DistEnv, all_reduce_scalar, barrier
@@ -52,6 +53,11 @@ class TrainArgs:
     warmup_steps: int = 0
     synthetic: bool = False
     synthetic_samples: int = 1024
+    synthetic_min_len: Optional[int] = None  # variable-length synthetic rows in [min, max_length]
+    pack_sequences: bool = True   # packed varlen rows (no pad compute) when the model supports it
+    pack_tokens: int = 0          # >0: micro-batch = whole sequences greedily packed up to this
+                                  # many tokens (token-budget batching) instead of a fixed count
+    prefetch: int = 2             # batches collated ahead on a host thread (0 = inline)
     init: str = "auto"
     experiment: str = "run"
     strategy: str = ""
@@ -98,8 +104,14 @@ class Trainer:
         pad = getattr(self.tokenizer, "pad_token_id", cfg.eos_token_id)
         self.dataset = build_dataset(args.dataset_path, self.tokenizer, args.max_length,
                                      args.synthetic, args.synthetic_samples, cfg.vocab_size,
-                                     seed=args.seed)
-        self.collator = CausalLMCollator(pad_id=pad, max_length=args.max_length)
+                                     seed=args.seed, synthetic_min_len=args.synthetic_min_len)
+        self.packed = bool(args.pack_sequences and getattr(self.model, "supports_packing", False))
+        if self.packed:
+            # token counts rounded to 256 on the GPU: the GEMM M dimension stays on the tuned grid
+            self.collator = PackedCollator(pad_id=pad, max_length=args.max_length,
+                                           pad_to_multiple_of=256 if env.device.type == "cuda" else 8)
+        else:
+            self.collator = CausalLMCollator(pad_id=pad, max_length=args.max_length)
         self.sampler = ShardedSampler(len(self.dataset), env.rank, env.world_size, seed=args.seed)
         self.log_history: List[Dict] = []
         self.ckpt = AsyncCheckpointer() if args.async_save else None
@@ -109,14 +121,39 @@ class Trainer:
     def _batches(self, epoch: int, skip_samples: int):
         mb = self.ds.micro_batch
         idx = self.sampler.indices(epoch)[skip_samples:]
+        if self.packed and self.args.pack_tokens > 0:
+            # token-budget batching: whole sequences, in sampler order, until the next one would
+            # overflow the budget -- every micro-step's GEMMs see ~pack_tokens rows
+            budget, cur, n = self.args.pack_tokens, [], 0
+            for j in idx:
+                ex = self.dataset[j]
+                L = min(len(ex["input_ids"]), self.args.max_length)
+                if cur and n + L > budget:
+                    yield cur
+                    cur, n = [], 0
+                cur.append(ex)
+                n += L
+            return
         for i in range(0, len(idx) - mb + 1, mb):
             yield [self.dataset[j] for j in idx[i:i + mb]]
 
     def _to_device(self, b):
         d = self.env.device
-        return {"input_ids": b["input_ids"].to(d, non_blocking=True),
-                "labels": b["labels"].to(d, non_blocking=True),
-                "n_valid": b["n_valid"], "n_tokens": b["n_tokens"]}
+        out = {"input_ids": b["input_ids"].to(d, non_blocking=True),
+               "labels": b["labels"].to(d, non_blocking=True),
+               "n_valid": b["n_valid"], "n_tokens": b["n_tokens"]}
+        if b.get("cu_seqlens") is not None:
+            out["cu_seqlens"] = b["cu_seqlens"]
+            out["pos"] = b["pos"].to(d, non_blocking=True)
+        return out
+
+    def _batch_stream(self, epoch: int, skip: int):
+        """(raw, collated) pairs; collation runs ``prefetch`` batches ahead on a host thread."""
+        if self.args.prefetch <= 0:
+            return (None, ((raw, self.collator(raw)) for raw in self._batches(epoch, skip)))
+        ld = PrefetchLoader(self._batches(epoch, skip), self.collator, depth=self.args.prefetch,
+                            pin=self.env.device.type == "cuda")
+        return ld, iter(ld)
 
     def steps_per_epoch(self) -> int:
         return len(self.sampler) // (self.ds.micro_batch * self.ds.grad_accum)
@@ -149,6 +186,7 @@ class Trainer:
         prof = StepProfiler(env.rank, self.print)
         t_start = time.time()
         tokens = 0
+        win_tokens, win_t = 0, t_start
         samples = 0
         loss_acc = torch.zeros((), device=env.device)
         loss_n = 0
@@ -160,9 +198,10 @@ class Trainer:
                 break
             samples_in_epoch = skip
             produced = 0
-            for raw in self._batches(epoch, skip):
+            loader, stream = self._batch_stream(epoch, skip)
+            for raw, cb in stream:
                 produced += 1
-                b = self._to_device(self.collator(raw))
+                b = self._to_device(cb)
                 loss = eng.forward(b)
                 check_finite("loss", loss, eng.global_step, env.rank)
                 eng.backward(loss)
@@ -181,8 +220,13 @@ class Trainer:
                         rec = {"loss": round(l, 4), "grad_norm": gn, "learning_rate": eng.last_lr,
                                "epoch": round(epoch + samples_in_epoch / max(len(self.sampler), 1), 4),
                                "step": eng.global_step}
-                        el = time.time() - t_start
+                        now = time.time()
+                        el = now - t_start
                         rec["tokens_per_second"] = round(tokens * env.world_size / max(el, 1e-9), 1)
+                        # steady-state rate over the last logging window (non-pad tokens)
+                        rec["window_tokens_per_second"] = round(
+                            (tokens - win_tokens) * env.world_size / max(now - win_t, 1e-9), 1)
+                        win_tokens, win_t = tokens, now
                         self.log_history.append(rec)
                         self.print(json.dumps(rec))
                         if ds.wall_clock_breakdown:
@@ -201,6 +245,8 @@ class Trainer:
                     if eng.global_step >= total_steps:
                         done = True
                         break
+            if loader is not None:
+                loader.close()
             skip = 0
             if produced == 0:
                 break
