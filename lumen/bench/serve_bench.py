@@ -37,7 +37,8 @@ def bench_engine(a) -> dict:
 
     cfg = EngineConfig(model=a.model, dtype="bf16", max_model_len=a.max_model_len,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_batched_tokens,
-                       use_graphs=not a.no_graphs, init="random")
+                       use_graphs=not a.no_graphs, init="random",
+                       async_scheduling=not a.sync_scheduling)
     t0 = time.time()
     eng = LLMEngine(cfg)
     setup = time.time() - t0
@@ -86,6 +87,7 @@ def bench_engine(a) -> dict:
             "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
             "kv_blocks": eng.blocks.num_blocks, "preemptions": eng.scheduler.num_preemptions,
             "max_batched_tokens": a.max_batched_tokens, "steps": eng.stats["steps"],
+            "async_scheduling": eng.async_sched,
             "setup_s": round(setup, 1), "graphs": sorted(eng.runner._graphs)}
 
 
@@ -147,6 +149,8 @@ def main():
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--sync-scheduling", action="store_true",
+                    help="engine mode: host waits for each step's tokens before the next step")
     a = ap.parse_args()
     res = bench_engine(a) if a.mode == "engine" else bench_http(a)
     res.update(metric="serve tok/s + p50 TTFT (Llama-2-7B, TP=1)", model=a.model, dtype="bf16",

@@ -49,6 +49,10 @@ class EngineConfig:
     # multi-LoRA serving (vLLM --enable-lora): {served name: PEFT adapter dir}, kept un-merged
     lora_modules: Optional[Dict[str, str]] = None
     max_loras: int = 4
+    # async scheduling (TP = 1): step t+1 is scheduled, built and launched while step t runs;
+    # its decode tokens come from step t's sampled tokens ON THE DEVICE, and step t's tokens
+    # reach the host afterwards (EOS / stop ids are seen one step late: one wasted row)
+    async_scheduling: bool = True
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -141,8 +145,11 @@ class LLMEngine:
             self.runner.lora = MultiLoRA(model.config, cfg.lora_modules, cfg.max_loras, self.rank,
                                          self.tp, dev, dt)
             self.lora_names = list(self.runner.lora.names)
-        self._pinned: Optional[torch.Tensor] = None
-        self._pinned_ready = None
+        self._pinned: List[Optional[torch.Tensor]] = [None, None]
+        self._pinned_ready: List[Optional[object]] = [None, None]
+        self._pin_i = 0
+        self.async_sched = bool(cfg.async_scheduling and self.tp == 1)
+        self._inflight: Optional[dict] = None
         self.scheduler = Scheduler(SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                                    cfg.max_model_len), self.blocks)
         if tokenizer is None:
@@ -202,7 +209,7 @@ class LLMEngine:
 
     @property
     def has_work(self) -> bool:
-        return self.scheduler.has_work
+        return self.scheduler.has_work or self._inflight is not None
 
     # --------------------------------------------------------------------------------------
     def _build_input(self, batch: Batch) -> StepInput:
@@ -258,6 +265,16 @@ class LLMEngine:
             extra += [pt.reshape(-1), np.asarray(kv_lens, dtype=np.int64)]
         if N:
             extra += [dec_bt.reshape(-1), lens]
+        src = None
+        if N and self._inflight is not None:
+            # decode inputs still being sampled by the in-flight step: row of its token tensor
+            row = self._inflight["row"]
+            src = np.fromiter((row.get(s.seq_id, -1) if s.has_pending else -1
+                               for s in batch.decodes), dtype=np.int64, count=N)
+            if not (src >= 0).any():
+                src = None
+            else:
+                extra.append(src)
         n_done = len(batch.completing())
         done_rows = [cu[i + 1] - 1 for i, (s, c) in enumerate(batch.prefills)
                      if s.num_cached + c == s.length]
@@ -285,6 +302,13 @@ class LLMEngine:
             inp.max_context = int(lens.max())
         inp.sample_rows = dev[o:o + len(rows)]
         o += len(rows)
+        if src is not None:
+            # dependent decode tokens: gathered from the previous step's sampled tokens here,
+            # on the stream, before the step reads (or its graph copies in) its token row
+            s_dev = dev[o:o + N]
+            o += N
+            prev = self._inflight["toks"]
+            inp.tokens[Tp:] = torch.where(s_dev >= 0, prev[s_dev.clamp(min=0)], inp.tokens[Tp:])
         if use_lora:
             inp.lora_ids = dev[o:o + T].int()
         return inp
@@ -293,16 +317,20 @@ class LLMEngine:
         t = torch.from_numpy(host)
         if self.device.type != "cuda":
             return t
-        if self._pinned_ready is not None:
-            self._pinned_ready.synchronize()  # previous step's copy out of the staging buffer
-        if self._pinned is None or self._pinned.numel() < t.numel():
-            self._pinned = torch.empty(max(t.numel(), 1 << 16), dtype=torch.long).pin_memory()
-        buf = self._pinned[:t.numel()]
+        # two pinned staging buffers, alternating: the copy of step t-1 (queued behind step t-2's
+        # kernels) never makes the host wait while it builds step t
+        i = self._pin_i
+        self._pin_i ^= 1
+        if self._pinned_ready[i] is not None:
+            self._pinned_ready[i].synchronize()  # that buffer's last copy has been read
+        if self._pinned[i] is None or self._pinned[i].numel() < t.numel():
+            self._pinned[i] = torch.empty(max(t.numel(), 1 << 16), dtype=torch.long).pin_memory()
+        buf = self._pinned[i][:t.numel()]
         buf.copy_(t)
         out = buf.to(self.device, non_blocking=True)
-        # the pinned staging buffer is reused next step: order that reuse after this copy
-        self._pinned_ready = torch.cuda.Event()
-        self._pinned_ready.record()
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pinned_ready[i] = ev
         return out
 
     def _broadcast(self, inp: Optional[StepInput]):
@@ -313,10 +341,99 @@ class LLMEngine:
 
     def step(self) -> List[Sequence]:
         """Run one engine iteration; returns sequences that received a token this step."""
+        if not self.async_sched:
+            batch = self.scheduler.schedule()
+            if batch is None:
+                return []
+            return self._run_batch(batch)
         batch = self.scheduler.schedule()
         if batch is None:
+            return self._resolve()
+        if self._inflight is not None and self._needs_host_tokens(batch):
+            done = self._resolve()     # this step reads real token values on the host
+            self._launch(batch)
+            return done
+        prev = self._inflight
+        self._launch(batch)            # step t+1 is queued behind step t ...
+        return self._resolve(prev)     # ... while the host collects step t's tokens
+
+    @staticmethod
+    def _needs_host_tokens(batch: Batch) -> bool:
+        """Prefill rows re-reading generated tokens (preemption recompute) and penalties need
+        the in-flight step's token VALUES on the host."""
+        return (any(s.has_pending for s, _ in batch.prefills)
+                or any(s.params.has_penalties for s in batch.sampled))
+
+    def _launch(self, batch: Batch) -> None:
+        inp = self._build_input(batch)
+        sampled = batch.sampled
+        if batch.kind == "decode":
+            logits = self.runner.decode(inp)
+        else:
+            logits = self.runner.execute(inp)
+        self.stats["prefill_tokens"] += inp.num_prefill_rows
+        self.stats["decode_tokens"] += len(batch.decodes)
+        rec = {"sampled": [], "row": {}, "toks": None}
+        if sampled:
+            ps = [s.params for s in sampled]
+            seed = self.cfg.seed if ps[0].seed is None else ps[0].seed
+            if any(p.has_penalties for p in ps):
+                logits = apply_penalties(logits, sampled)
+            t, lp = self.runner.sample(logits, [p.temperature for p in ps],
+                                       [p.top_p for p in ps], [p.top_k for p in ps], seed,
+                                       self.step_count, want_logprobs=True)
+            R = t.shape[0]
+            th = torch.empty(R, dtype=torch.long, pin_memory=self.device.type == "cuda")
+            th.copy_(t, non_blocking=True)
+            lh = None
+            if lp is not None:
+                lh = torch.empty(R, dtype=torch.float32, pin_memory=self.device.type == "cuda")
+                lh.copy_(lp, non_blocking=True)
+            ev = torch.cuda.Event() if self.device.type == "cuda" else None
+            if ev is not None:
+                ev.record()
+            rec.update(toks=t, th=th, lh=lh, ev=ev, sampled=sampled)
+        for s, c in batch.prefills:
+            s.num_cached += c
+        for s in batch.decodes:
+            s.num_cached = s.length
+        for i, s in enumerate(sampled):
+            s.prefilled = True
+            rec["row"][s.seq_id] = i
+            s.reserve()
+        self.stats["steps"] += 1
+        self.step_count += 1
+        self._inflight = rec if sampled else None
+
+    def _resolve(self, rec: Optional[dict] = None) -> List[Sequence]:
+        """Bring a launched step's sampled tokens to the host and apply them."""
+        if rec is None:
+            rec, self._inflight = self._inflight, None
+        if rec is None or not rec["sampled"]:
             return []
-        return self._run_batch(batch)
+        if rec["ev"] is not None:
+            rec["ev"].synchronize()
+        toks = rec["th"].tolist()
+        lps = rec["lh"].tolist() if rec["lh"] is not None else [None] * len(toks)
+        nxt = self._inflight if self._inflight is not rec else None
+        out, ended = [], []
+        for s in rec["sampled"]:
+            i = rec["row"].get(s.seq_id)
+            if i is None:
+                continue
+            if s.finished:            # aborted while in flight
+                s.n_pending = 0
+                continue
+            s.fill(int(toks[i]), lps[i], self.eos_id)
+            if s.finished:
+                ended.append(s)
+                if nxt is not None and nxt["row"].pop(s.seq_id, None) is not None:
+                    # EOS / stop id seen one step late: the next step's row for it is wasted
+                    s.n_pending -= 1
+            out.append(s)
+        self.runner.check_collectives()
+        self.stats["finished"] += len(self.scheduler.finish_seqs(ended))
+        return out
 
     def _run_batch(self, batch: Batch) -> List[Sequence]:
         inp = self._build_input(batch)

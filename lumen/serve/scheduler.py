@@ -93,7 +93,7 @@ class Scheduler:
         #    youngest running sequence when the cache is exhausted)
         preempted = set()
         for s in list(self.running):
-            if s.seq_id in preempted or not s.prefilled:
+            if s.seq_id in preempted or not s.prefilled or s.capped:
                 continue
             while True:
                 try:
@@ -149,7 +149,12 @@ class Scheduler:
         self.waiting.appendleft(s)
 
     def finish(self, batch: Batch) -> List[Sequence]:
-        done = [s for s in batch.seqs if s.finished]
+        return self.finish_seqs(batch.seqs)
+
+    def finish_seqs(self, seqs) -> List[Sequence]:
+        """Retire the finished ones among ``seqs`` (running list, KV blocks)."""
+        live = {s.seq_id for s in self.running}
+        done = [s for s in seqs if s.finished and s.seq_id in live]
         if done:
             ids = {s.seq_id for s in done}
             self.running = [s for s in self.running if s.seq_id not in ids]

@@ -52,6 +52,9 @@ class Status(enum.Enum):
 _ids = itertools.count()
 
 
+PENDING = -1  # last_token of a sequence whose next input token is still on the device
+
+
 @dataclass
 class Sequence:
     prompt_ids: List[int]
@@ -70,6 +73,8 @@ class Sequence:
     prefilled: bool = False      # prompt (incl. recomputed outputs) fully in the cache
     preemptions: int = 0
     lora_slot: int = 0           # multi-LoRA serving: adapter slot (0 = base model)
+    n_pending: int = 0           # async scheduling: sampled tokens still on the device
+    capped: bool = False         # max_tokens reached counting in-flight tokens
 
     @property
     def all_ids(self) -> List[int]:
@@ -77,15 +82,47 @@ class Sequence:
 
     @property
     def length(self) -> int:
-        return len(self.prompt_ids) + len(self.output_ids)
+        return len(self.prompt_ids) + len(self.output_ids) + self.n_pending
 
     @property
     def last_token(self) -> int:
+        if self.n_pending:
+            return PENDING
         return self.output_ids[-1] if self.output_ids else self.prompt_ids[-1]
 
     @property
     def finished(self) -> bool:
         return self.status == Status.FINISHED
+
+    def reserve(self) -> None:
+        """Async scheduling: a step that samples this sequence's next token is in flight.
+        Lengths / block tables count it now; ``output_ids`` only ever holds resolved tokens (a
+        streaming reader on another thread never sees a placeholder).  A sequence whose
+        max_tokens the in-flight tokens reach is ``capped``: no further steps are scheduled."""
+        self.n_pending += 1
+        if len(self.output_ids) + self.n_pending >= self.params.max_tokens:
+            self.capped = True
+
+    def fill(self, tok: int, logprob: Optional[float], eos_id: Optional[int]) -> None:
+        """The value of the oldest in-flight token (resolved in launch order)."""
+        now = time.perf_counter()
+        if self.first_token_time is None:
+            self.first_token_time = now
+        self.last_token_time = now
+        self.token_times.append(now)
+        if logprob is not None:
+            self.output_logprobs.append(logprob)
+        self.output_ids.append(tok)
+        self.n_pending -= 1
+        p = self.params
+        if (not p.ignore_eos and eos_id is not None and tok == eos_id) or tok in p.stop_token_ids:
+            self.status, self.finish_reason = Status.FINISHED, "stop"
+        elif len(self.output_ids) >= p.max_tokens:
+            self.status, self.finish_reason = Status.FINISHED, "length"
+
+    @property
+    def has_pending(self) -> bool:
+        return self.n_pending > 0
 
     def append(self, tok: int, logprob: Optional[float], eos_id: Optional[int]) -> None:
         now = time.perf_counter()

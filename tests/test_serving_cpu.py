@@ -406,3 +406,48 @@ def test_openai_stop_strings_n_best_of_penalties(model):
         ae.shutdown()
     # every aborted / finished request released its KV blocks
     assert eng.blocks.num_free == eng.blocks.num_blocks
+
+
+def test_async_scheduling_matches_sync(model):
+    """Async scheduling (step t+1 launched before step t's tokens reach the host, decode inputs
+    gathered on the device) gives the same tokens, finish reasons and logprobs as the
+    synchronous loop -- including EOS / stop ids found one step late, max_tokens, preemption and
+    an abort while a step is in flight."""
+    import random
+
+    rnd = random.Random(0)
+    prompts = [[rnd.randrange(3, 250) for _ in range(rnd.randrange(3, 40))] for _ in range(9)]
+    ref_eng = _engine(model, num_blocks=400, async_scheduling=False)
+    ref = ref_eng.generate(prompts, SamplingParams(max_tokens=12, temperature=0.0))
+    stop_tok = ref[2].output_ids[4]  # force a stop id mid-stream for one request
+
+    def run(async_, nb):
+        eng = _engine(model, num_blocks=nb, async_scheduling=async_, max_num_batched_tokens=48)
+        seqs = []
+        for i, p in enumerate(prompts):
+            sp = SamplingParams(max_tokens=12 if i != 5 else 3, temperature=0.0,
+                                stop_token_ids=[stop_tok] if i == 2 else [])
+            seqs.append(eng.add_request(p, sp, request_id=f"r{i}"))
+        steps = 0
+        while eng.has_work:
+            eng.step()
+            steps += 1
+            if steps == 4:
+                eng.abort("r7")
+        return eng, seqs
+
+    _, sync = run(False, 400)
+    eng, asy = run(True, 400)
+    assert eng.async_sched
+    for a, b in zip(sync, asy):
+        assert a.output_ids == b.output_ids and a.finish_reason == b.finish_reason
+        assert a.n_pending == 0 and b.n_pending == 0
+        torch.testing.assert_close(torch.tensor(a.output_logprobs), torch.tensor(b.output_logprobs))
+    assert asy[2].finish_reason == "stop" and asy[5].finish_reason == "length"
+    assert asy[7].finish_reason == "abort"
+    # tight cache: preemption + recompute under async scheduling
+    eng, tight = run(True, 40)
+    for a, b in zip(sync, tight):
+        if a.finish_reason != "abort":
+            assert a.output_ids == b.output_ids
+    assert eng.blocks.num_free == 40 and eng.scheduler.num_preemptions > 0
