@@ -15,7 +15,8 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
 from ..ops.lora import arena_reset
-from ..ops.attention import causal_attention
+from ..ops._native import use_native
+from ..ops.attention import causal_attention, flash_attention_qkv
 from ..ops.loss import lm_head_cross_entropy
 from ..ops.norm import layer_norm
 from .config import ModelConfig
@@ -39,16 +40,29 @@ class OPTDecoderLayer(nn.Module):
         for p in self.parameters():
             p.requires_grad_(False)
 
-    def forward(self, h, B: int, S: int):
+    def forward(self, h, B: int, S: int, cu=None):
         c = self.cfg
         nh, D = c.num_attention_heads, c.head_dim
         ln1, ln2 = self.self_attn_layer_norm, self.final_layer_norm
         x = layer_norm(h, ln1.weight, ln1.bias, ln1.eps)
-        qkv = self.qkv_proj(x).view(B, S, 3, nh, D)
-        q = qkv[:, :, 0].transpose(1, 2)
-        k = qkv[:, :, 1].transpose(1, 2)
-        v = qkv[:, :, 2].transpose(1, 2)
-        h = h + self.out_proj(causal_attention(q, k, v))
+        qkv2d = self.qkv_proj(x)
+        if qkv2d.is_cuda and use_native(qkv2d):
+            # HIP flash attention straight from the fused token-major q|k|v rows (head dim 64
+            # runs zero-padded to the kernels' 128, lumen.ops.attention._flash_padded)
+            cu_ = cu if cu is not None else tuple(range(0, B * S + 1, S))
+            o = flash_attention_qkv(qkv2d, cu_, nh, nh, D, True)
+        elif cu is not None:  # packed rows, portable path: one causal block per sequence
+            outs = []
+            for s0, s1 in zip(cu[:-1], cu[1:]):
+                t = qkv2d[s0:s1].view(1, s1 - s0, 3, nh, D)
+                outs.append(causal_attention(t[:, :, 0].transpose(1, 2), t[:, :, 1].transpose(1, 2),
+                                             t[:, :, 2].transpose(1, 2)))
+            o = torch.cat(outs, 0)
+        else:
+            qkv = qkv2d.view(B, S, 3, nh, D)
+            o = causal_attention(qkv[:, :, 0].transpose(1, 2), qkv[:, :, 1].transpose(1, 2),
+                                 qkv[:, :, 2].transpose(1, 2))
+        h = h + self.out_proj(o)
         x = layer_norm(h, ln2.weight, ln2.bias, ln2.eps)
         return h + self.fc2(F.relu(self.fc1(x)))
 
@@ -90,13 +104,24 @@ class OPTForCausalLM(nn.Module):
         out = fn(*args)
         return c.post_forward(idx, out)
 
+    supports_packing = True  # forward(..., cu_seqlens=...) runs packed varlen rows
+
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None,
-                n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None):
+                n_valid: Optional[int] = None, pos: Optional[torch.Tensor] = None,
+                cu_seqlens: Optional[tuple] = None):
         if self.training and torch.is_grad_enabled():
             arena_reset(input_ids.device)  # adapter scratch of the previous micro-step is dead
+        if input_ids.dim() == 1:
+            input_ids = input_ids.view(1, -1)
         B, S = input_ids.shape
+        cu = tuple(int(c) for c in cu_seqlens) if cu_seqlens is not None else None
         if pos is None:
-            pos = torch.arange(S, device=input_ids.device).expand(B, S)
+            if cu is not None:
+                pos = torch.cat([torch.arange(b - a) for a, b in zip(cu[:-1], cu[1:])]).to(
+                    input_ids.device)
+            else:
+                pos = torch.arange(S, device=input_ids.device).expand(B, S)
+        pos = pos.long().reshape(B, S)
 
         def embed(ids, p):
             return (F.embedding(ids, self.embed_tokens.weight)
@@ -105,9 +130,9 @@ class OPTForCausalLM(nn.Module):
         h = self._run_unit(0, embed, input_ids, pos)
         for i, layer in enumerate(self.layers):
             if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
-                fn = lambda h_, L=layer: cp.checkpoint(L, h_, B, S, use_reentrant=False)  # noqa: E731
+                fn = lambda h_, L=layer: cp.checkpoint(L, h_, B, S, cu, use_reentrant=False)  # noqa: E731
             else:
-                fn = lambda h_, L=layer: L(h_, B, S)  # noqa: E731
+                fn = lambda h_, L=layer: L(h_, B, S, cu)  # noqa: E731
             h = self._run_unit(i + 1, fn, h)
         last = len(self.layers) + 1
 

@@ -295,7 +295,7 @@ FA_DQ_DELTA = _os.environ.get("LUMEN_FA_DQ_DELTA", "0") == "1"
 
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cu, nh, nkv, D, causal, rope=None):
+    def forward(ctx, qkv, cu, nh, nkv, D, causal, rope=None, scale=None):
         C = native()
         T = qkv.shape[0]
         q = qkv[:, :nh * D]
@@ -304,7 +304,7 @@ class _FlashAttn(torch.autograd.Function):
         o = torch.empty(T, nh * D, device=qkv.device, dtype=qkv.dtype)
         lse = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
         cut = _cu_tensor(cu, qkv.device)
-        scale = 1.0 / math.sqrt(D)
+        scale = 1.0 / math.sqrt(D) if scale is None else scale
         C.flash_attn(0, causal, FA_FWD_MT, q, k, v, o, lse, cut,
                      _tiles(cu, FA_FWD_ROWS, qkv.device), nh, nkv, scale, None, None, None, None,
                      None, None, None, None)
@@ -354,7 +354,22 @@ class _FlashAttn(torch.autograd.Function):
                          scale, do, dq, dk, dv, delta, pos, cos, sin)
         if rp is not None:
             dqkv._lumen_rope_undone = True
-        return dqkv, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None
+
+
+KERNEL_D = 128  # head dim of the HIP flash-attention kernels
+
+
+def _flash_padded(qkv, cu, nh, nkv, D, causal):
+    """Head dims below the kernels' 128 (OPT-125m: 64): every head is zero-padded to 128
+    columns -- q.k over the padded heads is the same score, P.V leaves the pad columns of O
+    zero -- and the kernel runs with the true 1/sqrt(D) scale.  The pad / slice copies are
+    differentiated by autograd (their backward is the slice / pad of the gradient)."""
+    T = qkv.shape[0]
+    H3 = nh + 2 * nkv
+    qkvp = F.pad(qkv.view(T, H3, D), (0, KERNEL_D - D)).view(T, H3 * KERNEL_D)
+    o = _FlashAttn.apply(qkvp, cu, nh, nkv, KERNEL_D, causal, None, 1.0 / math.sqrt(D))
+    return o.view(T, nh, KERNEL_D)[:, :, :D].reshape(T, nh * D)
 
 
 def flash_attention_qkv(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int,
@@ -366,8 +381,10 @@ def flash_attention_qkv(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int
     then returns the gradient w.r.t. the PRE-rotation q/k (marked ``_lumen_rope_undone`` on the
     dQKV tensor so the producer's backward skips its inverse pass)."""
     cu = tuple(int(c) for c in cu_seqlens)
-    if use_native(qkv) and D == 128:
+    if use_native(qkv) and D == KERNEL_D:
         return _FlashAttn.apply(qkv, cu, nh, nkv, D, causal, rope)
+    if use_native(qkv) and D < KERNEL_D and D % 8 == 0 and rope is None:
+        return _flash_padded(qkv.contiguous(), cu, nh, nkv, D, causal)
     return flash_attention_ref(qkv, cu, nh, nkv, D, causal)
 
 

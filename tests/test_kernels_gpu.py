@@ -712,3 +712,60 @@ def test_flash_attention_paged_prefill(nh, nkv, dtype):
     ref = flash_attention_paged_ref(q.float(), kc.float(), vc.float(), cu, kl, bt, nh, nkv, D)
     assert torch.isfinite(got.float()).all()
     assert rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("D", [64, 96])
+@pytest.mark.parametrize("nh,nkv", [(12, 12), (8, 2)])
+def test_flash_attention_small_head_dim(D, nh, nkv):
+    """Head dims below 128 (OPT-125m: 64) run the HIP kernels zero-padded to 128 with the true
+    1/sqrt(D) scale: fwd + bwd vs the f32 reference."""
+    from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
+
+    cu = [0, 77, 333, 512]
+    T = cu[-1]
+    qkv = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(torch.bfloat16)
+    qkv.requires_grad_(True)
+    o = flash_attention_qkv(qkv, cu, nh, nkv, D, True)
+    q2 = qkv.detach().float().requires_grad_(True)
+    o2 = flash_attention_ref(q2, tuple(cu), nh, nkv, D, True)
+    assert o.shape == o2.shape and rel(o, o2) < 2e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    o2.backward(do.float())
+    assert rel(qkv.grad, q2.grad) < 3e-2
+
+
+def test_opt_gpu_flash_matches_reference(monkeypatch):
+    """OPT-125m (head dim 64) with the HIP flash attention == the same bf16 GPU model with the
+    torch reference attention, for loss and LoRA gradients."""
+    import lumen.models.opt as opt_mod
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+    from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
+
+    torch.manual_seed(0)
+    m = build_model("opt-125m", dtype=torch.bfloat16, device=torch.device("cuda"), init="random",
+                    seed=4)
+    apply_lora(m, LoraConfig(r=8, lora_dropout=0.0, target_modules=["q_proj", "v_proj"]))
+    with torch.no_grad():
+        for _, mod in m.lora_modules():
+            mod.lora.lora_B.normal_(0, 0.02)
+    m.train()
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(3, m.config.vocab_size, (2, 96), generator=g).cuda()
+    labels = torch.roll(ids, -1, 1)
+    outs = []
+    for attn in (flash_attention_qkv, lambda qkv, cu, nh, nkv, D, c: flash_attention_ref(
+            qkv.float(), tuple(cu), nh, nkv, D, c).to(qkv.dtype)):
+        monkeypatch.setattr(opt_mod, "flash_attention_qkv", attn)
+        m.zero_grad(set_to_none=True)
+        loss = m(ids, labels)
+        loss.backward()
+        outs.append((loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters()
+                                   if p.requires_grad}))
+    (l1, g1), (l2, g2) = outs
+    assert abs(l1 - l2) < 1e-2 * abs(l2)
+    # bf16 attention-gradient rounding compounds through the backward: measured 2.3% at the last
+    # layer growing smoothly to 8.5% at layer 0 of 12 (a kernel bug would show a step, not a ramp)
+    rels = [rel(g1[n], g2[n]) for n in g1]
+    assert rels[-1] < 3e-2 and max(rels) < 0.12, rels

@@ -112,3 +112,20 @@ def test_trainer_token_budget_batches(tmp_path):
     assert all(n <= 200 for n in sizes) and sum(sizes) > 0.8 * 200 * len(sizes)
     res = tr.train()
     assert res["global_step"] == 3
+
+
+def test_opt_packed_matches_padded():
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+
+    torch.manual_seed(0)
+    m = build_model("tiny-opt", dtype=torch.float32, device=torch.device("cpu"), init="random",
+                    seed=1)
+    apply_lora(m, LoraConfig(r=4, lora_dropout=0.0, target_modules=["q_proj", "v_proj"]))
+    m.train()
+    ex = _examples()
+    p = PackedCollator(pad_id=2, pad_to_multiple_of=16)(ex)
+    q = CausalLMCollator(pad_id=2)(ex)
+    lp = m(p["input_ids"], p["labels"], p["n_valid"], p["pos"], cu_seqlens=p["cu_seqlens"])
+    lq = m(q["input_ids"], q["labels"], q["n_valid"])
+    assert math.isclose(lp.item(), lq.item(), rel_tol=1e-5)
