@@ -191,12 +191,29 @@ def _v3_ok(r: int, R: int, segs, *mats) -> bool:
             and all(m.stride(1) == 1 and m.stride(0) % 8 == 0 for m in mats))
 
 
-def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope):
+def _lora3_down(x2d, A, Z, p, seed):
+    T, K = x2d.shape
+    R = A.shape[0]
+    native().lora3_down(x2d, x2d.stride(0), A, Z, R, T, K, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
+                        drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0)
+
+
+def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope, gemm=None):
+    """``gemm`` (overlap mode): callable producing y; the DOWN product runs on the side stream
+    while it executes, and the UP write-back joins both.  Returns (y, rope fused)."""
     T, K = x2d.shape
     R = A.shape[0]
     nat = native()
-    nat.lora3_down(x2d, x2d.stride(0), A, Z, R, T, K, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
-                   drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0)
+    if gemm is not None:
+        cur = torch.cuda.current_stream(x2d.device)
+        side = _side_stream(x2d.device)
+        side.wait_stream(cur)      # x and the zeroed Z are ready
+        with torch.cuda.stream(side):
+            _lora3_down(x2d, A, Z, p, seed)
+        y = gemm()
+        cur.wait_stream(side)
+    else:
+        _lora3_down(x2d, A, Z, p, seed)
     fuse = rope is not None and len(segs) <= 4 and _rope_covered(segs, rope[3])
     for i in range(0, len(segs), 4):
         ch = segs[i:i + 4]
@@ -210,7 +227,21 @@ def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope):
             _lora2(2, 1, B, Z, y, y.stride(0), 1, scale, T, r, 1,
                    [(b_off * r, r_off, n_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
                    rope=(rope[1], rope[2], rope[0], mask) if fuse else None)
-    return fuse
+    return y, fuse
+
+
+# LUMEN_LORA_OVERLAP=1: the memory-bound adapter products that depend only on the layer input
+# (forward DOWN) or only on the output gradient (backward dZ / dB pass) run on a side stream
+# concurrently with the compute-bound frozen-weight GEMM of the same linear
+OVERLAP = _os.environ.get("LUMEN_LORA_OVERLAP", "0") == "1"
+_SIDE = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
+    return s
 
 
 def _dy_tw(segs, T: int) -> int:
@@ -223,7 +254,7 @@ def _dy_tw(segs, T: int) -> int:
 
 
 def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train: bool = False,
-                    rope=None):
+                    rope=None, gemm=None):
     """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place).
 
     ``rope`` = (pos int32 [T], cos, sin, ncols): also rotate columns [0, ncols) of y (q|k heads,
@@ -231,12 +262,17 @@ def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train:
     (Z, rope_done)."""
     T, K = x2d.shape
     R = A.shape[0]
-    Ntot = y.shape[1]
+    v3 = (_v3_ok(r, R, segs, x2d, *(() if y is None else (y,))) and K % 8 == 0
+          and A.is_contiguous() and B.is_contiguous() and A.dtype == B.dtype == torch.float32)
+    if gemm is not None and not v3:
+        y = gemm()
+        return lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed, train, rope) + (y,)
+    Ntot = y.shape[1] if y is not None else 0
     act = DTYPE_CODE[x2d.dtype]
     Z = _zeros(T, R, device=x2d.device, train=train)
-    if (_v3_ok(r, R, segs, x2d, y) and K % 8 == 0 and A.is_contiguous() and B.is_contiguous()
-            and A.dtype == B.dtype == torch.float32):
-        return Z, _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope)
+    if v3:
+        y, fuse = _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope, gemm)
+        return (Z, fuse, y) if gemm is not None else (Z, fuse)
     if _v2_ok(r, R, x2d):
         _lora2(0, 1, x2d, A, Z, R, 1, 1.0, T, R, _split(math.ceil(T / 64), K, 256),
                [(0, 0, 0, K)], seed, p, K)
@@ -282,8 +318,13 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
     dev = dy.device
     v2 = _v2_ok(r, R, x2d, dy)
     v3 = (v2 and _v3_ok(r, R, segs, x2d, dy) and K % 8 == 0 and A.is_contiguous()
-          and B.is_contiguous() and A.dtype == B.dtype == torch.float32
-          and (dx is None or _v3_ok(r, R, segs, dx)))
+          and B.is_contiguous() and A.dtype == B.dtype == torch.float32)
+    if callable(dx):
+        if v3 and dy.is_cuda:
+            return _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB,
+                              v2 and DIRECT_GRAD and _direct_ok(A) and _direct_ok(B))
+        dx = dx()
+    v3 = v3 and (dx is None or _v3_ok(r, R, segs, dx))
     # dA / dB accumulate straight into the parameters' .grad (views of the engine's flat f32
     # gradient buffer) when they exist: no zero-filled temporaries and no autograd add kernels
     direct = v2 and DIRECT_GRAD and _direct_ok(A) and _direct_ok(B)
@@ -354,10 +395,26 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     ws = _zeros(T * R + nA + nB, device=dev)
     dZ = ws[:T * R].view(T, R)
     dB = B.grad if (direct and need_dB) else ws[T * R + nA:].view(B.shape[0], r)
-    for i in range(0, len(segs), 4):
-        ch = segs[i:i + 4]
-        nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
-                     [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+
+    def dy_pass():
+        for i in range(0, len(segs), 4):
+            ch = segs[i:i + 4]
+            nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
+                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+
+    if callable(dx):
+        # overlap: the dY pass (memory-bound) on the side stream under the dX GEMM
+        cur = torch.cuda.current_stream(dev)
+        side = _side_stream(dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            dy_pass()
+        dx = dx()
+        cur.wait_stream(side)
+        if dx is not None and not _v3_ok(r, R, segs, dx):
+            dx = dx.contiguous()
+    else:
+        dy_pass()
     dA = None
     if need_dA:
         dA = A.grad if direct else ws[T * R:T * R + nA].view(R, K)
@@ -395,12 +452,21 @@ class _LoraLinear(torch.autograd.Function):
                 rope):
         ctx.train = train
         W = weight_fn()
-        y = torch.matmul(x2d, W.t())
-        if bias is not None:
-            y.add_(bias)
+
+        def gemm():
+            y_ = torch.matmul(x2d, W.t())
+            if bias is not None:
+                y_.add_(bias)
+            return y_
+
         # autograd runs Function.forward with grad disabled: the training flag is passed in
-        Z, rope_done = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed, train=ctx.train,
-                                       rope=rope)
+        if OVERLAP and x2d.is_cuda:
+            Z, rope_done, y = lora_fwd_native(x2d, None, A, B, segs, r, scale, p, seed,
+                                              train=ctx.train, rope=rope, gemm=gemm)
+        else:
+            y = gemm()
+            Z, rope_done = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed,
+                                           train=ctx.train, rope=rope)
         if rope is not None and not rope_done:
             _rope_(y, rope, inverse=False)
         ctx.rope = rope
@@ -425,13 +491,21 @@ class _LoraLinear(torch.autograd.Function):
             if not getattr(dy, "_lumen_scratch", False):
                 dy = dy.clone()
             _rope_(dy, ctx.rope, inverse=True)
-        dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
+        held = {}
+        if OVERLAP and dy.is_cuda and ctx.needs_input_grad[0]:
+            def dx():  # runs while the side-stream dY pass is in flight
+                held["dx"] = _input_grad(ctx, dy)
+                return held["dx"]
+        else:
+            dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
         _IN_BACKWARD[0] = True
         try:
             dA, dB = lora_bwd_native(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed,
                                      ctx.needs_input_grad[3], ctx.needs_input_grad[4])
         finally:
             _IN_BACKWARD[0] = False
+        if callable(dx):
+            dx = held["dx"]
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
         return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None, None
