@@ -38,7 +38,7 @@ def bench_engine(a) -> dict:
     cfg = EngineConfig(model=a.model, dtype="bf16", max_model_len=a.max_model_len,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_batched_tokens,
                        use_graphs=not a.no_graphs, init="random",
-                       async_scheduling=not a.sync_scheduling)
+                       async_scheduling=not a.sync_scheduling, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.time()
     eng = LLMEngine(cfg)
     setup = time.time() - t0
@@ -87,7 +87,7 @@ def bench_engine(a) -> dict:
             "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
             "kv_blocks": eng.blocks.num_blocks, "preemptions": eng.scheduler.num_preemptions,
             "max_batched_tokens": a.max_batched_tokens, "steps": eng.stats["steps"],
-            "async_scheduling": eng.async_sched,
+            "async_scheduling": eng.async_sched, "kv_cache_dtype": a.kv_cache_dtype,
             "setup_s": round(setup, 1), "graphs": sorted(eng.runner._graphs)}
 
 
@@ -104,6 +104,8 @@ def bench_http(a) -> dict:
            "--max-num-batched-tokens", str(a.max_batched_tokens)]
     if a.no_graphs:
         cmd.append("--no-graphs")
+    if a.kv_cache_dtype != "auto":
+        cmd += ["--kv-cache-dtype", a.kv_cache_dtype]
     proc = subprocess.Popen(cmd, env=dict(os.environ, PYTHONPATH=ROOT))
     url = f"http://127.0.0.1:{port}"
     try:
@@ -149,6 +151,7 @@ def main():
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     ap.add_argument("--sync-scheduling", action="store_true",
                     help="engine mode: host waits for each step's tokens before the next step")
     a = ap.parse_args()

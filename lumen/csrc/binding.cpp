@@ -38,6 +38,7 @@ hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long
                        float, long long, long long, int, const long long*, const long long*,
                        const long long*, const int*, const float*, const float*, const int*, int,
                        hipStream_t);
+hipError_t lumen_embedding(const void*, const long long*, void*, int, int, int, hipStream_t);
 hipError_t lumen_lora3_down(int, const void*, long long, const float*, long long, float*, long long,
                             int, int, int, float, unsigned long long, unsigned int, float, long long,
                             long long, hipStream_t);
@@ -51,7 +52,7 @@ hipError_t lumen_lora3_dy(int, const void*, long long, const float*, int, const 
                           const long long*, const long long*, const int*, hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, const float*, void*,
-                            void*, const long long*, int, int, int, int, int, hipStream_t);
+                            void*, const long long*, int, int, int, int, int, int, hipStream_t);
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
 hipError_t lumen_gemv_swiglu(int, const void*, const void*, void*, int, int, long long, long long,
@@ -61,7 +62,10 @@ hipError_t lumen_dgemm(int, const void*, const void*, void*, int, int, int, long
                        float*, unsigned*, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
-                                        float, float*, float*, void*, int, unsigned*, int, hipStream_t);
+                                        float, float*, float*, void*, int, unsigned*, int, int,
+                                        hipStream_t);
+hipError_t lumen_kv_dequant(int, const void*, const void*, void*, void*, const int*, int,
+                            const int*, int, int, int, int, int, hipStream_t);
 hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, const long long*,
                                    int, int, int, int, long long, long long, int, hipStream_t);
 hipError_t lumen_sample(int, const void*, const float*, const float*, const int*,
@@ -337,6 +341,8 @@ void lora2(int64_t dtype, int64_t kind, int64_t flag, const at::Tensor& big, int
         "lora2");
 }
 
+bool is_fp8(const at::Tensor& t) { return t.scalar_type() == at::kFloat8_e4m3fn; }
+
 void need_cuda_f32(const at::Tensor& t, const char* what) {
   if (!t.is_cuda() || t.scalar_type() != at::kFloat)
     throw std::invalid_argument(std::string("lumen: ") + what + " must be an f32 GPU tensor");
@@ -413,6 +419,19 @@ void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r,
         "lora3_dy");
 }
 
+// out[t, :] = W[ids[t], :]  (16-bit table, int64 ids; out of range ids -> zero rows)
+void embedding(const at::Tensor& W, const at::Tensor& ids, at::Tensor& out) {
+  if (!W.is_cuda() || !ids.is_cuda() || !out.is_cuda() || W.dim() != 2 || !W.is_contiguous() ||
+      !out.is_contiguous() || ids.scalar_type() != at::kLong || !ids.is_contiguous() ||
+      out.numel() != ids.numel() * W.size(1) || out.scalar_type() != W.scalar_type() ||
+      W.element_size() != 2)
+    throw std::invalid_argument("lumen: embedding expects a contiguous 16-bit [V, H] table, int64 ids and a [T, H] output");
+  check(lumen_embedding(W.data_ptr(), reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()), out.data_ptr(),
+                        static_cast<int>(ids.numel()), static_cast<int>(W.size(0)),
+                        static_cast<int>(W.size(1)), cur_stream()),
+        "embedding");
+}
+
 void transpose2d(const at::Tensor& in, at::Tensor& out) {
   if (!in.is_cuda() || !out.is_cuda() || in.dim() != 2 || out.dim() != 2)
     throw std::invalid_argument("lumen: transpose2d needs 2-D GPU tensors");
@@ -449,8 +468,31 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                                      static_cast<int>(tmp_m.size(-1)), static_cast<float>(scale),
                                      tmp_m.data_ptr<float>(), tmp_l.data_ptr<float>(),
                                      tmp_o.data_ptr(), static_cast<int>(partition_size), cnt,
-                                     one_pass ? 1 : 0, cur_stream()),
+                                     one_pass ? 1 : 0, is_fp8(k_cache) ? 1 : 0, cur_stream()),
         "paged_attention_decode");
+}
+
+// fp8 KV cache -> 16-bit scratch for prefill attention: block b of sequence s (b * bs <
+// kv_lens[s]) lands at scratch block s * maxb + b
+void kv_dequant(const at::Tensor& k_cache, const at::Tensor& v_cache, at::Tensor& k_scr,
+                at::Tensor& v_scr, const at::Tensor& tables, const at::Tensor& kv_lens,
+                int64_t maxb) {
+  need_cuda(k_cache, "k_cache"); need_cuda(v_cache, "v_cache");
+  need_cuda(k_scr, "k_scr"); need_cuda(v_scr, "v_scr");
+  if (!is_fp8(k_cache) || !is_fp8(v_cache) || k_cache.dim() != 4 || k_scr.dim() != 4 ||
+      k_scr.size(1) != k_cache.size(1) || k_scr.size(2) != k_cache.size(2) ||
+      k_scr.size(3) != k_cache.size(3) || tables.scalar_type() != at::kInt ||
+      kv_lens.scalar_type() != at::kInt || tables.dim() != 2 ||
+      k_scr.size(0) < kv_lens.numel() * maxb || !k_scr.is_contiguous() || !v_scr.is_contiguous())
+    throw std::invalid_argument("lumen: kv_dequant: fp8 [nb, nkv, bs, D] caches, 16-bit scratch "
+                                ">= nseq * maxb blocks, int32 tables / kv_lens");
+  check(lumen_kv_dequant(dcode(k_scr), k_cache.data_ptr(), v_cache.data_ptr(), k_scr.data_ptr(),
+                         v_scr.data_ptr(), tables.data_ptr<int>(),
+                         static_cast<int>(tables.stride(0)), kv_lens.data_ptr<int>(),
+                         static_cast<int>(kv_lens.numel()), static_cast<int>(maxb),
+                         static_cast<int>(k_cache.size(1)), static_cast<int>(k_cache.size(2)),
+                         static_cast<int>(k_cache.size(3)), cur_stream()),
+        "kv_dequant");
 }
 
 void reshape_and_cache(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at::Tensor& v_cache,
@@ -460,7 +502,8 @@ void reshape_and_cache(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_c
   check(lumen_reshape_and_cache(dcode(k), k.data_ptr(), v.data_ptr(), k_cache.data_ptr(),
                                 v_cache.data_ptr(), reinterpret_cast<const long long*>(slot_mapping.data_ptr<int64_t>()), ntok,
                                 static_cast<int>(num_kv_heads), static_cast<int>(D),
-                                static_cast<int>(block_size), k_stride, v_stride, 0, cur_stream()),
+                                static_cast<int>(block_size), k_stride, v_stride,
+                                is_fp8(k_cache) ? 1 : 0, cur_stream()),
         "reshape_and_cache");
 }
 
@@ -483,7 +526,7 @@ void rope_cache_write(at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& 
                          reinterpret_cast<const long long*>(slots.data_ptr<int64_t>()),
                          static_cast<int>(qkv.size(0)), static_cast<int>(nh),
                          static_cast<int>(nkv), static_cast<int>(D),
-                         static_cast<int>(block_size), cur_stream()),
+                         static_cast<int>(block_size), is_fp8(k_cache) ? 1 : 0, cur_stream()),
         "rope_cache_write");
 }
 
@@ -665,6 +708,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "lumen native ops for MI355X (gfx950)";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("lora3_down", &lora3_down);
+  m.def("embedding", &embedding);
+  m.def("kv_dequant", &kv_dequant);
   m.def("lora3_up", &lora3_up);
   m.def("lora3_dy", &lora3_dy);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

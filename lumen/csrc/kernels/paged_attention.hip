@@ -16,9 +16,44 @@
 // one partition write unnormalised (m, l, o) partials that `pa_reduce_kernel` merges.
 #include "common.h"
 
+#include <type_traits>
+
 namespace lumen {
 
 constexpr int kMaxGroup = 8;
+
+// fp8 KV cache (vLLM --kv-cache-dtype fp8): one OCP e4m3fn byte per element, converted with the
+// gfx950 packed converts (v_cvt_pk_f32_fp8 / v_cvt_pk_fp8_f32), no scale (vLLM's uncalibrated
+// default of 1.0).  Halves the K/V bytes every decode step streams.
+using fp8 = unsigned char;
+
+template <typename T, typename KT>
+__device__ __forceinline__ void load8kv(const KT* __restrict__ p, float (&o)[8]) {
+  if constexpr (std::is_same<KT, fp8>::value) {
+    const uint2 r = *reinterpret_cast<const uint2*>(p);
+    const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(r.x), false);
+    const auto b = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(r.x), true);
+    const auto c = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(r.y), false);
+    const auto d = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(r.y), true);
+    o[0] = a[0]; o[1] = a[1]; o[2] = b[0]; o[3] = b[1];
+    o[4] = c[0]; o[5] = c[1]; o[6] = d[0]; o[7] = d[1];
+  } else {
+    load8(p, o);
+  }
+}
+
+template <typename T, typename KT>
+__device__ __forceinline__ void store8kv(KT* __restrict__ p, const float (&v)[8]) {
+  if constexpr (std::is_same<KT, fp8>::value) {
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+    *reinterpret_cast<uint2*>(p) = make_uint2(static_cast<unsigned>(lo), static_cast<unsigned>(hi));
+  } else {
+    store8(p, v);
+  }
+}
 
 template <int W>
 __device__ __forceinline__ float wave_sum_width(float v) {
@@ -235,10 +270,10 @@ __device__ __forceinline__ void pa_merge(float& m, float& l, float (&acc)[8], fl
   m = M;
 }
 
-template <typename T, int D, int G>
+template <typename T, int D, int G, typename KT = T>
 __global__ void __launch_bounds__(256) pa_decode1_kernel(
-    T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
-    const T* __restrict__ vc, const int* __restrict__ block_tables,
+    T* __restrict__ out, const T* __restrict__ q, const KT* __restrict__ kc,
+    const KT* __restrict__ vc, const int* __restrict__ block_tables,
     const int* __restrict__ context_lens, int nh, int nkv, int BS, int max_blocks, int max_parts,
     float scale, float* __restrict__ tmp_m, float* __restrict__ tmp_l, float* __restrict__ tmp_o,
     int PART) {
@@ -278,8 +313,8 @@ __global__ void __launch_bounds__(256) pa_decode1_kernel(
       const int t = t0 + u * NGR;
       if (t < end) {
         const size_t off = bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
-        load8(kc + off, kr[u]);
-        load8(vc + off, vr[u]);
+        load8kv<T, KT>(kc + off, kr[u]);
+        load8kv<T, KT>(vc + off, vr[u]);
       }
     }
 #pragma unroll
@@ -373,9 +408,9 @@ __global__ void __launch_bounds__(256) pa_reduce_kernel(T* __restrict__ out,
 
 // k, v: [ntok, nkv, D] rows with row strides k_stride / v_stride (elements), scattered to
 // cache[block][head][slot][:] by slot_mapping (slot = block * BS + offset; < 0 = skip).
-template <typename T>
+template <typename T, typename KT = T>
 __global__ void __launch_bounds__(256) cache_write_kernel(
-    const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ kc, T* __restrict__ vc,
+    const T* __restrict__ k, const T* __restrict__ v, KT* __restrict__ kc, KT* __restrict__ vc,
     const long long* __restrict__ slots, int ntok, int nkv, int D, int BS, long long k_stride,
     long long v_stride) {
   const int chunks = D / 8;
@@ -388,21 +423,29 @@ __global__ void __launch_bounds__(256) cache_write_kernel(
   if (slot < 0) return;
   const long long blk = slot / BS, off = slot % BS;
   const size_t dst = ((static_cast<size_t>(blk) * nkv + h) * BS + off) * D + c * 8;
-  *reinterpret_cast<uint4*>(kc + dst) =
-      *reinterpret_cast<const uint4*>(k + t * k_stride + static_cast<long long>(h) * D + c * 8);
-  *reinterpret_cast<uint4*>(vc + dst) =
-      *reinterpret_cast<const uint4*>(v + t * v_stride + static_cast<long long>(h) * D + c * 8);
+  if constexpr (std::is_same<KT, fp8>::value) {
+    float a[8], b[8];
+    load8(k + t * k_stride + static_cast<long long>(h) * D + c * 8, a);
+    load8(v + t * v_stride + static_cast<long long>(h) * D + c * 8, b);
+    store8kv<T, KT>(kc + dst, a);
+    store8kv<T, KT>(vc + dst, b);
+  } else {
+    *reinterpret_cast<uint4*>(kc + dst) =
+        *reinterpret_cast<const uint4*>(k + t * k_stride + static_cast<long long>(h) * D + c * 8);
+    *reinterpret_cast<uint4*>(vc + dst) =
+        *reinterpret_cast<const uint4*>(v + t * v_stride + static_cast<long long>(h) * D + c * 8);
+  }
 }
 
 // RoPE of the q and k heads of the fused token-major QKV rows AND the paged KV-cache write of
 // the rotated k and of v, in one pass (serving: prefill and decode).  Replaces rope_inplace +
 // cache_write: at batch-1 decode each of those was a ~5 us launch per layer for a few KB.
 // Thread = (token, head of q|k|v, 16-element chunk pair i0 / i0 + D/2).
-template <typename T>
+template <typename T, typename KT = T>
 __global__ void __launch_bounds__(256) rope_cache_kernel(
     T* __restrict__ qkv, long long ld, const int* __restrict__ pos,
-    const float* __restrict__ cos_t, const float* __restrict__ sin_t, T* __restrict__ kc,
-    T* __restrict__ vc, const long long* __restrict__ slots, int ntok, int nh, int nkv, int D,
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t, KT* __restrict__ kc,
+    KT* __restrict__ vc, const long long* __restrict__ slots, int ntok, int nh, int nkv, int D,
     int BS) {
   const int half = D / 2, chunks = D / 16, H = nh + 2 * nkv;
   const long long tid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -431,13 +474,43 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     store8(row + i0, oa);
     store8(row + i0 + half, ob);
     if (h >= nh && slot >= 0) {
-      store8(kc + dst + i0, oa);
-      store8(kc + dst + i0 + half, ob);
+      store8kv<T, KT>(kc + dst + i0, oa);
+      store8kv<T, KT>(kc + dst + i0 + half, ob);
     }
   } else if (slot >= 0) {
-    *reinterpret_cast<uint4*>(vc + dst + i0) = *reinterpret_cast<const uint4*>(row + i0);
-    *reinterpret_cast<uint4*>(vc + dst + i0 + half) =
-        *reinterpret_cast<const uint4*>(row + i0 + half);
+    if constexpr (std::is_same<KT, fp8>::value) {
+      float a[8], b[8];
+      load8(row + i0, a);
+      load8(row + i0 + half, b);
+      store8kv<T, KT>(vc + dst + i0, a);
+      store8kv<T, KT>(vc + dst + i0 + half, b);
+    } else {
+      *reinterpret_cast<uint4*>(vc + dst + i0) = *reinterpret_cast<const uint4*>(row + i0);
+      *reinterpret_cast<uint4*>(vc + dst + i0 + half) =
+          *reinterpret_cast<const uint4*>(row + i0 + half);
+    }
+  }
+}
+
+// fp8 cache -> 16-bit scratch for the prefill flash-attention kernel (whose LDS-DMA staging
+// moves raw 16-bit rows): block b of prefill sequence s (while b * BS < kv_len[s]) is copied,
+// converted, to scratch block s * maxb + b; the kernel then reads the scratch through the
+// identity table.  grid (nseq, maxb, 2 = K / V), block 256.
+template <typename T>
+__global__ void __launch_bounds__(256) kv_dequant_kernel(
+    const fp8* __restrict__ kc, const fp8* __restrict__ vc, T* __restrict__ ks,
+    T* __restrict__ vs, const int* __restrict__ tables, int tstride, const int* __restrict__ kv_lens,
+    int maxb, int nkv, int BS, int D) {
+  const int s = blockIdx.x, b = blockIdx.y;
+  if (b * BS >= kv_lens[s]) return;
+  const fp8* src = (blockIdx.z == 0 ? kc : vc) +
+                   static_cast<size_t>(tables[static_cast<size_t>(s) * tstride + b]) * nkv * BS * D;
+  T* dst = (blockIdx.z == 0 ? ks : vs) + (static_cast<size_t>(s) * maxb + b) * nkv * BS * D;
+  const int n8 = nkv * BS * D / 8;
+  for (int i = threadIdx.x; i < n8; i += 256) {
+    float f[8];
+    load8kv<T, fp8>(src + i * 8, f);
+    store8(dst + i * 8, f);
   }
 }
 
@@ -445,9 +518,13 @@ template <typename T, int D>
 static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out, const void* q,
                         const void* kc, const void* vc, const int* bt, const int* cl, int nh,
                         int nkv, int BS, int max_blocks, int max_parts, float scale, float* tm,
-                        float* tl, void* to, int PART, unsigned* cnt, bool one_pass) {
+                        float* tl, void* to, int PART, unsigned* cnt, bool one_pass, bool fp8kv) {
 #define LUMEN_PA_G(GG)                                                                         \
-  if (one_pass)                                                                                 \
+  if (fp8kv)                                                                                    \
+    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8>), grid, dim3(256), 0, st, (T*)out,     \
+                       (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, nkv, BS,        \
+                       max_blocks, max_parts, scale, tm, tl, (float*)to, PART);                 \
+  else if (one_pass)                                                                            \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG>), grid, dim3(256), 0, st, (T*)out,          \
                        (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, \
                        max_parts, scale, tm, tl, (float*)to, PART);                             \
@@ -466,15 +543,17 @@ template <typename T>
 static hipError_t launch_pa(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, const int* cl, int nseq, int nh, int nkv, int D, int BS,
                             int max_blocks, int max_parts, float scale, float* tm, float* tl,
-                            void* to, int PART, unsigned* cnt, int one_pass, hipStream_t st) {
+                            void* to, int PART, unsigned* cnt, int one_pass, int fp8kv,
+                            hipStream_t st) {
   const int G = nh / nkv;
+  if (fp8kv) one_pass = 1;  // the fp8 cache is read by the single-pass kernel only
   if (G != 1 && G != 2 && G != 4 && G != 8) return hipErrorInvalidValue;
   dim3 grid(nseq, nkv, max_parts);
   const size_t smem = (static_cast<size_t>(G) * PART + 4 * G * D + 2 * G + 8) * sizeof(float);
-  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
-  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
-  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
-  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0);
+  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
   else return hipErrorInvalidValue;
   if (max_parts > 1 && (cnt == nullptr || one_pass)) {  // unfused merge: second kernel
     dim3 g2(nseq, nh), b2(128);
@@ -494,7 +573,7 @@ extern "C" hipError_t lumen_paged_attention_decode(int dtype, void* out, const v
                                                    int max_parts, float scale, float* tmp_m,
                                                    float* tmp_l, void* tmp_o, int PART,
                                                    unsigned* counters, int one_pass,
-                                                   hipStream_t st) {
+                                                   int fp8kv, hipStream_t st) {
   // counters: nullptr = merge split contexts in a second kernel; else >= nseq * nkv zeroed
   // arrival counters (left zeroed again) and the last partition to finish merges in place.
   if (nseq == 0) return hipSuccess;
@@ -502,24 +581,32 @@ extern "C" hipError_t lumen_paged_attention_decode(int dtype, void* out, const v
   if (dtype == lumen::kBF16)
     return lumen::launch_pa<lumen::bf16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, counters, one_pass, st);
+                                         tmp_o, PART, counters, one_pass, fp8kv, st);
   if (dtype == lumen::kF16)
     return lumen::launch_pa<lumen::fp16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, counters, one_pass, st);
+                                         tmp_o, PART, counters, one_pass, fp8kv, st);
   return hipErrorInvalidValue;
 }
 
 extern "C" hipError_t lumen_reshape_and_cache(int dtype, const void* k, const void* v, void* kc,
                                               void* vc, const long long* slots, int ntok, int nkv,
                                               int D, int BS, long long k_stride,
-                                              long long v_stride, int /*unused*/,
+                                              long long v_stride, int fp8kv,
                                               hipStream_t st) {
   if (ntok == 0) return hipSuccess;
   if (D % 8 != 0) return hipErrorInvalidValue;
   const long long total = static_cast<long long>(ntok) * nkv * (D / 8);
   dim3 grid(static_cast<unsigned>((total + 255) / 256)), block(256);
-  if (dtype == lumen::kBF16)
+  if (fp8kv && dtype == lumen::kBF16)
+    hipLaunchKernelGGL((lumen::cache_write_kernel<lumen::bf16, lumen::fp8>), grid, block, 0, st,
+                       (const lumen::bf16*)k, (const lumen::bf16*)v, (lumen::fp8*)kc,
+                       (lumen::fp8*)vc, slots, ntok, nkv, D, BS, k_stride, v_stride);
+  else if (fp8kv && dtype == lumen::kF16)
+    hipLaunchKernelGGL((lumen::cache_write_kernel<lumen::fp16, lumen::fp8>), grid, block, 0, st,
+                       (const lumen::fp16*)k, (const lumen::fp16*)v, (lumen::fp8*)kc,
+                       (lumen::fp8*)vc, slots, ntok, nkv, D, BS, k_stride, v_stride);
+  else if (dtype == lumen::kBF16)
     hipLaunchKernelGGL(lumen::cache_write_kernel<lumen::bf16>, grid, block, 0, st,
                        (const lumen::bf16*)k, (const lumen::bf16*)v, (lumen::bf16*)kc,
                        (lumen::bf16*)vc, slots, ntok, nkv, D, BS, k_stride, v_stride);
@@ -535,12 +622,20 @@ extern "C" hipError_t lumen_reshape_and_cache(int dtype, const void* k, const vo
 extern "C" hipError_t lumen_rope_cache(int dtype, void* qkv, long long ld, const int* pos,
                                        const float* cos_t, const float* sin_t, void* kc, void* vc,
                                        const long long* slots, int ntok, int nh, int nkv, int D,
-                                       int BS, hipStream_t st) {
+                                       int BS, int fp8kv, hipStream_t st) {
   if (ntok == 0) return hipSuccess;
   if (D % 16 != 0) return hipErrorInvalidValue;
   const long long n = static_cast<long long>(ntok) * (nh + 2 * nkv) * (D / 16);
   dim3 block(256), grid(static_cast<unsigned>((n + 255) / 256));
-  if (dtype == lumen::kBF16)
+  if (fp8kv && dtype == lumen::kBF16)
+    hipLaunchKernelGGL((lumen::rope_cache_kernel<lumen::bf16, lumen::fp8>), grid, block, 0, st,
+                       (lumen::bf16*)qkv, ld, pos, cos_t, sin_t, (lumen::fp8*)kc,
+                       (lumen::fp8*)vc, slots, ntok, nh, nkv, D, BS);
+  else if (fp8kv && dtype == lumen::kF16)
+    hipLaunchKernelGGL((lumen::rope_cache_kernel<lumen::fp16, lumen::fp8>), grid, block, 0, st,
+                       (lumen::fp16*)qkv, ld, pos, cos_t, sin_t, (lumen::fp8*)kc,
+                       (lumen::fp8*)vc, slots, ntok, nh, nkv, D, BS);
+  else if (dtype == lumen::kBF16)
     hipLaunchKernelGGL(lumen::rope_cache_kernel<lumen::bf16>, grid, block, 0, st,
                        (lumen::bf16*)qkv, ld, pos, cos_t, sin_t, (lumen::bf16*)kc,
                        (lumen::bf16*)vc, slots, ntok, nh, nkv, D, BS);
@@ -548,6 +643,27 @@ extern "C" hipError_t lumen_rope_cache(int dtype, void* qkv, long long ld, const
     hipLaunchKernelGGL(lumen::rope_cache_kernel<lumen::fp16>, grid, block, 0, st,
                        (lumen::fp16*)qkv, ld, pos, cos_t, sin_t, (lumen::fp16*)kc,
                        (lumen::fp16*)vc, slots, ntok, nh, nkv, D, BS);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// fp8 cache blocks of the prefill sequences -> 16-bit scratch (see kv_dequant_kernel)
+extern "C" hipError_t lumen_kv_dequant(int dtype, const void* kc, const void* vc, void* ks,
+                                       void* vs, const int* tables, int tstride,
+                                       const int* kv_lens, int nseq, int maxb, int nkv, int BS,
+                                       int D, hipStream_t st) {
+  if (nseq == 0 || maxb == 0) return hipSuccess;
+  if ((nkv * BS * D) % 8) return hipErrorInvalidValue;
+  const dim3 grid(nseq, maxb, 2), block(256);
+  if (dtype == lumen::kBF16)
+    hipLaunchKernelGGL(lumen::kv_dequant_kernel<lumen::bf16>, grid, block, 0, st,
+                       (const lumen::fp8*)kc, (const lumen::fp8*)vc, (lumen::bf16*)ks,
+                       (lumen::bf16*)vs, tables, tstride, kv_lens, maxb, nkv, BS, D);
+  else if (dtype == lumen::kF16)
+    hipLaunchKernelGGL(lumen::kv_dequant_kernel<lumen::fp16>, grid, block, 0, st,
+                       (const lumen::fp8*)kc, (const lumen::fp8*)vc, (lumen::fp16*)ks,
+                       (lumen::fp16*)vs, tables, tstride, kv_lens, maxb, nkv, BS, D);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
+from ..ops.embedding import embedding
 from ..ops.lora import arena_reset
 from ..ops.activation import swiglu
 from ..ops.attention import causal_attention, flash_attention_qkv, prepare_varlen
@@ -172,7 +173,7 @@ class LlamaForCausalLM(nn.Module):
                                  zip(cu[:-1], cu[1:])]).to(input_ids.device)
             if input_ids.is_cuda:
                 prepare_varlen(cu, input_ids.device)  # tile lists: one async copy per step
-        h = self._run_unit(0, lambda ids: F.embedding(ids, self.embed_tokens.weight),
+        h = self._run_unit(0, lambda ids: embedding(ids, self.embed_tokens.weight),
                            input_ids.reshape(-1))
         res = None
         for i, layer in enumerate(self.layers):

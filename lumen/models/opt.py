@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
+from ..ops.embedding import embedding
 from ..ops.lora import arena_reset
 from ..ops._native import use_native
 from ..ops.attention import causal_attention, flash_attention_qkv
@@ -124,8 +125,8 @@ class OPTForCausalLM(nn.Module):
         pos = pos.long().reshape(B, S)
 
         def embed(ids, p):
-            return (F.embedding(ids, self.embed_tokens.weight)
-                    + F.embedding(p + 2, self.embed_positions.weight)).reshape(B * S, -1)
+            return (embedding(ids, self.embed_tokens.weight)
+                    + embedding(p + 2, self.embed_positions.weight)).reshape(B * S, -1)
 
         h = self._run_unit(0, embed, input_ids, pos)
         for i, layer in enumerate(self.layers):

@@ -132,13 +132,40 @@ def flash_attention_paged(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch
         cut = _cu_tensor(cu, dev)
         kl = (kv_lens if isinstance(kv_lens, torch.Tensor)
               else torch.tensor(list(kv_lens), dtype=torch.int32, device=dev))
-        native().flash_attn_paged(True, q, k_cache, v_cache, out, cut, kl.to(torch.int32),
-                                  _tiles(cu, 128, dev), block_tables.to(torch.int32), nh, nkv,
-                                  scale)
+        kl = kl.to(torch.int32)
+        bt = block_tables.to(torch.int32)
+        if k_cache.dtype == FP8_KV:
+            k_cache, v_cache, bt = _dequant_blocks(k_cache, v_cache, bt, kl, q.dtype)
+        native().flash_attn_paged(True, q, k_cache, v_cache, out, cut, kl,
+                                  _tiles(cu, 128, dev), bt, nh, nkv, scale)
         return out
     out.copy_(flash_attention_paged_ref(q, k_cache, v_cache, cu_q, kv_lens, block_tables, nh,
                                         nkv, D, scale))
     return out
+
+
+FP8_KV = torch.float8_e4m3fn  # fp8 KV-cache element type (OCP e4m3fn: gfx950's fp8 converts)
+_SCRATCH: dict = {}
+
+
+def _dequant_blocks(k_cache, v_cache, bt, kv_lens, dtype):
+    """fp8 cache -> 16-bit scratch holding only the prefill sequences' blocks (block b of
+    sequence s at s * maxb + b), plus the identity block table into it: the prefill kernel's
+    LDS-DMA staging moves raw 16-bit rows.  The scratch is reused by every layer and grows."""
+    P, maxb = bt.shape
+    nb, nkv, bs, D = k_cache.shape
+    need = P * maxb
+    key = (k_cache.device, dtype, nkv, bs, D)
+    scr = _SCRATCH.get(key)
+    if scr is None or scr[0].shape[0] < need:
+        n = max(need, 256)
+        scr = (torch.empty(n, nkv, bs, D, device=k_cache.device, dtype=dtype),
+               torch.empty(n, nkv, bs, D, device=k_cache.device, dtype=dtype),
+               torch.arange(n, device=k_cache.device, dtype=torch.int32))
+        _SCRATCH[key] = scr
+    ks, vs, ident = scr
+    native().kv_dequant(k_cache, v_cache, ks, vs, bt, kv_lens, maxb)
+    return ks, vs, ident[:need].view(P, maxb)
 
 
 def flash_attention_paged_ref(q, k_cache, v_cache, cu_q, kv_lens, block_tables, nh, nkv, D,

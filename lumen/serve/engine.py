@@ -53,6 +53,9 @@ class EngineConfig:
     # its decode tokens come from step t's sampled tokens ON THE DEVICE, and step t's tokens
     # reach the host afterwards (EOS / stop ids are seen one step late: one wasted row)
     async_scheduling: bool = True
+    # KV-cache element type: "auto" = model dtype; "fp8" = e4m3 (vLLM --kv-cache-dtype fp8):
+    # twice the cache capacity and half the K/V bytes per decode step, at fp8 K/V precision
+    kv_cache_dtype: str = "auto"
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -121,7 +124,10 @@ class LLMEngine:
         self.model_config = model.config
         tp_group = dist.group.WORLD if self.tp > 1 else None
         self.weights = ServeWeights(model, self.rank, self.tp)
-        nb = cfg.num_blocks or self._auto_blocks(dt)
+        if cfg.kv_cache_dtype not in ("auto", "fp8"):
+            raise ValueError(f"kv_cache_dtype must be 'auto' or 'fp8', got {cfg.kv_cache_dtype}")
+        self.kv_dtype = torch.float8_e4m3fn if cfg.kv_cache_dtype == "fp8" else dt
+        nb = cfg.num_blocks or self._auto_blocks(self.kv_dtype)
         self.blocks = BlockManager(nb, cfg.block_size)
         car = None
         if self.tp > 1 and dev.type == "cuda":
@@ -137,7 +143,8 @@ class LLMEngine:
                                    rows * vshard * esz))
         self.runner = ModelRunner(self.weights, nb, cfg.block_size, dev, cfg.max_model_len,
                                   tp_group, use_graphs=cfg.use_graphs,
-                                  max_graph_batch=min(256, cfg.max_num_seqs), custom_ar=car)
+                                  max_graph_batch=min(256, cfg.max_num_seqs), custom_ar=car,
+                                  kv_dtype=self.kv_dtype)
         self.lora_names: List[str] = []
         if cfg.lora_modules:
             from .multi_lora import MultiLoRA

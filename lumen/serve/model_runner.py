@@ -31,6 +31,7 @@ import torch.nn.functional as F
 from ..models.config import ModelConfig
 from ..ops._native import native, use_native
 from ..ops.activation import swiglu
+from ..ops.embedding import embedding
 from ..ops.attention import flash_attention_paged, paged_decode, rope_write_kv
 from ..ops.gemm import linear_nt, swiglu_linear_nt
 from ..ops.norm import rms_norm
@@ -116,7 +117,8 @@ def kv_bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2, tp_size: int = 1)
 class ModelRunner:
     def __init__(self, weights: ServeWeights, num_blocks: int, block_size: int,
                  device: torch.device, max_model_len: int = 4096, tp_group=None,
-                 use_graphs: bool = True, max_graph_batch: int = 256, custom_ar=None):
+                 use_graphs: bool = True, max_graph_batch: int = 256, custom_ar=None,
+                 kv_dtype: Optional[torch.dtype] = None):
         self.w = weights
         self.cfg = weights.cfg
         self.device = device
@@ -130,7 +132,11 @@ class ModelRunner:
         self.q_size, self.kv_size = self.w.nh * D, self.w.nkv * D
         self.max_blocks = (max_model_len + block_size - 1) // block_size
         dt = weights.dtype
-        self.k_cache = [torch.zeros(num_blocks, self.w.nkv, block_size, D, dtype=dt, device=device)
+        # KV-cache element type: the model dtype, or fp8 e4m3 (vLLM --kv-cache-dtype fp8: half
+        # the K/V bytes every decode step streams)
+        self.kv_dtype = kv_dtype or dt
+        self.k_cache = [torch.zeros(num_blocks, self.w.nkv, block_size, D, dtype=self.kv_dtype,
+                                    device=device)
                         for _ in range(cfg.num_hidden_layers)]
         self.v_cache = [torch.zeros_like(k) for k in self.k_cache]
         self.cos, self.sin = rope_tables(D, max(cfg.max_position_embeddings, max_model_len),
@@ -233,7 +239,7 @@ class ModelRunner:
     @torch.no_grad()
     def execute(self, inp: StepInput) -> torch.Tensor:
         """Logits [len(sample_rows), V] of one mixed step (see StepInput)."""
-        h = F.embedding(inp.tokens, self.w.embed)
+        h = embedding(inp.tokens, self.w.embed)
         T = inp.tokens.shape[0]
         Tp = inp.num_prefill_rows
         N = T - Tp
@@ -263,7 +269,7 @@ class ModelRunner:
     # ---- decode: one token per sequence ----------------------------------------------------
     def _decode_eager(self, tokens, positions, slots, block_tables, context_lens, max_context,
                       lora_ids=None, gather: bool = True):
-        h = F.embedding(tokens, self.w.embed)
+        h = embedding(tokens, self.w.embed)
         N = tokens.shape[0]
         nh, D = self.w.nh, self.cfg.head_dim
 

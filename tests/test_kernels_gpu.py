@@ -769,3 +769,84 @@ def test_opt_gpu_flash_matches_reference(monkeypatch):
     # layer growing smoothly to 8.5% at layer 0 of 12 (a kernel bug would show a step, not a ramp)
     rels = [rel(g1[n], g2[n]) for n in g1]
     assert rels[-1] < 3e-2 and max(rels) < 0.12, rels
+
+
+@pytest.mark.parametrize("H", [768, 4096, 8192])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_embedding_gather(H, dtype):
+    """HIP token-embedding gather == F.embedding (exact copy); out-of-range ids give zero rows."""
+    import torch.nn.functional as F
+
+    from lumen.ops._native import native
+    from lumen.ops.embedding import embedding
+
+    V = 1000
+    W = torch.randn(V, H, device=DEV).to(dtype)
+    ids = torch.randint(0, V, (3, 333), device=DEV)
+    out = embedding(ids, W)
+    assert out.shape == (3, 333, H)
+    assert torch.equal(out, F.embedding(ids, W))
+    bad = torch.tensor([0, V, -1, 5], device=DEV)
+    o = torch.empty(4, H, device=DEV, dtype=dtype)
+    native().embedding(W, bad, o)
+    assert torch.equal(o[0], W[0]) and torch.equal(o[3], W[5])
+    assert (o[1] == 0).all() and (o[2] == 0).all()
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (64, 8, 128), (12, 12, 64)])
+def test_fp8_kv_cache_kernels(nh, nkv, D):
+    """fp8 (e4m3fn) KV cache: the cache-write kernels round like torch's float8_e4m3fn cast, and
+    paged decode / chunked-prefill attention over the fp8 cache match the references computed
+    on the same (dequantised) cache."""
+    from lumen.ops.attention import (flash_attention_paged, flash_attention_paged_ref,
+                                     paged_decode, paged_decode_ref, rope_write_kv,
+                                     write_kv_cache)
+    from lumen.ops.rope import rope_tables
+
+    torch.manual_seed(0)
+    f8 = torch.float8_e4m3fn
+    bs, nseq, ctx = 16, 4, 300
+    maxb = (ctx + bs - 1) // bs
+    nblocks = nseq * maxb + 5
+    kc = torch.zeros(nblocks, nkv, bs, D, device=DEV, dtype=f8)
+    vc = torch.zeros_like(kc)
+    perm = torch.randperm(nblocks)[: nseq * maxb].view(nseq, maxb).int().to(DEV)
+    lens = torch.tensor([ctx, 17, 200, 129])
+    for i in range(nseq):
+        L = int(lens[i])
+        k = torch.randn(L, nkv, D, device=DEV, dtype=torch.bfloat16) * 3
+        v = torch.randn(L, nkv, D, device=DEV, dtype=torch.bfloat16)
+        t = torch.arange(L, device=DEV)
+        slots = perm[i, t // bs].long() * bs + t % bs
+        write_kv_cache(k, v, kc, vc, slots)
+        got_k = kc[perm[i, t // bs].long(), :, t % bs]
+        assert (got_k.float() == k.to(f8).float()).float().mean().item() > 0.999
+    q = torch.randn(nseq, nh, D, device=DEV, dtype=torch.bfloat16)
+    cl = lens.int().to(DEV)
+    scale = 1 / math.sqrt(D)
+    o2 = paged_decode_ref(q, kc, vc, perm, cl, scale)
+    for part in (512, 64):
+        assert rel(paged_decode(q, kc, vc, perm, cl, ctx, scale, part), o2) < 1e-2
+    if D == 128:  # chunked prefill over the fp8 cache (dequantised into the 16-bit scratch)
+        cu, kl = [0, 20, 37, 137, 138], [300, 17, 200, 129]
+        qr = (torch.randn(cu[-1], (nh + 2 * nkv) * D, device=DEV) * 0.5).to(torch.bfloat16)
+        got = flash_attention_paged(qr, kc, vc, cu, kl, perm, nh, nkv, D)
+        ref = flash_attention_paged_ref(qr.float(), kc, vc, cu, kl, perm, nh, nkv, D)
+        assert rel(got, ref) < 1e-2
+    # fused RoPE + fp8 cache write == RoPE + bf16 write, then cast
+    T = 50
+    qkv = torch.randn(T, (nh + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 400, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.arange(T, device=DEV, dtype=torch.int64) + 3 * bs
+    cos, sin = rope_tables(D, 4096, 10000.0, DEV)
+    k8, v8 = torch.zeros_like(kc), torch.zeros_like(vc)
+    kb = torch.zeros(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vb = torch.zeros_like(kb)
+    x1, x2 = qkv.clone(), qkv.clone()
+    rope_write_kv(x1, pos, nh, nkv, D, cos, sin, k8, v8, slots)
+    rope_write_kv(x2, pos, nh, nkv, D, cos, sin, kb, vb, slots)
+    assert torch.equal(x1, x2)
+    # rotated k goes f32 -> fp8 in the kernel, the reference f32 -> bf16 -> fp8: double rounding
+    # moves ~0.1% of elements by one fp8 step
+    assert (k8.float() == kb.to(f8).float()).float().mean().item() > 0.995
+    assert (v8.float() == vb.to(f8).float()).float().mean().item() > 0.999

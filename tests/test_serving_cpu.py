@@ -451,3 +451,24 @@ def test_async_scheduling_matches_sync(model):
         if a.finish_reason != "abort":
             assert a.output_ids == b.output_ids
     assert eng.blocks.num_free == 40 and eng.scheduler.num_preemptions > 0
+
+
+def test_fp8_kv_cache_engine_cpu(model):
+    """kv_cache_dtype="fp8": the cache holds float8_e4m3fn, the engine runs end to end
+    (reference paths on CPU), and the logits of a prefill + decode over the fp8 cache stay close
+    to the full-precision cache's (e4m3 keeps 3 mantissa bits: a few % per K/V element)."""
+    def logits(kv):
+        eng = _engine(model, num_blocks=200, kv_cache_dtype=kv)
+        eng.add_request(list(range(3, 40)), SamplingParams(max_tokens=4, temperature=0.0))
+        eng.step()  # prefill (writes the cache)
+        b = eng.scheduler.schedule()
+        return eng, eng.runner.execute(eng._build_input(b)).float()  # decode over the cache
+
+    e8, l8 = logits("fp8")
+    assert e8.runner.k_cache[0].dtype == torch.float8_e4m3fn
+    _, l16 = logits("auto")
+    rel = ((l8 - l16).norm() / l16.norm()).item()
+    assert rel < 0.1, rel
+    out = _engine(model, num_blocks=200, kv_cache_dtype="fp8").generate(
+        [[5, 17, 33, 9]], SamplingParams(max_tokens=8, temperature=0.0))
+    assert len(out[0].output_ids) == 8
