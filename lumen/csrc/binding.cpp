@@ -38,6 +38,11 @@ hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long
                        float, long long, long long, int, const long long*, const long long*,
                        const long long*, const int*, const float*, const float*, const int*, int,
                        hipStream_t);
+hipError_t lumen_rmsnorm_fwd_ld(int, const void*, const void*, const void*, void*, void*, float*,
+                                int, int, float, long long, hipStream_t);
+hipError_t lumen_lora3_z_tail(int, const float*, int, void*, long long, int, int, int, hipStream_t);
+hipError_t lumen_lora3_w_tail(int, void*, long long, int, const float*, int, int, const long long*,
+                              const long long*, const int*, const int*, float, hipStream_t);
 hipError_t lumen_embedding(const void*, const long long*, void*, int, int, int, hipStream_t);
 hipError_t lumen_lora3_down(int, const void*, long long, const float*, long long, float*, long long,
                             int, int, int, float, unsigned long long, unsigned int, float, long long,
@@ -129,12 +134,17 @@ T* ptr(const std::optional<at::Tensor>& t) {
 
 void rmsnorm_fwd(const at::Tensor& x, const std::optional<at::Tensor>& residual, const at::Tensor& w,
                  at::Tensor& y, const std::optional<at::Tensor>& s_out, at::Tensor& rstd, double eps) {
-  need_cuda(x, "x"); need_cuda(w, "w"); need_cuda(y, "y");
+  need_cuda(x, "x"); need_cuda(w, "w");
+  if (!y.is_cuda()) throw std::invalid_argument("lumen: y must be a GPU tensor");
   const int H = static_cast<int>(x.size(-1));
   const int rows = static_cast<int>(x.numel() / H);
-  check(lumen_rmsnorm_fwd(dcode(x), x.data_ptr(), ptr(residual), w.data_ptr(), y.data_ptr(),
-                          ptr(s_out), rstd.data_ptr<float>(), rows, H, static_cast<float>(eps),
-                          cur_stream()),
+  // y may be a row-strided view (unit column stride): ldy = its row stride
+  if (y.stride(-1) != 1 || y.numel() != x.numel())
+    throw std::invalid_argument("lumen: rmsnorm_fwd output must have x's shape and unit column stride");
+  const long long ldy = y.dim() >= 2 ? y.stride(-2) : H;
+  check(lumen_rmsnorm_fwd_ld(dcode(x), x.data_ptr(), ptr(residual), w.data_ptr(), y.data_ptr(),
+                             ptr(s_out), rstd.data_ptr<float>(), rows, H, static_cast<float>(eps),
+                             ldy, cur_stream()),
         "rmsnorm_fwd");
 }
 
@@ -432,6 +442,38 @@ void embedding(const at::Tensor& W, const at::Tensor& ids, at::Tensor& out) {
         "embedding");
 }
 
+// K-extended LoRA GEMM operands (see kernels/lora_v3.hip): Z tail of the activation buffer
+void lora3_z_tail(const at::Tensor& Z, at::Tensor& xe, int64_t K, int64_t KP) {
+  need_cuda_f32(Z, "lora3_z_tail Z");
+  if (!xe.is_cuda() || xe.dim() != 2 || xe.stride(1) != 1 || !Z.is_contiguous() ||
+      Z.size(0) > xe.size(0) || xe.size(1) < K + KP)
+    throw std::invalid_argument("lumen: lora3_z_tail: Z [T, R] f32, xe [T, >= K + KP] 16-bit");
+  check(lumen_lora3_z_tail(dcode(xe), Z.data_ptr<float>(), static_cast<int>(Z.size(1)),
+                           xe.data_ptr(), xe.stride(0), static_cast<int>(K), static_cast<int>(KP),
+                           static_cast<int>(Z.size(0)), cur_stream()),
+        "lora3_z_tail");
+}
+
+// segs: (n_off, b_off, n_len, r_off)
+void lora3_w_tail(at::Tensor& w, int64_t K, const at::Tensor& B, int64_t r,
+                  const std::vector<std::vector<int64_t>>& segs, double scale) {
+  need_cuda_f32(B, "lora3_w_tail B");
+  if (!w.is_cuda() || w.dim() != 2 || w.stride(1) != 1 || !B.is_contiguous())
+    throw std::invalid_argument("lumen: lora3_w_tail: w [N, K + KP] 16-bit, B [*, r] f32");
+  const int nseg = static_cast<int>(segs.size());
+  if (nseg < 1 || nseg > 4) throw std::invalid_argument("lumen: lora3_w_tail needs 1..4 segments");
+  long long no[4] = {0}, bo[4] = {0};
+  int nl[4] = {0}, ro[4] = {0};
+  for (int i = 0; i < nseg; ++i) {
+    no[i] = segs[i][0]; bo[i] = segs[i][1]; nl[i] = static_cast<int>(segs[i][2]);
+    ro[i] = static_cast<int>(segs[i][3]);
+  }
+  check(lumen_lora3_w_tail(dcode(w), w.data_ptr(), w.stride(0), static_cast<int>(K),
+                           B.data_ptr<float>(), static_cast<int>(r), nseg, no, bo, nl, ro,
+                           static_cast<float>(scale), cur_stream()),
+        "lora3_w_tail");
+}
+
 void transpose2d(const at::Tensor& in, at::Tensor& out) {
   if (!in.is_cuda() || !out.is_cuda() || in.dim() != 2 || out.dim() != 2)
     throw std::invalid_argument("lumen: transpose2d needs 2-D GPU tensors");
@@ -709,6 +751,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("lora3_down", &lora3_down);
   m.def("embedding", &embedding);
+  m.def("lora3_z_tail", &lora3_z_tail);
+  m.def("lora3_w_tail", &lora3_w_tail);
   m.def("kv_dequant", &kv_dequant);
   m.def("lora3_up", &lora3_up);
   m.def("lora3_dy", &lora3_dy);

@@ -499,6 +499,50 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// K-extension ("fold") of the forward UP into the frozen-weight GEMM:
+//   y = [x | Z | 0] [W | s B_bd | 0]^T   with the adapter tail of 64 extra K columns.
+// z_tail writes the (16-bit) Z tail of the activation operand next to x (which its producer --
+// RMSNorm / flash attention -- already wrote into the first K columns); w_tail refreshes the
+// weight tail s * B of every segment after an optimizer step (block-diagonal over segments:
+// rows of segment i use tail columns r_off_i .. r_off_i + r).
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) z_tail_kernel(const float* __restrict__ Z, int R,
+                                                     T* __restrict__ xe, long long ldx, int K,
+                                                     int KP, int T_) {
+  const int nch = KP / 8;
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= static_cast<long long>(T_) * nch) return;
+  const int t = static_cast<int>(i / nch), c = static_cast<int>(i % nch) * 8;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = c + e < R ? Z[static_cast<long long>(t) * R + c + e] : 0.f;
+  store8(xe + static_cast<long long>(t) * ldx + K + c, v);
+}
+
+struct TailSeg {
+  long long n_off[4], b_off[4];
+  int n_len[4], r_off[4];
+  int nseg;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) w_tail_kernel(T* __restrict__ w, long long ldw, int K,
+                                                     const float* __restrict__ B, int r,
+                                                     TailSeg sg, float scale) {
+  const int seg = blockIdx.y;
+  const int nch = r / 8;
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= static_cast<long long>(sg.n_len[seg]) * nch) return;
+  const int n = static_cast<int>(i / nch), c = static_cast<int>(i % nch) * 8;
+  float v[8];
+  load8(B + (sg.b_off[seg] + n) * r + c, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= scale;
+  store8(w + (sg.n_off[seg] + n) * ldw + K + sg.r_off[seg] + c, v);
+}
+
 }  // namespace lv3
 }  // namespace lumen
 
@@ -623,5 +667,43 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
   else if (dtype == kF16) { LV3_DY(fp16) }
   else return hipErrorInvalidValue;
 #undef LV3_DY
+  return hipGetLastError();
+}
+
+// xe[t, K + c] = c < R ? Z[t, c] : 0 for c < KP (16-bit xe, row stride ldx)
+extern "C" hipError_t lumen_lora3_z_tail(int dtype, const float* Z, int R, void* xe, long long ldx,
+                                         int K, int KP, int T, hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  if ((KP & 7) || R > KP || (ldx & 7) || (K & 7)) return hipErrorInvalidValue;
+  const long long n = static_cast<long long>(T) * (KP / 8);
+  const dim3 grid(static_cast<unsigned>((n + 255) / 256)), block(256);
+  if (dtype == kBF16) hipLaunchKernelGGL(lv3::z_tail_kernel<bf16>, grid, block, 0, st, Z, R, (bf16*)xe, ldx, K, KP, T);
+  else if (dtype == kF16) hipLaunchKernelGGL(lv3::z_tail_kernel<fp16>, grid, block, 0, st, Z, R, (fp16*)xe, ldx, K, KP, T);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// w[n_off + n, K + r_off + j] = scale * B[(b_off + n) * r + j] per segment (n < n_len, j < r)
+extern "C" hipError_t lumen_lora3_w_tail(int dtype, void* w, long long ldw, int K, const float* B,
+                                         int r, int nseg, const long long* n_off,
+                                         const long long* b_off, const int* n_len,
+                                         const int* r_off, float scale, hipStream_t st) {
+  if (nseg < 1 || nseg > 4 || (r & 7) || (ldw & 7) || (K & 7)) return hipErrorInvalidValue;
+  lv3::TailSeg sg;
+  sg.nseg = nseg;
+  int maxn = 0;
+  for (int i = 0; i < 4; ++i) {
+    const bool v = i < nseg;
+    sg.n_off[i] = v ? n_off[i] : 0; sg.b_off[i] = v ? b_off[i] : 0;
+    sg.n_len[i] = v ? n_len[i] : 0; sg.r_off[i] = v ? r_off[i] : 0;
+    if (v && (r_off[i] & 7)) return hipErrorInvalidValue;
+    if (v && n_len[i] > maxn) maxn = n_len[i];
+  }
+  if (maxn == 0) return hipSuccess;
+  const long long n = static_cast<long long>(maxn) * (r / 8);
+  const dim3 grid(static_cast<unsigned>((n + 255) / 256), nseg), block(256);
+  if (dtype == kBF16) hipLaunchKernelGGL(lv3::w_tail_kernel<bf16>, grid, block, 0, st, (bf16*)w, ldw, K, B, r, sg, scale);
+  else if (dtype == kF16) hipLaunchKernelGGL(lv3::w_tail_kernel<fp16>, grid, block, 0, st, (fp16*)w, ldw, K, B, r, sg, scale);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -25,7 +25,7 @@ template <typename T, int VPL, int WPR = 1>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
     const T* __restrict__ x, const T* __restrict__ residual, const T* __restrict__ w,
     T* __restrict__ y, T* __restrict__ s_out, float* __restrict__ rstd_out, int rows, int H,
-    float eps) {
+    float eps, long long ldy) {
   // WPR waves per row (2 at H > 2048: half the row registers per lane, more waves in flight);
   // their partial sums of squares meet in LDS
   __shared__ float part[4];
@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
       load8(w + c, wv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[j];
-      store8(y + base + c, o);
+      store8(y + static_cast<size_t>((rok ? row : 0)) * ldy + c, o);
     }
   }
 }
@@ -89,7 +89,7 @@ template <typename T, int VPT>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_row_kernel(
     const T* __restrict__ x, const T* __restrict__ residual, const T* __restrict__ w,
     T* __restrict__ y, T* __restrict__ s_out, float* __restrict__ rstd_out, int rows, int H,
-    float eps) {
+    float eps, long long ldy) {
   __shared__ float part[4];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row = blockIdx.x;
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_row_kernel(
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[i][j];
-      store8(y + base + c, o);
+      store8(y + static_cast<size_t>(row) * ldy + c, o);
     }
   }
 }
@@ -209,14 +209,15 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
 
 template <typename T>
 static hipError_t launch_fwd(const void* x, const void* res, const void* w, void* y, void* s_out,
-                             float* rstd, int rows, int H, float eps, hipStream_t st) {
+                             float* rstd, int rows, int H, float eps, long long ldy,
+                             hipStream_t st) {
   dim3 block(256);
   if (rows < 1024 && H <= 8192) {  // under ~4 waves per CU: one workgroup per row
     dim3 grid(rows);
     const int vpt = (H + 2047) / 2048;
 #define LUMEN_RMS_ROW(V)                                                                          \
   hipLaunchKernelGGL((rmsnorm_fwd_row_kernel<T, V>), grid, block, 0, st, (const T*)x,            \
-                     (const T*)res, (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps)
+                     (const T*)res, (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps, ldy)
     if (vpt <= 1) LUMEN_RMS_ROW(1);
     else if (vpt <= 2) LUMEN_RMS_ROW(2);
     else LUMEN_RMS_ROW(4);
@@ -233,7 +234,7 @@ static hipError_t launch_fwd(const void* x, const void* res, const void* w, void
   const int vpl = (H + 512 * wpr - 1) / (512 * wpr);
 #define LUMEN_RMS_FWD(V, W)                                                                       \
   hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, V, W>), grid, block, 0, st, (const T*)x,             \
-                     (const T*)res, (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps)
+                     (const T*)res, (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps, ldy)
   if (wpr == 1) {
     if (vpl <= 1) LUMEN_RMS_FWD(1, 1);
     else if (vpl <= 2) LUMEN_RMS_FWD(2, 1);
@@ -278,17 +279,26 @@ static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const
 
 }  // namespace lumen
 
+// y rows may be strided (ldy >= H): the q|k|v input of a K-extended LoRA GEMM is written straight
+// into the first H columns of its [rows, H + 64] operand buffer
+extern "C" hipError_t lumen_rmsnorm_fwd_ld(int dtype, const void* x, const void* residual,
+                                           const void* w, void* y, void* s_out, float* rstd,
+                                           int rows, int H, float eps, long long ldy,
+                                           hipStream_t st) {
+  if (H % 8 != 0 || ldy < H || (ldy % 8) != 0) return hipErrorInvalidValue;
+  if (dtype == lumen::kBF16)
+    return lumen::launch_fwd<lumen::bf16>(x, residual, w, y, s_out, rstd, rows, H, eps, ldy, st);
+  if (dtype == lumen::kF16)
+    return lumen::launch_fwd<lumen::fp16>(x, residual, w, y, s_out, rstd, rows, H, eps, ldy, st);
+  if (dtype == lumen::kF32)
+    return lumen::launch_fwd<float>(x, residual, w, y, s_out, rstd, rows, H, eps, ldy, st);
+  return hipErrorInvalidValue;
+}
+
 extern "C" hipError_t lumen_rmsnorm_fwd(int dtype, const void* x, const void* residual,
                                         const void* w, void* y, void* s_out, float* rstd, int rows,
                                         int H, float eps, hipStream_t st) {
-  if (H % 8 != 0) return hipErrorInvalidValue;
-  if (dtype == lumen::kBF16)
-    return lumen::launch_fwd<lumen::bf16>(x, residual, w, y, s_out, rstd, rows, H, eps, st);
-  if (dtype == lumen::kF16)
-    return lumen::launch_fwd<lumen::fp16>(x, residual, w, y, s_out, rstd, rows, H, eps, st);
-  if (dtype == lumen::kF32)
-    return lumen::launch_fwd<float>(x, residual, w, y, s_out, rstd, rows, H, eps, st);
-  return hipErrorInvalidValue;
+  return lumen_rmsnorm_fwd_ld(dtype, x, residual, w, y, s_out, rstd, rows, H, eps, H, st);
 }
 
 extern "C" hipError_t lumen_rmsnorm_bwd(int dtype, const void* dy, const void* s, const void* w,

@@ -14,6 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
+from ..ops import lora as lora_ops
 from ..ops.lora import lora_linear, linear
 from ..ops.transpose import transpose_2d
 from ..ops.norm import rms_norm
@@ -77,6 +78,9 @@ class Linear(nn.Module):
         self.transpose_gathered = False  # ... also for ZeRO-3-gathered weights (per step)
         self._wt: Optional[torch.Tensor] = None
         self._wt_key = None
+        self._wext: Optional[torch.Tensor] = None  # [W | s B_bd | 0] (LoRA fold), see fold_weight
+        self._wext_key = None
+        self._tail_key = None
 
     def weight_fn(self) -> torch.Tensor:
         return self.weight
@@ -106,6 +110,49 @@ class Linear(nn.Module):
 
     def invalidate_weight_cache(self):
         self._wt, self._wt_key = None, None
+        self._wext, self._wext_key, self._tail_key = None, None, None
+
+    # ---- LoRA fold: forward UP folded into the frozen-weight GEMM as 64 extra K columns --------
+    def fold_ext(self) -> int:
+        """Extra operand columns this linear's producer should leave after x (0 = no fold)."""
+        lo, W = self.lora, self.weight
+        if (not lora_ops.FOLD or lo is None or not self.lora_enabled or W.requires_grad
+                or not W.is_cuda or W.dtype not in (torch.bfloat16, torch.float16)
+                or getattr(W, "_lumen_gathered", False) or W.dim() != 2 or W.numel() == 0):
+            return 0
+        K = self.in_features
+        R = lo.lora_A.shape[0]
+        if (lo.r not in (16, 32, 64) or R > lora_ops.FOLD_KP or K % 8
+                or any(sg[0] % 8 or sg[1] % 8 or sg[2] % 8 for sg in lo.segs)
+                or lo.lora_A.dtype != torch.float32 or not lo.lora_B.is_contiguous()):
+            return 0
+        return lora_ops.FOLD_KP
+
+    def fold_weight(self) -> Optional[torch.Tensor]:
+        """[N, K + 64] bf16/fp16 = [W | s B_bd | 0]: W copied when the weight changes, the tail
+        (scale x lora_B, block-diagonal over segments) refreshed when lora_B changes (the
+        optimizer's publish bumps its version counter)."""
+        if not self.fold_ext():
+            return None
+        lo, W = self.lora, self.weight
+        K, KP = self.in_features, lora_ops.FOLD_KP
+        key = (W.data_ptr(), W._version, tuple(W.shape), W.dtype)
+        if self._wext is None or self._wext_key != key:
+            with torch.no_grad():
+                self._wext = torch.zeros(W.shape[0], K + KP, dtype=W.dtype, device=W.device)
+                self._wext[:, :K].copy_(W)
+            self._wext_key = key
+            self._tail_key = None
+        B = lo.lora_B
+        tkey = (B.data_ptr(), B._version, lo.scale)
+        if self._tail_key != tkey:
+            from ..ops._native import native
+
+            native().lora3_w_tail(self._wext, K, B.detach(), lo.r,
+                                  [(n_off, b_off, n_len, r_off)
+                                   for (n_off, n_len, r_off, b_off) in lo.segs], lo.scale)
+            self._tail_key = tkey
+        return self._wext
 
     def seg_offset(self, name: str) -> Tuple[int, int]:
         i = self.seg_names.index(name)
@@ -131,8 +178,10 @@ class Linear(nn.Module):
             # seed drawn from torch's global CPU RNG: activation checkpointing restores that state
             # before recomputing, so the recomputed forward regenerates the same dropout mask
             seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+            fold = (self.fold_weight() if x.dim() == 2
+                    and lora_ops.fold_operand(x, self.in_features) is not None else None)
             return lora_linear(x, self.weight_fn, self.bias, lo.lora_A, lo.lora_B, lo.segs, lo.r,
-                               lo.scale, p, seed, self.weight, self._wt_fn(), rope)
+                               lo.scale, p, seed, self.weight, self._wt_fn(), rope, fold)
         if rope is not None:
             raise ValueError("fused RoPE needs an active LoRA adapter on this linear")
         return linear(x, self.weight_fn, self.bias, self.weight, self._wt_fn())
@@ -226,5 +275,7 @@ class RMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.ones(hidden, dtype=dtype, device=device), requires_grad=False)
 
-    def forward(self, x, residual=None):
-        return rms_norm(x, self.weight, self.eps, residual)
+    def forward(self, x, residual=None, ext: int = 0):
+        """``ext`` > 0: y is written into the first H columns of a [rows, H + ext] buffer and
+        returned as that view (the operand of a K-extended LoRA GEMM, ``Linear.fold_ext``)."""
+        return rms_norm(x, self.weight, self.eps, residual, ext)

@@ -60,7 +60,8 @@ class LlamaAttention(nn.Module):
             # the FA backward undoes the rotation in its dQ / dK epilogues (FUSED_ROPE_BWD)
             o = flash_attention_qkv(qkv, cu if cu is not None else tuple(range(0, B * S + 1, S)),
                                     nh, nkv, D, True,
-                                    rope=(pos, cos, sin) if FUSED_ROPE_BWD else None)
+                                    rope=(pos, cos, sin) if FUSED_ROPE_BWD else None,
+                                    out_ext=self.o_proj.fold_ext())
             return self.o_proj(o)
         qkv = self.qkv_proj(x2d)
         if cu is not None:  # packed rows, portable path: one causal block per sequence
@@ -111,7 +112,8 @@ class LlamaDecoderLayer(nn.Module):
         self.mlp = LlamaMLP(cfg, dtype, device)
 
     def forward(self, h, res, B: int, S: int, pos=None, cu=None):
-        y, s = self.input_layernorm(h, res)
+        # q|k|v LoRA fold: RMSNorm writes y into the first H columns of the GEMM's extended operand
+        y, s = self.input_layernorm(h, res, self.self_attn.qkv_proj.fold_ext())
         a = self.self_attn(y, B, S, pos, cu)
         y2, s2 = self.post_attention_layernorm(a, s)
         return self.mlp(y2), s2

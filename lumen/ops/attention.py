@@ -322,13 +322,15 @@ FA_DQ_DELTA = _os.environ.get("LUMEN_FA_DQ_DELTA", "0") == "1"
 
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cu, nh, nkv, D, causal, rope=None, scale=None):
+    def forward(ctx, qkv, cu, nh, nkv, D, causal, rope=None, scale=None, out_ext=0):
         C = native()
         T = qkv.shape[0]
         q = qkv[:, :nh * D]
         k = qkv[:, nh * D:(nh + nkv) * D]
         v = qkv[:, (nh + nkv) * D:]
-        o = torch.empty(T, nh * D, device=qkv.device, dtype=qkv.dtype)
+        # out_ext > 0: O is the first nh*D columns of a [T, nh*D + out_ext] buffer (the operand
+        # of the o_proj's K-extended LoRA GEMM); the kernels take the row stride
+        o = torch.empty(T, nh * D + out_ext, device=qkv.device, dtype=qkv.dtype)[:, :nh * D]
         lse = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
         cut = _cu_tensor(cu, qkv.device)
         scale = 1.0 / math.sqrt(D) if scale is None else scale
@@ -381,7 +383,7 @@ class _FlashAttn(torch.autograd.Function):
                          scale, do, dq, dk, dv, delta, pos, cos, sin)
         if rp is not None:
             dqkv._lumen_rope_undone = True
-        return dqkv, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None
 
 
 KERNEL_D = 128  # head dim of the HIP flash-attention kernels
@@ -400,7 +402,7 @@ def _flash_padded(qkv, cu, nh, nkv, D, causal):
 
 
 def flash_attention_qkv(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int,
-                        causal: bool = True, rope=None) -> torch.Tensor:
+                        causal: bool = True, rope=None, out_ext: int = 0) -> torch.Tensor:
     """Causal attention straight from the fused token-major QKV buffer [T, (nh+2nkv)*D]
     (q/k already rotated); returns O token-major [T, nh*D].  ``cu_seqlens``: sequence offsets.
 
@@ -409,7 +411,7 @@ def flash_attention_qkv(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int
     dQKV tensor so the producer's backward skips its inverse pass)."""
     cu = tuple(int(c) for c in cu_seqlens)
     if use_native(qkv) and D == KERNEL_D:
-        return _FlashAttn.apply(qkv, cu, nh, nkv, D, causal, rope)
+        return _FlashAttn.apply(qkv, cu, nh, nkv, D, causal, rope, None, out_ext)
     if use_native(qkv) and D < KERNEL_D and D % 8 == 0 and rope is None:
         return _flash_padded(qkv.contiguous(), cu, nh, nkv, D, causal)
     return flash_attention_ref(qkv, cu, nh, nkv, D, causal)

@@ -244,6 +244,23 @@ def _side_stream(device) -> "torch.cuda.Stream":
     return s
 
 
+# LUMEN_LORA_FOLD (default on): the forward UP product is folded into the frozen-weight GEMM as
+# 64 extra K columns, y = [x | Z | 0] [W | s B_bd | 0]^T, for persistent 16-bit weights whose
+# input producer wrote x into the first K columns of a [T, K + 64] buffer (RMSNorm for q|k|v,
+# flash attention for o): the 16-bit read-modify-write of y disappears; RoPE then runs as its
+# own pass over q|k.
+FOLD = _os.environ.get("LUMEN_LORA_FOLD", "1") != "0"
+FOLD_KP = 64
+
+
+def fold_operand(x2d: torch.Tensor, K: int) -> Optional[torch.Tensor]:
+    """The [T, K + FOLD_KP] operand behind a producer's [T, K] view of it, else None."""
+    if (x2d.dim() == 2 and x2d.shape[1] == K and x2d.stride(1) == 1
+            and x2d.stride(0) == K + FOLD_KP and x2d.is_cuda):
+        return x2d.as_strided((x2d.shape[0], K + FOLD_KP), (K + FOLD_KP, 1))
+    return None
+
+
 def _dy_tw(segs, T: int) -> int:
     """dY rows per block of lora3_dy: 256 unless that leaves fewer than 512 blocks (dZ / dB
     atomics grow as the tile shrinks: 128 only for narrow outputs such as o_proj)."""
@@ -449,9 +466,9 @@ def _direct_ok(prm: torch.Tensor) -> bool:
 class _LoraLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, weight_fn, bias, A, B, segs, r, scale, p, seed, w_param, wt_fn, train,
-                rope):
+                rope, fold=None):
         ctx.train = train
-        W = weight_fn()
+        W = weight_fn() if fold is None else None
 
         def gemm():
             y_ = torch.matmul(x2d, W.t())
@@ -460,7 +477,18 @@ class _LoraLinear(torch.autograd.Function):
             return y_
 
         # autograd runs Function.forward with grad disabled: the training flag is passed in
-        if OVERLAP and x2d.is_cuda:
+        if fold is not None:
+            T, K = x2d.shape
+            R = A.shape[0]
+            xe = fold_operand(x2d, K)
+            Z = _zeros(T, R, device=x2d.device, train=ctx.train)
+            _lora3_down(x2d, A, Z, p, seed)
+            native().lora3_z_tail(Z, xe, K, FOLD_KP)
+            y = torch.matmul(xe, fold.t())
+            if bias is not None:
+                y.add_(bias)
+            rope_done = False
+        elif OVERLAP and x2d.is_cuda:
             Z, rope_done, y = lora_fwd_native(x2d, None, A, B, segs, r, scale, p, seed,
                                               train=ctx.train, rope=rope, gemm=gemm)
         else:
@@ -508,7 +536,7 @@ class _LoraLinear(torch.autograd.Function):
             dx = held["dx"]
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
-        return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None, None
+        return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None, None, None
 
 
 class _Linear(torch.autograd.Function):
@@ -575,14 +603,20 @@ def _frozen(W: torch.Tensor) -> torch.Tensor:
 
 def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: torch.Tensor,
                 B: torch.Tensor, segs: List[Seg], r: int, scale: float, p: float, seed: int,
-                w_param: Optional[torch.Tensor] = None, wt_fn=None, rope=None) -> torch.Tensor:
+                w_param: Optional[torch.Tensor] = None, wt_fn=None, rope=None,
+                fold: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``rope`` (GPU path only) = (pos int32 [T], cos, sin, ncols): the output's columns
-    [0, ncols) come back rotated (RoPE fused into the adapter write-back when possible)."""
+    [0, ncols) come back rotated (RoPE fused into the adapter write-back when possible).
+    ``fold`` = the [N, K + 64] extended weight [W | s B_bd | 0] (x must then be the [T, K] view
+    of a [T, K + 64] buffer, see ``fold_operand``)."""
     shp = x.shape
     x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
     if use_native(x2d):
-        y = _LoraLinear.apply(x2d.contiguous(), weight_fn, bias, A, B, segs, r, scale, p, seed,
-                              w_param, wt_fn, torch.is_grad_enabled(), rope)
+        if fold is not None and fold_operand(x2d, x2d.shape[1]) is None:
+            fold = None
+        y = _LoraLinear.apply(x2d if fold is not None else x2d.contiguous(), weight_fn, bias, A,
+                              B, segs, r, scale, p, seed, w_param, wt_fn,
+                              torch.is_grad_enabled(), rope, fold)
     else:
         y = lora_linear_ref(x2d, _frozen(weight_fn()), bias, A, B, segs, r, scale, p, seed)
     return y if x.dim() == 2 else y.view(*shp[:-1], y.shape[-1])

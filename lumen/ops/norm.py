@@ -25,10 +25,15 @@ def rms_norm_ref(x, w, eps, residual=None):
 
 class _FusedAddRMSNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, w, eps):
+    def forward(ctx, x, residual, w, eps, ext=0):
         C = native()
         x = x.contiguous()
-        y = torch.empty_like(x)
+        if ext and x.dim() == 2:
+            # y as the first H columns of a [rows, H + ext] buffer (row-strided kernel output)
+            y = torch.empty(x.shape[0], x.shape[1] + ext, dtype=x.dtype,
+                            device=x.device)[:, :x.shape[1]]
+        else:
+            y = torch.empty_like(x)
         rows = x.numel() // x.shape[-1]
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
         if residual is not None:
@@ -54,13 +59,14 @@ class _FusedAddRMSNorm(torch.autograd.Function):
         C.rmsnorm_bwd(dy.contiguous(), s, w, rstd,
                       ds.contiguous() if ds is not None else None, dx, dw)
         dres = dx if ctx.has_res else None
-        return dx, dres, (dw.to(w.dtype) if dw is not None else None), None
+        return dx, dres, (dw.to(w.dtype) if dw is not None else None), None, None
 
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
-             residual: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+             residual: Optional[torch.Tensor] = None,
+             ext: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     if use_native(x):
-        return _FusedAddRMSNorm.apply(x, residual, w, eps)
+        return _FusedAddRMSNorm.apply(x, residual, w, eps, ext)
     return rms_norm_ref(x, w, eps, residual)
 
 

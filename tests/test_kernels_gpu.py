@@ -850,3 +850,49 @@ def test_fp8_kv_cache_kernels(nh, nkv, D):
     # moves ~0.1% of elements by one fp8 step
     assert (k8.float() == kb.to(f8).float()).float().mean().item() > 0.995
     assert (v8.float() == vb.to(f8).float()).float().mean().item() > 0.999
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_llama_lora_fold_matches_unfolded(p_drop, monkeypatch):
+    """The K-extended forward ([x | Z | 0] [W | s B_bd | 0]^T GEMM, RMSNorm / flash attention
+    writing into the extended operand, RoPE as its own pass) == the unfolded UP write-back:
+    same loss and adapter gradients, and the folded path is really taken."""
+    import lumen.ops.lora as lora_mod
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+
+    torch.manual_seed(0)
+    m = build_model("small-llama", dtype=torch.bfloat16, device=torch.device("cuda"), init="random",
+                    seed=5)
+    apply_lora(m, LoraConfig(r=16, lora_dropout=p_drop))
+    with torch.no_grad():
+        for _, mod in m.lora_modules():
+            mod.lora.lora_B.normal_(0, 0.02)
+    m.train()
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(3, m.config.vocab_size, (2, 200), generator=g).cuda()
+    labels = torch.roll(ids, -1, 1)
+    outs = []
+    for fold in (True, False):
+        monkeypatch.setattr(lora_mod, "FOLD", fold)
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(7)  # same dropout seeds on both passes
+        loss = m(ids, labels)
+        loss.backward()
+        outs.append((loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters()
+                                   if p.requires_grad}))
+        if fold:
+            assert all(mod._wext is not None for _, mod in m.lora_modules())
+    (l1, g1), (l2, g2) = outs
+    assert abs(l1 - l2) < 2e-3 * abs(l2)
+    for n in g1:
+        assert rel(g1[n], g2[n]) < 3e-2, n
+    # an optimizer-style in-place update of lora_B refreshes the folded weight's tail
+    monkeypatch.setattr(lora_mod, "FOLD", True)
+    mod = next(mod for _, mod in m.lora_modules())
+    w1 = mod.fold_weight().clone()
+    with torch.no_grad():
+        mod.lora.lora_B.add_(0.01)
+    w2 = mod.fold_weight()
+    K = mod.in_features
+    assert torch.equal(w1[:, :K], w2[:, :K]) and not torch.equal(w1[:, K:], w2[:, K:])
