@@ -113,13 +113,22 @@ class Linear(nn.Module):
         self._wext, self._wext_key, self._tail_key = None, None, None
 
     # ---- LoRA fold: forward UP folded into the frozen-weight GEMM as 64 extra K columns --------
-    def fold_ext(self) -> int:
-        """Extra operand columns this linear's producer should leave after x (0 = no fold)."""
+    def fold_ext(self, static: bool = False) -> int:
+        """Extra operand columns this linear's producer should leave after x (0 = no fold).
+        ``static``: eligibility of the layer itself (the ZeRO-3 layout asks before the weight
+        is partitioned); otherwise also of the weight as currently bound."""
         lo, W = self.lora, self.weight
         if (not lora_ops.FOLD or lo is None or not self.lora_enabled or W.requires_grad
-                or not W.is_cuda or W.dtype not in (torch.bfloat16, torch.float16)
-                or getattr(W, "_lumen_gathered", False) or W.dim() != 2 or W.numel() == 0):
+                or not W.is_cuda or W.dtype not in (torch.bfloat16, torch.float16)):
             return 0
+        if not static:
+            if W.dim() != 2 or W.numel() == 0:
+                return 0
+            # gathered ZeRO-3 weights fold only when the partitioned layout reserved the tail
+            if getattr(W, "_lumen_gathered", False) and (
+                    getattr(W, "_lumen_fold_kp", 0) != lora_ops.FOLD_KP
+                    or W.stride(0) != self.in_features + lora_ops.FOLD_KP):
+                return 0
         K = self.in_features
         R = lo.lora_A.shape[0]
         if (lo.r not in (16, 32, 64) or R > lora_ops.FOLD_KP or K % 8
@@ -136,6 +145,16 @@ class Linear(nn.Module):
             return None
         lo, W = self.lora, self.weight
         K, KP = self.in_features, lora_ops.FOLD_KP
+        if W.stride(0) == K + KP and W.stride(1) == 1:
+            # the weight itself lives in [N, K + KP] rows (ZeRO-3 layout): fold in place
+            wext = W.as_strided((W.shape[0], K + KP), (K + KP, 1))
+            if getattr(W, "_lumen_gathered", False):
+                return wext  # tail filled by the coordinator when the unit was bound
+            tkey = (W.data_ptr(), lo.lora_B.data_ptr(), lo.lora_B._version, lo.scale)
+            if self._tail_key != tkey:
+                self._fill_tail(wext)
+                self._tail_key = tkey
+            return wext
         key = (W.data_ptr(), W._version, tuple(W.shape), W.dtype)
         if self._wext is None or self._wext_key != key:
             with torch.no_grad():
@@ -146,13 +165,24 @@ class Linear(nn.Module):
         B = lo.lora_B
         tkey = (B.data_ptr(), B._version, lo.scale)
         if self._tail_key != tkey:
-            from ..ops._native import native
-
-            native().lora3_w_tail(self._wext, K, B.detach(), lo.r,
-                                  [(n_off, b_off, n_len, r_off)
-                                   for (n_off, n_len, r_off, b_off) in lo.segs], lo.scale)
+            self._fill_tail(self._wext)
             self._tail_key = tkey
         return self._wext
+
+    def _fill_tail(self, wext: torch.Tensor) -> None:
+        from ..ops._native import native
+
+        lo = self.lora
+        native().lora3_w_tail(wext, self.in_features, lo.lora_B.detach(), lo.r,
+                              [(n_off, b_off, n_len, r_off)
+                               for (n_off, n_len, r_off, b_off) in lo.segs], lo.scale)
+
+    def fill_fold_tail(self) -> None:
+        """ZeRO-3: write s * lora_B into the tail of the freshly gathered [N, K + KP] weight."""
+        W = self.weight
+        K, KP = self.in_features, lora_ops.FOLD_KP
+        if self.lora is not None and W.numel() and W.stride(0) == K + KP:
+            self._fill_tail(W.as_strided((W.shape[0], K + KP), (K + KP, 1)))
 
     def seg_offset(self, name: str) -> Tuple[int, int]:
         i = self.seg_names.index(name)

@@ -113,6 +113,9 @@ class _Unit:
         self.dtype = None
         # W^T copies made off the critical path (keep / pipelined): (param idx, off, wt_off)
         self.tn: List[tuple] = []
+        # LoRA-folded linears of this unit: their weights are stored as [N, K + KP] rows (the
+        # adapter tail of the K-extended GEMM); the tail is filled at every bind
+        self.folds: List[nn.Module] = []
         self.wt_numel = 0
         self.wt_bufs: List[Optional[torch.Tensor]] = []
         self.wt_events: List[Optional[object]] = []
@@ -144,6 +147,7 @@ class ParamCoordinator:
         elif schedule == "identity":
             raise ValueError("the identity schedule needs world size 1 and no param offload")
         mark_zero_shapes(model)
+        fold_lin = _mark_fold_weights(model)
         owner: Dict[int, int] = {}
         self.units: List[_Unit] = []
         self.persistent: List[nn.Parameter] = []
@@ -164,6 +168,8 @@ class ParamCoordinator:
                         continue
                     owner[id(p)] = i
                     u.params.append(p)
+                    if id(p) in fold_lin:
+                        u.folds.append(fold_lin[id(p)])
             self.units.append(u)
         total = 0
         for u in self.units:
@@ -171,12 +177,13 @@ class ParamCoordinator:
                 continue
             u.dtype = u.params[0].dtype
             assert all(p.dtype == u.dtype for p in u.params), "a unit must have one dtype"
-            u.numel = sum(p.numel() for p in u.params)
+            u.numel = sum(_store_numel(p) for p in u.params)
             u.padded = _round_up(u.numel, W * ALIGN)
             total += u.padded
             s = u.padded // W
             r0 = env.rank * s
-            flat = torch.cat([p.data.reshape(-1) for p in u.params])
+            flat = torch.cat([_stored(p.data, getattr(p, "_lumen_fold_kp", 0)).reshape(-1)
+                              for p in u.params])
             if flat.numel() < u.padded:
                 flat = torch.cat([flat, flat.new_zeros(u.padded - flat.numel())])
             shard = flat[r0:r0 + s].clone() if W > 1 else flat
@@ -382,8 +389,9 @@ class ParamCoordinator:
             full, wt = u.bufs[slot], u.wt_bufs[slot]
             for k, off, wt_off in u.tn:
                 rows, cols = u.params[k]._zero_shape
-                transpose_2d(full[off:off + rows * cols].view(rows, cols),
-                             out=wt[wt_off:wt_off + rows * cols].view(cols, rows))
+                kp = getattr(u.params[k], "_lumen_fold_kp", 0)
+                src = full[off:off + rows * (cols + kp)].view(rows, cols + kp)[:, :cols]
+                transpose_2d(src, out=wt[wt_off:wt_off + rows * cols].view(cols, rows))
             ev = torch.cuda.Event()
             ev.record(side)
         u.wt_events[slot] = ev
@@ -406,7 +414,7 @@ class ParamCoordinator:
                         and shape[1] % 8 == 0 and p.dtype in (torch.bfloat16, torch.float16)):
                     tn.append((k, o, wo))
                     wo += n
-                o += n
+                o += _store_numel(p)
             plan.append((u, tn, wo))
             need += wo * (u.dtype.itemsize if u.dtype is not None else 2) * len(u.bufs)
         free, total = torch.cuda.mem_get_info(self.device)
@@ -426,8 +434,12 @@ class ParamCoordinator:
         o = 0
         for p in u.params:
             shape = p._zero_shape
-            n = math.prod(shape)
-            p.data = full[o:o + n].view(shape)
+            n = _store_numel(p)
+            kp = getattr(p, "_lumen_fold_kp", 0)
+            if kp:  # [N, K + KP] storage rows, the parameter is the [N, K] view
+                p.data = full[o:o + n].view(shape[0], shape[1] + kp)[:, :shape[1]]
+            else:
+                p.data = full[o:o + n].view(shape)
             o += n
 
     def _wait_work(self, work):
@@ -472,6 +484,8 @@ class ParamCoordinator:
             u.states[s] = "ready"
         if u.bound != s:
             self._bind_views(u, u.bufs[s])
+            for lin in u.folds:  # freshly gathered: the adapter tail comes from lora_B
+                lin.fill_fold_tail()
             if u.tn:
                 if u.wt_events[s] is not None:
                     torch.cuda.current_stream(self.device).wait_event(u.wt_events[s])
@@ -645,6 +659,29 @@ class ParamCoordinator:
 
 def units_dtype_bytes(units: Sequence[_Unit]) -> int:
     return max((u.dtype.itemsize for u in units if u.params), default=2)
+
+
+def _store_numel(p) -> int:
+    """Elements of p in the unit's flat storage ([N, K + KP] rows for a LoRA-folded weight)."""
+    kp = getattr(p, "_lumen_fold_kp", 0)
+    shape = getattr(p, "_zero_shape", tuple(p.shape))
+    return shape[0] * (shape[1] + kp) if kp else math.prod(shape)
+
+
+def _stored(t: torch.Tensor, kp: int) -> torch.Tensor:
+    return torch.nn.functional.pad(t, (0, kp)) if kp else t
+
+
+def _mark_fold_weights(model: nn.Module) -> Dict[int, nn.Module]:
+    """Linears whose LoRA forward will run K-extended: tag their frozen weight with the tail
+    width (``_lumen_fold_kp``) so the partitioned layout reserves it.  {id(weight): linear}"""
+    out: Dict[int, nn.Module] = {}
+    for m in model.modules():
+        f = getattr(m, "fold_ext", None)
+        if f is not None and f(static=True):
+            m.weight._lumen_fold_kp = f(static=True)
+            out[id(m.weight)] = m
+    return out
 
 
 def mark_zero_shapes(model: nn.Module):

@@ -12,17 +12,23 @@ pytestmark = pytest.mark.gpu
 
 
 def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_wt="none",
-           config=None, max_live=None):
+           config=None, max_live=None, fold=False):
     from lumen.lora import LoraConfig, adapter_state_dict, apply_lora
     from lumen.models import build_model
     from lumen.parallel.dist import init
     from lumen.train.config import load_ds_config
     from lumen.train.engine import ZeroEngine
 
+    import lumen.ops.lora as lora_mod
+
     monkeypatch.setenv("LUMEN_ZERO3_SINGLE", "1")
     # same backward GEMM layout on both sides (persistent weights would otherwise use cached
-    # W^T while gathered ones do not: bf16 rounding differences that Adam amplifies)
+    # W^T while gathered ones do not: bf16 rounding differences that Adam amplifies); for the
+    # same reason no LoRA fold here (a folded gathered weight is a row-strided [N, K + 64] view,
+    # a persistent one contiguous: different GEMM algorithms) -- the fold on gathered weights
+    # has its own test below
     monkeypatch.setenv("LUMEN_BWD_WT", bwd_wt)
+    monkeypatch.setattr(lora_mod, "FOLD", fold)
     if schedule:
         monkeypatch.setenv("LUMEN_ZERO3_SCHEDULE", schedule)
     torch.manual_seed(0)
@@ -134,3 +140,53 @@ def test_zero3_schedules_race_free_under_nan_poison(schedule, monkeypatch):
     for k in ref:
         assert torch.isfinite(got[k]).all(), k
         torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)
+
+
+@pytest.mark.parametrize("schedule", ["pipelined", "release"])
+def test_zero3_gathered_lora_fold(schedule, monkeypatch):
+    """LoRA fold on ZeRO-3-gathered weights: the partitioned layout reserves the [N, K + 64]
+    adapter tail, the coordinator fills it (s * lora_B) at every bind, and one micro-step's loss
+    and adapter gradients equal the unfolded UP write-back's (gradients compared before any
+    optimizer step, where bf16 rounding is not amplified)."""
+    import lumen.ops.lora as lora_mod
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+    from lumen.parallel.dist import init
+    from lumen.train.config import load_ds_config
+    from lumen.train.engine import ZeroEngine
+
+    monkeypatch.setenv("LUMEN_ZERO3_SINGLE", "1")
+    monkeypatch.setenv("LUMEN_ZERO3_SCHEDULE", schedule)
+    out = []
+    for fold in (True, False):
+        monkeypatch.setattr(lora_mod, "FOLD", fold)
+        torch.manual_seed(0)
+        m = build_model("small-llama", dtype=torch.bfloat16, device=torch.device("cuda"), seed=3)
+        apply_lora(m, LoraConfig(r=16, lora_dropout=0.0))
+        with torch.no_grad():
+            for _, mod in m.lora_modules():
+                mod.lora.lora_B.normal_(0, 0.02, generator=torch.Generator(
+                    device="cuda").manual_seed(11))
+        m.train()
+        z = {"stage": 3, "stage3_param_persistence_threshold": 1e4}
+        if schedule == "release":
+            z["stage3_max_live_parameters"] = 1
+        eng = ZeroEngine(m, load_ds_config({"zero_optimization": z}, 2, 1, 1, 1e-3), init())
+        coord = eng.coordinator
+        assert coord is not None and coord.schedule == schedule
+        if fold:
+            assert all(len(u.folds) == 2 for u in coord.units[1:-1])  # q|k|v and o per layer
+        g = torch.Generator(device="cpu").manual_seed(5)
+        ids = torch.randint(3, m.config.vocab_size, (2, 64), generator=g).cuda()
+        loss = eng.forward({"input_ids": ids, "labels": torch.roll(ids, -1, 1)})
+        eng.backward(loss)
+        torch.cuda.synchronize()
+        grads = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.requires_grad}
+        out.append((float(loss), grads))
+        eng.step()
+        eng.close()
+    (l1, g1), (l2, g2) = out
+    assert abs(l1 - l2) < 2e-3 * abs(l2)
+    for n in g1:
+        r = ((g1[n] - g2[n]).norm() / g2[n].norm().clamp_min(1e-12)).item()
+        assert r < 3e-2, (n, r)
