@@ -43,6 +43,9 @@ hipError_t lumen_rmsnorm_fwd_ld(int, const void*, const void*, const void*, void
 hipError_t lumen_lora3_z_tail(int, const float*, int, void*, long long, int, int, int, hipStream_t);
 hipError_t lumen_lora3_w_tail(int, void*, long long, int, const float*, int, int, const long long*,
                               const long long*, const int*, const int*, float, hipStream_t);
+hipError_t lumen_lora3_dxa(int, const void*, long long, void*, long long, const float*, const float*,
+                           long long, float*, long long, int, int, int, int, unsigned long long,
+                           unsigned int, float, long long, long long, hipStream_t);
 hipError_t lumen_embedding(const void*, const long long*, void*, int, int, int, hipStream_t);
 hipError_t lumen_lora3_down(int, const void*, long long, const float*, long long, float*, long long,
                             int, int, int, float, unsigned long long, unsigned int, float, long long,
@@ -474,6 +477,29 @@ void lora3_w_tail(at::Tensor& w, int64_t K, const at::Tensor& B, int64_t r,
         "lora3_w_tail");
 }
 
+// fused x-side LoRA backward (kernels/lora_v3.hip dxa3_kernel)
+void lora3_dxa(const at::Tensor& x, at::Tensor& dx, const at::Tensor& dZ, const at::Tensor& A,
+               at::Tensor& dA, int64_t tw, int64_t seed, int64_t thresh, double drop_scale,
+               int64_t drop_ld, int64_t drop_col0) {
+  need_cuda_f32(dZ, "lora3_dxa dZ");
+  need_cuda_f32(A, "lora3_dxa A");
+  need_cuda_f32(dA, "lora3_dxa dA");
+  if (!x.is_cuda() || !dx.is_cuda() || x.dim() != 2 || dx.dim() != 2 || x.stride(1) != 1 ||
+      dx.stride(1) != 1 || x.sizes() != dx.sizes() || dx.scalar_type() != x.scalar_type() ||
+      !dZ.is_contiguous() || dZ.size(0) != x.size(0) || A.stride(1) != 1 || dA.stride(1) != 1 ||
+      A.size(0) != dZ.size(1) || dA.size(0) != dZ.size(1) || A.size(1) != x.size(1) ||
+      dA.size(1) != x.size(1))
+    throw std::invalid_argument("lumen: lora3_dxa: x/dx [T, K] 16-bit, dZ [T, R] f32, A/dA [R, K] f32");
+  check(lumen_lora3_dxa(dcode(x), x.data_ptr(), x.stride(0), dx.data_ptr(), dx.stride(0),
+                        dZ.data_ptr<float>(), A.data_ptr<float>(), A.stride(0),
+                        dA.data_ptr<float>(), dA.stride(0), static_cast<int>(x.size(0)),
+                        static_cast<int>(x.size(1)), static_cast<int>(dZ.size(1)),
+                        static_cast<int>(tw), static_cast<unsigned long long>(seed),
+                        static_cast<unsigned int>(thresh), static_cast<float>(drop_scale), drop_ld,
+                        drop_col0, cur_stream()),
+        "lora3_dxa");
+}
+
 void transpose2d(const at::Tensor& in, at::Tensor& out) {
   if (!in.is_cuda() || !out.is_cuda() || in.dim() != 2 || out.dim() != 2)
     throw std::invalid_argument("lumen: transpose2d needs 2-D GPU tensors");
@@ -751,6 +777,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("lora3_down", &lora3_down);
   m.def("embedding", &embedding);
+  m.def("lora3_dxa", &lora3_dxa);
   m.def("lora3_z_tail", &lora3_z_tail);
   m.def("lora3_w_tail", &lora3_w_tail);
   m.def("kv_dequant", &kv_dequant);

@@ -500,6 +500,182 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// dxa3: ONE pass over the [T, K] activation rows for both x-side backward products
+//   dA[j, k] += scale * sum_t dZ[t, j] * drop(x)[t, k]          (keep-scale folded into scale)
+//   dx[t, k] += drop'(sum_j dZ[t, j] * A[j, k])                 (16-bit read-modify-write)
+// Block (4 waves) = 128 columns of K x TW rows (64-row sub-tiles).  Per sub-tile the x tile is
+// staged (dropout-masked) as a swizzled LDS image and dZ^T as a 16-bit LDS tile: dA MFMAs read
+// x^T with ds_read_b64_tr_b16 (wave w: columns 32w..32w+31, accumulators live across the row
+// range and land with one f32 atomic each at the end); wave w also updates the dx rows
+// 16w..16w+15 of the sub-tile lane-locally (the up3 column map: 4 x 16-byte vectors per lane),
+// its dx / dZ loads issued before the dA products so they land under them.
+// grid (ceil(K / 128), ceil(T / TW)), block 256.
+// ------------------------------------------------------------------------------------------
+struct DxaArgs {
+  const void* x; long long ldx;
+  void* dx; long long lddx;
+  const float* dZ;            // [T][R]
+  const float* A;             // [R][lda]
+  long long lda;
+  float* dA;                  // [R][ldda]
+  long long ldda;
+  int T, K, R, TW;
+  float da_scale, dx_scale;   // dA: keep-scale; dx: keep-scale (dZ already carries s)
+  Drop drop;
+};
+
+constexpr int kDxST = 72;     // dZ^T LDS row stride (16-bit): 144 B
+
+template <typename T, bool DROP, int NJ>
+__global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
+  constexpr int J = NJ * 16, KJ = J > 32 ? 64 : 32, NKS = KJ / 32, SP = KJ + 8;
+  __shared__ __attribute__((aligned(16))) char img[2][64 * 256];
+  __shared__ __attribute__((aligned(16))) T st[2][J * kDxST];
+  __shared__ __attribute__((aligned(16))) T s2[128 * SP];
+  const int c0 = blockIdx.x * 128;
+  const int tb = blockIdx.y * a.TW, te = min(a.T, tb + a.TW);
+  if (c0 >= a.K || tb >= a.T) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, L = lane & 15, g = lane >> 4;
+  const T* x = reinterpret_cast<const T*>(a.x);
+  T* dx = reinterpret_cast<T*>(a.dx);
+  // A^T slice for the dx products: s2[c][j] = A[j][c0 + c] (zero beyond R / K)
+  for (int idx = threadIdx.x; idx < 32 * KJ; idx += 256) {
+    const int j = idx / 32, c = (idx % 32) * 4;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < a.R && c0 + c < a.K) f = *reinterpret_cast<const float4*>(a.A + (long long)j * a.lda + c0 + c);
+    s2[(c + 0) * SP + j] = from_f32<T>(f.x);
+    s2[(c + 1) * SP + j] = from_f32<T>(f.y);
+    s2[(c + 2) * SP + j] = from_f32<T>(f.z);
+    s2[(c + 3) * SP + j] = from_f32<T>(f.w);
+  }
+  f32x4 da[2][NJ];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int jt = 0; jt < NJ; ++jt) da[m][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // staging registers: x tile (4 x 16 B per thread) and dZ tile (J / 4 float4 per row)
+  uint4 xv[4];
+  float4 zv[(64 * J / 4 + 255) / 256];
+  const auto load_stage = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = threadIdx.x + i * 256;
+      const int r = t0 + (idx >> 4), c = c0 + (idx & 15) * 8;
+      xv[i] = (r < te && c < a.K) ? *reinterpret_cast<const uint4*>(x + (long long)r * a.ldx + c)
+                                  : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < (64 * J / 4 + 255) / 256; ++i) {
+      const int idx = threadIdx.x + i * 256;
+      const int r = idx / (J / 4), j = (idx % (J / 4)) * 4;
+      zv[i] = (r < 64 && t0 + r < te) ? *reinterpret_cast<const float4*>(a.dZ + (long long)(t0 + r) * a.R + j)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  const auto store_stage = [&](int t0, int b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = threadIdx.x + i * 256;
+      const int row = idx >> 4, ch = idx & 15;
+      uint4 u = xv[i];
+      if (DROP)
+        u = mask8(u, dropout_keep8(a.drop.seed,
+                                   (unsigned long long)((long long)(t0 + row) * a.drop.ld + a.drop.col0 + c0 + ch * 8),
+                                   a.drop.thresh));
+      *reinterpret_cast<uint4*>(img[b] + img_off(row, ch)) = u;
+    }
+#pragma unroll
+    for (int i = 0; i < (64 * J / 4 + 255) / 256; ++i) {
+      const int idx = threadIdx.x + i * 256;
+      const int r = idx / (J / 4), j = (idx % (J / 4)) * 4;
+      if (r < 64) {
+        st[b][(j + 0) * kDxST + r] = from_f32<T>(zv[i].x);
+        st[b][(j + 1) * kDxST + r] = from_f32<T>(zv[i].y);
+        st[b][(j + 2) * kDxST + r] = from_f32<T>(zv[i].z);
+        st[b][(j + 3) * kDxST + r] = from_f32<T>(zv[i].w);
+      }
+    }
+  };
+  load_stage(tb);
+  int buf = 0;
+  for (int t0 = tb; t0 < te; t0 += 64, buf ^= 1) {
+    store_stage(t0, buf);
+    __syncthreads();
+    if (t0 + 64 < te) load_stage(t0 + 64);
+    // dx operands of this wave's 16 rows, in flight under the dA products
+    const int t = t0 + wid * 16 + L;
+    const bool tok = t < te;
+    uint4 bop[NKS], dv[4];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int j = ks * 32 + g * 8;
+      bop[ks] = ld_f32x8<T>(a.dZ + (long long)t * a.R + j, tok && j < a.R);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + 32 * i + 8 * g;
+      dv[i] = (tok && c < a.K) ? *reinterpret_cast<const uint4*>(dx + (long long)t * a.lddx + c)
+                               : make_uint4(0, 0, 0, 0);
+    }
+    // dA: D[j][k] += dZ^T[j][t] x[t][k] over the sub-tile's 64 rows
+    const char* im = img[buf];
+    const T* sz = st[buf];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 xt[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) xt[m] = tr_read_img(im, ks * 32, wid * 32 + m * 16, lane);
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt) {
+        const uint4 zt = *reinterpret_cast<const uint4*>(sz + (jt * 16 + L) * kDxST + ks * 32 + g * 8);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) da[m][jt] = Mfma<T>::run(zt, xt[m], da[m][jt]);
+      }
+    }
+    // dx += drop'(dZ A) for rows t (lane-local, column map as in up3)
+    f32x4 acc[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int n = 0; n < 8; ++n)  // A^T operand re-read from LDS (keeps 2 waves per SIMD)
+        acc[n] = Mfma<T>::run(*reinterpret_cast<const uint4*>(s2 + up_cmap(n, L) * SP + ks * 32 + g * 8),
+                              bop[ks], acc[n]);
+    if (tok) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 + 32 * i + 8 * g;
+        if (c >= a.K) continue;
+        float y[8];
+        unpack8<T>(dv[i], y);
+        const uint32_t keep = DROP ? dropout_keep8(a.drop.seed,
+                                                   (unsigned long long)((long long)t * a.drop.ld + a.drop.col0 + c),
+                                                   a.drop.thresh)
+                                   : 0xFFu;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = acc[2 * i + (e >> 2)][e & 3];
+          y[e] += ((keep >> e) & 1u) ? a.dx_scale * d : 0.f;
+        }
+        store8(dx + (long long)t * a.lddx + c, y);
+      }
+    }
+  }
+  // dA flush: accumulator (row j = 16 jt + 4 g + r, column k = c0 + 32 wid + 16 m + L)
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = c0 + wid * 32 + m * 16 + L, j = jt * 16 + g * 4 + r;
+        if (k < a.K && j < a.R) atomicAdd(a.dA + (long long)j * a.ldda + k, a.da_scale * da[m][jt][r]);
+      }
+}
+
+// ------------------------------------------------------------------------------------------
 // K-extension ("fold") of the forward UP into the frozen-weight GEMM:
 //   y = [x | Z | 0] [W | s B_bd | 0]^T   with the adapter tail of 64 extra K columns.
 // z_tail writes the (16-bit) Z tail of the activation operand next to x (which its producer --
@@ -705,5 +881,45 @@ extern "C" hipError_t lumen_lora3_w_tail(int dtype, void* w, long long ldw, int 
   if (dtype == kBF16) hipLaunchKernelGGL(lv3::w_tail_kernel<bf16>, grid, block, 0, st, (bf16*)w, ldw, K, B, r, sg, scale);
   else if (dtype == kF16) hipLaunchKernelGGL(lv3::w_tail_kernel<fp16>, grid, block, 0, st, (fp16*)w, ldw, K, B, r, sg, scale);
   else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// fused x-side backward: dA += scale * dZ^T drop(x) and dx += drop'(dZ A) in one pass over the
+// [T, K] rows (see dxa3_kernel); R = 16 * nj (nj 1..4), K, ldx, lddx multiples of 8
+extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, void* dx,
+                                      long long lddx, const float* dZ, const float* A,
+                                      long long lda, float* dA, long long ldda, int T, int K,
+                                      int R, int tw, unsigned long long seed, unsigned int thresh,
+                                      float drop_scale, long long drop_ld, long long drop_col0,
+                                      hipStream_t st) {
+  if (T <= 0 || K <= 0 || R < 16 || R > 64 || (R & 15) || (K & 7) || (ldx & 7) || (lddx & 7) ||
+      (lda & 3) || tw < 64 || (tw & 63))
+    return hipErrorInvalidValue;
+  lv3::DxaArgs a;
+  a.x = x; a.ldx = ldx; a.dx = dx; a.lddx = lddx; a.dZ = dZ; a.A = A; a.lda = lda; a.dA = dA;
+  a.ldda = ldda; a.T = T; a.K = K; a.R = R; a.TW = tw;
+  const bool drop = thresh != 0;
+  a.da_scale = drop ? drop_scale : 1.f;
+  a.dx_scale = drop ? drop_scale : 1.f;
+  a.drop = {static_cast<unsigned>(seed) ^ static_cast<unsigned>(seed >> 32), thresh, drop_scale,
+            drop_ld, drop_col0};
+  const dim3 grid((K + 127) / 128, (T + tw - 1) / tw), block(256);
+#define LV3_DXA(TT, NJ)                                                                            \
+  do {                                                                                           \
+    if (drop) hipLaunchKernelGGL((lv3::dxa3_kernel<TT, true, NJ>), grid, block, 0, st, a);      \
+    else hipLaunchKernelGGL((lv3::dxa3_kernel<TT, false, NJ>), grid, block, 0, st, a);          \
+  } while (0)
+#define LV3_DXA_NJ(TT)                                                                             \
+  switch (R / 16) {                                                                              \
+    case 1: LV3_DXA(TT, 1); break;                                                               \
+    case 2: LV3_DXA(TT, 2); break;                                                               \
+    case 3: LV3_DXA(TT, 3); break;                                                               \
+    default: LV3_DXA(TT, 4); break;                                                              \
+  }
+  if (dtype == kBF16) { LV3_DXA_NJ(bf16) }
+  else if (dtype == kF16) { LV3_DXA_NJ(fp16) }
+  else return hipErrorInvalidValue;
+#undef LV3_DXA_NJ
+#undef LV3_DXA
   return hipGetLastError();
 }

@@ -181,6 +181,8 @@ DY_TW = int(_os.environ.get("LUMEN_LORA_DY_TW", "0"))  # dY rows per block of lo
 # without RoPE (o_proj 15.0 vs 14.3) and slower with it (q|k|v 55.7 vs 45.6), so v2 stays the
 # forward UP; v3's DOWN (17.3 vs 21.9), fused dY pass (32.5 vs 53.3) and dx update win
 UP_V3 = _os.environ.get("LUMEN_LORA_UP_V3", "0") == "1"
+# fused x-side backward (dA + dx in one pass over the activation rows, lora3_dxa)
+DXA = _os.environ.get("LUMEN_LORA_DXA", "1") != "0"
 
 
 def _v3_ok(r: int, R: int, segs, *mats) -> bool:
@@ -435,12 +437,20 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     dA = None
     if need_dA:
         dA = A.grad if direct else ws[T * R:T * R + nA].view(R, K)
-        _lora2(1, 1, x2d, dZ, dA, 1, K, 1.0, T, R, _split(math.ceil(K / 128), T, 128),
-               [(0, 0, 0, K)], seed, p, K)
-    if dx is not None:
-        nat.lora3_up(0, dx, dx.stride(0), dZ, R, A, K, T, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
-                     drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, [(0, 0, 0, K)],
-                     None, None, None, 0)
+    if need_dA and dx is not None and DXA:
+        # one pass over the [T, K] rows: dA from the staged x tiles, dx updated lane-locally
+        tw = 256 if math.ceil(K / 128) * math.ceil(T / 256) >= 512 else 128
+        nat.lora3_dxa(x2d, dx, dZ, A, dA, tw, int(seed) & 0x7FFFFFFFFFFFFFFF, drop_threshold(p),
+                      1.0 / (1.0 - p) if p > 0 else 1.0, K, 0)
+    else:
+        if need_dA:
+            _lora2(1, 1, x2d, dZ, dA, 1, K, 1.0, T, R, _split(math.ceil(K / 128), T, 128),
+                   [(0, 0, 0, K)], seed, p, K)
+        if dx is not None:
+            nat.lora3_up(0, dx, dx.stride(0), dZ, R, A, K, T, R, 1.0,
+                         int(seed) & 0x7FFFFFFFFFFFFFFF, drop_threshold(p),
+                         1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, [(0, 0, 0, K)],
+                         None, None, None, 0)
     if direct:
         for prm, need in ((A, need_dA), (B, need_dB)):
             cb = getattr(prm, "_lumen_grad_ready", None)

@@ -87,5 +87,8 @@ for name, segs, rope_cols in (("qkv", [(0, 4096, 0, 0), (4096, 4096, 16, 4096), 
     t3 = _time(lambda: nat.lora3_up(0, dx, K, dZ, R, A, K, T, R, 1.0, seed, th, ds, K, 0,
                                     [(0, 0, 0, K)], None, None, None, 0))
     out[name + "_dx"] = (t2, t3, round(dx.numel() * 4 / t3 / 1e3, 0))
+    tw = 256 if math.ceil(K / 128) * math.ceil(T / 256) >= 512 else 128
+    t4 = _time(lambda: nat.lora3_dxa(x, dx, dZ, A, dA, tw, seed, th, ds, K, 0))
+    out[name + "_dxa_fused"] = (t4, round((x.numel() * 2 + dx.numel() * 4) / t4 / 1e3, 0))
 out["note"] = "(v2 us, v3 us, v3 GB/s)"
 print(json.dumps(out), flush=True)

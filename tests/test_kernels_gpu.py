@@ -195,7 +195,7 @@ def test_adamw_device_step_counter():
 
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
-@pytest.mark.parametrize("impl", ["v3", "v2", "f32"])
+@pytest.mark.parametrize("impl", ["v3", "v3-nodxa", "v2", "f32"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch, dtype):
     """impl v3: one-shot DOWN / lane-local UP / fused dY pass (lora_v3.hip); v2: 16-bit MFMA
@@ -204,7 +204,8 @@ def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch, dtype):
     from lumen.ops.lora import lora_linear, lora_linear_ref
 
     monkeypatch.setattr(lora_mod, "USE_V2", impl != "f32")
-    monkeypatch.setattr(lora_mod, "USE_V3", impl == "v3")
+    monkeypatch.setattr(lora_mod, "USE_V3", impl.startswith("v3"))
+    monkeypatch.setattr(lora_mod, "DXA", impl == "v3")
 
     T, K, r = 512 + 64, 1024, 16
     if segs_kind == "qkv":
