@@ -54,6 +54,21 @@ __device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >>
 __device__ __forceinline__ int img_off(int row, int chunk) {
   return row * 256 + ((chunk ^ swz(row)) << 4);
 }
+// Alternative swizzle (SW = 1) for images read by 16-row ds_read_b128 row reads AND the dK/dV
+// kernel's ds_read_b64_tr_b16 reads of rows {32ks + 4g + 0..3}: the default swz maps rows r and
+// r + 4 of those reads to the same bank pair (2-way conflict on both kinds: measured
+// SQ_LDS_BANK_CONFLICT = 47% of SQ_LDS_IDX_ACTIVE in bwd_dkdv_kernel).  Reversing row bits 0..2
+// into chunk bits 3..1 makes both access patterns conflict-free (exhaustive search over linear
+// XOR swizzles against the gfx950 lane-group banking model, scripts/probes/fa_bank_model.py).
+template <int SW>
+__device__ __forceinline__ int swz_t(int row) {
+  if constexpr (SW == 0) return swz(row);
+  else return ((row & 1) << 3) | ((row & 2) << 1) | ((row & 4) >> 1);
+}
+template <int SW>
+__device__ __forceinline__ int img_off_t(int row, int chunk) {
+  return row * 256 + ((chunk ^ swz_t<SW>(row)) << 4);
+}
 
 // stage rows [r0, r0+64) x 128 cols of a token-major matrix (row stride ld elements) into img;
 // rows >= rmax are zero-filled.  256 threads x 4 chunks of 16 bytes.
@@ -74,14 +89,14 @@ __device__ __forceinline__ void stage64(char* img, const T* base, long long ld, 
 // [16w, 16w+16) in 4 instructions.  The swizzle moves to the per-lane SOURCE address (the LDS side
 // of an LDS-DMA is lane-linear).  Rows >= rmax are clamped to row rmax-1 (finite data; the
 // softmax masks those keys).  Completion: the issuing wave's vmcnt, then a barrier.
-template <typename T>
+template <typename T, int SW = 0>
 __device__ __forceinline__ void stage64_async(char* img, const T* base, long long ld, int r0,
                                               int rmax) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (wid * 4 + i) * 4 + (lane >> 4);
-    const int ch = (lane & 15) ^ swz(row);
+    const int ch = (lane & 15) ^ swz_t<SW>(row);
     int gr = r0 + row;
     gr = gr < rmax ? gr : rmax - 1;
     __builtin_amdgcn_global_load_lds(
@@ -125,8 +140,9 @@ __device__ __forceinline__ void lds_fence_barrier() {
 }
 
 // 16-byte row read: 8 consecutive columns [8*chunk, 8*chunk+8) of `row`
+template <int SW = 0>
 __device__ __forceinline__ uint4 row_read(const char* img, int row, int chunk) {
-  return *reinterpret_cast<const uint4*>(img + img_off(row, chunk));
+  return *reinterpret_cast<const uint4*>(img + img_off_t<SW>(row, chunk));
 }
 
 __device__ __forceinline__ uint2 tr_read_raw(const char* p) {
@@ -400,12 +416,13 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(Args a) {
 
 // V^T operand rows for the permuted key order: lane (L, g) gets column n0 + L of rows
 // rlo + 0..3 (lo) and rhi + 0..3 (hi)
+template <int SW = 0>
 __device__ __forceinline__ uint4 tr_read_img2(const char* img, int rlo, int rhi, int n0, int lane) {
   const int L = lane & 15;
   const int col = n0 + 4 * (L & 3);
   const int ch = col >> 3, half = (col >> 2) & 1;
-  const uint2 lo = tr_read_raw(img + img_off(rlo + (L >> 2), ch) + 8 * half);
-  const uint2 hi = tr_read_raw(img + img_off(rhi + (L >> 2), ch) + 8 * half);
+  const uint2 lo = tr_read_raw(img + img_off_t<SW>(rlo + (L >> 2), ch) + 8 * half);
+  const uint2 hi = tr_read_raw(img + img_off_t<SW>(rhi + (L >> 2), ch) + 8 * half);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
@@ -625,9 +642,9 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   auto stage = [&](int j, char* st) {
     const int hh = j / nq, q0 = qstart + (j % nq) * 64;
     const int head = kvh * grp + hh;
-    stage64_async(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
+    stage64_async<T, 1>(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
                   q0, L);
-    stage64_async(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D,
+    stage64_async<T, 1>(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D,
                   a.lddo, q0, L);
     if (wid < 2) {
       const float* src = (wid == 0 ? a.lse : a.delta) + (long long)head * a.T + s0;
@@ -662,8 +679,8 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        sc[nt] = Mfma<T>::run(row_read(qimg, nt * 16 + lr, 4 * ks + lg), kf[ks], sc[nt]);
-        dp[nt] = Mfma<T>::run(row_read(oimg, nt * 16 + lr, 4 * ks + lg), vf[ks], dp[nt]);
+        sc[nt] = Mfma<T>::run(row_read<1>(qimg, nt * 16 + lr, 4 * ks + lg), kf[ks], sc[nt]);
+        dp[nt] = Mfma<T>::run(row_read<1>(oimg, nt * 16 + lr, 4 * ks + lg), vf[ks], dp[nt]);
       }
     }
     // lane: key krow, queries q0 + 16nt + 4lg + r
@@ -689,8 +706,8 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
       const uint4 da = pack_p<T>(dp[2 * ks], dp[2 * ks + 1]);
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
-        dv[n] = Mfma<T>::run(pa, tr_read_img2(oimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dv[n]);
-        dk[n] = Mfma<T>::run(da, tr_read_img2(qimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dk[n]);
+        dv[n] = Mfma<T>::run(pa, tr_read_img2<1>(oimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dv[n]);
+        dk[n] = Mfma<T>::run(da, tr_read_img2<1>(qimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dk[n]);
       }
     }
     lds_fence_barrier();  // stage buffer free for the DMA two steps ahead

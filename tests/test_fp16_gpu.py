@@ -71,10 +71,13 @@ def test_fp16_forced_overflow_skips_and_backs_off():
     """Run A: batches 0..5 with +inf injected into the gradient at steps 2 and 3.  Run B: the
     same engine on batches 0, 1, 4, 5 with the loss scale set to what A's scaler reached.  Step
     2 (first overflow) only spends hysteresis; step 3 halves the scale; neither advances Adam's
-    step counter or the LR schedule, so A's adapters equal B's bit for bit."""
+    step counter or the LR schedule, so A's adapters equal B's up to the reduction order of the
+    LoRA backward's f32 atomics (dA / dB / dZ sums are order-nondeterministic): the A-B distance
+    must be tiny next to the distance either run moved from the initial adapters."""
     from lumen.lora import adapter_state_dict
 
     engA, mA, _ = _engine()
+    init = {k: v.clone() for k, v in adapter_state_dict(mA).items()}
     bs = _batches(6, mA.config.vocab_size)
     scales = []
     for i, b in enumerate(bs):
@@ -98,7 +101,10 @@ def test_fp16_forced_overflow_skips_and_backs_off():
         engB.step()
     a, b = adapter_state_dict(mA), adapter_state_dict(mB)
     for k in a:
-        assert torch.equal(a[k], b[k]), k
+        assert torch.isfinite(a[k]).all(), k
+        moved = (a[k].float() - init[k].float()).norm()
+        diff = (a[k].float() - b[k].float()).norm()
+        assert diff <= 1e-2 * moved + 1e-7, (k, float(diff), float(moved))
     assert any(v.abs().sum() > 0 for k, v in a.items() if "lora_B" in k)
 
 
