@@ -86,6 +86,11 @@ hipError_t lumen_flash_attn(int, int, int, int, const void*, const void*, const 
                             int, int, int, int, float, const void*, long long, void*, void*, void*,
                             long long, long long, long long, const float*, const int*, const float*,
                             const float*, hipStream_t);
+hipError_t lumen_flash_attn_ds(int, int, int, const void*, const void*, const void*, long long,
+                               long long, long long, const float*, const int*, const int*, int, int,
+                               int, int, float, const void*, long long, void*, void*, void*,
+                               long long, long long, long long, const float*, const int*,
+                               const float*, const float*, void*, const int*, int, hipStream_t);
 long long lumen_car_signal_bytes();
 int lumen_car_max_blocks();
 int lumen_car_max_ranks();
@@ -631,7 +636,7 @@ void flash_attn(int64_t which, bool causal, int64_t mt, const at::Tensor& q, con
     throw std::invalid_argument("lumen: flash_attn rope needs int32 pos [T] and f32 cos/sin [*, 64]");
   auto st = [](const std::optional<at::Tensor>& t) -> long long { return t.has_value() ? t->stride(0) : 0; };
   const int T = static_cast<int>(q.size(0));
-  const int ntiles = static_cast<int>(tiles.numel() / 2);
+  const int ntiles = static_cast<int>(tiles.numel() / ((which & 0x100) ? 3 : 2));
   check(lumen_flash_attn(dcode(q), static_cast<int>(which), causal ? 1 : 0, static_cast<int>(mt),
                          q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
                          v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr<float>(),
@@ -641,6 +646,41 @@ void flash_attn(int64_t which, bool causal, int64_t mt, const at::Tensor& q, con
                          ptr<const int>(rope_pos), ptr<const float>(rope_cos),
                          ptr<const float>(rope_sin), cur_stream()),
         "flash_attn");
+}
+
+// Backward with the dS hand-off (which 7 = dK/dV + dS store, 8 = dQ from dS); ds is a
+// [nh, ds_total, 64*64] 16-bit buffer, ds_off int32 [nseq] the per-sequence first tile.
+void flash_attn_ds(int64_t which, bool causal, const at::Tensor& q, const at::Tensor& k,
+                   const at::Tensor& v, const at::Tensor& lse, const at::Tensor& cu,
+                   const at::Tensor& tiles, int64_t nh, int64_t nkv, double scale,
+                   const at::Tensor& dout, const at::Tensor& dq, const at::Tensor& dk,
+                   const at::Tensor& dv, const at::Tensor& delta, const at::Tensor& ds,
+                   const at::Tensor& ds_off, int64_t ds_total,
+                   const std::optional<at::Tensor>& rope_pos, const std::optional<at::Tensor>& rope_cos,
+                   const std::optional<at::Tensor>& rope_sin) {
+  if (!q.is_cuda() || !ds.is_cuda() || !ds_off.is_cuda())
+    throw std::invalid_argument("lumen: flash_attn_ds needs GPU tensors");
+  if (ds_off.scalar_type() != at::kInt || ds.scalar_type() != q.scalar_type() || !ds.is_contiguous() ||
+      ds.numel() < nh * ds_total * 4096 || ds_off.numel() + 1 < cu.numel())
+    throw std::invalid_argument("lumen: flash_attn_ds needs ds [nh, ds_total, 4096] of q's dtype and "
+                                "int32 ds_off [nseq]");
+  if (rope_pos.has_value() &&
+      (!rope_cos.has_value() || !rope_sin.has_value() || rope_pos->scalar_type() != at::kInt ||
+       rope_cos->scalar_type() != at::kFloat || rope_sin->scalar_type() != at::kFloat ||
+       rope_cos->size(-1) != 64 || rope_pos->numel() < q.size(0)))
+    throw std::invalid_argument("lumen: flash_attn_ds rope needs int32 pos [T] and f32 cos/sin [*, 64]");
+  check(lumen_flash_attn_ds(dcode(q), static_cast<int>(which), causal ? 1 : 0, q.data_ptr(),
+                            k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
+                            lse.data_ptr<float>(), cu.data_ptr<int>(), tiles.data_ptr<int>(),
+                            static_cast<int>(tiles.numel() / ((which & 0x100) ? 3 : 2)),
+                            static_cast<int>(nh),
+                            static_cast<int>(nkv), static_cast<int>(q.size(0)),
+                            static_cast<float>(scale), dout.data_ptr(), dout.stride(0),
+                            dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq.stride(0), dk.stride(0),
+                            dv.stride(0), delta.data_ptr<float>(), ptr<const int>(rope_pos),
+                            ptr<const float>(rope_cos), ptr<const float>(rope_sin), ds.data_ptr(),
+                            ds_off.data_ptr<int>(), static_cast<int>(ds_total), cur_stream()),
+        "flash_attn_ds");
 }
 
 // q [T, >= nh*D] token-major rows (any row stride), caches [nblocks, nkv, bs, D], o [T, nh*D]
@@ -803,6 +843,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample", &sample);
   m.def("flash_attn", &flash_attn);
   m.def("flash_attn_paged", &flash_attn_paged);
+  m.def("flash_attn_ds", &flash_attn_ds);
   m.def("car_alloc", &car_alloc);
   m.def("car_free", &car_free);
   m.def("car_handle", &car_handle);

@@ -65,6 +65,10 @@ __device__ __forceinline__ int swz_t(int row) {
   if constexpr (SW == 0) return swz(row);
   else return ((row & 1) << 3) | ((row & 2) << 1) | ((row & 4) >> 1);
 }
+__device__ __forceinline__ unsigned lds_off_g(const char* p) {
+  return static_cast<unsigned>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)(p)));
+}
 template <int SW>
 __device__ __forceinline__ int img_off_t(int row, int chunk) {
   return row * 256 + ((chunk ^ swz_t<SW>(row)) << 4);
@@ -102,6 +106,37 @@ __device__ __forceinline__ void stage64_async(char* img, const T* base, long lon
     __builtin_amdgcn_global_load_lds(
         (const void*)(base + (long long)gr * ld + ch * 8),
         (__attribute__((address_space(3))) void*)(img + (wid * 4 + i) * 1024), 16, 0, 0);
+  }
+}
+
+// Opaque LDS-DMA: the same global_load_lds as the builtin, as inline asm.  hipcc's wait
+// insertion cannot tell an in-flight LDS-DMA into one ping-pong buffer from the ds_reads of the
+// other and puts s_waitcnt vmcnt(0) before them (seen after the barrier of every step in the
+// dK/dV and dQ-from-dS kernels, with builtin ds_read / ds_read_tr reads); hidden from it, the
+// DMA is retired only by the kernels' own counted vmcnt waits.  Extra in-flight operations the
+// compiler cannot see only make its own counted waits stricter (counters retire in order).
+// M0 = wave-uniform LDS base of the lane-linear destination (+16 B per lane).
+__device__ __forceinline__ void dma16_o(const void* g, const char* lds_wave_base) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_off_g(lds_wave_base));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(g), "s"(m0) : "memory", "m0");
+}
+__device__ __forceinline__ void dma4_o(const void* g, const char* lds_wave_base) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_off_g(lds_wave_base));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+               :: "v"(g), "s"(m0) : "memory", "m0");
+}
+template <typename T, int SW>
+__device__ __forceinline__ void stage64_async_o(char* img, const T* base, long long ld, int r0,
+                                                int rmax) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ swz_t<SW>(row);
+    int gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;
+    dma16_o(base + (long long)gr * ld + ch * 8, img + (wid * 4 + i) * 1024);
   }
 }
 
@@ -246,7 +281,28 @@ struct Args {
   const int* block_tables;
   int bt_stride;
   int block_size;
+  // optional (backward, dS hand-off): the dK/dV kernel stores dS (16-bit, the exact operand it
+  // feeds its own dK product) per 64 x 64 (query tile, key tile) into ds; the dQ kernel then
+  // forms dQ = dS K from it instead of recomputing S and dP.  Tile (head, seq, qt, kt) is
+  // ds + (head * ds_total + ds_off[seq] + tri(qt, kt)) * 8 KiB, tri = qt(qt+1)/2 + kt (causal)
+  // or qt * ntiles(seq) + kt.
+  void* ds;
+  const int* ds_off;
+  int ds_total;
+  // tiles3: 1-D grid over (seq, row start, head) triples (head = the kernel's head or kv head),
+  // ordered on the host so that the tiles of one (sequence, head) land on one XCD together and
+  // share its L2 (blocks go to XCDs round-robin by id; seq < 0 = padding); 0: pairs, head = y
+  int tiles3;
 };
+
+struct Work { int seq, r0, head; };
+__device__ __forceinline__ Work work_item(const Args& a) {
+  if (a.tiles3) {
+    const int* t = a.tiles + 3 * blockIdx.x;
+    return Work{t[0], t[1], t[2]};
+  }
+  return Work{a.tiles[2 * blockIdx.x], a.tiles[2 * blockIdx.x + 1], (int)blockIdx.y};
+}
 
 // Inverse rotary embedding of one (x, x ^ 64) column pair: the forward rotation
 // y1 = x1 c - x2 s, y2 = x2 c + x1 s has the transpose dx1 = dy1 c + dy2 s, dx2 = dy2 c - dy1 s.
@@ -602,18 +658,37 @@ __global__ void __launch_bounds__(256) delta_kernel(Args a) {
 // =============================================================================================
 // backward: dK, dV  (workgroup = 64 keys of one kv head; loops over q tiles and group heads)
 // =============================================================================================
-template <typename T, bool CAUSAL>
+// dS hand-off layout inside one 8 KiB tile: block (wave w = key / 16, ks = query / 32) of 1 KiB
+// holds 64 lanes' packed 16-byte P^T-order registers (queries 4m..4m+3 | 16+4m..16+4m+3 of the
+// 32-query slice for key row lr) at slot m * 16 + (lr ^ 8 (m & 1)): the dK/dV kernel stores one
+// coalesced KiB per instruction, and the dQ kernel's 8-byte transposed reads of one half are at
+// most 2-way bank-conflicted (4 of its 36 LDS reads per key tile).
+__device__ __forceinline__ int ds_slot(int m, int lr) { return (m * 16 + (lr ^ ((m & 1) << 3))) * 16; }
+// seq_base = ds_off[seq], loaded once before the DMA ring starts (a load of it inside the loop
+// would make the compiler drain every LDS-DMA in flight with vmcnt(0) before using it)
+__device__ __forceinline__ long long ds_tile(const Args& a, int head, int seq_base, int qt, int kt,
+                                             int ns, bool causal) {
+  return ((long long)head * a.ds_total + seq_base + (causal ? qt * (qt + 1) / 2 + kt : qt * ns + kt)) * 8192;
+}
+
+template <typename T, bool CAUSAL, bool WDS = false>
 __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   constexpr int STAGE = 2 * IMG + 512;  // Q image | dO image | lse[64] | delta[64]
   // two stages filled by LDS-DMA one (head, q-tile) step ahead.  S = Q K^T and dP = dO V^T are
   // computed with the queries as MFMA rows, so the accumulator lane (key L, queries 4g + r of each
   // 16-query tile) already holds P^T / dS^T rows in the permuted-k order of the fwd_t kernel:
   // they feed dV += P^T dO and dK += dS^T Q straight from registers (no LDS round trip).
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // two SEPARATE LDS objects, the loop unrolled by two (see fwd32_kernel): with one array indexed
+  // by (j & 1) the compiler put s_waitcnt vmcnt(0) after the barrier of every step (it could not
+  // tell the in-flight prefetch from the tile being read), serialising the DMA ring
+  __shared__ __attribute__((aligned(16))) char bufA[STAGE];
+  __shared__ __attribute__((aligned(16))) char bufB[STAGE];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int seq = a.tiles[2 * blockIdx.x], k0 = a.tiles[2 * blockIdx.x + 1];
-  const int kvh = blockIdx.y;
+  const Work wk = work_item(a);
+  if (wk.seq < 0) return;
+  const int seq = wk.seq, k0 = wk.r0;
+  const int kvh = wk.head;
   const int grp = a.nh / a.nkv;
   const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
   const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
@@ -628,6 +703,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
       vf[ks] = gload16(V + (long long)krow * a.ldv + (4 * ks + lg) * 8, krow < L);
     }
   }
+  const int ds_base = WDS ? a.ds_off[seq] : 0;
   wait_vm_all();
   f32x4 dk[8], dv[8];
 #pragma unroll
@@ -642,35 +718,46 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   auto stage = [&](int j, char* st) {
     const int hh = j / nq, q0 = qstart + (j % nq) * 64;
     const int head = kvh * grp + hh;
-    stage64_async<T, 1>(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
+    stage64_async_o<T, 1>(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
                   q0, L);
-    stage64_async<T, 1>(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D,
+    stage64_async_o<T, 1>(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D,
                   a.lddo, q0, L);
     if (wid < 2) {
       const float* src = (wid == 0 ? a.lse : a.delta) + (long long)head * a.T + s0;
       int qr = q0 + lane;
       qr = qr < L ? qr : L - 1;
-      __builtin_amdgcn_global_load_lds((const void*)(src + qr),
-                                       (__attribute__((address_space(3))) void*)(st + 2 * IMG + wid * 256),
-                                       4, 0, 0);
+      dma4_o(src + qr, st + 2 * IMG + wid * 256);
     }
   };
-  if (nsteps > 0) stage(0, smem);
-  for (int j = 0; j < nsteps; ++j) {
-    char* st = smem + (j & 1) * STAGE;
+  // WDS: step j's dS is held in registers and stored right after step j+1's wait, so the stores
+  // are older than step j+2's DMA and retire under step j+1's compute: the counted vmcnt waits
+  // stay exact and no step waits for a store it just issued
+  uint4 pend[2];
+  long long pend_off = -1;
+  auto store_pend = [&]() {
+    if (pend_off < 0) return;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      char* dst = reinterpret_cast<char*>(a.ds) + pend_off + (wid * 2 + ks) * 1024 + ds_slot(lg, lr);
+      *reinterpret_cast<uint4*>(dst) = pend[ks];
+    }
+  };
+  if (nsteps > 0) stage(0, bufA);
+  auto step = [&](int j, char* st, char* nx) {
     char* qimg = st;
     char* oimg = st + IMG;
     const float* s_lse = reinterpret_cast<const float*>(st + 2 * IMG);
     const float* s_del = s_lse + 64;
     const int q0 = qstart + (j % nq) * 64;
     if (j + 1 < nsteps) {
-      stage(j + 1, smem + ((j + 1) & 1) * STAGE);
+      stage(j + 1, nx);
       if (wid < 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
       wait_vm_all();
     }
     lds_fence_barrier();
+    if constexpr (WDS) store_pend();
     // S = Q K^T and dP = dO V^T: [64 queries x 16 keys] per wave as 4 query tiles
     f32x4 sc[4], dp[4];
 #pragma unroll
@@ -684,7 +771,9 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
       }
     }
     // lane: key krow, queries q0 + 16nt + 4lg + r
-    const bool need_mask = (q0 + 64 > L) || (CAUSAL && wk0 + 15 > q0);
+    // (WDS: keys past the end must also store dS = 0 -- dQ multiplies it by the clamped K rows;
+    // without the hand-off those keys' dK / dV rows are simply never written)
+    const bool need_mask = (q0 + 64 > L) || (CAUSAL && wk0 + 15 > q0) || (WDS && k0 + 64 > L);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const float4 l4 = *reinterpret_cast<const float4*>(s_lse + nt * 16 + 4 * lg);
@@ -704,14 +793,22 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     for (int ks = 0; ks < 2; ++ks) {
       const uint4 pa = pack_p<T>(sc[2 * ks], sc[2 * ks + 1]);
       const uint4 da = pack_p<T>(dp[2 * ks], dp[2 * ks + 1]);
+      if constexpr (WDS) pend[ks] = da;
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
         dv[n] = Mfma<T>::run(pa, tr_read_img2<1>(oimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dv[n]);
         dk[n] = Mfma<T>::run(da, tr_read_img2<1>(qimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dk[n]);
       }
     }
+    if constexpr (WDS)
+      pend_off = ds_tile(a, kvh * grp + j / nq, ds_base, q0 / 64, k0 / 64, (L + 63) / 64, CAUSAL);
     lds_fence_barrier();  // stage buffer free for the DMA two steps ahead
+  };
+  for (int j = 0; j < nsteps; j += 2) {
+    step(j, bufA, bufB);
+    if (j + 1 < nsteps) step(j + 1, bufB, bufA);
   }
+  if constexpr (WDS) store_pend();
   // write dK (x softmax scale), dV : rows wk0 + 4lg + r, cols 16n + lr
   T* dK = reinterpret_cast<T*>(a.dk) + (long long)s0 * a.lddk + kvh * D;
   T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D;
@@ -1056,8 +1153,10 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char bufB[2 * IMG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lq = lane & 31, hi = lane >> 5;
-  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
-  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
+  const Work wk = work_item(a);
+  if (wk.seq < 0) return;
+  const int seq = wk.seq, q0 = wk.r0;
+  const int head = wk.head, kvh = head / (a.nh / a.nkv);
   const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;  // L = this sequence's query rows
   // keys: self-attention over the same rows, or (PAGED) the cached context + this chunk, the
   // chunk's queries sitting at key positions qoff .. qoff + L - 1
@@ -1326,8 +1425,10 @@ __global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lq = lane & 31, hi = lane >> 5;
-  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
-  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
+  const Work wk = work_item(a);
+  if (wk.seq < 0) return;
+  const int seq = wk.seq, q0 = wk.r0;
+  const int head = wk.head, kvh = head / (a.nh / a.nkv);
   const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
   const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
   const T* dO = reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D;
@@ -1436,11 +1537,96 @@ __global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
   }
 }
 
+// ---- backward dQ from the dK/dV kernel's dS tiles (no recompute of S and dP) ----------------
+// Workgroup = one 64-query tile of one head, wave v = queries 16v..16v+15 (16x16x32 MFMA).  Per
+// key tile: the 8 KiB dS tile and the 16 KiB K tile arrive by LDS-DMA one tile ahead; dQ[16 x 128]
+// += dS[16 x 64] K[64 x 128] is 16 MFMAs per wave with both operands read transposed
+// (ds_read_b64_tr_b16): dS rows = keys in the hand-off layout (ds_slot), K in the SW = 1 image.
+template <typename T, bool CAUSAL>
+__global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
+  constexpr int TILE = IMG + 8192;  // K image | dS tile
+  __shared__ __attribute__((aligned(16))) char bufA[TILE];  // ping-pong as in bwd_dkdv_kernel
+  __shared__ __attribute__((aligned(16))) char bufB[TILE];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const Work wk = work_item(a);
+  if (wk.seq < 0) return;
+  const int seq = wk.seq, q0 = wk.r0;
+  const int head = wk.head, kvh = head / (a.nh / a.nkv);
+  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
+  const int ns = (L + 63) / 64, qt = q0 / 64;
+  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
+  const char* dsq = reinterpret_cast<const char*>(a.ds) + ds_tile(a, head, a.ds_off[seq], qt, 0, ns, CAUSAL);
+  const int nkt = CAUSAL ? qt + 1 : ns;  // key tiles (contiguous in the hand-off buffer)
+  // per-lane dS read offsets (tile-relative): source lane s = 4i + m of each 16-lane group g reads
+  // keys 4g + i (+16 for the hi half) of the 32-key slice ks, queries 16 wid + 4m .. +3
+  const int si = lr >> 2, sm = lr & 3;
+  const int dso = ((wid >> 1) * 1024) + (wid & 1) * 8 + ds_slot(sm, 4 * lg + si);
+  auto stage = [&](char* buf, int kt) {
+    stage64_async_o<T, 1>(buf, K, a.ldk, kt * 64, L);
+    const char* src = dsq + (long long)kt * 8192;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int off = (wid * 2 + i) * 1024;
+      dma16_o(src + off + lane * 16, buf + IMG + off);
+    }
+  };
+  f32x4 dq[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) dq[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nkt > 0) stage(bufA, 0);
+  auto step = [&](int kt, char* buf, char* nx) {
+    if (kt + 1 < nkt) {
+      stage(nx, kt + 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      wait_vm_all();
+    }
+    lds_fence_barrier();
+    const char* kimg = buf;
+    const char* dsi = buf + IMG;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // A = dS[query 16 wid + lr][keys 32ks + 4lg + 0..3 | 32ks + 16 + 4lg + 0..3]: the wave
+      // w = key / 16 blocks 2ks and 2ks + 1 of the hand-off layout
+      const uint2 lo = tr_read_raw(dsi + (2 * ks) * 2048 + dso);
+      const uint2 hi = tr_read_raw(dsi + (2 * ks + 1) * 2048 + dso);
+      const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        dq[n] = Mfma<T>::run(af, tr_read_img2<1>(kimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dq[n]);
+    }
+    lds_fence_barrier();
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    step(kt, bufA, bufB);
+    if (kt + 1 < nkt) step(kt + 1, bufB, bufA);
+  }
+  // lane: queries q0 + 16 wid + 4lg + r, columns 16n + lr
+  T* dQ = reinterpret_cast<T*>(a.dq) + (long long)s0 * a.lddq + head * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qr = q0 + wid * 16 + 4 * lg + r;
+    if (qr >= L) continue;
+    float qv[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) qv[n] = dq[n][r] * a.scale;
+    if (a.rope_pos != nullptr) {  // column 16n + lr pairs with 16(n + 4) + lr: same lane
+      const long long pb = (long long)a.rope_pos[s0 + qr] * 64 + lr;
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        rope_inv_pair(qv[n], qv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
+    }
+#pragma unroll
+    for (int n = 0; n < 8; ++n) dQ[(long long)qr * a.lddq + n * 16 + lr] = from_f32<T>(qv[n]);
+  }
+}
+
 template <typename T>
 static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& a, hipStream_t st) {
   dim3 block(256);
   if (which == 0) {
-    dim3 grid(ntiles, a.nh);
+    dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
     if (mt == 20) {  // 32x32x16 kernel, 128-row tiles
       if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
       else hipLaunchKernelGGL((fwd32_kernel<T, false>), grid, block, 0, st, a);
@@ -1464,7 +1650,7 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     dim3 grid((unsigned)((a.T + 3) / 4));
     hipLaunchKernelGGL(delta_kernel<T>, grid, block, 0, st, a);
   } else if (which == 2) {
-    dim3 grid(ntiles, a.nkv);
+    dim3 grid(ntiles, a.tiles3 ? 1 : a.nkv);
     if (causal) hipLaunchKernelGGL((bwd_dkdv_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dkdv_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 3) {
@@ -1476,7 +1662,7 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     if (causal) hipLaunchKernelGGL((bwd_dkdv32_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dkdv32_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 5) {  // dQ, 32x32x16 kernel, 128-query tiles (mt == 2: + delta)
-    dim3 grid(ntiles, a.nh);
+    dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
     if (mt == 2) {
       if (causal) hipLaunchKernelGGL((bwd_dq32_kernel<T, true, true>), grid, block, 0, st, a);
       else hipLaunchKernelGGL((bwd_dq32_kernel<T, false, true>), grid, block, 0, st, a);
@@ -1485,6 +1671,14 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     } else {
       hipLaunchKernelGGL((bwd_dq32_kernel<T, false>), grid, block, 0, st, a);
     }
+  } else if (which == 7) {  // dK/dV (64-key tiles) + dS hand-off
+    dim3 grid(ntiles, a.tiles3 ? 1 : a.nkv);
+    if (causal) hipLaunchKernelGGL((bwd_dkdv_kernel<T, true, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((bwd_dkdv_kernel<T, false, true>), grid, block, 0, st, a);
+  } else if (which == 8) {  // dQ from the dS hand-off (64-query tiles)
+    dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
+    if (causal) hipLaunchKernelGGL((bwd_dq_ds_kernel<T, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((bwd_dq_ds_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 6) {  // forward over the paged KV cache (32x32x16, 128-row tiles)
     dim3 grid(ntiles, a.nh);
     if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true, true>), grid, block, 0, st, a);
@@ -1514,6 +1708,9 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
                                        const float* rope_cos, const float* rope_sin,
                                        hipStream_t st) {
   if (nkv <= 0 || nh % nkv != 0) return hipErrorInvalidValue;
+  const int tiles3 = (which >> 8) & 1;  // 0x100: (seq, row, head) triples, 1-D grid
+  which &= 0xff;
+  if (tiles3 && which != 0 && which != 2 && which != 5) return hipErrorInvalidValue;
   // the fused inverse RoPE exists in the dK/dV kernel (which 2) and the 32x32 dQ kernel (which 5)
   if (rope_pos != nullptr && which != 2 && which != 5) return hipErrorInvalidValue;
   if (which != 1 && ntiles == 0) return hipSuccess;
@@ -1525,7 +1722,8 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.lddv = lddv; a.delta = delta;
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
-  if (which == 6) return hipErrorInvalidValue;  // paged: lumen_flash_attn_paged
+  a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3;
+  if (which == 6 || which == 7 || which == 8) return hipErrorInvalidValue;  // other entries
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
   return hipErrorInvalidValue;
@@ -1552,5 +1750,35 @@ extern "C" hipError_t lumen_flash_attn_paged(int dtype, int causal, const void* 
   a.block_size = block_size;
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(6, causal, 20, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(6, causal, 20, ntiles, a, st);
+  return hipErrorInvalidValue;
+}
+
+// Backward with the dS hand-off: which 7 = dK/dV + dS store (64-key tiles), 8 = dQ from dS
+// (64-query tiles).  ds: [nh][ds_total][64 x 64] 16-bit, ds_off[seq] = the sequence's first tile.
+extern "C" hipError_t lumen_flash_attn_ds(int dtype, int which, int causal, const void* q,
+                                          const void* k, const void* v, long long ldq,
+                                          long long ldk, long long ldv, const float* lse,
+                                          const int* cu, const int* tiles, int ntiles, int nh,
+                                          int nkv, int T, float scale, const void* dout,
+                                          long long lddo, void* dq, void* dk, void* dv,
+                                          long long lddq, long long lddk, long long lddv,
+                                          const float* delta, const int* rope_pos,
+                                          const float* rope_cos, const float* rope_sin, void* ds,
+                                          const int* ds_off, int ds_total, hipStream_t st) {
+  const int tiles3 = (which >> 8) & 1;
+  which &= 0xff;
+  if (nkv <= 0 || nh % nkv != 0 || (which != 7 && which != 8) || ds == nullptr || ds_off == nullptr)
+    return hipErrorInvalidValue;
+  if (ntiles == 0) return hipSuccess;
+  lumen::fa::Args a{};
+  a.q = q; a.k = k; a.v = v; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv;
+  a.lse = const_cast<float*>(lse); a.cu = cu; a.tiles = tiles; a.nh = nh; a.nkv = nkv; a.T = T;
+  a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
+  a.dout = dout; a.lddo = lddo; a.dq = dq; a.dk = dk; a.dv = dv; a.lddq = lddq; a.lddk = lddk;
+  a.lddv = lddv; a.delta = delta;
+  a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
+  a.ds = ds; a.ds_off = ds_off; a.ds_total = ds_total; a.tiles3 = tiles3;
+  if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, 1, ntiles, a, st);
+  if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, 1, ntiles, a, st);
   return hipErrorInvalidValue;
 }

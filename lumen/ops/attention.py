@@ -261,6 +261,47 @@ def _tiles(cu: tuple, rows: int, device, heavy_first: bool = True) -> torch.Tens
     return t
 
 
+N_XCD = 8  # MI355X: 8 XCDs, each with its own L2; workgroups go to XCDs round-robin by id
+
+
+def _xcd_tiles(cu: tuple, rows: int, nheads: int, device, heavy_low: bool) -> torch.Tensor:
+    """(seq, row start, head) triples for a 1-D launch, ordered so that all row tiles of one
+    (sequence, head) run on ONE XCD at the same time: group g goes to XCD g % 8 and takes
+    consecutive slots of that XCD's share of the block ids (id = slot * 8 + xcd), so the group's
+    Q / dO (dK/dV kernel) or K / V (forward, dQ) tiles are fetched from HBM once into that L2
+    instead of once per tile.  Longest sequences first; inside a group the heaviest causal tile
+    first (heavy_low: low row starts carry the most work, as in dK/dV).  Unequal XCD queues are
+    padded with seq = -1 entries (empty workgroups)."""
+    key = ("xcd", cu, rows, nheads, str(device), heavy_low)
+    t = _TILE_CACHE.get(key)
+    if t is None:
+        seqs = sorted(range(len(cu) - 1), key=lambda s: -(cu[s + 1] - cu[s]))
+        queues = [[] for _ in range(N_XCD)]
+        g = 0
+        for s in seqs:
+            L = cu[s + 1] - cu[s]
+            if L <= 0:
+                continue
+            starts = list(range(0, L, rows))
+            if not heavy_low:
+                starts.reverse()
+            for h in range(nheads):
+                queues[g % N_XCD] += [(s, r, h) for r in starts]
+                g += 1
+        n = max(len(q) for q in queues)
+        flat = []
+        for slot in range(n):
+            for x in range(N_XCD):
+                flat += queues[x][slot] if slot < len(queues[x]) else (-1, 0, 0)
+        t = torch.tensor(flat if flat else [0], dtype=torch.int32, device=device)
+        if not flat:
+            t = t[:0]
+        if len(_TILE_CACHE) > 256:
+            _TILE_CACHE.clear()
+        _TILE_CACHE[key] = t
+    return t
+
+
 def _cu_tensor(cu: tuple, device) -> torch.Tensor:
     key = ("cu", cu, str(device))
     t = _TILE_CACHE.get(key)
@@ -318,6 +359,28 @@ FA_BWD = _os.environ.get("LUMEN_FA_BWD", "mix")
 # LUMEN_FA_DQ_DELTA=1: the 32x32 dQ kernel forms delta itself and runs before dK/dV (opt-in:
 # measured neutral end to end and +0.22 ms/step of kernel time, profiles/r04_train)
 FA_DQ_DELTA = _os.environ.get("LUMEN_FA_DQ_DELTA", "0") == "1"
+# dS hand-off (mix kernels): the dK/dV kernel stores dS per 64x64 tile and the dQ kernel forms
+# dQ = dS K from it, instead of recomputing S = Q K^T and dP = dO V^T (2 of its 3 products).
+# Used while the [nh, tiles, 64, 64] 16-bit buffer stays under LUMEN_FA_DS_MB (0 = off).
+FA_DS_MB = float(_os.environ.get("LUMEN_FA_DS_MB", "2048"))
+# XCD-grouped 1-D launches (_xcd_tiles) for the forward and the dS hand-off backward: opt-in,
+# measured neutral at B=8 S=512 (dK/dV 108 -> 110 us, dQ 30 -> 31 us, gpurun r2_34)
+FA_XCD = _os.environ.get("LUMEN_FA_XCD", "0") == "1"
+
+
+def _ds_offsets(cu: tuple, causal: bool, device):
+    """Per-sequence first tile of the dS hand-off buffer and the total tile count."""
+    key = ("ds", cu, causal, str(device))
+    hit = _TILE_CACHE.get(key)
+    if hit is None:
+        offs, tot = [], 0
+        for s in range(len(cu) - 1):
+            n = (cu[s + 1] - cu[s] + 63) // 64
+            offs.append(tot)
+            tot += n * (n + 1) // 2 if causal else n * n
+        hit = (torch.tensor(offs if offs else [0], dtype=torch.int32, device=device), tot)
+        _TILE_CACHE[key] = hit
+    return hit
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -334,9 +397,12 @@ class _FlashAttn(torch.autograd.Function):
         lse = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
         cut = _cu_tensor(cu, qkv.device)
         scale = 1.0 / math.sqrt(D) if scale is None else scale
-        C.flash_attn(0, causal, FA_FWD_MT, q, k, v, o, lse, cut,
-                     _tiles(cu, FA_FWD_ROWS, qkv.device), nh, nkv, scale, None, None, None, None,
-                     None, None, None, None)
+        if FA_XCD and FA_FWD_MT == 20:
+            tl, w = _xcd_tiles(cu, FA_FWD_ROWS, nh, qkv.device, False), 0x100
+        else:
+            tl, w = _tiles(cu, FA_FWD_ROWS, qkv.device), 0
+        C.flash_attn(w, causal, FA_FWD_MT, q, k, v, o, lse, cut, tl, nh, nkv, scale, None, None,
+                     None, None, None, None, None, None)
         ctx.save_for_backward(qkv, o, lse)
         ctx.meta = (cu, nh, nkv, D, causal, scale)
         ctx.rope = rope
@@ -368,7 +434,23 @@ class _FlashAttn(torch.autograd.Function):
         rp = ctx.rope if (ctx.rope is not None and wkv == 2 and wq == 5) else None
         pos, cos, sin = rp if rp is not None else (None, None, None)
         qtiles = _tiles(cu, rq, qkv.device)
-        if wq == 5 and FA_DQ_DELTA:
+        ds_off, ds_total = (_ds_offsets(cu, causal, qkv.device) if wkv == 2 and FA_DS_MB > 0
+                            else (None, 0))
+        if ds_off is not None and nh * ds_total * 8192 <= FA_DS_MB * 2 ** 20:
+            ds = torch.empty(nh, ds_total, 4096, device=qkv.device, dtype=qkv.dtype)
+            C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
+                         scale, do, None, None, None, delta, None, None, None)
+            if FA_XCD:
+                t7, w7 = _xcd_tiles(cu, 64, nkv, qkv.device, causal), 0x107
+                t8, w8 = _xcd_tiles(cu, 64, nh, qkv.device, False), 0x108
+            else:
+                t7 = t8 = _tiles(cu, 64, qkv.device)
+                w7, w8 = 7, 8
+            C.flash_attn_ds(w7, causal, q, k, v, lse, cut, t7, nh, nkv,
+                            scale, do, dq, dk, dv, delta, ds, ds_off, ds_total, pos, cos, sin)
+            C.flash_attn_ds(w8, causal, q, k, v, lse, cut, t8, nh, nkv,
+                            scale, do, dq, dk, dv, delta, ds, ds_off, ds_total, pos, cos, sin)
+        elif wq == 5 and FA_DQ_DELTA:
             # the 32x32 dQ kernel forms delta = rowsum(dO * O) itself and runs first
             C.flash_attn(wq, causal, 2, q, k, v, o, lse, cut, qtiles, nh, nkv,
                          scale, do, dq, dk, dv, delta, pos, cos, sin)

@@ -10,6 +10,13 @@ for i in 1 2; do
 timeout -k 10 120 python lumen/bench/attn_bench.py --B 8 --S 512 --iters 50 > $O/attn_$i.json 2>&1 || exit 1
 tail -1 $O/attn_$i.json
 done
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 lumen/bench/attn_bench.py --only ${FA_ONLY:-all} --B 8 --S 512 --iters 20 > $O/kt.log 2>&1 || exit 1
+python3 - $(find $O/kt -name "*kernel_stats.csv" | head -1) <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "lumen" in r["Name"]:
+        print(f'{float(r["AverageNs"])/1e3:8.1f} us  x{r["Calls"]:>4}  {r["Name"][:80]}')
+PY
 C1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_IDX_ACTIVE"
 timeout -s KILL 90 rocprofv3 --pmc $C1 --output-format csv -d $O/pmc_1 -o run -- python3 lumen/bench/attn_bench.py --only bwd --B 8 --S 512 --iters 3 > $O/pmc_1.log 2>&1 || exit 1
 python3 - $O/pmc_1/run_counter_collection.csv <<'PY'

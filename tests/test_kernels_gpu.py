@@ -336,6 +336,7 @@ def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch, dtype):
     monkeypatch.setattr(att, "FA_FWD_ROWS", att._fwd_rows(mt))
     monkeypatch.setattr(att, "FA_DQ_DELTA", bwd != "mix-sep")
     monkeypatch.setattr(att, "FA_BWD", "mix" if bwd == "mix-sep" else bwd)
+    monkeypatch.setattr(att, "FA_DS_MB", 0)  # the recompute dQ kernels (dS hand-off: below)
 
     D = 128
     cu = [0]
@@ -356,6 +357,41 @@ def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch, dtype):
     assert rel(g[:, :qs], g2[:, :qs]) < 3e-2, "dq"
     assert rel(g[:, qs:qs + ks], g2[:, qs:qs + ks]) < 3e-2, "dk"
     assert rel(g[:, qs + ks:], g2[:, qs + ks:]) < 3e-2, "dv"
+
+
+@pytest.mark.parametrize("nh,nkv,lens", [(8, 8, [512, 512]), (8, 2, [512, 300, 77]),
+                                         (4, 4, [1000, 64, 129])])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_flash_attention_ds_handoff(nh, nkv, lens, causal, monkeypatch, dtype):
+    """dS hand-off backward (dK/dV kernel stores dS tiles, dQ = dS K from them) vs the fp32
+    reference, and dQ vs the recompute kernel (same bf16 dS operand: near-identical)."""
+    import lumen.ops.attention as att
+    from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
+
+    D = 128
+    cu = [0]
+    for L in lens:
+        cu.append(cu[-1] + L)
+    T = cu[-1]
+    qkv = (torch.randn(T, (nh + 2 * nkv) * D, device=DEV) * 0.5).to(dtype)
+    do = torch.randn(T, nh * D, device=DEV).to(dtype)
+    grads = {}
+    for mb in (2048, 0):
+        monkeypatch.setattr(att, "FA_DS_MB", mb)
+        x = qkv.clone().requires_grad_(True)
+        o = flash_attention_qkv(x, cu, nh, nkv, D, causal)
+        (grads[mb],) = torch.autograd.grad(o, x, do)
+    q2 = qkv.float().requires_grad_(True)
+    o2 = flash_attention_ref(q2, tuple(cu), nh, nkv, D, causal)
+    (g2,) = torch.autograd.grad(o2, q2, do.float())
+    g = grads[2048].float()
+    qs, ks = nh * D, nkv * D
+    assert rel(g[:, :qs], g2[:, :qs]) < 3e-2, "dq"
+    assert rel(g[:, qs:qs + ks], g2[:, qs:qs + ks]) < 3e-2, "dk"
+    assert rel(g[:, qs + ks:], g2[:, qs + ks:]) < 3e-2, "dv"
+    assert rel(g[:, :qs], grads[0][:, :qs].float()) < 1e-2, "dq vs recompute"
+    assert torch.equal(grads[2048][:, qs:], grads[0][:, qs:]), "dk/dv unchanged"
 
 
 @pytest.mark.parametrize("nh,nkv", [(8, 8), (8, 2)])
