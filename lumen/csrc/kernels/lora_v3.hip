@@ -371,7 +371,7 @@ __device__ __forceinline__ void dy_store(char* img, const uint4 (&v)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int idx = threadIdx.x + i * 256;
-    *reinterpret_cast<uint4*>(img + img_off(idx >> 4, idx & 15)) = v[i];
+    *reinterpret_cast<uint4*>(img + img_off_b(idx >> 4, idx & 15)) = v[i];
   }
 }
 
@@ -452,7 +452,7 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
     // dZ: rows 16 wid + L, k = chunk columns
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint4 av = row_read(im, wid * 16 + L, i * 4 + g);
+      const uint4 av = row_read_b(im, wid * 16 + L, i * 4 + g);
 #pragma unroll
       for (int c2 = 0; c2 < kDyCC; ++c2)
         if (c2 == cc) {
@@ -465,7 +465,7 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        const uint4 tv = tr_read_img(im, ks * 32, wid * 32 + m * 16, lane);
+        const uint4 tv = tr_read_img_b(im, ks * 32, wid * 32 + m * 16, lane);
 #pragma unroll
         for (int c2 = 0; c2 < kDyCC; ++c2)
           if (c2 == cc) {

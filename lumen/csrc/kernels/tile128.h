@@ -60,6 +60,29 @@ __device__ __forceinline__ uint4 tr_read_img(const char* img, int k0, int n0, in
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
+// Alternative swizzle for images read BOTH by 16-row ds_read_b128 row reads (rows 16w + L,
+// chunks 4i + g) and by tr_read_img (rows k0 + 8g + 0..7): the default swz is 2-way
+// bank-conflicted on the row reads (dy3: 20% of LDS cycles); this one (row bits 0, 1, 3 ->
+// chunk bits 3, 2, 1) is conflict-free on both (scripts/probes/fa_bank_model.py model).
+__device__ __forceinline__ int swz_b(int row) {
+  return ((row & 1) << 3) | ((row & 2) << 1) | (((row >> 3) & 1) << 1);
+}
+__device__ __forceinline__ int img_off_b(int row, int chunk) {
+  return row * 256 + ((chunk ^ swz_b(row)) << 4);
+}
+__device__ __forceinline__ uint4 row_read_b(const char* img, int row, int chunk) {
+  return *reinterpret_cast<const uint4*>(img + img_off_b(row, chunk));
+}
+__device__ __forceinline__ uint4 tr_read_img_b(const char* img, int k0, int n0, int lane) {
+  const int L = lane & 15, g = lane >> 4;
+  const int col = n0 + 4 * (L & 3);
+  const int ch = col >> 3, half = (col >> 2) & 1;
+  const int r = k0 + 8 * g + (L >> 2);
+  const uint2 lo = tr_read_raw(img + img_off_b(r, ch) + 8 * half);
+  const uint2 hi = tr_read_raw(img + img_off_b(r + 4, ch) + 8 * half);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
 // 8 floats -> 8 packed 16-bit values (round to nearest even)
 template <typename T>
 __device__ __forceinline__ uint4 pack8(const float (&v)[8]) {

@@ -242,15 +242,20 @@ def rope_write_kv(qkv: torch.Tensor, positions: torch.Tensor, nh: int, nkv: int,
 _TILE_CACHE = {}
 
 
-def _tiles(cu: tuple, rows: int, device, heavy_first: bool = True) -> torch.Tensor:
-    key = (cu, rows, str(device), heavy_first)
+def _tiles(cu: tuple, rows: int, device, heavy_first: bool = True,
+           heavy_low: bool = False) -> torch.Tensor:
+    """(seq, row start) pairs; heavy_first: causal query tiles (last rows = most keys) first;
+    heavy_low: key tiles of the dK/dV kernels (first rows = most queries) first."""
+    key = (cu, rows, str(device), heavy_first, heavy_low)
     t = _TILE_CACHE.get(key)
     if t is None:
         lst = []
         for s in range(len(cu) - 1):
             L = cu[s + 1] - cu[s]
             lst += [(s, r) for r in range(0, L, rows)]
-        if heavy_first:  # causal: the last tiles of a sequence carry the most keys
+        if heavy_low:
+            lst.sort(key=lambda x: (x[1], -(cu[x[0] + 1] - cu[x[0]])))
+        elif heavy_first:  # causal: the last tiles of a sequence carry the most keys
             lst.sort(key=lambda x: -x[1])
         t = torch.tensor(lst if lst else [(0, 0)], dtype=torch.int32, device=device).reshape(-1)
         if not lst:
@@ -316,7 +321,7 @@ def prepare_varlen(cu: tuple, device) -> None:
     host-to-device copy, before the layer loop: every layer's forward and backward then hits
     the cache instead of building (and synchronously uploading) its tile lists."""
     rows_set = (FA_FWD_ROWS, 64, 128)
-    keys = [("cu", cu, str(device))] + [(cu, r, str(device), True) for r in rows_set]
+    keys = [("cu", cu, str(device))] + [(cu, r, str(device), True, False) for r in rows_set]
     if all(k in _TILE_CACHE for k in keys):
         return
     parts = [list(cu)]
@@ -363,6 +368,10 @@ FA_DQ_DELTA = _os.environ.get("LUMEN_FA_DQ_DELTA", "0") == "1"
 # dQ = dS K from it, instead of recomputing S = Q K^T and dP = dO V^T (2 of its 3 products).
 # Used while the [nh, tiles, 64, 64] 16-bit buffer stays under LUMEN_FA_DS_MB (0 = off).
 FA_DS_MB = float(_os.environ.get("LUMEN_FA_DS_MB", "2048"))
+# dK/dV kernel of the dS hand-off path: "8" = 8 waves x 16 keys (128-key tiles, 3-stage DMA ring,
+# one barrier per step; opt-in: 117.6 vs 108.0 us at B=8 S=512, gpurun r2_36), "4" = the 4-wave
+# 64-key kernel
+FA_DKDV = _os.environ.get("LUMEN_FA_DKDV", "4")
 # XCD-grouped 1-D launches (_xcd_tiles) for the forward and the dS hand-off backward: opt-in,
 # measured neutral at B=8 S=512 (dK/dV 108 -> 110 us, dQ 30 -> 31 us, gpurun r2_34)
 FA_XCD = _os.environ.get("LUMEN_FA_XCD", "0") == "1"
@@ -440,7 +449,11 @@ class _FlashAttn(torch.autograd.Function):
             ds = torch.empty(nh, ds_total, 4096, device=qkv.device, dtype=qkv.dtype)
             C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
                          scale, do, None, None, None, delta, None, None, None)
-            if FA_XCD:
+            if FA_DKDV == "8":
+                t7, w7 = _tiles(cu, 128, qkv.device, heavy_low=causal), 10
+                t8, w8 = ((_xcd_tiles(cu, 64, nh, qkv.device, False), 0x108) if FA_XCD
+                          else (_tiles(cu, 64, qkv.device), 8))
+            elif FA_XCD:
                 t7, w7 = _xcd_tiles(cu, 64, nkv, qkv.device, causal), 0x107
                 t8, w8 = _xcd_tiles(cu, 64, nh, qkv.device, False), 0x108
             else:

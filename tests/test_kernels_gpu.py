@@ -363,11 +363,15 @@ def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch, dtype):
                                          (4, 4, [1000, 64, 129])])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_flash_attention_ds_handoff(nh, nkv, lens, causal, monkeypatch, dtype):
+@pytest.mark.parametrize("dkdv", ["8", "4"])
+def test_flash_attention_ds_handoff(nh, nkv, lens, causal, monkeypatch, dtype, dkdv):
     """dS hand-off backward (dK/dV kernel stores dS tiles, dQ = dS K from them) vs the fp32
-    reference, and dQ vs the recompute kernel (same bf16 dS operand: near-identical)."""
+    reference, and dQ vs the recompute kernel (same bf16 dS operand: near-identical); dkdv = the
+    8-wave 128-key or the 4-wave 64-key dK/dV kernel."""
     import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
+
+    monkeypatch.setattr(att, "FA_DKDV", dkdv)
 
     D = 128
     cu = [0]
@@ -391,7 +395,10 @@ def test_flash_attention_ds_handoff(nh, nkv, lens, causal, monkeypatch, dtype):
     assert rel(g[:, qs:qs + ks], g2[:, qs:qs + ks]) < 3e-2, "dk"
     assert rel(g[:, qs + ks:], g2[:, qs + ks:]) < 3e-2, "dv"
     assert rel(g[:, :qs], grads[0][:, :qs].float()) < 1e-2, "dq vs recompute"
-    assert torch.equal(grads[2048][:, qs:], grads[0][:, qs:]), "dk/dv unchanged"
+    if dkdv == "4":  # same dK/dV kernel with and without the dS store
+        assert torch.equal(grads[2048][:, qs:], grads[0][:, qs:]), "dk/dv unchanged"
+    else:
+        assert rel(g[:, qs:], grads[0][:, qs:].float()) < 1e-2, "dk/dv vs 4-wave kernel"
 
 
 @pytest.mark.parametrize("nh,nkv", [(8, 8), (8, 2)])
