@@ -351,6 +351,7 @@ struct DyArgs {
   int T, TW;
   float alpha;
   DySeg seg;
+  int probe;  // cost probes (0 in production): 16 dZ atomics, 32 dB atomics only when v == 1234.5
 };
 
 constexpr int kDyCC = 2;
@@ -480,7 +481,8 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int t = t0 + wid * 16 + g * 4 + r;
-          if (t < te) atomicAdd(dZ + (long long)t * a.lddz + jt * 16 + L, a.alpha * dzacc[jt][r]);
+          if (t < te && (!(a.probe & 16) || dzacc[jt][r] == 1234.5f))
+            atomicAdd(dZ + (long long)t * a.lddz + jt * 16 + L, a.alpha * dzacc[jt][r]);
         }
     }
   }
@@ -490,12 +492,14 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int jt = 0; jt < NJ; ++jt)
+      for (int jt = 0; jt < NJ; ++jt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = cb + cc * 128 + wid * 32 + m * 16 + g * 4 + r;
-          if (c < NL) atomicAdd(dB + (long long)c * a.r + jt * 16 + L, a.alpha * dbacc[cc][m][jt][r]);
+          if (c < NL && (!(a.probe & 32) || dbacc[cc][m][jt][r] == 1234.5f))
+            atomicAdd(dB + (long long)c * a.r + jt * 16 + L, a.alpha * dbacc[cc][m][jt][r]);
         }
+      }
   }
 }
 
@@ -522,6 +526,7 @@ struct DxaArgs {
   int T, K, R, TW;
   float da_scale, dx_scale;   // dA: keep-scale; dx: keep-scale (dZ already carries s)
   Drop drop;
+  int probe;  // cost probe (0 in production): 64 dA atomics only when v == 1234.5
 };
 
 constexpr int kDxST = 72;     // dZ^T LDS row stride (16-bit): 144 B
@@ -671,7 +676,8 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int k = c0 + wid * 32 + m * 16 + L, j = jt * 16 + g * 4 + r;
-        if (k < a.K && j < a.R) atomicAdd(a.dA + (long long)j * a.ldda + k, a.da_scale * da[m][jt][r]);
+        if (k < a.K && j < a.R && (!(a.probe & 64) || da[m][jt][r] == 1234.5f))
+          atomicAdd(a.dA + (long long)j * a.ldda + k, a.da_scale * da[m][jt][r]);
       }
 }
 
@@ -820,6 +826,7 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
       (ldy & 7))
     return hipErrorInvalidValue;
   lv3::DyArgs a;
+  a.probe = lv3_probe();
   a.dy = dy; a.ldy = ldy; a.B = B; a.r = r; a.Z = Z; a.ldz = ldz; a.dZ = dZ; a.lddz = lddz;
   a.dB = dB; a.T = T; a.TW = tw; a.alpha = alpha;
   a.seg.nseg = nseg;
@@ -896,6 +903,7 @@ extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, v
       (lda & 3) || tw < 64 || (tw & 63))
     return hipErrorInvalidValue;
   lv3::DxaArgs a;
+  a.probe = lv3_probe();
   a.x = x; a.ldx = ldx; a.dx = dx; a.lddx = lddx; a.dZ = dZ; a.A = A; a.lda = lda; a.dA = dA;
   a.ldda = ldda; a.T = T; a.K = K; a.R = R; a.TW = tw;
   const bool drop = thresh != 0;
