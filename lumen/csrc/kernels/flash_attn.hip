@@ -308,6 +308,9 @@ struct Args {
   // ordered on the host so that the tiles of one (sequence, head) land on one XCD together and
   // share its L2 (blocks go to XCDs round-robin by id; seq < 0 = padding); 0: pairs, head = y
   int tiles3;
+  int probe;  // cost probes (0 in production; LUMEN_FA_PROBE, dK/dV kernel only): 1 no DMA after
+              // step 1, 2 no S / dP products, 4 no dV / dK products, 8 no exp, 16 no dS
+              // stores, 32 no dK / dV epilogue stores
 };
 
 struct Work { int seq, r0, head; };
@@ -710,19 +713,6 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
   const int wk0 = k0 + wid * 16;  // this wave's 16 keys
   const int krow = wk0 + lr;      // the key of this lane's accumulator column
-  uint4 kf[4], vf[4];
-  {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      kf[ks] = gload16(K + (long long)krow * a.ldk + (4 * ks + lg) * 8, krow < L);
-      vf[ks] = gload16(V + (long long)krow * a.ldv + (4 * ks + lg) * 8, krow < L);
-    }
-  }
-  const int ds_base = WDS ? a.ds_off[seq] : 0;
-  wait_vm_all();
-  f32x4 dk[8], dv[8];
-#pragma unroll
-  for (int n = 0; n < 8; ++n) { dk[n] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[n] = dk[n]; }
   const int qstart = CAUSAL ? (k0 / 64) * 64 : 0;
   const int nq = qstart < L ? (L - qstart + 63) / 64 : 0;
   const int nsteps = grp * nq;  // (group head, query tile) pairs
@@ -731,6 +721,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   // counted vmcnt waits below stay exact: every wave keeps the same count per step, waves 0/1
   // issue one more, waited with vmcnt(0) on the last step only)
   auto stage = [&](int j, char* st) {
+    if ((a.probe & 1) && j >= 2) return;
     const int hh = j / nq, q0 = qstart + (j % nq) * 64;
     const int head = kvh * grp + hh;
     stage64_async_o<T, 1>(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
@@ -750,14 +741,27 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   uint4 pend[2];
   long long pend_off = -1;
   auto store_pend = [&]() {
-    if (pend_off < 0) return;
+    if (pend_off < 0 || (a.probe & 16)) return;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       char* dst = reinterpret_cast<char*>(a.ds) + pend_off + (wid * 2 + ks) * 1024 + ds_slot(lg, lr);
       *reinterpret_cast<uint4*>(dst) = pend[ks];
     }
   };
+  // stage 0's DMA and this wave's K / V fragment loads are in flight together (one latency,
+  // not two, before the first step); the full drain below retires both
   if (nsteps > 0) stage(0, bufA);
+  uint4 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = gload16(K + (long long)krow * a.ldk + (4 * ks + lg) * 8, krow < L);
+    vf[ks] = gload16(V + (long long)krow * a.ldv + (4 * ks + lg) * 8, krow < L);
+  }
+  const int ds_base = WDS ? a.ds_off[seq] : 0;
+  wait_vm_all();
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) { dk[n] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[n] = dk[n]; }
   auto step = [&](int j, char* st, char* nx) {
     char* qimg = st;
     char* oimg = st + IMG;
@@ -777,6 +781,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     f32x4 sc[4], dp[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) { sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[nt] = sc[nt]; }
+    if (!(a.probe & 2)) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
@@ -784,6 +789,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
         sc[nt] = Mfma<T>::run(row_read<1>(qimg, nt * 16 + lr, 4 * ks + lg), kf[ks], sc[nt]);
         dp[nt] = Mfma<T>::run(row_read<1>(oimg, nt * 16 + lr, 4 * ks + lg), vf[ks], dp[nt]);
       }
+    }
     }
     // lane: key krow, queries q0 + 16nt + 4lg + r
     // (WDS: keys past the end must also store dS = 0 -- dQ multiplies it by the clamped K rows;
@@ -797,7 +803,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qc = nt * 16 + 4 * lg + r;
-        float pv = fexp2(sc[nt][r] * a.scale_log2 - lq[r]);
+        float pv = (a.probe & 8) ? sc[nt][r] * a.scale_log2 - lq[r] : fexp2(sc[nt][r] * a.scale_log2 - lq[r]);
         if (need_mask && (krow >= L || q0 + qc >= L || (CAUSAL && krow > q0 + qc))) pv = 0.f;
         sc[nt][r] = pv;
         dp[nt][r] = pv * (dp[nt][r] - dq4[r]);
@@ -809,10 +815,15 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
       const uint4 pa = pack_p<T>(sc[2 * ks], sc[2 * ks + 1]);
       const uint4 da = pack_p<T>(dp[2 * ks], dp[2 * ks + 1]);
       if constexpr (WDS) pend[ks] = da;
+      if (!(a.probe & 4)) {
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
         dv[n] = Mfma<T>::run(pa, tr_read_img2<1>(oimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dv[n]);
         dk[n] = Mfma<T>::run(da, tr_read_img2<1>(qimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dk[n]);
+      }
+      } else {
+        dv[0][0] += __builtin_bit_cast(float, pa.x);  // keep P / dS live
+        dk[0][0] += __builtin_bit_cast(float, da.y);
       }
     }
     if constexpr (WDS)
@@ -830,7 +841,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int kr = wk0 + 4 * lg + r;
-    if (kr >= L) continue;
+    if (kr >= L || ((a.probe & 32) && dk[0][r] != 1234.5f)) continue;
     float kv[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
@@ -1878,6 +1889,12 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 }  // namespace fa
 }  // namespace lumen
 
+#include <cstdlib>
+static int fa_probe() {
+  static int v = [] { const char* e = std::getenv("LUMEN_FA_PROBE"); return e ? std::atoi(e) : 0; }();
+  return v;
+}
+
 // which: 0 = forward (tiles of 64*mt query rows; mt >= 10 selects the transposed-formulation
 //        kernel with 64*(mt-10)-row tiles; mt == 20 the 32x32x16 kernel, 128-row tiles),
 //        1 = delta, 2 = dK/dV (64-key tiles), 3 = dQ (64-query tiles),
@@ -1909,7 +1926,7 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.lddv = lddv; a.delta = delta;
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
-  a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3;
+  a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3; a.probe = 0;
   if (which == 6 || which == 7 || which == 8) return hipErrorInvalidValue;  // other entries
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
@@ -1966,6 +1983,7 @@ extern "C" hipError_t lumen_flash_attn_ds(int dtype, int which, int causal, cons
   a.lddv = lddv; a.delta = delta;
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.ds = ds; a.ds_off = ds_off; a.ds_total = ds_total; a.tiles3 = tiles3;
+  a.probe = fa_probe();
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, 1, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, 1, ntiles, a, st);
   return hipErrorInvalidValue;

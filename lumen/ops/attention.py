@@ -321,15 +321,19 @@ def prepare_varlen(cu: tuple, device) -> None:
     host-to-device copy, before the layer loop: every layer's forward and backward then hits
     the cache instead of building (and synchronously uploading) its tile lists."""
     rows_set = (FA_FWD_ROWS, 64, 128)
-    keys = [("cu", cu, str(device))] + [(cu, r, str(device), True, False) for r in rows_set]
+    keys = ([("cu", cu, str(device))] + [(cu, r, str(device), True, False) for r in rows_set]
+            + [(cu, 64, str(device), True, True)])
     if all(k in _TILE_CACHE for k in keys):
         return
     parts = [list(cu)]
-    for rows in rows_set:
+    for rows, low in [(r, False) for r in rows_set] + [(64, True)]:
         lst = []
         for s in range(len(cu) - 1):
             lst += [(s, r) for r in range(0, cu[s + 1] - cu[s], rows)]
-        lst.sort(key=lambda x: -x[1])
+        if low:  # dK/dV key tiles, heaviest (lowest) first
+            lst.sort(key=lambda x: (x[1], -(cu[x[0] + 1] - cu[x[0]])))
+        else:
+            lst.sort(key=lambda x: -x[1])
         parts.append([v for t in lst for v in t])
     flat = torch.tensor([v for p in parts for v in p], dtype=torch.int32)
     if torch.cuda.is_available():
@@ -372,6 +376,7 @@ FA_DS_MB = float(_os.environ.get("LUMEN_FA_DS_MB", "2048"))
 # one barrier per step; opt-in: 117.6 vs 108.0 us at B=8 S=512, gpurun r2_36), "4" = the 4-wave
 # 64-key kernel
 FA_DKDV = _os.environ.get("LUMEN_FA_DKDV", "4")
+FA_DKDV_HEAVY = _os.environ.get("LUMEN_FA_DKDV_HEAVY", "1") == "1"  # A/B switch of that order
 # XCD-grouped 1-D launches (_xcd_tiles) for the forward and the dS hand-off backward: opt-in,
 # measured neutral at B=8 S=512 (dK/dV 108 -> 110 us, dQ 30 -> 31 us, gpurun r2_34)
 FA_XCD = _os.environ.get("LUMEN_FA_XCD", "0") == "1"
@@ -457,7 +462,9 @@ class _FlashAttn(torch.autograd.Function):
                 t7, w7 = _xcd_tiles(cu, 64, nkv, qkv.device, causal), 0x107
                 t8, w8 = _xcd_tiles(cu, 64, nh, qkv.device, False), 0x108
             else:
-                t7 = t8 = _tiles(cu, 64, qkv.device)
+                # dK/dV: low key tiles carry the most (causal) query steps -> launched first
+                t7 = _tiles(cu, 64, qkv.device, heavy_low=causal and FA_DKDV_HEAVY)
+                t8 = _tiles(cu, 64, qkv.device)
                 w7, w8 = 7, 8
             C.flash_attn_ds(w7, causal, q, k, v, lse, cut, t7, nh, nkv,
                             scale, do, dq, dk, dv, delta, ds, ds_off, ds_total, pos, cos, sin)
