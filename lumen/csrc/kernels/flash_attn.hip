@@ -308,9 +308,10 @@ struct Args {
   // ordered on the host so that the tiles of one (sequence, head) land on one XCD together and
   // share its L2 (blocks go to XCDs round-robin by id; seq < 0 = padding); 0: pairs, head = y
   int tiles3;
+  int nitems;  // > 0: persistent dK/dV launch over nitems = ntiles * nkv items (1-D grid)
   int probe;  // cost probes (0 in production; LUMEN_FA_PROBE, dK/dV kernel only): 1 no DMA after
               // step 1, 2 no S / dP products, 4 no dV / dK products, 8 no exp, 16 no dS
-              // stores, 32 no dK / dV epilogue stores
+              // stores, 32 no dK / dV epilogue stores, 128 no steps (prologue + epilogue only)
 };
 
 struct Work { int seq, r0, head; };
@@ -703,10 +704,12 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char bufB[STAGE];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const Work wk = work_item(a);
-  if (wk.seq < 0) return;
-  const int seq = wk.seq, k0 = wk.r0;
-  const int kvh = wk.head;
+  // persistent (a.nitems > 0): a grid of ~2 workgroups per CU walks the (key tile, kv head)
+  // items in the host's heaviest-first order.  One workgroup's dK/dV stores (and dS flush) are
+  // then still draining while its next item's K / V fragments and first Q / dO stage load,
+  // instead of the workgroup slot idling on both latencies (prologue + epilogue alone measured
+  // 35 us of a ~110 us call as one-shot workgroups, probe 128)
+  auto run = [&](const int seq, const int k0, const int kvh) {
   const int grp = a.nh / a.nkv;
   const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
   const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
@@ -715,7 +718,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   const int krow = wk0 + lr;      // the key of this lane's accumulator column
   const int qstart = CAUSAL ? (k0 / 64) * 64 : 0;
   const int nq = qstart < L ? (L - qstart + 63) / 64 : 0;
-  const int nsteps = grp * nq;  // (group head, query tile) pairs
+  const int nsteps = (a.probe & 128) ? 0 : grp * nq;  // (group head, query tile) pairs
   // stage step j: Q / dO tiles via 8 DMA instructions per wave, lse / delta via one 4-byte DMA
   // instruction on waves 0 / 1 (the DMA ring stays the only in-loop global traffic, so the
   // counted vmcnt waits below stay exact: every wave keeps the same count per step, waves 0/1
@@ -794,20 +797,39 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     // lane: key krow, queries q0 + 16nt + 4lg + r
     // (WDS: keys past the end must also store dS = 0 -- dQ multiplies it by the clamped K rows;
     // without the hand-off those keys' dK / dV rows are simply never written)
-    const bool need_mask = (q0 + 64 > L) || (CAUSAL && wk0 + 15 > q0) || (WDS && k0 + 64 > L);
+    // wave-uniform (readfirstlane: an SGPR, so ONE scalar branch picks the masked or the plain
+    // copy below); a per-element `if (need_mask && ...)` compiled to exec-mask save / branch /
+    // restore around every element, ~200 scalar instructions per step on unmasked tiles
+    const int need_mask = __builtin_amdgcn_readfirstlane(
+        ((q0 + 64 > L) || (CAUSAL && wk0 + 15 > q0) || (WDS && k0 + 64 > L)) ? 1 : 0);
+    float lq[4][4], dq4[4][4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const float4 l4 = *reinterpret_cast<const float4*>(s_lse + nt * 16 + 4 * lg);
       const float4 d4 = *reinterpret_cast<const float4*>(s_del + nt * 16 + 4 * lg);
-      const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
+      lq[nt][0] = l4.x; lq[nt][1] = l4.y; lq[nt][2] = l4.z; lq[nt][3] = l4.w;
+      dq4[nt][0] = d4.x; dq4[nt][1] = d4.y; dq4[nt][2] = d4.z; dq4[nt][3] = d4.w;
+    }
+    if (need_mask) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qc = nt * 16 + 4 * lg + r;
-        float pv = (a.probe & 8) ? sc[nt][r] * a.scale_log2 - lq[r] : fexp2(sc[nt][r] * a.scale_log2 - lq[r]);
-        if (need_mask && (krow >= L || q0 + qc >= L || (CAUSAL && krow > q0 + qc))) pv = 0.f;
-        sc[nt][r] = pv;
-        dp[nt][r] = pv * (dp[nt][r] - dq4[r]);
-      }
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qc = nt * 16 + 4 * lg + r;
+          const bool out = (krow >= L) | (q0 + qc >= L) | (CAUSAL & (krow > q0 + qc));
+          const float pv = out ? 0.f : fexp2(sc[nt][r] * a.scale_log2 - lq[nt][r]);
+          sc[nt][r] = pv;
+          dp[nt][r] = pv * (dp[nt][r] - dq4[nt][r]);
+        }
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = fexp2(sc[nt][r] * a.scale_log2 - lq[nt][r]);
+          sc[nt][r] = pv;
+          dp[nt][r] = pv * (dp[nt][r] - dq4[nt][r]);
+        }
     }
     // dV += P^T dO ; dK += dS^T Q   (k = queries in the permuted order)
 #pragma unroll
@@ -856,6 +878,17 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
       dK[(long long)kr * a.lddk + n * 16 + lr] = from_f32<T>(kv[n]);
       dV[(long long)kr * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
     }
+  }
+  };
+  if (a.nitems > 0) {
+    for (int it = blockIdx.x; it < a.nitems; it += gridDim.x) {
+      const int ti = it / a.nkv;
+      run(a.tiles[2 * ti], a.tiles[2 * ti + 1], it - ti * a.nkv);
+    }
+  } else {
+    const Work wk = work_item(a);
+    if (wk.seq < 0) return;
+    run(wk.seq, wk.r0, wk.head);
   }
 }
 
@@ -1810,6 +1843,17 @@ __global__ void __launch_bounds__(512) bwd_dkdv8_kernel(Args a) {
   }
 }
 
+static int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 template <typename T>
 static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& a, hipStream_t st) {
   dim3 block(256);
@@ -1861,6 +1905,7 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     }
   } else if (which == 7) {  // dK/dV (64-key tiles) + dS hand-off
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nkv);
+    if (a.nitems > 0) grid = dim3(std::min(a.nitems, 2 * cu_count()), 1);
     if (causal) hipLaunchKernelGGL((bwd_dkdv_kernel<T, true, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dkdv_kernel<T, false, true>), grid, block, 0, st, a);
   } else if (which == 9 || which == 10) {  // dK/dV, 8 waves, 128-key tiles (10: + dS hand-off)
@@ -1889,7 +1934,12 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 }  // namespace fa
 }  // namespace lumen
 
+#include <algorithm>
 #include <cstdlib>
+static bool fa_persist() {
+  static bool v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return !e || std::atoi(e) != 0; }();
+  return v;
+}
 static int fa_probe() {
   static int v = [] { const char* e = std::getenv("LUMEN_FA_PROBE"); return e ? std::atoi(e) : 0; }();
   return v;
@@ -1927,6 +1977,7 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
   a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3; a.probe = 0;
+  a.nitems = 0;
   if (which == 6 || which == 7 || which == 8) return hipErrorInvalidValue;  // other entries
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
@@ -1984,6 +2035,7 @@ extern "C" hipError_t lumen_flash_attn_ds(int dtype, int which, int causal, cons
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.ds = ds; a.ds_off = ds_off; a.ds_total = ds_total; a.tiles3 = tiles3;
   a.probe = fa_probe();
+  a.nitems = (which == 7 && !tiles3 && fa_persist()) ? ntiles * nkv : 0;
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, 1, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, 1, ntiles, a, st);
   return hipErrorInvalidValue;
