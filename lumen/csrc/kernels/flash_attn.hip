@@ -1212,10 +1212,10 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char bufB[2 * IMG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lq = lane & 31, hi = lane >> 5;
-  const Work wk = work_item(a);
-  if (wk.seq < 0) return;
-  const int seq = wk.seq, q0 = wk.r0;
-  const int head = wk.head, kvh = head / (a.nh / a.nkv);
+  // persistent (a.nitems > 0, as bwd_dkdv_kernel): the workgroups walk the (query tile, head)
+  // items, so one item's O / LSE stores drain under the next item's Q loads and first K / V DMA
+  auto run = [&](const int seq, const int q0, const int head) {
+  const int kvh = head / (a.nh / a.nkv);
   const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;  // L = this sequence's query rows
   // keys: self-attention over the same rows, or (PAGED) the cached context + this chunk, the
   // chunk's queries sitting at key positions qoff .. qoff + L - 1
@@ -1290,6 +1290,17 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
       }
     if (hi == 0 && a.lse)
       a.lse[(long long)head * a.T + s0 + qrow] = l_i > 0.f ? m_i + __log2f(l_i) : INFINITY;
+  }
+  };
+  if (a.nitems > 0) {
+    for (int it = blockIdx.x; it < a.nitems; it += gridDim.x) {
+      const int ti = it / a.nh;
+      run(a.tiles[2 * ti], a.tiles[2 * ti + 1], it - ti * a.nh);
+    }
+  } else {
+    const Work wk = work_item(a);
+    if (wk.seq < 0) return;
+    run(wk.seq, wk.r0, wk.head);
   }
 }
 
@@ -1608,10 +1619,9 @@ __global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char bufB[TILE];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const Work wk = work_item(a);
-  if (wk.seq < 0) return;
-  const int seq = wk.seq, q0 = wk.r0;
-  const int head = wk.head, kvh = head / (a.nh / a.nkv);
+  // persistent (a.nitems > 0, as bwd_dkdv_kernel) over (query tile, head) items
+  auto run = [&](const int seq, const int q0, const int head) {
+  const int kvh = head / (a.nh / a.nkv);
   const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
   const int ns = (L + 63) / 64, qt = q0 / 64;
   const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
@@ -1678,6 +1688,17 @@ __global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
     }
 #pragma unroll
     for (int n = 0; n < 8; ++n) dQ[(long long)qr * a.lddq + n * 16 + lr] = from_f32<T>(qv[n]);
+  }
+  };
+  if (a.nitems > 0) {
+    for (int it = blockIdx.x; it < a.nitems; it += gridDim.x) {
+      const int ti = it / a.nh;
+      run(a.tiles[2 * ti], a.tiles[2 * ti + 1], it - ti * a.nh);
+    }
+  } else {
+    const Work wk = work_item(a);
+    if (wk.seq < 0) return;
+    run(wk.seq, wk.r0, wk.head);
   }
 }
 
@@ -1860,6 +1881,7 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
   if (which == 0) {
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
     if (mt == 20) {  // 32x32x16 kernel, 128-row tiles
+      if (a.nitems > 0) grid = dim3(std::min(a.nitems, (causal ? 2 : 1) * cu_count()), 1);
       if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
       else hipLaunchKernelGGL((fwd32_kernel<T, false>), grid, block, 0, st, a);
     } else if (mt >= 10) {  // transposed-formulation kernel, QG = mt - 10 query groups per wave
@@ -1919,6 +1941,7 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     }
   } else if (which == 8) {  // dQ from the dS hand-off (64-query tiles)
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
+    if (a.nitems > 0) grid = dim3(std::min(a.nitems, 3 * cu_count()), 1);  // 48 KiB LDS: 3 / CU
     if (causal) hipLaunchKernelGGL((bwd_dq_ds_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dq_ds_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 6) {  // forward over the paged KV cache (32x32x16, 128-row tiles)
@@ -1936,8 +1959,11 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 
 #include <algorithm>
 #include <cstdlib>
-static bool fa_persist() {
-  static bool v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return !e || std::atoi(e) != 0; }();
+// persistent launches (bit 0 dK/dV, 1 forward, 2 dQ-from-dS); LUMEN_FA_PERSIST overrides.
+// Default dK/dV only: same-box A/B at B=8 S=512 (gpurun r2_51) dK/dV 109.6 -> 91.6 us, forward
+// 52.4 -> 55.6, dQ 35.2 -> 39.4 (those two lose the hardware's dynamic load balance)
+static int fa_persist() {
+  static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 1; }();
   return v;
 }
 static int fa_probe() {
@@ -1977,7 +2003,7 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
   a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3; a.probe = 0;
-  a.nitems = 0;
+  a.nitems = (which == 0 && mt == 20 && !tiles3 && (fa_persist() & 2)) ? ntiles * nh : 0;
   if (which == 6 || which == 7 || which == 8) return hipErrorInvalidValue;  // other entries
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
@@ -2035,7 +2061,8 @@ extern "C" hipError_t lumen_flash_attn_ds(int dtype, int which, int causal, cons
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.ds = ds; a.ds_off = ds_off; a.ds_total = ds_total; a.tiles3 = tiles3;
   a.probe = fa_probe();
-  a.nitems = (which == 7 && !tiles3 && fa_persist()) ? ntiles * nkv : 0;
+  a.nitems = tiles3 ? 0 : (which == 7 && (fa_persist() & 1)) ? ntiles * nkv
+                        : (which == 8 && (fa_persist() & 4)) ? ntiles * nh : 0;
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, 1, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, 1, ntiles, a, st);
   return hipErrorInvalidValue;
