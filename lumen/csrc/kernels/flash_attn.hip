@@ -309,6 +309,7 @@ struct Args {
   // share its L2 (blocks go to XCDs round-robin by id; seq < 0 = padding); 0: pairs, head = y
   int tiles3;
   int nitems;  // > 0: persistent dK/dV launch over nitems = ntiles * nkv items (1-D grid)
+  int snake;   // persistent item order: 1 snake rounds, 0 plain strided
   int probe;  // cost probes (0 in production; LUMEN_FA_PROBE, dK/dV kernel only): 1 no DMA after
               // step 1, 2 no S / dP products, 4 no dV / dK products, 8 no exp, 16 no dS
               // stores, 32 no dK / dV epilogue stores, 128 no steps (prologue + epilogue only)
@@ -881,7 +882,12 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   }
   };
   if (a.nitems > 0) {
-    for (int it = blockIdx.x; it < a.nitems; it += gridDim.x) {
+    // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
+    // r*G + G-1-w (odd r), pairing heavy with light items per workgroup (static balance)
+    const int G = gridDim.x, w = blockIdx.x;
+    for (int base = 0; base < a.nitems; base += G) {
+      const int it = (a.snake && ((base / G) & 1)) ? base + G - 1 - w : base + w;
+      if (it >= a.nitems) continue;
       const int ti = it / a.nkv;
       run(a.tiles[2 * ti], a.tiles[2 * ti + 1], it - ti * a.nkv);
     }
@@ -1293,7 +1299,12 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   }
   };
   if (a.nitems > 0) {
-    for (int it = blockIdx.x; it < a.nitems; it += gridDim.x) {
+    // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
+    // r*G + G-1-w (odd r), pairing heavy with light items per workgroup (static balance)
+    const int G = gridDim.x, w = blockIdx.x;
+    for (int base = 0; base < a.nitems; base += G) {
+      const int it = (a.snake && ((base / G) & 1)) ? base + G - 1 - w : base + w;
+      if (it >= a.nitems) continue;
       const int ti = it / a.nh;
       run(a.tiles[2 * ti], a.tiles[2 * ti + 1], it - ti * a.nh);
     }
@@ -1691,7 +1702,12 @@ __global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
   }
   };
   if (a.nitems > 0) {
-    for (int it = blockIdx.x; it < a.nitems; it += gridDim.x) {
+    // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
+    // r*G + G-1-w (odd r), pairing heavy with light items per workgroup (static balance)
+    const int G = gridDim.x, w = blockIdx.x;
+    for (int base = 0; base < a.nitems; base += G) {
+      const int it = (a.snake && ((base / G) & 1)) ? base + G - 1 - w : base + w;
+      if (it >= a.nitems) continue;
       const int ti = it / a.nh;
       run(a.tiles[2 * ti], a.tiles[2 * ti + 1], it - ti * a.nh);
     }
@@ -1959,11 +1975,13 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 
 #include <algorithm>
 #include <cstdlib>
-// persistent launches (bit 0 dK/dV, 1 forward, 2 dQ-from-dS); LUMEN_FA_PERSIST overrides.
-// Default dK/dV only: same-box A/B at B=8 S=512 (gpurun r2_51) dK/dV 109.6 -> 91.6 us, forward
+// persistent launches (bit 0 dK/dV, 1 forward, 2 dQ-from-dS; bit 3 snake item order);
+// LUMEN_FA_PERSIST overrides.
+// Default 9 = dK/dV only, snake order (r2_55: 98.0 -> 96.3 us same box); same-box A/B at B=8
+// S=512 (gpurun r2_51) dK/dV 109.6 -> 91.6 us persistent, forward
 // 52.4 -> 55.6, dQ 35.2 -> 39.4 (those two lose the hardware's dynamic load balance)
 static int fa_persist() {
-  static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 1; }();
+  static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 9; }();
   return v;
 }
 static int fa_probe() {
@@ -2004,6 +2022,7 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
   a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3; a.probe = 0;
   a.nitems = (which == 0 && mt == 20 && !tiles3 && (fa_persist() & 2)) ? ntiles * nh : 0;
+  a.snake = (fa_persist() >> 3) & 1;
   if (which == 6 || which == 7 || which == 8) return hipErrorInvalidValue;  // other entries
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(which, causal, mt, ntiles, a, st);
@@ -2061,6 +2080,7 @@ extern "C" hipError_t lumen_flash_attn_ds(int dtype, int which, int causal, cons
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.ds = ds; a.ds_off = ds_off; a.ds_total = ds_total; a.tiles3 = tiles3;
   a.probe = fa_probe();
+  a.snake = (fa_persist() >> 3) & 1;
   a.nitems = tiles3 ? 0 : (which == 7 && (fa_persist() & 1)) ? ntiles * nkv
                         : (which == 8 && (fa_persist() & 4)) ? ntiles * nh : 0;
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, 1, ntiles, a, st);
