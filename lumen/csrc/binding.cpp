@@ -49,7 +49,7 @@ hipError_t lumen_lora3_dxa(int, const void*, long long, void*, long long, const 
 hipError_t lumen_embedding(const void*, const long long*, void*, int, int, int, hipStream_t);
 hipError_t lumen_lora3_down(int, const void*, long long, const float*, long long, float*, long long,
                             int, int, int, float, unsigned long long, unsigned int, float, long long,
-                            long long, hipStream_t);
+                            long long, void*, long long, int, int, unsigned*, hipStream_t);
 hipError_t lumen_lora3_up(int, int, void*, long long, const float*, long long, const float*,
                           long long, int, int, float, unsigned long long, unsigned int, float,
                           long long, long long, int, const long long*, const long long*,
@@ -369,17 +369,33 @@ void need_cuda_f32(const at::Tensor& t, const char* what) {
 // Z[t, :R] += alpha * drop(x) A^T   (x [T, K] 16-bit, row stride ldx; A [R, K] f32; Z f32)
 void lora3_down(const at::Tensor& x, int64_t ldx, const at::Tensor& A, at::Tensor& Z, int64_t ldz,
                 int64_t T, int64_t K, int64_t R, double alpha, int64_t seed, int64_t thresh,
-                double drop_scale, int64_t drop_ld, int64_t drop_col0) {
+                double drop_scale, int64_t drop_ld, int64_t drop_col0,
+                const c10::optional<at::Tensor>& xe, int64_t xk, int64_t KP,
+                const c10::optional<at::Tensor>& cnt) {
   if (!x.is_cuda()) throw std::invalid_argument("lumen: lora3_down needs GPU tensors");
   need_cuda_f32(A, "lora3_down A");
   need_cuda_f32(Z, "lora3_down Z");
   if (A.stride(1) != 1 || A.size(0) < R || A.size(1) < K || x.size(0) < T || Z.size(0) < T)
     throw std::invalid_argument("lumen: lora3_down shape mismatch");
+  void* xp = nullptr;
+  long long ldxe = 0;
+  unsigned* cp = nullptr;
+  if (xe && xe->defined()) {
+    // fused fold tail: xe [>= T, >= xk + KP] 16-bit like x, cnt int32 [>= ceil(T / 64)] zeroed
+    if (!cnt || !cnt->defined() || cnt->scalar_type() != at::kInt || !cnt->is_cuda() ||
+        cnt->numel() < (T + 63) / 64 || xe->scalar_type() != x.scalar_type() || xe->dim() != 2 ||
+        xe->stride(1) != 1 || xe->size(0) < T || xe->size(1) < xk + KP || Z.size(1) < R)
+      throw std::invalid_argument("lumen: lora3_down fold tail: xe [T, >= xk + KP], cnt int32 [T / 64]");
+    xp = xe->data_ptr();
+    ldxe = xe->stride(0);
+    cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+  }
   check(lumen_lora3_down(dcode(x), x.data_ptr(), ldx, A.data_ptr<float>(), A.stride(0),
                          Z.data_ptr<float>(), ldz, static_cast<int>(T), static_cast<int>(K),
                          static_cast<int>(R), static_cast<float>(alpha),
                          static_cast<unsigned long long>(seed), static_cast<unsigned int>(thresh),
-                         static_cast<float>(drop_scale), drop_ld, drop_col0, cur_stream()),
+                         static_cast<float>(drop_scale), drop_ld, drop_col0, xp, ldxe,
+                         static_cast<int>(xk), static_cast<int>(KP), cp, cur_stream()),
         "lora3_down");
 }
 
@@ -815,7 +831,11 @@ void car_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>&
 PYBIND11_MODULE(_C, m) {
   m.doc() = "lumen native ops for MI355X (gfx950)";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
-  m.def("lora3_down", &lora3_down);
+  m.def("lora3_down", &lora3_down, py::arg("x"), py::arg("ldx"), py::arg("A"), py::arg("Z"),
+        py::arg("ldz"), py::arg("T"), py::arg("K"), py::arg("R"), py::arg("alpha"), py::arg("seed"),
+        py::arg("thresh"), py::arg("drop_scale"), py::arg("drop_ld"), py::arg("drop_col0"),
+        py::arg("xe") = py::none(), py::arg("xk") = 0, py::arg("KP") = 0,
+        py::arg("cnt") = py::none());
   m.def("embedding", &embedding);
   m.def("lora3_dxa", &lora3_dxa);
   m.def("lora3_z_tail", &lora3_z_tail);

@@ -63,6 +63,11 @@ struct DownArgs {
   Drop drop;
   int probe;   // cost probes (0 in production): 1 no dropout hash, 2 no A loads, 4 no reduction,
                // 8 no global atomics
+  // fused fold tail (xe != nullptr): the last of the gridDim.y K-blocks of a 64-row tile to
+  // arrive writes xe[t, xk + c] = c < J ? Z[t, c] : 0 for c < KP (16-bit), so no separate
+  // z_tail launch.  cnt[blockIdx.x] arrival counters: zero on entry, left at zero.
+  void* xe; long long ldxe; int xk, KP;
+  unsigned* cnt;
 };
 
 template <typename T, bool DROP, int NJ>
@@ -156,6 +161,36 @@ __global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
       if (a.probe & 8) { if (v == 1234.5f) a.Z[i] = v; }
       else atomicAdd(a.Z + (long long)t * a.ldz + j, v);
     }
+  }
+  if (a.xe == nullptr) return;
+  // last-arriver tail.  No fences: an agent-scope fence writes back the whole L2 (measured
+  // +36 us per call); the Z atomics are agent-scope already, so waiting for this wave's vector
+  // memory counter to drain is enough before the block counts in (same protocol as
+  // decode_gemm.hip's split-K reduction).
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    unsigned* cp = a.cnt + blockIdx.x;
+    const unsigned prev = __hip_atomic_fetch_add(cp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int l = prev == gridDim.y - 1;
+    if (l) __hip_atomic_store(cp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = l;
+  }
+  __syncthreads();
+  if (!last) return;
+  T* xe = reinterpret_cast<T*>(a.xe);
+  const int nch = a.KP / 8;
+  for (int i = threadIdx.x; i < 64 * nch; i += 512) {
+    const int row = i / nch, c = (i % nch) * 8, t = t0 + row;
+    if (t >= a.T) continue;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = c + e < J ? __hip_atomic_load(a.Z + (long long)t * a.ldz + c + e, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0.f;
+    store8(xe + (long long)t * a.ldxe + a.xk + c, v);
   }
 }
 
@@ -741,12 +776,15 @@ extern "C" hipError_t lumen_lora3_down(int dtype, const void* x, long long ldx, 
                                        long long lda, float* Z, long long ldz, int T, int K, int R,
                                        float alpha, unsigned long long seed, unsigned int thresh,
                                        float drop_scale, long long drop_ld, long long drop_col0,
+                                       void* xe, long long ldxe, int xk, int KP, unsigned* cnt,
                                        hipStream_t st) {
   if (T <= 0 || K <= 0 || R < 16 || R > 64 || (R & 15) || (K & 7) || (ldx & 7) || (lda & 3))
     return hipErrorInvalidValue;
+  if (xe != nullptr && (cnt == nullptr || (KP & 7) || KP < R || (ldxe & 7) || (xk & 7)))
+    return hipErrorInvalidValue;
   lv3::DownArgs a{x, ldx, A, lda, Z, ldz, T, K, alpha,
                   {static_cast<unsigned>(seed) ^ static_cast<unsigned>(seed >> 32), thresh, drop_scale,
-                   drop_ld, drop_col0}, lv3_probe()};
+                   drop_ld, drop_col0}, lv3_probe(), xe, ldxe, xk, KP, cnt};
   const dim3 grid((T + 63) / 64, (K + 1023) / 1024), block(512);
   const bool drop = thresh != 0;
 #define LV3_DOWN(TT, NJ)                                                                           \

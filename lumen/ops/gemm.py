@@ -94,6 +94,76 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None) -> tor
     return y
 
 
+# Training-shape GEMMs run 256 x 256 macro tiles, one per CU at a time, so a GEMM with 5.375 or
+# 2.69 waves of tiles on the 256-CU chip takes 6 or 3 waves (Llama-2-7B at T = 4096: gate|up
+# forward 16 x 86 tiles, down input-grad 16 x 43).  ``mm_nt`` splits the output columns at the
+# last whole wave and runs the remainder as its own (separately tuned) GEMM, both writing column
+# views of one buffer (ldc = full width, no copies).  lumen/bench/split_gemm_probe.py measures it.
+GEMM_SPLIT = os.environ.get("LUMEN_GEMM_SPLIT", "1") != "0"
+SPLIT_TILE, SPLIT_CUS, SPLIT_MAX_TAIL = 256, 256, 0.5
+
+
+def split_cols(M: int, N: int) -> int:
+    """Column count of the whole-wave part of an [M, N] output (0: no split).  Splits only when
+    the last wave is at most ``SPLIT_MAX_TAIL`` full and the wave boundary is a column-tile
+    boundary."""
+    if M % SPLIT_TILE or N % 8:
+        return 0
+    tm, tn = M // SPLIT_TILE, -(-N // SPLIT_TILE)
+    total = tm * tn
+    waves, tail = divmod(total, SPLIT_CUS)
+    if waves == 0 or tail == 0 or tail > SPLIT_MAX_TAIL * SPLIT_CUS or SPLIT_CUS % tm:
+        return 0
+    n1 = waves * (SPLIT_CUS // tm) * SPLIT_TILE
+    return n1 if 0 < n1 < N else 0
+
+
+_tuned: dict = {"n": -1, "sigs": frozenset()}
+
+
+def _tuned_sigs() -> frozenset:
+    """Problem signatures of the loaded TunableOp table (refreshed when its size changes)."""
+    try:
+        import torch.cuda.tunable as tn
+
+        if not tn.is_enabled():
+            return frozenset()
+        res = tn.get_results()
+    except Exception:  # noqa: BLE001
+        return frozenset()
+    if len(res) != _tuned["n"]:
+        _tuned["n"], _tuned["sigs"] = len(res), frozenset(r[1] for r in res)
+    return _tuned["sigs"]
+
+
+def _split_plan(x: torch.Tensor, w: torch.Tensor) -> int:
+    if not (GEMM_SPLIT and x.is_cuda and x.dim() == 2 and w.dim() == 2 and x.stride(1) == 1
+            and w.stride(1) == 1):
+        return 0
+    (M, K), N = x.shape, w.shape[0]
+    n1 = split_cols(M, N)
+    if not n1:
+        return 0
+    # only where both parts have tuned solutions (untuned shapes would fall to the heuristic)
+    sigs = _tuned_sigs()
+    lds = f"ld_{w.stride(0)}_{x.stride(0)}_{N}"
+    if f"tn_{n1}_{M}_{K}_{lds}" not in sigs or f"tn_{N - n1}_{M}_{K}_{lds}" not in sigs:
+        return 0
+    return n1
+
+
+def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x [M, K] @ w[N, K]^T -> [M, N] (w row-contiguous), split at the last whole wave of tiles
+    on the GPU (see ``split_cols``)."""
+    n1 = _split_plan(x, w)
+    if not n1:
+        return torch.matmul(x, w.t())
+    y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=torch.result_type(x, w))
+    torch.mm(x, w[:n1].t(), out=y[:, :n1])
+    torch.mm(x, w[n1:].t(), out=y[:, n1:])
+    return y
+
+
 def linear_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """x [M, K] @ w[N, K]^T -> [M, N]."""
     if skinny_ok(x, w):

@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from ._native import DTYPE_CODE, native, use_native
+from .gemm import mm_nt
 
 Seg = Tuple[int, int, int, int]
 
@@ -193,11 +194,32 @@ def _v3_ok(r: int, R: int, segs, *mats) -> bool:
             and all(m.stride(1) == 1 and m.stride(0) % 8 == 0 for m in mats))
 
 
-def _lora3_down(x2d, A, Z, p, seed):
+# fold: the DOWN kernel's last-arriving K-block writes the 16-bit Z tail of the extended operand
+# itself (no z_tail launch per adapted linear); LUMEN_LORA_FUSED_TAIL=0 keeps the separate kernel
+FUSED_TAIL = _os.environ.get("LUMEN_LORA_FUSED_TAIL", "0") == "1"
+_tail_counters: dict = {}
+
+
+def _tail_cnt(T: int, device) -> torch.Tensor:
+    """Arrival counters of the fused tail, one per 64-row tile: zeroed once, and the kernel
+    leaves them at zero (first use is in an eager step, before any graph capture)."""
+    key = (device.type, device.index)
+    c = _tail_counters.get(key)
+    need = (T + 63) // 64
+    if c is None or c.numel() < need:
+        c = torch.zeros(max(need, 1024), device=device, dtype=torch.int32)
+        _tail_counters[key] = c
+    return c
+
+
+def _lora3_down(x2d, A, Z, p, seed, xe=None, KP=0):
+    """Z += drop(x) A^T; with ``xe`` (the [T, K + KP] fold operand) also writes its Z tail."""
     T, K = x2d.shape
     R = A.shape[0]
     native().lora3_down(x2d, x2d.stride(0), A, Z, R, T, K, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
-                        drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0)
+                        drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0,
+                        xe, K if xe is not None else 0, KP,
+                        _tail_cnt(T, x2d.device) if xe is not None else None)
 
 
 def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope, gemm=None):
@@ -492,8 +514,11 @@ class _LoraLinear(torch.autograd.Function):
             R = A.shape[0]
             xe = fold_operand(x2d, K)
             Z = _zeros(T, R, device=x2d.device, train=ctx.train)
-            _lora3_down(x2d, A, Z, p, seed)
-            native().lora3_z_tail(Z, xe, K, FOLD_KP)
+            if FUSED_TAIL:
+                _lora3_down(x2d, A, Z, p, seed, xe, FOLD_KP)
+            else:
+                _lora3_down(x2d, A, Z, p, seed)
+                native().lora3_z_tail(Z, xe, K, FOLD_KP)
             y = torch.matmul(xe, fold.t())
             if bias is not None:
                 y.add_(bias)
@@ -555,7 +580,7 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, weight_fn, bias, w_param, wt_fn):
         W = weight_fn()
-        y = torch.matmul(x2d, W.t())
+        y = mm_nt(x2d, W)
         if bias is not None:
             y.add_(bias)
         ctx.weight_fn = weight_fn

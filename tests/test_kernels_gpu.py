@@ -940,3 +940,38 @@ def test_llama_lora_fold_matches_unfolded(p_drop, monkeypatch):
     w2 = mod.fold_weight()
     K = mod.in_features
     assert torch.equal(w1[:, :K], w2[:, :K]) and not torch.equal(w1[:, K:], w2[:, K:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,R", [(4096, 48), (1000, 16), (64, 64)])
+def test_lora3_down_fused_fold_tail(T, R):
+    """The DOWN kernel's last-arriving K-block writes the 16-bit Z tail of the fold operand:
+    bit-identical to the separate z_tail kernel, x columns untouched, counters back at zero."""
+    from lumen.ops import lora as L
+    from lumen.ops._native import native
+
+    dev = torch.device("cuda")
+    K, KP = 4096, L.FOLD_KP
+    g = torch.Generator(device=dev).manual_seed(3)
+    xe = torch.randn(T, K + KP, device=dev, generator=g).bfloat16()
+    A = torch.randn(R, K, device=dev, generator=g) * 0.02
+    x2d = xe[:, :K]
+    outs = []
+    for fused in (True, False):
+        buf = xe.clone()
+        Z = torch.zeros(T, R, device=dev)
+        if fused:
+            L._lora3_down(buf[:, :K], A, Z, 0.05, 1234, buf, KP)
+        else:
+            L._lora3_down(buf[:, :K], A, Z, 0.05, 1234)
+            native().lora3_z_tail(Z, buf, K, KP)
+        torch.cuda.synchronize()
+        outs.append((buf, Z))
+    (b1, z1), (b2, z2) = outs
+    assert torch.equal(b1[:, :K], x2d)
+    assert torch.allclose(z1, z2, atol=1e-4, rtol=1e-4)  # f32 atomics: order may differ
+    ref = torch.zeros(T, KP, device=dev)
+    ref[:, :R] = z1
+    assert torch.equal(b1[:, K:].float(), ref.bfloat16().float())
+    assert torch.allclose(b1[:, K:].float(), b2[:, K:].float(), atol=1e-2, rtol=1e-2)
+    assert int(L._tail_cnt(T, dev).abs().sum()) == 0

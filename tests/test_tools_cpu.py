@@ -252,3 +252,17 @@ def test_bench_contract_torchrun(world):
     assert "peak_hbm_gb_max_rank" in x and x["setup_s"] > 0
     tokens = 2 * world * 32 * 2
     assert abs(j["value"] - tokens / (j["ms_per_step"] * 2 / 1000)) / j["value"] < 0.02
+
+
+def test_gemm_wave_split_plan():
+    """Whole-wave column split of the training GEMMs (lumen/ops/gemm.py): only where the last
+    wave of 256x256 tiles on 256 CUs is at most half full, at a column-tile boundary."""
+    from lumen.ops.gemm import mm_nt, split_cols
+
+    assert split_cols(4096, 22016) == 20480      # gate|up fwd: 1376 tiles -> 1280 + 96
+    assert split_cols(1024, 22016) == 16384      # 344 tiles -> 256 + 88
+    for M, N in [(4096, 4096), (4096, 12288), (4096, 11008), (4096, 32000), (4000, 22016),
+                 (256, 1024)]:
+        assert split_cols(M, N) == 0, (M, N)     # whole waves, >half-full tail, or ragged M
+    x, w = torch.randn(8, 16), torch.randn(24, 16)
+    assert torch.allclose(mm_nt(x, w), x @ w.t())  # CPU: plain matmul
