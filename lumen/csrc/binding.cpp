@@ -66,6 +66,7 @@ hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int
 hipError_t lumen_gemv_swiglu(int, const void*, const void*, void*, int, int, long long, long long,
                              hipStream_t);
 void lumen_set_gemv_form(int);
+void lumen_set_rms_lds(int, int);
 hipError_t lumen_dgemm(int, const void*, const void*, void*, int, int, int, long long, long long, int,
                        float*, unsigned*, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
@@ -857,6 +858,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemv_swiglu", &gemv_swiglu);
   m.def("dgemm", &dgemm);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
+  m.def("set_rms_lds", [](int64_t f, int64_t b) {
+    lumen_set_rms_lds(static_cast<int>(f), static_cast<int>(b));
+  });
   m.def("rope_cache_write", &rope_cache_write);
   m.def("paged_attention_decode", &paged_attention_decode);
   m.def("reshape_and_cache", &reshape_and_cache);

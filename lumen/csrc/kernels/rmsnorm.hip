@@ -207,6 +207,12 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
   }
 }
 
+// Occupancy caps (dynamic LDS bytes reserved per workgroup, 0 = none).  At the training shape
+// (4096 rows x 4096) the backward grid is 2048 workgroups = 8 per CU, all resident at once:
+// every workgroup loads, reduces and stores in the same phase, so HBM reads and writes do not
+// overlap.  Capping residency gives a second round whose loads run under the first's stores.
+static int g_rms_lds[2] = {0, 0};  // [fwd, bwd]
+
 template <typename T>
 static hipError_t launch_fwd(const void* x, const void* res, const void* w, void* y, void* s_out,
                              float* rstd, int rows, int H, float eps, long long ldy,
@@ -233,7 +239,7 @@ static hipError_t launch_fwd(const void* x, const void* res, const void* w, void
   dim3 grid((rows + 4 / wpr - 1) / (4 / wpr));
   const int vpl = (H + 512 * wpr - 1) / (512 * wpr);
 #define LUMEN_RMS_FWD(V, W)                                                                       \
-  hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, V, W>), grid, block, 0, st, (const T*)x,             \
+  hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, V, W>), grid, block, g_rms_lds[0], st, (const T*)x,  \
                      (const T*)res, (const T*)w, (T*)y, (T*)s_out, rstd, rows, H, eps, ldy)
   if (wpr == 1) {
     if (vpl <= 1) LUMEN_RMS_FWD(1, 1);
@@ -251,6 +257,7 @@ static hipError_t launch_fwd(const void* x, const void* res, const void* w, void
   return hipGetLastError();
 }
 
+
 template <typename T>
 static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const float* rstd,
                              const void* ds_res, void* dx, float* dw, int rows, int H,
@@ -261,7 +268,7 @@ static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const
   dim3 grid((rows + 4 / wpr - 1) / (4 / wpr));
   const int vpl = (H + 512 * wpr - 1) / (512 * wpr);
 #define LUMEN_RMS_BWD(V, W)                                                                     \
-  hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, V, W>), grid, block, 0, st, (const T*)dy,          \
+  hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, V, W>), grid, block, g_rms_lds[1], st, (const T*)dy, \
                      (const T*)s, (const T*)w, rstd, (const T*)ds_res, (T*)dx, dw, rows, H)
   if (wpr == 1) {
     if (vpl <= 1) LUMEN_RMS_BWD(1, 1);
@@ -281,6 +288,11 @@ static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const
 
 // y rows may be strided (ldy >= H): the q|k|v input of a K-extended LoRA GEMM is written straight
 // into the first H columns of its [rows, H + 64] operand buffer
+extern "C" void lumen_set_rms_lds(int fwd_bytes, int bwd_bytes) {
+  lumen::g_rms_lds[0] = fwd_bytes < 0 ? 0 : fwd_bytes;
+  lumen::g_rms_lds[1] = bwd_bytes < 0 ? 0 : bwd_bytes;
+}
+
 extern "C" hipError_t lumen_rmsnorm_fwd_ld(int dtype, const void* x, const void* residual,
                                            const void* w, void* y, void* s_out, float* rstd,
                                            int rows, int H, float eps, long long ldy,

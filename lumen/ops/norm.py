@@ -13,6 +13,22 @@ import torch
 
 from ._native import native, use_native
 
+_LDS_SET = [False]
+
+
+def _occupancy_cap(C) -> None:
+    """``LUMEN_RMS_LDS=fwd,bwd``: dynamic LDS bytes reserved per workgroup, which caps how many
+    RMSNorm workgroups share a CU (lumen/bench/rmsnorm_probe.py measures the effect)."""
+    if _LDS_SET[0]:
+        return
+    _LDS_SET[0] = True
+    import os
+
+    v = os.environ.get("LUMEN_RMS_LDS")
+    if v:
+        f, _, b = v.partition(",")
+        C.set_rms_lds(int(f or 0), int(b or f or 0))
+
 
 def rms_norm_ref(x, w, eps, residual=None):
     s = x if residual is None else (x.float() + residual.float()).to(x.dtype)
@@ -27,6 +43,7 @@ class _FusedAddRMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, w, eps, ext=0):
         C = native()
+        _occupancy_cap(C)
         x = x.contiguous()
         if ext and x.dim() == 2:
             # y as the first H columns of a [rows, H + ext] buffer (row-strided kernel output)
@@ -53,6 +70,7 @@ class _FusedAddRMSNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, ds):
         C = native()
+        _occupancy_cap(C)
         s, w, rstd = ctx.saved_tensors
         dx = torch.empty_like(s)
         dw = torch.zeros(w.shape, dtype=torch.float32, device=w.device) if ctx.w_grad else None
