@@ -45,7 +45,7 @@ hipError_t lumen_lora3_w_tail(int, void*, long long, int, const float*, int, int
                               const long long*, const int*, const int*, float, hipStream_t);
 hipError_t lumen_lora3_dxa(int, const void*, long long, void*, long long, const float*, const float*,
                            long long, float*, long long, int, int, int, int, unsigned long long,
-                           unsigned int, float, long long, long long, hipStream_t);
+                           unsigned int, float, long long, long long, float*, hipStream_t);
 hipError_t lumen_embedding(const void*, const long long*, void*, int, int, int, hipStream_t);
 hipError_t lumen_lora3_down(int, const void*, long long, const float*, long long, float*, long long,
                             int, int, int, float, unsigned long long, unsigned int, float, long long,
@@ -502,8 +502,17 @@ void lora3_w_tail(at::Tensor& w, int64_t K, const at::Tensor& B, int64_t r,
 // fused x-side LoRA backward (kernels/lora_v3.hip dxa3_kernel)
 void lora3_dxa(const at::Tensor& x, at::Tensor& dx, const at::Tensor& dZ, const at::Tensor& A,
                at::Tensor& dA, int64_t tw, int64_t seed, int64_t thresh, double drop_scale,
-               int64_t drop_ld, int64_t drop_col0) {
+               int64_t drop_ld, int64_t drop_col0, const c10::optional<at::Tensor>& delta) {
   need_cuda_f32(dZ, "lora3_dxa dZ");
+  float* dp = nullptr;
+  if (delta && delta->defined()) {
+    // attention delta hand-off: [K / 128 heads, T] f32, head dim 128, R = 16 (o_proj)
+    need_cuda_f32(*delta, "lora3_dxa delta");
+    if (!delta->is_contiguous() || delta->dim() != 2 || x.size(1) % 128 != 0 ||
+        delta->size(0) != x.size(1) / 128 || delta->size(1) != x.size(0) || dZ.size(1) != 16)
+      throw std::invalid_argument("lumen: lora3_dxa delta: [K / 128, T] f32 with R = 16");
+    dp = delta->data_ptr<float>();
+  }
   need_cuda_f32(A, "lora3_dxa A");
   need_cuda_f32(dA, "lora3_dxa dA");
   if (!x.is_cuda() || !dx.is_cuda() || x.dim() != 2 || dx.dim() != 2 || x.stride(1) != 1 ||
@@ -518,7 +527,7 @@ void lora3_dxa(const at::Tensor& x, at::Tensor& dx, const at::Tensor& dZ, const 
                         static_cast<int>(x.size(1)), static_cast<int>(dZ.size(1)),
                         static_cast<int>(tw), static_cast<unsigned long long>(seed),
                         static_cast<unsigned int>(thresh), static_cast<float>(drop_scale), drop_ld,
-                        drop_col0, cur_stream()),
+                        drop_col0, dp, cur_stream()),
         "lora3_dxa");
 }
 
@@ -838,7 +847,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("xe") = py::none(), py::arg("xk") = 0, py::arg("KP") = 0,
         py::arg("cnt") = py::none());
   m.def("embedding", &embedding);
-  m.def("lora3_dxa", &lora3_dxa);
+  m.def("lora3_dxa", &lora3_dxa, py::arg("x"), py::arg("dx"), py::arg("dZ"), py::arg("A"),
+        py::arg("dA"), py::arg("tw"), py::arg("seed"), py::arg("thresh"), py::arg("drop_scale"),
+        py::arg("drop_ld"), py::arg("drop_col0"), py::arg("delta") = py::none());
   m.def("lora3_z_tail", &lora3_z_tail);
   m.def("lora3_w_tail", &lora3_w_tail);
   m.def("kv_dequant", &kv_dequant);

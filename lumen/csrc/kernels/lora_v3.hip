@@ -562,11 +562,15 @@ struct DxaArgs {
   float da_scale, dx_scale;   // dA: keep-scale; dx: keep-scale (dZ already carries s)
   Drop drop;
   int probe;  // cost probe (0 in production): 64 dA atomics only when v == 1234.5
+  // flash-attention delta hand-off (DELTA instantiation; x = the attention output O, dx = dO
+  // once updated, 128-column blocks = heads): delta[c0 / 128][t] = sum_c dO[t][c] O[t][c] over
+  // the block, written here so the attention backward skips its delta pass.
+  float* delta;
 };
 
 constexpr int kDxST = 72;     // dZ^T LDS row stride (16-bit): 144 B
 
-template <typename T, bool DROP, int NJ>
+template <typename T, bool DROP, int NJ, bool DELTA = false>
 __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
   constexpr int J = NJ * 16, KJ = J > 32 ? 64 : 32, NKS = KJ / 32, SP = KJ + 8;
   __shared__ __attribute__((aligned(16))) char img[2][64 * 256];
@@ -658,6 +662,15 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
       dv[i] = (tok && c < a.K) ? *reinterpret_cast<const uint4*>(dx + (long long)t * a.lddx + c)
                                : make_uint4(0, 0, 0, 0);
     }
+    uint4 ov[DELTA ? 4 : 1];  // O (un-dropped x) in the dx lane layout, for the delta dot
+    if constexpr (DELTA) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 + 32 * i + 8 * g;
+        ov[i] = (tok && c < a.K) ? *reinterpret_cast<const uint4*>(x + (long long)t * a.ldx + c)
+                                 : make_uint4(0, 0, 0, 0);
+      }
+    }
     // dA: D[j][k] += dZ^T[j][t] x[t][k] over the sub-tile's 64 rows
     const char* im = img[buf];
     const T* sz = st[buf];
@@ -683,6 +696,7 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
       for (int n = 0; n < 8; ++n)  // A^T operand re-read from LDS (keeps 2 waves per SIMD)
         acc[n] = Mfma<T>::run(*reinterpret_cast<const uint4*>(s2 + up_cmap(n, L) * SP + ks * 32 + g * 8),
                               bop[ks], acc[n]);
+    float dot = 0.f;
     if (tok) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -699,8 +713,20 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
           const float d = acc[2 * i + (e >> 2)][e & 3];
           y[e] += ((keep >> e) & 1u) ? a.dx_scale * d : 0.f;
         }
+        if constexpr (DELTA) {  // the dot of the 16-bit values the attention backward reads
+          float o[8];
+          unpack8<T>(ov[i], o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dot = fmaf(to_f32(from_f32<T>(y[e])), o[e], dot);
+        }
         store8(dx + (long long)t * a.lddx + c, y);
       }
+    }
+    if constexpr (DELTA) {
+      // lanes L, L + 16, L + 32, L + 48 hold the four 32-column quarters of row t's head
+      dot += __shfl_xor(dot, 16);
+      dot += __shfl_xor(dot, 32);
+      if (tok && g == 0) a.delta[(long long)(c0 >> 7) * a.T + t] = dot;
     }
   }
   // dA flush: accumulator (row j = 16 jt + 4 g + r, column k = c0 + 32 wid + 16 m + L)
@@ -936,14 +962,15 @@ extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, v
                                       long long lda, float* dA, long long ldda, int T, int K,
                                       int R, int tw, unsigned long long seed, unsigned int thresh,
                                       float drop_scale, long long drop_ld, long long drop_col0,
-                                      hipStream_t st) {
+                                      float* delta, hipStream_t st) {
   if (T <= 0 || K <= 0 || R < 16 || R > 64 || (R & 15) || (K & 7) || (ldx & 7) || (lddx & 7) ||
       (lda & 3) || tw < 64 || (tw & 63))
     return hipErrorInvalidValue;
+  if (delta != nullptr && ((K & 127) || R != 16)) return hipErrorInvalidValue;
   lv3::DxaArgs a;
   a.probe = lv3_probe();
   a.x = x; a.ldx = ldx; a.dx = dx; a.lddx = lddx; a.dZ = dZ; a.A = A; a.lda = lda; a.dA = dA;
-  a.ldda = ldda; a.T = T; a.K = K; a.R = R; a.TW = tw;
+  a.ldda = ldda; a.T = T; a.K = K; a.R = R; a.TW = tw; a.delta = delta;
   const bool drop = thresh != 0;
   a.da_scale = drop ? drop_scale : 1.f;
   a.dx_scale = drop ? drop_scale : 1.f;
@@ -961,6 +988,18 @@ extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, v
     case 2: LV3_DXA(TT, 2); break;                                                               \
     case 3: LV3_DXA(TT, 3); break;                                                               \
     default: LV3_DXA(TT, 4); break;                                                              \
+  }
+  if (delta != nullptr) {  // o_proj (R = 16) with the attention delta hand-off
+#define LV3_DXA_D(TT)                                                                              \
+  do {                                                                                           \
+    if (drop) hipLaunchKernelGGL((lv3::dxa3_kernel<TT, true, 1, true>), grid, block, 0, st, a);  \
+    else hipLaunchKernelGGL((lv3::dxa3_kernel<TT, false, 1, true>), grid, block, 0, st, a);      \
+  } while (0)
+    if (dtype == kBF16) LV3_DXA_D(bf16);
+    else if (dtype == kF16) LV3_DXA_D(fp16);
+    else return hipErrorInvalidValue;
+#undef LV3_DXA_D
+    return hipGetLastError();
   }
   if (dtype == kBF16) { LV3_DXA_NJ(bf16) }
   else if (dtype == kF16) { LV3_DXA_NJ(fp16) }

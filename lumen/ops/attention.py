@@ -397,6 +397,9 @@ def _ds_offsets(cu: tuple, causal: bool, device):
     return hit
 
 
+DELTA_HANDOFFS = [0]  # backward calls that used a delta handed over by the o_proj backward
+
+
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, cu, nh, nkv, D, causal, rope=None, scale=None, out_ext=0):
@@ -420,6 +423,10 @@ class _FlashAttn(torch.autograd.Function):
         ctx.save_for_backward(qkv, o, lse)
         ctx.meta = (cu, nh, nkv, D, causal, scale)
         ctx.rope = rope
+        # delta hand-off: the o_proj backward (lumen.ops.lora, fused dA + dx kernel) may leave
+        # delta = rowsum(dO * O) here for exactly the dO this backward receives
+        ctx.delta_slot = {}
+        o._lumen_delta_slot = ctx.delta_slot
         return o
 
     @staticmethod
@@ -437,7 +444,13 @@ class _FlashAttn(torch.autograd.Function):
         dq = dqkv[:, :nh * D]
         dk = dqkv[:, nh * D:(nh + nkv) * D]
         dv = dqkv[:, (nh + nkv) * D:]
-        delta = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
+        slot = ctx.delta_slot
+        handed = (slot.get("key") == (do.data_ptr(), do._version)
+                  and tuple(slot["delta"].shape) == (nh, T))
+        delta = (slot.pop("delta") if handed
+                 else torch.empty(nh, T, device=qkv.device, dtype=torch.float32))
+        DELTA_HANDOFFS[0] += int(handed)
+        slot.clear()
         cut = _cu_tensor(cu, qkv.device)
         # dK/dV and dQ kernels per FA_BWD: "v16" both 16x16x32 (64-row tiles), "v32" both
         # 32x32x16 (128-row tiles), "mix" = 16x16x32 dK/dV + 32x32x16 dQ
@@ -452,8 +465,9 @@ class _FlashAttn(torch.autograd.Function):
                             else (None, 0))
         if ds_off is not None and nh * ds_total * 8192 <= FA_DS_MB * 2 ** 20:
             ds = torch.empty(nh, ds_total, 4096, device=qkv.device, dtype=qkv.dtype)
-            C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
-                         scale, do, None, None, None, delta, None, None, None)
+            if not handed:
+                C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh,
+                             nkv, scale, do, None, None, None, delta, None, None, None)
             if FA_DKDV == "8":
                 t7, w7 = _tiles(cu, 128, qkv.device, heavy_low=causal), 10
                 t8, w8 = ((_xcd_tiles(cu, 64, nh, qkv.device, False), 0x108) if FA_XCD
@@ -477,8 +491,9 @@ class _FlashAttn(torch.autograd.Function):
             C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh,
                          nkv, scale, do, dq, dk, dv, delta, pos, cos, sin)
         else:
-            C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh, nkv,
-                         scale, do, None, None, None, delta, None, None, None)
+            if not handed:
+                C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh,
+                             nkv, scale, do, None, None, None, delta, None, None, None)
             C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh,
                          nkv, scale, do, dq, dk, dv, delta, pos, cos, sin)
             C.flash_attn(wq, causal, 1, q, k, v, o, lse, cut, qtiles, nh, nkv,

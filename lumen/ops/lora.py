@@ -184,6 +184,12 @@ DY_TW = int(_os.environ.get("LUMEN_LORA_DY_TW", "0"))  # dY rows per block of lo
 UP_V3 = _os.environ.get("LUMEN_LORA_UP_V3", "0") == "1"
 # fused x-side backward (dA + dx in one pass over the activation rows, lora3_dxa)
 DXA = _os.environ.get("LUMEN_LORA_DXA", "1") != "0"
+# flash-attention delta hand-off: when this linear's input is a flash-attention output O (it
+# carries ``_lumen_delta_slot``), the fused dA + dx kernel also writes delta = rowsum(dO * O) per
+# head for the attention backward, which then skips its own delta pass (LUMEN_FA_DELTA_HANDOFF=0:
+# off).  The slot of the linear whose backward is running:
+DELTA_HANDOFF = _os.environ.get("LUMEN_FA_DELTA_HANDOFF", "1") != "0"
+_DELTA_SLOT = [None]
 
 
 def _v3_ok(r: int, R: int, segs, *mats) -> bool:
@@ -462,8 +468,14 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     if need_dA and dx is not None and DXA:
         # one pass over the [T, K] rows: dA from the staged x tiles, dx updated lane-locally
         tw = 256 if math.ceil(K / 128) * math.ceil(T / 256) >= 512 else 128
+        slot = _DELTA_SLOT[0]
+        delta = None
+        if slot is not None and R == 16 and K % 128 == 0 and dx.shape == x2d.shape:
+            delta = torch.empty(K // 128, T, device=dev, dtype=torch.float32)
         nat.lora3_dxa(x2d, dx, dZ, A, dA, tw, int(seed) & 0x7FFFFFFFFFFFFFFF, drop_threshold(p),
-                      1.0 / (1.0 - p) if p > 0 else 1.0, K, 0)
+                      1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, delta)
+        if delta is not None:
+            slot["delta"], slot["key"] = delta, (dx.data_ptr(), dx._version)
     else:
         if need_dA:
             _lora2(1, 1, x2d, dZ, dA, 1, K, 1.0, T, R, _split(math.ceil(K / 128), T, 128),
@@ -533,6 +545,7 @@ class _LoraLinear(torch.autograd.Function):
         if rope is not None and not rope_done:
             _rope_(y, rope, inverse=False)
         ctx.rope = rope
+        ctx.delta_slot = getattr(x2d, "_lumen_delta_slot", None) if DELTA_HANDOFF else None
         ctx.weight_fn = weight_fn
         ctx.wt_fn = wt_fn
         ctx.meta = (segs, r, scale, p, seed)
@@ -562,11 +575,13 @@ class _LoraLinear(torch.autograd.Function):
         else:
             dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
         _IN_BACKWARD[0] = True
+        _DELTA_SLOT[0] = ctx.delta_slot
         try:
             dA, dB = lora_bwd_native(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed,
                                      ctx.needs_input_grad[3], ctx.needs_input_grad[4])
         finally:
             _IN_BACKWARD[0] = False
+            _DELTA_SLOT[0] = None
         if callable(dx):
             dx = held["dx"]
         dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None

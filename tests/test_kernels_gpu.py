@@ -975,3 +975,67 @@ def test_lora3_down_fused_fold_tail(T, R):
     assert torch.equal(b1[:, K:].float(), ref.bfloat16().float())
     assert torch.allclose(b1[:, K:].float(), b2[:, K:].float(), atol=1e-2, rtol=1e-2)
     assert int(L._tail_cnt(T, dev).abs().sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_lora3_dxa_delta_handoff_kernel(p_drop):
+    """The o_proj fused dA + dx kernel's delta output == rowsum(dO * O) per 128-column head,
+    taken over the 16-bit dO it writes and the un-dropped O (fp32 reference)."""
+    from lumen.ops import lora as L
+    from lumen.ops._native import native
+
+    dev = torch.device("cuda")
+    T, K, R = 1000, 1024, 16
+    g = torch.Generator(device=dev).manual_seed(11)
+    ob = torch.randn(T, K + 64, device=dev, generator=g).bfloat16()  # fold operand buffer
+    o = ob[:, :K]
+    dx = torch.randn(T, K, device=dev, generator=g).bfloat16()
+    dZ = torch.randn(T, R, device=dev, generator=g) * 0.1
+    A = torch.randn(R, K, device=dev, generator=g) * 0.05
+    dA = torch.zeros(R, K, device=dev)
+    delta = torch.full((K // 128, T), float("nan"), device=dev)
+    th = L.drop_threshold(p_drop)
+    native().lora3_dxa(o, dx, dZ, A, dA, 128, 99, th, 1.0 / (1.0 - p_drop), K, 0, delta)
+    torch.cuda.synchronize()
+    ref = (dx.float() * o.float()).view(T, K // 128, 128).sum(-1).t()
+    assert torch.allclose(delta, ref, atol=1e-3, rtol=1e-4), (delta - ref).abs().max()
+
+
+@pytest.mark.gpu
+def test_llama_delta_handoff_matches(monkeypatch):
+    """Training step with the attention delta handed over by the o_proj backward == with the
+    attention backward's own delta pass (loss and adapter gradients), and the hand-off is
+    really taken in every layer."""
+    import lumen.ops.attention as attn_mod
+    import lumen.ops.lora as lora_mod
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+
+    torch.manual_seed(0)
+    m = build_model("small-llama", dtype=torch.bfloat16, device=torch.device("cuda"),
+                    init="random", seed=5)
+    apply_lora(m, LoraConfig(r=16, lora_dropout=0.05))
+    with torch.no_grad():
+        for _, mod in m.lora_modules():
+            mod.lora.lora_B.normal_(0, 0.02)
+    m.train()
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(3, m.config.vocab_size, (2, 256), generator=g).cuda()
+    labels = torch.roll(ids, -1, 1)
+    outs = []
+    for on in (True, False):
+        monkeypatch.setattr(lora_mod, "DELTA_HANDOFF", on)
+        attn_mod.DELTA_HANDOFFS[0] = 0
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(7)
+        loss = m(ids, labels)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs.append((loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters()
+                                   if p.requires_grad}, attn_mod.DELTA_HANDOFFS[0]))
+    (l1, g1, n1), (l2, g2, n2) = outs
+    assert n1 == m.config.num_hidden_layers and n2 == 0
+    assert abs(l1 - l2) <= 1e-6 * abs(l2)
+    for n in g1:
+        assert rel(g1[n], g2[n]) < 1e-2, n
