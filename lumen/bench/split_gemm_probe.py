@@ -79,8 +79,8 @@ def main():
     variants = {"gate_up_one": gu_one, "down_dx_one": dx_one}
     for n1 in (20480, 16384):
         variants[f"gate_up_split{n1}"] = make_split(Wgu, y, n1)
-    for n1 in (8192, 9216):
-        variants[f"down_dx_split{n1}"] = make_split(WdnT, dx, n1)
+    # (down input-grad split at 8192 + 2816: the 2816-column tail GEMM fails with "invalid
+    # argument" inside TunableOp tuning, with and without rotating buffers -- not pursued)
     for name, fn in variants.items():
         y.zero_()
         dx.zero_()

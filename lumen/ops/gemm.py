@@ -100,7 +100,8 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None) -> tor
 # last whole wave and runs the remainder as its own (separately tuned) GEMM, both writing column
 # views of one buffer (ldc = full width, no copies).  lumen/bench/split_gemm_probe.py measures it.
 GEMM_SPLIT = os.environ.get("LUMEN_GEMM_SPLIT", "1") != "0"
-SPLIT_TILE, SPLIT_CUS, SPLIT_MAX_TAIL = 256, 256, 0.5
+SPLIT_TILE, SPLIT_CUS = 256, 256
+SPLIT_MAX_TAIL = float(os.environ.get("LUMEN_GEMM_SPLIT_MAX_TAIL", "0.5"))
 
 
 def split_cols(M: int, N: int) -> int:
@@ -144,12 +145,20 @@ def _split_plan(x: torch.Tensor, w: torch.Tensor) -> int:
     n1 = split_cols(M, N)
     if not n1:
         return 0
-    # only where both parts have tuned solutions (untuned shapes would fall to the heuristic)
-    sigs = _tuned_sigs()
-    lds = f"ld_{w.stride(0)}_{x.stride(0)}_{N}"
-    if f"tn_{n1}_{M}_{K}_{lds}" not in sigs or f"tn_{N - n1}_{M}_{K}_{lds}" not in sigs:
-        return 0
-    return n1
+    # only where both parts have tuned solutions (untuned shapes would fall to the heuristic);
+    # decided once per problem (the table is loaded before the first training GEMM)
+    key = (M, N, K, w.stride(0), x.stride(0))
+    hit = _plans.get(key)
+    if hit is None:
+        sigs = _tuned_sigs()
+        lds = f"ld_{w.stride(0)}_{x.stride(0)}_{N}"
+        hit = n1 if (f"tn_{n1}_{M}_{K}_{lds}" in sigs
+                     and f"tn_{N - n1}_{M}_{K}_{lds}" in sigs) else 0
+        _plans[key] = hit
+    return hit
+
+
+_plans: dict = {}
 
 
 def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -628,7 +628,7 @@ def _input_grad(ctx, dy):
     """dX = dY @ W, as the TN GEMM dY @ (W^T)^T when the layer keeps a transposed copy."""
     Wt = ctx.wt_fn() if ctx.wt_fn is not None else None
     if Wt is not None:
-        return torch.matmul(dy, Wt.t())
+        return mm_nt(dy, Wt)
     return torch.matmul(dy, ctx.weight_fn())
 
 

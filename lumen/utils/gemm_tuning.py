@@ -50,8 +50,9 @@ def start_gemm_tuning(out_path: str, max_ms: int = 60, rotating_mb: Optional[int
 
     if rotating_mb is None:
         rotating_mb = int(os.environ.get("LUMEN_TUNE_ROTATING_MB", "1024"))
-    if rotating_mb > 0:
-        tn.set_rotating_buffer_size(rotating_mb)
+    # 0 disables the rotating buffers: they copy ldc * n elements from C's own pointer, which
+    # overruns a column-view output (lumen.ops.gemm.mm_nt tails) at the end of its allocation
+    tn.set_rotating_buffer_size(max(rotating_mb, 0))
 
     os.makedirs(os.path.dirname(os.path.abspath(out_path)), exist_ok=True)
     tn.enable(True)
