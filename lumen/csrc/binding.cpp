@@ -57,7 +57,10 @@ hipError_t lumen_lora3_up(int, int, void*, long long, const float*, long long, c
                           int, hipStream_t);
 hipError_t lumen_lora3_dy(int, const void*, long long, const float*, int, const float*, long long,
                           float*, long long, float*, int, int, float, int, const long long*,
-                          const long long*, const long long*, const int*, hipStream_t);
+                          const long long*, const long long*, const int*, float*, long long,
+                          float*, long long, hipStream_t);
+hipError_t lumen_lora3_dy_reduce(const float*, int, long long, float*, long long, const float*, int,
+                                 long long, float*, long long, hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, const float*, void*,
                             void*, const long long*, int, int, int, int, int, int, hipStream_t);
@@ -433,8 +436,26 @@ void lora3_up(int64_t fwd, at::Tensor& out, int64_t ldo, const at::Tensor& s1, i
 // segs: (n_off, r_off, b_off, n_len)
 void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r, const at::Tensor& Z,
               int64_t ldz, at::Tensor& dZ, int64_t lddz, at::Tensor& dB, int64_t T, int64_t tw,
-              double alpha, const std::vector<std::vector<int64_t>>& segs) {
+              double alpha, const std::vector<std::vector<int64_t>>& segs,
+              const c10::optional<at::Tensor>& pz, const c10::optional<at::Tensor>& pb) {
   if (!dy.is_cuda()) throw std::invalid_argument("lumen: lora3_dy needs GPU tensors");
+  float* pzp = nullptr;
+  float* pbp = nullptr;
+  long long pzs = 0, pbs = 0;
+  if (pz && pz->defined()) {
+    // partial mode: pz [column blocks, T, ldz], pb [row blocks, dB rows, r] f32 (see kernel)
+    if (!pb || !pb->defined()) throw std::invalid_argument("lumen: lora3_dy partial mode needs pz and pb");
+    need_cuda_f32(*pz, "lora3_dy pz");
+    need_cuda_f32(*pb, "lora3_dy pb");
+    if (!pz->is_contiguous() || !pb->is_contiguous() || pz->dim() != 3 || pb->dim() != 3 ||
+        pz->size(1) < T || pz->size(2) != lddz || pb->size(1) < dB.size(0) || pb->size(2) != r ||
+        tw <= 0 || pb->size(0) < (T + tw - 1) / tw)
+      throw std::invalid_argument("lumen: lora3_dy partial buffers: pz [gx, T, ldz], pb [gy, NB, r]");
+    pzp = pz->data_ptr<float>();
+    pbp = pb->data_ptr<float>();
+    pzs = pz->stride(0);
+    pbs = pb->stride(0);
+  }
   need_cuda_f32(B, "lora3_dy B");
   need_cuda_f32(Z, "lora3_dy Z");
   need_cuda_f32(dZ, "lora3_dy dZ");
@@ -447,11 +468,34 @@ void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r,
     if (segs[i].size() != 4) throw std::invalid_argument("lumen: lora3_dy segment = (n_off, r_off, b_off, n_len)");
     no[i] = segs[i][0]; ro[i] = segs[i][1]; bo[i] = segs[i][2]; nl[i] = static_cast<int>(segs[i][3]);
   }
+  if (pzp != nullptr) {
+    // every dZ slot of every segment must be written: equal segment widths, gx column blocks
+    const int gx = (nl[0] + 255) / 256;
+    for (int i = 1; i < nseg; ++i)
+      if (nl[i] != nl[0]) throw std::invalid_argument("lumen: lora3_dy partial mode needs equal segment widths");
+    if (pz->size(0) != gx) throw std::invalid_argument("lumen: lora3_dy pz needs ceil(n_len / 256) slots");
+  }
   check(lumen_lora3_dy(dcode(dy), dy.data_ptr(), ldy, B.data_ptr<float>(), static_cast<int>(r),
                        Z.data_ptr<float>(), ldz, dZ.data_ptr<float>(), lddz, dB.data_ptr<float>(),
                        static_cast<int>(T), static_cast<int>(tw), static_cast<float>(alpha), nseg,
-                       no, ro, bo, nl, cur_stream()),
+                       no, ro, bo, nl, pzp, pzs, pbp, pbs, cur_stream()),
         "lora3_dy");
+}
+
+void lora3_dy_reduce(const at::Tensor& pz, at::Tensor& dZ, const at::Tensor& pb, at::Tensor& dB) {
+  need_cuda_f32(pz, "lora3_dy_reduce pz");
+  need_cuda_f32(pb, "lora3_dy_reduce pb");
+  need_cuda_f32(dZ, "lora3_dy_reduce dZ");
+  need_cuda_f32(dB, "lora3_dy_reduce dB");
+  if (!pz.is_contiguous() || !pb.is_contiguous() || !dZ.is_contiguous() || !dB.is_contiguous() ||
+      pz.dim() != 3 || pb.dim() != 3 || pz.size(1) * pz.size(2) != dZ.numel() ||
+      pb.size(1) * pb.size(2) != dB.numel())
+    throw std::invalid_argument("lumen: lora3_dy_reduce: pz [S, T, R] -> dZ [T, R], pb [S, NB, r] -> dB [NB, r]");
+  check(lumen_lora3_dy_reduce(pz.data_ptr<float>(), static_cast<int>(pz.size(0)), pz.stride(0),
+                              dZ.data_ptr<float>(), dZ.numel(), pb.data_ptr<float>(),
+                              static_cast<int>(pb.size(0)), pb.stride(0), dB.data_ptr<float>(),
+                              dB.numel(), cur_stream()),
+        "lora3_dy_reduce");
 }
 
 // out[t, :] = W[ids[t], :]  (16-bit table, int64 ids; out of range ids -> zero rows)
@@ -847,6 +891,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("xe") = py::none(), py::arg("xk") = 0, py::arg("KP") = 0,
         py::arg("cnt") = py::none());
   m.def("embedding", &embedding);
+  m.def("lora3_dy", &lora3_dy, py::arg("dy"), py::arg("ldy"), py::arg("B"), py::arg("r"),
+        py::arg("Z"), py::arg("ldz"), py::arg("dZ"), py::arg("lddz"), py::arg("dB"), py::arg("T"),
+        py::arg("tw"), py::arg("alpha"), py::arg("segs"), py::arg("pz") = py::none(),
+        py::arg("pb") = py::none());
+  m.def("lora3_dy_reduce", &lora3_dy_reduce);
   m.def("lora3_dxa", &lora3_dxa, py::arg("x"), py::arg("dx"), py::arg("dZ"), py::arg("A"),
         py::arg("dA"), py::arg("tw"), py::arg("seed"), py::arg("thresh"), py::arg("drop_scale"),
         py::arg("drop_ld"), py::arg("drop_col0"), py::arg("delta") = py::none());
@@ -854,7 +903,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora3_w_tail", &lora3_w_tail);
   m.def("kv_dequant", &kv_dequant);
   m.def("lora3_up", &lora3_up);
-  m.def("lora3_dy", &lora3_dy);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("qkv_rope", &qkv_rope);
   m.def("rope_inplace", &rope_inplace);

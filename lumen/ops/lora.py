@@ -178,6 +178,9 @@ def _zeros(*shape, device, train: bool = False):
 
 USE_V3 = _os.environ.get("LUMEN_LORA_V3", "1") != "0"
 DY_TW = int(_os.environ.get("LUMEN_LORA_DY_TW", "0"))  # dY rows per block of lora3_dy (0 = auto)
+# lora3_dy writes per-workgroup partial dZ / dB sums and one reduce kernel adds them up, instead
+# of f32 atomics into dZ / dB (LUMEN_LORA_DY_PARTIAL=1; measured neutral, profiles/r2_lora)
+DY_PARTIAL = _os.environ.get("LUMEN_LORA_DY_PARTIAL", "0") == "1"
 # per-call A/B (scripts/probes/lora_kernels.py, us): the v3 UP write-back is on par with v2
 # without RoPE (o_proj 15.0 vs 14.3) and slower with it (q|k|v 55.7 vs 45.6), so v2 stays the
 # forward UP; v3's DOWN (17.3 vs 21.9), fused dY pass (32.5 vs 53.3) and dx update win
@@ -444,6 +447,16 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     dB = B.grad if (direct and need_dB) else ws[T * R + nA:].view(B.shape[0], r)
 
     def dy_pass():
+        if DY_PARTIAL and len(segs) <= 4 and len({sg[1] for sg in segs}) == 1:
+            # per-workgroup partial sums + one reduce launch instead of contended f32 atomics
+            tw = _dy_tw(segs, T)
+            pz = torch.empty(math.ceil(segs[0][1] / 256), T, R, device=dev, dtype=torch.float32)
+            pb = torch.empty(math.ceil(T / tw), B.shape[0], r, device=dev, dtype=torch.float32)
+            nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, tw, scale,
+                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in segs],
+                         pz, pb)
+            nat.lora3_dy_reduce(pz, dZ, pb, dB)
+            return
         for i in range(0, len(segs), 4):
             ch = segs[i:i + 4]
             nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,

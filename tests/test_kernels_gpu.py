@@ -195,17 +195,19 @@ def test_adamw_device_step_counter():
 
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
-@pytest.mark.parametrize("impl", ["v3", "v3-nodxa", "v2", "f32"])
+@pytest.mark.parametrize("impl", ["v3", "v3-atomic", "v3-nodxa", "v2", "f32"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch, dtype):
-    """impl v3: one-shot DOWN / lane-local UP / fused dY pass (lora_v3.hip); v2: 16-bit MFMA
-    kernels (lora_v2.hip); f32: exact-f32 MFMA kernel (lora.hip)."""
+    """impl v3: one-shot DOWN / lane-local UP / fused dY pass (lora_v3.hip) with the opt-in
+    partial-sum dZ / dB slots + reduce (v3-atomic: the default f32 atomics); v2: 16-bit MFMA kernels (lora_v2.hip); f32:
+    exact-f32 MFMA kernel (lora.hip)."""
     import lumen.ops.lora as lora_mod
     from lumen.ops.lora import lora_linear, lora_linear_ref
 
     monkeypatch.setattr(lora_mod, "USE_V2", impl != "f32")
     monkeypatch.setattr(lora_mod, "USE_V3", impl.startswith("v3"))
-    monkeypatch.setattr(lora_mod, "DXA", impl == "v3")
+    monkeypatch.setattr(lora_mod, "DXA", impl in ("v3", "v3-atomic"))
+    monkeypatch.setattr(lora_mod, "DY_PARTIAL", impl == "v3")
 
     T, K, r = 512 + 64, 1024, 16
     if segs_kind == "qkv":
