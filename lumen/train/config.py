@@ -111,6 +111,11 @@ def load_ds_config(src, micro_batch: int, grad_accum: int, world_size: int,
     c.warmup_max_lr = float(_auto(sp.get("warmup_max_lr"), c.lr))
     c.warmup_num_steps = int(_auto(sp.get("warmup_num_steps"), warmup_steps))
     c.warmup_type = sp.get("warmup_type", "log")
+    if not sch:
+        # no "scheduler" section: DeepSpeed builds no WarmupLR (HF's default linear schedule
+        # with 0 warm-up steps also starts at the full rate), so the rate is constant -- not
+        # WarmupLR's lr = warmup_min_lr on the first step
+        c.warmup_min_lr = c.warmup_max_lr = c.lr
     c.gradient_clipping = float(_auto(raw.get("gradient_clipping"), max_grad_norm))
     c.micro_batch = int(_auto(raw.get("train_micro_batch_size_per_gpu"), micro_batch))
     c.grad_accum = int(_auto(raw.get("gradient_accumulation_steps"), grad_accum))

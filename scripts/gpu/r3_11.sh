@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-end rehearsal: build check import, smoke(), full GPU suite, default bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3_11}; mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
+tail -1 $O/smoke.txt
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1
+rc=$?; grep -E "FAILED|ERROR" $O/gpu_tests.txt | head -20; tail -1 $O/gpu_tests.txt
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
+python -c "import json;d=json.load(open('$O/bench.json'));print('bench', d['ms_per_step'], d['value'], d['config']['parallelism'])"

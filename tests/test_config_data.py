@@ -172,3 +172,18 @@ def test_stage3_max_live_auto():
     assert c.stage3_max_live_parameters == -1
     c = load_ds_config(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "ds_config_zero3_mi355x.json"), 8, 1, 8, 1e-4)
     assert c.stage3_max_live_parameters == -1 and c.stage == 3
+
+
+def test_no_scheduler_section_means_constant_lr():
+    """A DeepSpeed config without a "scheduler" section builds no WarmupLR: the first optimizer
+    step already runs at the full rate (a WarmupLR config starts at warmup_min_lr)."""
+    from lumen.train.config import load_ds_config, warmup_lr
+
+    c = load_ds_config({"zero_optimization": {"stage": 1}}, 2, 1, 1, 3e-4)
+    assert warmup_lr(0, c) == warmup_lr(1, c) == warmup_lr(100, c) == 3e-4
+    w = load_ds_config({"zero_optimization": {"stage": 1},
+                        "scheduler": {"type": "WarmupLR", "params": {"warmup_min_lr": 0,
+                                                                     "warmup_max_lr": "auto",
+                                                                     "warmup_num_steps": "auto"}}},
+                       2, 1, 1, 3e-4)
+    assert warmup_lr(0, w) == 0.0 and warmup_lr(1, w) == 3e-4
