@@ -44,7 +44,13 @@ def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_
         z = {"stage": stage, "stage3_param_persistence_threshold": 1e4}
         if max_live is not None:
             z["stage3_max_live_parameters"] = max_live
-        ds = load_ds_config({"zero_optimization": z}, 2, accum, 1, 1e-3)
+        # WarmupLR like the reference configs (first step at warmup_min_lr), so the dict runs
+        # and the configs/ds_config_zero3.json run follow the same schedule
+        ds = load_ds_config({"zero_optimization": z,
+                             "scheduler": {"type": "WarmupLR",
+                                           "params": {"warmup_min_lr": 0, "warmup_max_lr": "auto",
+                                                      "warmup_num_steps": "auto"}}},
+                            2, accum, 1, 1e-3)
     eng = ZeroEngine(m, ds, env)
     g = torch.Generator(device="cpu").manual_seed(5)
     losses = []
