@@ -158,6 +158,9 @@ def main():
 
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
+    # every timed step must really update the adapters: a non-finite gradient makes the fused
+    # AdamW skip the step on the device (a NaN-producing kernel would otherwise time as "fast")
+    sk0 = engine.skipped_steps
     gb0 = coord.gathered_bytes if coord else 0
     if coord is not None:
         coord.pop_exposed_wait_ms()
@@ -181,6 +184,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, exposed_ms, peak_gb = (float(x) for x in t.tolist())
     final_loss = float(loss.item())
+    skipped = engine.skipped_steps - sk0
+    if skipped and env.is_main:
+        print(f"[bench] WARNING: {skipped} of {args.steps} timed optimizer steps were skipped "
+              "(non-finite gradients): this number is not a valid training throughput",
+              file=sys.stderr)
     tokens = world * B * ds.grad_accum * S * args.steps
     value = tokens / dt
     if coord is None:
@@ -223,6 +231,7 @@ def main():
                 "samples_per_second": round(B * ds.grad_accum * world * args.steps / dt, 2),
                 "peak_hbm_gb_max_rank": round(peak_gb, 2),
                 "final_loss": round(final_loss, 4),
+                "timed_steps_skipped_nonfinite": skipped,
                 "setup_s": round(setup_s, 2),
                 "model_build_s": round(build_s, 3),
                 "rccl_world": rccl_world,
