@@ -111,10 +111,10 @@ def load_ds_config(src, micro_batch: int, grad_accum: int, world_size: int,
     c.warmup_max_lr = float(_auto(sp.get("warmup_max_lr"), c.lr))
     c.warmup_num_steps = int(_auto(sp.get("warmup_num_steps"), warmup_steps))
     c.warmup_type = sp.get("warmup_type", "log")
-    if not sch:
-        # no "scheduler" section: DeepSpeed builds no WarmupLR (HF's default linear schedule
-        # with 0 warm-up steps also starts at the full rate), so the rate is constant -- not
-        # WarmupLR's lr = warmup_min_lr on the first step
+    if not sch and not warmup_steps:
+        # no "scheduler" section and no warm-up asked for: DeepSpeed builds no WarmupLR (HF's
+        # default schedule with 0 warm-up steps also starts at the full rate), so the first step
+        # runs at the full rate -- not WarmupLR's lr = warmup_min_lr
         c.warmup_min_lr = c.warmup_max_lr = c.lr
     c.gradient_clipping = float(_auto(raw.get("gradient_clipping"), max_grad_norm))
     c.micro_batch = int(_auto(raw.get("train_micro_batch_size_per_gpu"), micro_batch))
