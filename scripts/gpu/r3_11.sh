@@ -10,4 +10,4 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
 rc=$?; grep -E "FAILED|ERROR" $O/gpu_tests.txt | head -20; tail -1 $O/gpu_tests.txt
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
-python -c "import json;d=json.load(open('$O/bench.json'));print('bench', d['ms_per_step'], d['value'], d['config']['parallelism'])"
+python -c "import json;d=json.load(open('$O/bench.json'));print('bench', d['ms_per_step'], d['value'], d['config']['parallelism'], 'skipped', d['extra']['timed_steps_skipped_nonfinite'])"
