@@ -63,7 +63,9 @@ _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
 
 def apply_penalties(logits: torch.Tensor, seqs: List[Sequence]) -> torch.Tensor:
     """Presence / frequency / repetition penalties on the rows of ``logits`` (f32 result), one
-    scatter-add of the rows' token ids into a [rows, V] count table on the device."""
+    scatter-add of the rows' token ids into a [rows, V] count table on the device.  Order as in
+    vLLM's ``apply_penalties``: the repetition penalty first (on the raw logit's sign), then the
+    frequency and presence subtractions."""
     out = logits.float().clone()
     rows = [i for i, s in enumerate(seqs) if s.params.has_penalties]
     V = out.shape[1]
@@ -84,14 +86,14 @@ def apply_penalties(logits: torch.Tensor, seqs: List[Sequence]) -> torch.Tensor:
     sel = [seqs[i] for i in rows]
     ridx = torch.tensor(rows, dtype=torch.long, device=dev)
     lg = out[ridx]
-    out_c = counts([s.output_ids for s in sel])
-    fp = torch.tensor([s.params.frequency_penalty for s in sel], device=dev)[:, None]
-    pp = torch.tensor([s.params.presence_penalty for s in sel], device=dev)[:, None]
-    lg -= fp * out_c + pp * (out_c > 0).float()
     rp = torch.tensor([s.params.repetition_penalty for s in sel], device=dev)[:, None]
     if bool((rp != 1.0).any()):
         seen = (counts([s.all_ids for s in sel]) > 0) & (rp != 1.0)
         lg = torch.where(seen, torch.where(lg > 0, lg / rp, lg * rp), lg)
+    out_c = counts([s.output_ids for s in sel])
+    fp = torch.tensor([s.params.frequency_penalty for s in sel], device=dev)[:, None]
+    pp = torch.tensor([s.params.presence_penalty for s in sel], device=dev)[:, None]
+    lg = lg - (fp * out_c + pp * (out_c > 0).float())
     out[ridx] = lg
     return out
 
@@ -167,7 +169,7 @@ class LLMEngine:
         self.eos_id = getattr(tokenizer, "eos_token_id", self.model_config.eos_token_id)
         self.step_count = 0
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "requests": 0,
-                      "finished": 0}
+                      "finished": 0, "overlapped_steps": 0}
 
     # --------------------------------------------------------------------------------------
     def _auto_blocks(self, dt) -> int:
@@ -307,8 +309,6 @@ class LLMEngine:
             inp.context_lens = dev[o:o + N].int()
             o += N
             inp.max_context = int(lens.max())
-        inp.sample_rows = dev[o:o + len(rows)]
-        o += len(rows)
         if src is not None:
             # dependent decode tokens: gathered from the previous step's sampled tokens here,
             # on the stream, before the step reads (or its graph copies in) its token row
@@ -316,6 +316,8 @@ class LLMEngine:
             o += N
             prev = self._inflight["toks"]
             inp.tokens[Tp:] = torch.where(s_dev >= 0, prev[s_dev.clamp(min=0)], inp.tokens[Tp:])
+        inp.sample_rows = dev[o:o + len(rows)]
+        o += len(rows)
         if use_lora:
             inp.lora_ids = dev[o:o + T].int()
         return inp
@@ -358,11 +360,29 @@ class LLMEngine:
             return self._resolve()
         if self._inflight is not None and self._needs_host_tokens(batch):
             done = self._resolve()     # this step reads real token values on the host
-            self._launch(batch)
+            # the resolved tokens may have finished (EOS / stop id / max_tokens) sequences of
+            # the batch just built: their KV tables are freed, so they must not run again
+            batch = self._drop_finished(batch)
+            if batch is not None:
+                self._launch(batch)
             return done
         prev = self._inflight
         self._launch(batch)            # step t+1 is queued behind step t ...
+        if prev is None:               # (nothing older in flight: t+1 stays in flight)
+            return []
+        self.stats["overlapped_steps"] += 1
         return self._resolve(prev)     # ... while the host collects step t's tokens
+
+    @staticmethod
+    def _drop_finished(batch: Batch) -> Optional[Batch]:
+        """The batch without the sequences that finished after it was scheduled (None if
+        nothing is left).  A finished prefill's chunk and a finished decode's row just vanish:
+        their blocks were already returned by ``finish_seqs``."""
+        pre = [(s, c) for s, c in batch.prefills if not s.finished]
+        dec = [s for s in batch.decodes if not s.finished]
+        if not pre and not dec:
+            return None
+        return Batch("mixed" if pre else "decode", pre, dec)
 
     @staticmethod
     def _needs_host_tokens(batch: Batch) -> bool:

@@ -440,9 +440,15 @@ def test_async_scheduling_matches_sync(model):
     eng, asy = run(True, 400)
     assert eng.async_sched
     for a, b in zip(sync, asy):
-        assert a.output_ids == b.output_ids and a.finish_reason == b.finish_reason
+        assert a.finish_reason == b.finish_reason
         assert a.n_pending == 0 and b.n_pending == 0
+        if a.finish_reason == "abort":
+            # aborted with a step in flight: its unresolved token is dropped, never delivered
+            assert b.output_ids == a.output_ids[:len(b.output_ids)]
+            continue
+        assert a.output_ids == b.output_ids
         torch.testing.assert_close(torch.tensor(a.output_logprobs), torch.tensor(b.output_logprobs))
+    assert eng.stats["overlapped_steps"] > 0  # steps really launched behind an in-flight one
     assert asy[2].finish_reason == "stop" and asy[5].finish_reason == "length"
     assert asy[7].finish_reason == "abort"
     # tight cache: preemption + recompute under async scheduling
@@ -451,6 +457,48 @@ def test_async_scheduling_matches_sync(model):
         if a.finish_reason != "abort":
             assert a.output_ids == b.output_ids
     assert eng.blocks.num_free == 40 and eng.scheduler.num_preemptions > 0
+
+
+def test_async_penalties_with_stop_hit(model):
+    """Async scheduling + a penalty request (its steps need the in-flight tokens on the host)
+    whose resolved token is a stop id / EOS: the already-scheduled batch must drop the finished
+    sequence (its KV table is freed) instead of running it again.  Same tokens as sync."""
+    sp = dict(max_tokens=16, temperature=0.0, frequency_penalty=1.5)
+    ref = _engine(model, num_blocks=200, async_scheduling=False).generate(
+        [[5, 5, 5, 5]], SamplingParams(ignore_eos=True, **sp))[0].output_ids
+    stop = ref[3]
+
+    def run(async_):
+        eng = _engine(model, num_blocks=200, async_scheduling=async_)
+        eng.eos_id = ref[6]  # a second finish path: EOS found while a step is in flight
+        a = eng.add_request([5, 5, 5, 5], SamplingParams(stop_token_ids=[stop], **sp))
+        b = eng.add_request([9, 8, 7], SamplingParams(**sp))
+        c = eng.add_request([11, 12, 13], SamplingParams(max_tokens=12, temperature=0.0,
+                                                         ignore_eos=True))
+        while eng.has_work:
+            eng.step()
+        assert eng.blocks.num_free == eng.blocks.num_blocks
+        return a, b, c
+
+    sync = run(False)
+    asy = run(True)
+    for x, y in zip(sync, asy):
+        assert x.output_ids == y.output_ids and x.finish_reason == y.finish_reason
+    assert asy[0].finish_reason == "stop" and asy[0].output_ids[-1] == stop
+
+
+def test_penalty_order_matches_vllm():
+    """Repetition penalty on the raw logit's sign first, then frequency / presence."""
+    from lumen.serve.engine import apply_penalties
+    from lumen.serve.sequence import Sequence
+
+    s = Sequence([1], SamplingParams(frequency_penalty=1.0, repetition_penalty=2.0))
+    s.output_ids = [2, 2]
+    logits = torch.tensor([[0.0, 0.0, 1.5, 0.0]])
+    out = apply_penalties(logits, [s])
+    # token 2: 1.5 / 2 (repetition) - 2 * 1.0 (frequency) = -1.25
+    assert out[0, 2].item() == pytest.approx(-1.25)
+    assert out[0, 1].item() == 0.0  # prompt token 1: seen, logit 0 stays 0
 
 
 def test_fp8_kv_cache_engine_cpu(model):
