@@ -32,6 +32,41 @@ BASELINE_TOK_S = 3.12 * 512  # training/train.ipynb:442 (samples/s) x max_length
 METRIC = "train tok/s Llama-2-7B ZeRO-3+LoRA at 1/2/4/8 GPUs; serve tok/s + p50 TTFT"
 
 
+def run_serve_bench(args) -> dict:
+    """Engine-mode serving bench (lumen/bench/serve_bench.py): continuous batching, chunked
+    prefill (2048-token step budget), hipGraph decode, async scheduling, bf16 KV, greedy, all
+    256 requests arriving at once.  A failure is reported in the record, never fatal to the
+    training number already measured."""
+    import gc
+    import types
+
+    import torch
+
+    gc.collect()
+    torch.cuda.empty_cache()
+    from lumen.bench.serve_bench import bench_engine
+
+    a = types.SimpleNamespace(
+        model=args.serve_model or args.model, max_model_len=1024, max_num_seqs=256,
+        max_batched_tokens=2048, no_graphs=False, sync_scheduling=False, kv_cache_dtype="auto",
+        num_requests=256, prompt_len=512, max_tokens=128, temperature=0.0, request_rate=None)
+    t0 = time.time()
+    try:
+        r = bench_engine(a)
+    except Exception as e:  # noqa: BLE001 - keep the training result
+        return {"error": repr(e)[:500]}
+    keep = ("output_tok_s", "ttft_p50_ms", "ttft_p99_ms", "itl_p50_ms", "itl_p99_ms", "wall_s",
+            "total_tok_s", "output_tokens", "preemptions", "steps", "setup_s")
+    out = {k: r[k] for k in keep if k in r}
+    out["bench_s"] = round(time.time() - t0, 1)
+    out["config"] = {"model": a.model, "tp": 1, "requests": a.num_requests,
+                     "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
+                     "max_num_batched_tokens": a.max_batched_tokens, "kv_cache_dtype": "bf16",
+                     "sampling": "greedy, ignore_eos", "arrival": "all at t=0",
+                     "async_scheduling": r.get("async_scheduling"), "mode": "in-process engine"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -43,6 +78,8 @@ def main():
     ap.add_argument("--seq_len", type=int, default=512)
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "ds_config_zero3_mi355x.json"))
     ap.add_argument("--lora_r", type=int, default=16)
+    ap.add_argument("--dtype", default=None, choices=[None, "bf16", "fp16"],
+                    help="override the config's precision (fp16: dynamic loss scaling)")
     ap.add_argument("--gradient_checkpointing", action="store_true")
     ap.add_argument("--profile_dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--gemm_table", default=None,
@@ -50,6 +87,11 @@ def main():
                          "configs/tunableop/mi355x_gemms.csv when present")
     ap.add_argument("--tune_gemms", default=None, metavar="OUT_CSV",
                     help="tune the GEMM shapes during warmup and write the table at exit")
+    ap.add_argument("--serve", dest="serve", action="store_true", default=True,
+                    help="(default) at N=1 on a GPU, after the timed training steps: the serving "
+                         "bench (Llama-2-7B TP=1, 256 requests x 512 in / 128 out) -> extra.serve")
+    ap.add_argument("--no_serve", dest="serve", action="store_false")
+    ap.add_argument("--serve_model", default=None, help="serving model (default: --model)")
     args = ap.parse_args()
 
     import torch
@@ -87,7 +129,8 @@ def main():
         gemm_table = "tuned" if load_tuned_gemms(args.gemm_table) else "heuristic"
     if world != args.gpus and env.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    ds = load_ds_config(args.config, args.micro_batch, args.grad_accum, world, 2e-4)
+    ds = load_ds_config(args.config, args.micro_batch, args.grad_accum, world, 2e-4,
+                        dtype_override=args.dtype)
     torch.manual_seed(1234)
     cfg = get_config(args.model)
     t_build = time.time()
@@ -127,6 +170,13 @@ def main():
         batches.append({"input_ids": ids.to(env.device), "labels": labels.to(env.device),
                         "n_valid": int((labels != -100).sum())})
 
+    # multi-rank: a hung collective ends the run with a diagnosis (exit 19) before the RCCL
+    # watchdog's LUMEN_DIST_TIMEOUT, naming the LUMEN_ZERO3_SHARED_GROUP=1 escape hatch
+    from lumen.utils.debug import StepWatchdog
+
+    wd = (StepWatchdog.from_env(env.rank, coord, "training step")
+          if world > 1 and not args.tune_gemms else None)
+
     def run_steps(n, offset):
         for s in range(n):
             for a in range(ds.grad_accum):
@@ -134,6 +184,8 @@ def main():
                 loss = engine.forward(b)
                 engine.backward(loss)
                 engine.step()
+            if wd is not None:
+                wd.kick()
         return loss
 
     def sync():
@@ -145,6 +197,8 @@ def main():
             barrier()  # device-bound barrier on RCCL, plain on gloo (CPU plumbing runs)
             if on_gpu:
                 torch.cuda.synchronize()
+        if wd is not None:
+            wd.kick()
 
     loss = run_steps(args.warmup, 0)
     sync()
@@ -198,6 +252,17 @@ def main():
     else:
         par = f"dp{world}-zero{ds.stage}"
     gathered_mb = ((coord.gathered_bytes - gb0) / 1e6 / args.steps) if coord else 0.0
+    zstats = coord.stats() if coord else None
+    if wd is not None:
+        wd.close()
+    serve = None
+    if args.serve and world == 1 and on_gpu:
+        # second half of the BASELINE metric ("serve tok/s + p50 TTFT"), after the timed
+        # training region: the training model and engine are freed first
+        engine.close()
+        del engine, model, coord, batches
+        serve = run_serve_bench(args)
+        engine = None
     if env.is_main:
         from lumen.train.trainer import model_flops_per_token
 
@@ -237,17 +302,19 @@ def main():
                 "rccl_world": rccl_world,
                 "gather_group_world": gather_world,
                 "backend": env.backend,
-                "zero3": coord.stats() if coord else None,
+                "zero3": zstats,
                 "zero3_gathered_mb_per_step": round(gathered_mb, 1),
                 "zero3_received_mb_per_step_per_rank": round(gathered_mb * (world - 1) / world, 1),
                 "zero3_exposed_wait_ms_per_step_max_rank": round(exposed_ms / args.steps, 2),
                 "baseline_tok_s": BASELINE_TOK_S,
                 "gemm_algos": gemm_table,
                 "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,
+                "serve": serve,
             },
         }
         print(json.dumps(out), flush=True)
-    engine.close()  # drain in-flight (next-step) gathers before teardown
+    if engine is not None:
+        engine.close()  # drain in-flight (next-step) gathers before teardown
     if dist.is_initialized():
         from lumen.parallel.dist import barrier
 

@@ -290,6 +290,8 @@ void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                                 "(lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, "
                                 "window, hysteresis, min_scale)");
   if (p.scalar_type() != at::kFloat) throw std::invalid_argument("lumen: adamw master must be f32");
+  std::vector<double> sched10 = sched;  // optional 10th value (decay_total) defaults to 0
+  if (!sched10.empty() && sched10.size() < 10) sched10.resize(10, 0.0);
   const int od = out_copy.has_value() ? dcode(*out_copy) : 0;
   check(lumen_adamw(p.data_ptr<float>(), dcode(g), g.data_ptr(), m.data_ptr<float>(),
                     v.data_ptr<float>(), od, ptr(out_copy), p.numel(), static_cast<float>(lr),
@@ -297,7 +299,7 @@ void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                     static_cast<float>(wd), static_cast<float>(bc1), static_cast<float>(bc2),
                     static_cast<float>(inv_scale), ptr<const float>(norm_sq),
                     static_cast<float>(max_norm), ptr<float>(step_state),
-                    sched.empty() ? nullptr : sched.data(), cur_stream()),
+                    sched10.empty() ? nullptr : sched10.data(), cur_stream()),
         "adamw");
 }
 

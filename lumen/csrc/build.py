@@ -61,22 +61,55 @@ def _newer(src_list, obj):
 
 
 def _run(cmd):
+    """Run a compile / link; its ``-o`` target is written under a temporary name and renamed
+    on success, so an interrupted build never leaves a truncated object that looks current."""
     t0 = time.time()
+    cmd = list(cmd)
+    i = cmd.index("-o") + 1
+    final = cmd[i]
+    cmd[i] = tmp = f"{final}.part{os.getpid()}"
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
-        raise RuntimeError(f"compile failed: {cmd[-1]}")
+        if os.path.exists(tmp):
+            os.remove(tmp)
+        raise RuntimeError(f"compile failed: {final}")
+    os.replace(tmp, final)
     return time.time() - t0, r.stderr
 
 
-def build(jobs: int = 8, force: bool = False, asm: bool = False, verbose: bool = True) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(jobs: int = 8, force: bool = False, asm: bool = False, verbose: bool = True,
+          build_dir: str = None, out: str = None) -> str:
+    """Compile + link under an exclusive file lock next to the output ``.so``.
+
+    Several processes may call this at once (every rank of a ``torch.distributed.run`` job whose
+    extension is missing): the first one builds, the others block on the lock and then find
+    everything up to date.  The link writes a temporary file that is renamed over the output,
+    so no process can ever load a half-written shared object."""
+    import fcntl
+
+    build_dir = build_dir or os.environ.get("LUMEN_BUILD_DIR") or BUILD
+    out = out or ext_path()
+    os.makedirs(build_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    with open(out + ".lock", "a+") as lk:
+        t0 = time.time()
+        fcntl.flock(lk.fileno(), fcntl.LOCK_EX)
+        if verbose and time.time() - t0 > 1.0:
+            print(f"[lumen.build] waited {time.time() - t0:.1f}s for a concurrent build", flush=True)
+        try:
+            return _build_locked(jobs, force, asm, verbose, build_dir, out)
+        finally:
+            fcntl.flock(lk.fileno(), fcntl.LOCK_UN)
+
+
+def _build_locked(jobs, force, asm, verbose, build_dir, out) -> str:
     headers = glob.glob(os.path.join(HERE, "kernels", "*.h"))
     common = ["-O3", "-fPIC", "-std=c++17"]
     jobs_list = []
     objs = []
     for src in sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip"))):
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer([src] + headers, obj):
             cmd = [HIPCC, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, "-c", src,
@@ -85,20 +118,19 @@ def build(jobs: int = 8, force: bool = False, asm: bool = False, verbose: bool =
                 cmd.insert(1, "-save-temps")
             jobs_list.append(cmd)
     cpu_src = os.path.join(HERE, "cpu", "cpu_adam.cpp")
-    cpu_obj = os.path.join(BUILD, "cpu_adam.o")
+    cpu_obj = os.path.join(build_dir, "cpu_adam.o")
     objs.append(cpu_obj)
     if force or _newer([cpu_src], cpu_obj):
         jobs_list.append(["g++", "-O3", "-fPIC", "-std=c++17", "-fopenmp", "-c", cpu_src, "-o",
                           cpu_obj])
     bind_src = os.path.join(HERE, "binding.cpp")
-    bind_obj = os.path.join(BUILD, "binding.o")
+    bind_obj = os.path.join(build_dir, "binding.o")
     objs.append(bind_obj)
     cflags, ldflags = _torch_flags()
     if force or _newer([bind_src], bind_obj):
         # host-only translation unit: plain g++ against the HIP host API headers
         jobs_list.append(["g++", "-O2", "-fPIC", "-std=c++17", f"-I{ROCM}/include", *cflags, "-c",
                           bind_src, "-o", bind_obj])
-    out = ext_path()
     if jobs_list:
         with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             for cmd, (dt, _) in zip(jobs_list, ex.map(_run, jobs_list)):
@@ -106,6 +138,7 @@ def build(jobs: int = 8, force: bool = False, asm: bool = False, verbose: bool =
                     print(f"[lumen.build] {os.path.basename(cmd[-3] if cmd[-2] == '-o' else cmd[-1])}"
                           f" {dt:.1f}s", flush=True)
     if jobs_list or not os.path.exists(out) or _newer(objs, out):
+        # atomic rename inside _run: a concurrent loader sees the old or the new file
         _run([HIPCC, "-shared", "-fPIC", "-fopenmp", *objs, "-o", out, *ldflags])
         if verbose:
             print(f"[lumen.build] linked {out}", flush=True)

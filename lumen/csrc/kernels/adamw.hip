@@ -33,9 +33,17 @@ struct OptSched {
   float scale_window;
   int hysteresis;
   float min_scale;
+  float decay_total;  // > 0: HF get_linear_schedule_with_warmup over this many steps
 };
 
 __device__ __forceinline__ float sched_lr(const OptSched& s, float it) {
+  if (s.decay_total > 0.f) {
+    // HF Trainer's default (no DeepSpeed scheduler): linear warm-up from 0, then linear decay
+    // to 0 at decay_total (transformers get_linear_schedule_with_warmup)
+    const float w = (float)s.warm_n;
+    if (it < w) return s.lr_max * it / w;
+    return s.lr_max * fmaxf(0.f, (s.decay_total - it) / fmaxf(1.f, s.decay_total - w));
+  }
   const float n = (float)(s.warm_n > 2 ? s.warm_n : 2);
   if (it >= n) return s.lr_max;
   const float gamma = s.warm_linear ? it / n : logf(it + 1.f) / logf(n);
@@ -184,7 +192,8 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
   lumen::OptSched sc{};
   sc.state = step_state;
   if (step_state) {
-    // sched: lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, window, hysteresis, min
+    // sched: lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, window, hysteresis, min,
+    // decay_total (the binding pads the list to 10 values)
     sc.lr_min = (float)sched[0];
     sc.lr_max = (float)sched[1];
     sc.warm_n = (int)sched[2];
@@ -194,6 +203,7 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
     sc.scale_window = (float)sched[6];
     sc.hysteresis = (int)sched[7];
     sc.min_scale = (float)sched[8];
+    sc.decay_total = (float)sched[9];
   }
   if (n == 0) return hipSuccess;
   dim3 grid(lumen::grid_for(n)), block(256);

@@ -25,12 +25,18 @@ class SyntheticTokenDataset:
     def __len__(self):
         return self.n
 
+    def _len(self, g) -> int:
+        if self.min_len is not None and self.min_len < self.seq_len:
+            return int(torch.randint(self.min_len, self.seq_len + 1, (1,), generator=g))
+        return self.seq_len
+
+    def length(self, i) -> int:
+        """Row length without generating the row (token-budget batch planning)."""
+        return self._len(torch.Generator().manual_seed(self.seed * 1_000_003 + i))
+
     def __getitem__(self, i):
         g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
-        L = self.seq_len
-        if self.min_len is not None and self.min_len < L:
-            L = int(torch.randint(self.min_len, self.seq_len + 1, (1,), generator=g))
-        ids = torch.randint(3, self.vocab, (L,), generator=g)
+        ids = torch.randint(3, self.vocab, (self._len(g),), generator=g)
         return {"input_ids": ids.tolist()}
 
 
@@ -43,6 +49,9 @@ class TokenizedDataset:
 
     def __getitem__(self, i):
         return {"input_ids": self.rows[i]}
+
+    def length(self, i) -> int:
+        return len(self.rows[i])
 
 
 def load_text_dataset(path: str):

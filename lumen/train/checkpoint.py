@@ -109,13 +109,19 @@ def load_checkpoint(path: str, engine, model, env) -> Dict:
 
     load_engine_state(os.path.join(path, tag), engine, env.rank)
     rng = os.path.join(path, f"rng_state_{env.rank}.pth")
-    if not os.path.exists(rng):  # resumed at a larger world size: new ranks take rank 0's
-        rng = os.path.join(path, "rng_state_0.pth")
     if os.path.exists(rng):
         st = torch.load(rng, map_location="cpu", weights_only=True)
         torch.set_rng_state(st["cpu"])
         if "cuda" in st and torch.cuda.is_available():
             torch.cuda.set_rng_state(st["cuda"])
+    else:
+        # resumed at a larger world size: a rank with no saved state gets its own stream
+        # (seeded from the checkpoint step and its rank), never a copy of another rank's --
+        # copied states would draw the same LoRA-dropout masks on several ranks
+        with open(os.path.join(path, "trainer_state.json")) as f:
+            step = int(json.load(f).get("global_step", 0))
+        seed = (step * 1_000_003 + 7919 * (env.rank + 1)) % (2**63)
+        torch.manual_seed(seed)
     with open(os.path.join(path, "trainer_state.json")) as f:
         return json.load(f)
 

@@ -42,6 +42,15 @@ class DSConfig:
     warmup_max_lr: float = 2e-4
     warmup_num_steps: int = 0
     warmup_type: str = "log"
+    # "warmup": DeepSpeed WarmupLR (constant after the warm-up: every reference DeepSpeed config
+    # has a WarmupLR section, and its ZeRO-2 run logged 'learning_rate': 0.0002 for 2,856 steps,
+    # training/train.ipynb:339-644; a config without one runs at a constant LR).
+    # "hf_linear": no DeepSpeed config at all (the
+    # reference train_baseline.py's plain HF Trainer): linear warm-up, then linear decay to 0 at
+    # ``decay_total_steps`` (transformers get_linear_schedule_with_warmup; set by the trainer
+    # once the run length is known)
+    lr_schedule: str = "warmup"
+    decay_total_steps: int = 0
     gradient_clipping: float = 1.0
     # batch
     train_batch_size: int = 1
@@ -111,7 +120,10 @@ def load_ds_config(src, micro_batch: int, grad_accum: int, world_size: int,
     c.warmup_max_lr = float(_auto(sp.get("warmup_max_lr"), c.lr))
     c.warmup_num_steps = int(_auto(sp.get("warmup_num_steps"), warmup_steps))
     c.warmup_type = sp.get("warmup_type", "log")
-    if not sch and not warmup_steps:
+    if not raw:
+        c.lr_schedule = "hf_linear"
+        c.warmup_min_lr, c.warmup_max_lr = 0.0, c.lr
+    elif not sch and not warmup_steps:
         # no "scheduler" section and no warm-up asked for: DeepSpeed builds no WarmupLR (HF's
         # default schedule with 0 warm-up steps also starts at the full rate), so the first step
         # runs at the full rate -- not WarmupLR's lr = warmup_min_lr
@@ -162,7 +174,13 @@ def warmup_lr(step: int, c: DSConfig) -> float:
 
     DeepSpeed clamps the warm-up length to ``max(2, warmup_num_steps)`` and the first optimizer
     step runs at iteration 0, i.e. at ``warmup_min_lr`` (gamma = log(1) = 0); with the "auto"
-    configs (HF fills ``warmup_num_steps`` = 0) every later step runs at ``warmup_max_lr``."""
+    configs (HF fills ``warmup_num_steps`` = 0) every later step runs at ``warmup_max_lr``.
+    ``hf_linear`` (no DeepSpeed config): HF's linear warm-up / linear decay to 0."""
+    if c.lr_schedule == "hf_linear" and c.decay_total_steps > 0:
+        w, T = c.warmup_num_steps, c.decay_total_steps
+        if step < w:
+            return c.warmup_max_lr * step / w
+        return c.warmup_max_lr * max(0.0, (T - step) / max(1, T - w))
     n = max(2, c.warmup_num_steps)
     if step >= n:
         return c.warmup_max_lr

@@ -133,7 +133,8 @@ class ZeroEngine:
         # the applied-step counter (no host sync per step, bf16 or fp16); host logic otherwise
         self.device_sched = self.opt.configure_schedule(
             cfg.warmup_min_lr, cfg.warmup_max_lr, cfg.warmup_num_steps,
-            cfg.warmup_type == "linear", W, self.scaler)
+            cfg.warmup_type == "linear", W, self.scaler,
+            cfg.decay_total_steps if cfg.lr_schedule == "hf_linear" else 0)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._gscale = torch.ones(1, dtype=torch.float32, device=self.device)
         self._works: List = []
@@ -156,6 +157,14 @@ class ZeroEngine:
         overflow-skipped step does not advance the scheduler)."""
         applied = self.opt.step_count
         return warmup_lr(max(applied - 1, 0), self.cfg) if applied else warmup_lr(0, self.cfg)
+
+    def set_total_steps(self, n: int) -> None:
+        """Run length for a decaying schedule (HF linear: no DeepSpeed config)."""
+        if self.cfg.lr_schedule != "hf_linear":
+            return
+        self.cfg.decay_total_steps = int(n)
+        if self.device_sched:
+            self.opt.sched[9] = float(n)
 
     def is_boundary(self) -> bool:
         return (self.micro_step + 1) % self.cfg.grad_accum == 0

@@ -22,7 +22,7 @@ from ..data import (CausalLMCollator, PackedCollator, PrefetchLoader, ShardedSam
 from ..lora import LoraConfig, apply_lora, print_trainable_parameters, save_adapter
 from ..models import build_model, get_config
 from ..parallel.dist import DistEnv, all_reduce_scalar, barrier
-from ..utils.debug import StepProfiler, check_finite, maybe_inject_fault
+from ..utils.debug import StepProfiler, StepWatchdog, check_finite, maybe_inject_fault
 from .checkpoint import AsyncCheckpointer, latest_checkpoint, load_checkpoint, save_checkpoint
 from .config import DSConfig
 from .engine import ZeroEngine
@@ -116,26 +116,55 @@ class Trainer:
         self.log_history: List[Dict] = []
         self.ckpt = AsyncCheckpointer() if args.async_save else None
         self.flops_per_token = model_flops_per_token(cfg, args.max_length)
+        self._plans: Dict[int, List[List[int]]] = {}
 
     # ---------------------------------------------------------------------------------------
-    def _batches(self, epoch: int, skip_samples: int):
-        mb = self.ds.micro_batch
-        idx = self.sampler.indices(epoch)[skip_samples:]
-        if self.packed and self.args.pack_tokens > 0:
-            # token-budget batching: whole sequences, in sampler order, until the next one would
-            # overflow the budget -- every micro-step's GEMMs see ~pack_tokens rows
-            budget, cur, n = self.args.pack_tokens, [], 0
+    @property
+    def token_budget(self) -> bool:
+        return self.packed and self.args.pack_tokens > 0
+
+    def _length(self, j: int) -> int:
+        f = getattr(self.dataset, "length", None)
+        n = f(j) if f is not None else len(self.dataset[j]["input_ids"])
+        return min(n, self.args.max_length)
+
+    def _plan(self, epoch: int) -> List[List[int]]:
+        """This rank's micro-batches (sample indices) for ``epoch``.
+
+        Fixed count: ``micro_batch`` samples each (the tail that does not fill one is dropped,
+        like a drop_last loader).  Token budget (``--pack_tokens``): whole sequences in sampler
+        order until the next would overflow the budget, tail batch included.  Each rank's shard
+        has its own length mix, so the counts differ: every rank truncates to the MIN over ranks
+        -- an extra micro-step on one rank would issue ZeRO-3 gathers / reduce-scatters that no
+        other rank matches (a hang at the end of the epoch)."""
+        if epoch in self._plans:
+            return self._plans[epoch]
+        idx = self.sampler.indices(epoch)
+        if not self.token_budget:
+            mb = self.ds.micro_batch
+            plan = [idx[i:i + mb] for i in range(0, len(idx) - mb + 1, mb)]
+        else:
+            budget, plan, cur, n = self.args.pack_tokens, [], [], 0
             for j in idx:
-                ex = self.dataset[j]
-                L = min(len(ex["input_ids"]), self.args.max_length)
+                L = self._length(j)
                 if cur and n + L > budget:
-                    yield cur
+                    plan.append(cur)
                     cur, n = [], 0
-                cur.append(ex)
+                cur.append(j)
                 n += L
-            return
-        for i in range(0, len(idx) - mb + 1, mb):
-            yield [self.dataset[j] for j in idx[i:i + mb]]
+            if cur:
+                plan.append(cur)
+            if self.env.world_size > 1:
+                import torch.distributed as dist
+
+                k = int(all_reduce_scalar(float(len(plan)), op=dist.ReduceOp.MIN))
+                plan = plan[:k]
+        self._plans = {epoch: plan}
+        return plan
+
+    def _batches(self, epoch: int, skip_batches: int):
+        for b in self._plan(epoch)[skip_batches:]:
+            yield [self.dataset[j] for j in b]
 
     def _to_device(self, b):
         d = self.env.device
@@ -156,11 +185,13 @@ class Trainer:
         return ld, iter(ld)
 
     def steps_per_epoch(self) -> int:
+        if self.token_budget:
+            return len(self._plan(0)) // self.ds.grad_accum
         return len(self.sampler) // (self.ds.micro_batch * self.ds.grad_accum)
 
     def train(self) -> Dict:
         a, ds, env, eng = self.args, self.ds, self.env, self.engine
-        start_epoch, skip = 0, 0
+        start_epoch, skip, skip_b = 0, 0, 0
         if a.resume_from_checkpoint:
             ck = latest_checkpoint(a.output_dir)
             if ck:
@@ -169,21 +200,35 @@ class Trainer:
                 start_epoch = int(st.get("epoch_int", 0))
                 skip = int(st.get("samples_in_epoch", 0))
                 old_world = int(st.get("world_size", env.world_size))
+                if self.token_budget:
+                    # token-budget plans are agreed over ranks: the micro-batch count is the
+                    # rank-independent position (samples consumed differ per rank)
+                    skip_b = int(st.get("batches_in_epoch", 0))
+                    if old_world != env.world_size:
+                        skip_b = skip_b * old_world // env.world_size
+                        self.print("[lumen] warning: --pack_tokens resume at a new world size "
+                                   "restarts at the proportional micro-batch (approximate)")
                 if old_world != env.world_size:
                     # per-rank position -> same GLOBAL position: step k covers the contiguous
                     # permutation block [k*G, (k+1)*G) at any world size (ShardedSampler)
                     skip = skip * old_world // env.world_size
                     self.print(f"[lumen] resharded checkpoint: world {old_world} -> "
                                f"{env.world_size}")
+                if not self.token_budget:
+                    skip_b = skip // ds.micro_batch
                 self.print(f"[lumen] resumed from {ck} (step {eng.global_step})")
             else:
                 self.print("[lumen] no checkpoint found; starting fresh")
         spe = max(self.steps_per_epoch(), 1)
         total_steps = a.max_steps if a.max_steps > 0 else spe * a.num_train_epochs
+        eng.set_total_steps(total_steps)  # HF linear decay (baseline: no DeepSpeed config)
         self.print(f"[lumen] ZeRO-{ds.stage} world={env.world_size} micro={ds.micro_batch} "
                    f"accum={ds.grad_accum} effective batch={ds.train_batch_size} "
                    f"steps={total_steps}")
         prof = StepProfiler(env.rank, self.print)
+        # multi-rank: a hung collective ends the job with a diagnosis (exit 19)
+        wd = (StepWatchdog.from_env(env.rank, eng.coordinator, "micro-step")
+              if env.world_size > 1 else None)
         t_start = time.time()
         tokens = 0
         win_tokens, win_t = 0, t_start
@@ -197,10 +242,14 @@ class Trainer:
             if a.max_steps <= 0 and epoch >= a.num_train_epochs:
                 break
             samples_in_epoch = skip
+            self._batches_in_epoch = skip_b
             produced = 0
-            loader, stream = self._batch_stream(epoch, skip)
+            loader, stream = self._batch_stream(epoch, skip_b)
             for raw, cb in stream:
                 produced += 1
+                self._batches_in_epoch += 1
+                if wd is not None:
+                    wd.kick()
                 b = self._to_device(cb)
                 loss = eng.forward(b)
                 check_finite("loss", loss, eng.global_step, env.rank)
@@ -247,7 +296,7 @@ class Trainer:
                         break
             if loader is not None:
                 loader.close()
-            skip = 0
+            skip, skip_b = 0, 0
             if produced == 0:
                 break
             if not done and a.save_strategy == "epoch":
@@ -255,6 +304,8 @@ class Trainer:
             epoch += 1
         prof.close()
         eng.close()  # no ZeRO-3 gather left in flight past the loop
+        if wd is not None:
+            wd.close()
         if self.ckpt is not None:
             self.ckpt.wait()  # the last periodic checkpoint is complete before we report / exit
         if env.device.type == "cuda":
@@ -275,7 +326,9 @@ class Trainer:
 
     def _trainer_state(self, epoch: int, samples_in_epoch: int) -> Dict:
         return {"global_step": self.engine.global_step, "epoch_int": epoch,
-                "samples_in_epoch": samples_in_epoch, "log_history": self.log_history,
+                "samples_in_epoch": samples_in_epoch,
+                "batches_in_epoch": getattr(self, "_batches_in_epoch", 0) if samples_in_epoch else 0,
+                "log_history": self.log_history,
                 "world_size": self.env.world_size, "zero_stage": self.ds.stage,
                 "train_batch_size": self.ds.train_batch_size, "args": asdict(self.args)}
 

@@ -137,5 +137,70 @@ def maybe_inject_fault(step: int, rank: int) -> None:
         os._exit(FAULT_EXIT_CODE)
 
 
+HANG_EXIT_CODE = 19
+
+
+class StepWatchdog:
+    """Host-side progress watchdog: ends the process (exit code 19) when no ``kick()`` arrives
+    within ``timeout_s`` -- a hung collective must end a multi-rank job with a message that
+    names the escape hatch, not eat the job's time budget.  It fires before the RCCL watchdog
+    (``LUMEN_DIST_TIMEOUT``), prints what the ZeRO-3 coordinator had in flight, and exits with
+    ``os._exit`` (no re-exec, no cleanup that could block on the hung device)."""
+
+    def __init__(self, timeout_s: float, rank: int = 0, coordinator=None, what: str = "step"):
+        import threading
+        import time
+
+        self.timeout_s = float(timeout_s)
+        self.rank = rank
+        self.coordinator = coordinator
+        self.what = what
+        self._time = time
+        self._last = time.monotonic()
+        self._stop = threading.Event()
+        self._thread = None
+        if self.timeout_s > 0:
+            self._thread = threading.Thread(target=self._run, name="lumen-watchdog", daemon=True)
+            self._thread.start()
+
+    @classmethod
+    def from_env(cls, rank: int = 0, coordinator=None, what: str = "step"):
+        """Timeout from ``LUMEN_WATCHDOG_S``, else 60 s under ``LUMEN_DIST_TIMEOUT`` (0: off)."""
+        v = os.environ.get("LUMEN_WATCHDOG_S")
+        if v is None:
+            d = float(os.environ.get("LUMEN_DIST_TIMEOUT", "1800"))
+            v = max(60.0, d - 60.0)
+        return cls(float(v), rank, coordinator, what)
+
+    def kick(self) -> None:
+        self._last = self._time.monotonic()
+
+    def message(self, waited: float) -> str:
+        msg = (f"[lumen watchdog] rank {self.rank}: no {self.what} completed in {waited:.0f} s "
+               f"(limit {self.timeout_s:.0f} s); a collective or kernel is hung.")
+        c = self.coordinator
+        if c is not None and not getattr(c, "identity", True):
+            inflight = sum(st == "inflight" for u in c.units for st in u.states)
+            msg += (f" ZeRO-3 schedule '{c.schedule}', {inflight} weight gather(s) in flight on "
+                    f"{'a separate' if c.group is not None else 'the default'} communicator.")
+            if c.group is not None:
+                msg += (" If concurrent communicators hang on this system, rerun with "
+                        "LUMEN_ZERO3_SHARED_GROUP=1 (weight gathers on the default group).")
+        return msg
+
+    def _run(self):
+        import sys
+
+        while not self._stop.wait(min(5.0, self.timeout_s / 4)):
+            waited = self._time.monotonic() - self._last
+            if waited > self.timeout_s:
+                sys.stderr.write(self.message(waited) + "\n")
+                sys.stderr.flush()
+                os._exit(HANG_EXIT_CODE)
+
+    def close(self) -> None:
+        self._stop.set()
+
+
 def zero3_poison_enabled() -> bool:
     return debug_enabled() or os.environ.get("LUMEN_ZERO3_POISON", "0") not in ("", "0")

@@ -104,6 +104,38 @@ def test_warmup_lr_auto_matches_deepspeed():
     assert warmup_lr(0, lin) == 0.0 and warmup_lr(1, lin) == 0.5 and warmup_lr(2, lin) == 1.0
 
 
+def test_lr_schedules_hf_linear_and_deepspeed_constant(tmp_path):
+    """No DeepSpeed config (reference train_baseline.py: plain HF Trainer) -> HF's default
+    linear schedule: warm-up from 0, then linear decay to 0 at the last step.  DeepSpeed
+    configs run WarmupLR, constant after the warm-up, as the reference's ZeRO-2 run logged
+    (training/train.ipynb:339-644: 'learning_rate': 0.0002 for 2,856 steps)."""
+    c = load_ds_config(None, 1, 1, 1, 2e-4, warmup_steps=0)
+    assert c.lr_schedule == "hf_linear"
+    c.decay_total_steps = 100
+    assert warmup_lr(0, c) == pytest.approx(2e-4)
+    assert warmup_lr(50, c) == pytest.approx(1e-4)
+    assert warmup_lr(99, c) == pytest.approx(2e-6)
+    w = load_ds_config(None, 1, 1, 1, 2e-4, warmup_steps=10)
+    w.decay_total_steps = 110
+    assert warmup_lr(0, w) == 0.0 and warmup_lr(5, w) == pytest.approx(1e-4)
+    assert warmup_lr(10, w) == pytest.approx(2e-4) and warmup_lr(60, w) == pytest.approx(1e-4)
+    ds2 = load_ds_config({"zero_optimization": {"stage": 2}}, 1, 1, 1, 2e-4)
+    assert ds2.lr_schedule == "warmup"
+    assert warmup_lr(0, ds2) == 2e-4 and warmup_lr(5000, ds2) == 2e-4
+    # end to end through the trainer (host path on CPU): the logged LR decays to ~0
+    from lumen.parallel.dist import init
+    from lumen.train.trainer import TrainArgs, Trainer
+
+    a = TrainArgs(model_name="tiny-llama", dataset_path=None, output_dir=str(tmp_path),
+                  synthetic=True, synthetic_samples=16, max_length=32, max_steps=4,
+                  logging_steps=1, save_strategy="no", init="random", save_final=False)
+    ds = load_ds_config(None, 1, 1, 1, 2e-4, dtype_override="fp32")
+    tr = Trainer(a, ds, init(), printer=lambda *x, **k: None)
+    tr.train()
+    lrs = [r["learning_rate"] for r in tr.log_history]
+    assert lrs == pytest.approx([2e-4, 1.5e-4, 1e-4, 5e-5])
+
+
 def test_loss_scaler_deepspeed_semantics():
     s = DynamicLossScaler(2 ** 16, window=3, hysteresis=2)
     s.update(True)  # first overflow absorbed by hysteresis

@@ -14,7 +14,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FP16_CFG = os.path.join(ROOT, "configs", "ds_config_zero2_fp16.json")
+FP16_CFG = os.path.join(ROOT, "configs", "ds_config_zero2.json")  # the reference config: fp16
 
 
 def _engine(dtype_cfg=FP16_CFG, seed=3):
@@ -110,7 +110,7 @@ def test_fp16_forced_overflow_skips_and_backs_off():
 
 def test_fp16_trajectory_tracks_bf16():
     """Same data and init in fp16 (dynamic scaling) and bf16: the losses agree to rounding."""
-    cfg_bf16 = os.path.join(ROOT, "configs", "ds_config_zero2.json")
+    cfg_bf16 = os.path.join(ROOT, "configs", "ds_config_zero2_mi355x.json")
     res = {}
     for name, cfg in (("fp16", FP16_CFG), ("bf16", cfg_bf16)):
         eng, m, _ = _engine(cfg)

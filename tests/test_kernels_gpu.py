@@ -193,6 +193,34 @@ def test_adamw_device_step_counter():
     assert (v - v2).abs().max().item() < 1e-6
 
 
+def test_adamw_device_hf_linear_schedule():
+    """Device LR schedule with decay_total (HF linear warm-up + decay, the no-DeepSpeed
+    baseline): each applied step uses lr_max * sched(t), same as the host ``warmup_lr``."""
+    from lumen.ops._native import native
+    from lumen.parallel.zero import _adamw_torch
+    from lumen.train.config import load_ds_config, warmup_lr
+
+    C = native()
+    n = 4096 + 7
+    p = torch.randn(n, device=DEV)
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    st = torch.zeros(8, device=DEV)
+    st[2] = 1.0
+    c = load_ds_config(None, 1, 1, 1, 1e-2, warmup_steps=2)
+    c.decay_total_steps = 6
+    b1, b2 = 0.9, 0.999
+    sched = [0.0, 1e-2, 2, 0, 1.0, 0, 1000, 2, 1.0, 6]
+    g = torch.randn(n, device=DEV)
+    norm = torch.zeros(1, device=DEV)
+    C.grad_norm_sq(g, norm)
+    for t in range(1, 7):
+        C.adamw(p, g, m, v, None, 0.0, b1, b2, 1e-8, 0.0, 1.0, 1.0, 0.0, norm, 0.0, st, sched)
+        _adamw_torch(p2, g, m2, v2, warmup_lr(t - 1, c), b1, b2, 1e-8, 0.0, 1 - b1 ** t,
+                     1 - b2 ** t, 1.0)
+        assert (p - p2).abs().max().item() < 1e-5, t
+
+
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
 @pytest.mark.parametrize("impl", ["v3", "v3-atomic", "v3-nodxa", "v2", "f32"])

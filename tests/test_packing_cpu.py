@@ -114,6 +114,71 @@ def test_trainer_token_budget_batches(tmp_path):
     assert res["global_step"] == 3
 
 
+def test_token_budget_world2_epoch_end(tmp_path):
+    """--pack_tokens at world 2 with ZeRO-3 over a whole epoch: each rank's shard has its own
+    length mix, so the token-budget plans differ in length; the ranks agree on the MIN and the
+    run reaches the epoch end (an extra micro-step on one rank would hang its ZeRO-3 gathers).
+    Resume from a mid-epoch checkpoint continues at the same micro-batch on both ranks."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    from lumen.data.datasets import SyntheticTokenDataset
+    from lumen.data.sampler import ShardedSampler
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n, budget, maxlen = 48, 120, 64
+    ds = SyntheticTokenDataset(n, maxlen, 256, seed=42, min_len=8)
+
+    def count(rank):
+        c, cur = 0, 0
+        for j in ShardedSampler(n, rank, 2, seed=42).indices(0):
+            L = ds.length(j)
+            if cur and cur + L > budget:
+                c, cur = c + 1, 0
+            cur += L
+        return c + (cur > 0)
+
+    assert count(0) != count(1)  # the case the MIN agreement exists for
+
+    def run(out, extra):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={port}",
+               os.path.join(root, "training", "train_deepspeed_zero3.py"),
+               "--model_name", "tiny-llama", "--synthetic", "--synthetic_samples", str(n),
+               "--synthetic_min_len", "8", "--max_length", str(maxlen), "--pack_tokens",
+               str(budget), "--num_train_epochs", "1", "--logging_steps", "1",
+               "--per_device_train_batch_size", "1", "--gradient_accumulation_steps", "1",
+               "--device", "cpu", "--output_dir", out, "--metrics_csv",
+               os.path.join(out, "m.csv"), "--save_strategy", "steps", "--save_steps", "3",
+               "--deepspeed", os.path.join(root, "configs", "ds_config_zero3_mi355x.json"),
+               *extra]
+        env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=root, LUMEN_WATCHDOG_S="120")
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env,
+                           cwd=str(tmp_path))
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        return r.stdout
+
+    out = str(tmp_path / "ck")
+    log = run(out, [])
+    steps = min(count(0), count(1))
+    assert f'"step": {steps}' in log
+    # resume from checkpoint-3 (delete later ones): finishes the same epoch at the same step
+    import shutil
+
+    for d in os.listdir(out):
+        if d.startswith("checkpoint-") and int(d.split("-")[1]) > 3:
+            shutil.rmtree(os.path.join(out, d))
+    log2 = run(out, ["--resume_from_checkpoint"])
+    assert "resumed from" in log2 and f'"step": {steps}' in log2
+    assert '"step": 4' in log2
+
+
 def test_opt_packed_matches_padded():
     from lumen.lora import LoraConfig, apply_lora
     from lumen.models import build_model

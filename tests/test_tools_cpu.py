@@ -213,7 +213,60 @@ def test_profiler_and_debug_guards(tmp_path, monkeypatch):
         check_finite("x", torch.tensor([1.0, float("nan")]))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+def test_step_watchdog_names_escape_hatch():
+    """A rank whose steps stop (hung collective) exits 19 with a message naming
+    LUMEN_ZERO3_SHARED_GROUP=1 when ZeRO-3 gathers run on their own communicator; a kicked
+    watchdog never fires."""
+    code = ("import sys, time, types; sys.path.insert(0, %r)\n"
+            "from lumen.utils.debug import StepWatchdog\n"
+            "u = types.SimpleNamespace(states=['inflight', 'empty'])\n"
+            "c = types.SimpleNamespace(identity=False, units=[u, u], schedule='keep', group=object())\n"
+            "ok = StepWatchdog(1.0, 3, c)\n"
+            "for _ in range(8):\n    ok.kick(); time.sleep(0.25)\n"
+            "ok.close()\nprint('kicked ok', flush=True)\n"
+            "StepWatchdog(0.5, 3, c)\ntime.sleep(30)\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 19, (r.returncode, r.stderr)
+    assert "kicked ok" in r.stdout
+    assert "rank 3" in r.stderr and "2 weight gather(s) in flight" in r.stderr
+    assert "LUMEN_ZERO3_SHARED_GROUP=1" in r.stderr
+
+
+def test_concurrent_native_builds(tmp_path):
+    """4 processes call ``lumen.csrc.build.build`` on the same fresh build dir at once (what 8
+    ranks of a torchrun job do when the extension is missing): the file lock serialises them,
+    exactly one links, and the result is one loadable extension with no temp files left.
+    The fresh dir is seeded with the big objects of the in-tree build (when present) so the
+    test recompiles + links in seconds; every kernel object still has to be current."""
+    import shutil
+
+    from lumen.csrc import build as B
+
+    seed_dir = os.path.join(ROOT, "build", "lumen_native")
+    bdir = tmp_path / "build"
+    bdir.mkdir()
+    for name in ("binding.o", "flash_attn.hip.o", "paged_attention.hip.o", "lora_v3.hip.o"):
+        if os.path.exists(os.path.join(seed_dir, name)):
+            shutil.copy2(os.path.join(seed_dir, name), bdir / name)
+    out = tmp_path / "ext" / "_C.so"
+    code = ("import sys; sys.path.insert(0, %r); from lumen.csrc.build import build; "
+            "build(jobs=2, build_dir=%r, out=%r)" % (ROOT, str(bdir), str(out)))
+    procs = [subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for _ in range(4)]
+    logs = [p.communicate(timeout=900)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)[-3000:]
+    assert sum(l.count("[lumen.build] linked") for l in logs) == 1, logs
+    assert not [f for f in os.listdir(out.parent) if ".part" in f]
+    assert not [f for f in os.listdir(bdir) if ".part" in f]
+    chk = ("import importlib.util as u, sys; import torch; s = u.spec_from_file_location('_C', %r);"
+           " m = u.module_from_spec(s); s.loader.exec_module(m); print('ok', len(dir(m)))"
+           % str(out))
+    r = subprocess.run([sys.executable, "-c", chk], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stderr[-2000:]
+    assert B.ext_path().endswith(".so")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_contract_torchrun(world):
     """bench.py under torch.distributed.run (2 / 4 ranks, gloo, tiny model): one JSON line from
     rank 0 with the driver's fields, whole-job tokens/s, ZeRO-3 partitioning active on its own

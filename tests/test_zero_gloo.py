@@ -173,6 +173,22 @@ def test_zero3_world4_split_groups(case, deep_reference, tmp_path):
         assert z["gathers"] >= 2 * 2 * n_units
 
 
+@pytest.mark.parametrize("schedule", ["pipelined", "keep", "release"])
+def test_zero3_world8_split_groups(schedule, tmp_path):
+    """World 8 over gloo (the rank count of the headline 8-GPU run): the schedule on its own
+    weight-gather communicator next to the gradient group == single-process stage 0."""
+    ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama-deep", micro=8, accum=1, steps=2)
+    extra = {"schedule": schedule}
+    if schedule == "release":
+        extra["max_live"] = int(3 * _layer_numel() * 1.02)
+    r = _run(8, 3, str(tmp_path / "b"), model="tiny-llama-deep", micro=1, accum=1, steps=2,
+             extra=extra)
+    _close(r["sd"], ref["sd"])
+    z = r["zero3"]
+    assert z["schedule"] == schedule and z["world"] == 8 and z["gather_group_separate"]
+    assert z["pool_overflows"] == 0
+
+
 def test_zero3_world1_identity(tmp_path):
     """World size 1 without forced partitioning: the one-rank partition is the whole unit, the
     coordinator binds parameters to it once and never gathers; == stage 0."""
