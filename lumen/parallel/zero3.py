@@ -22,10 +22,13 @@ MI355X-first design (not a DeepSpeed translation):
       micro-step's gathers are issued, in forward order, when the current one starts.  One step
       of compute hides one step of xGMI traffic: at 2 GPUs each rank receives 6.75 GB per step
       over ONE ~77 GB/s link (~90 ms), against a ~96 ms step.
-  ``keep`` (model <= budget < 2x model: Llama-2-70B on 8 GPUs).  One buffer per unit, kept from
+  ``keep`` (auto from 4 GPUs, or model <= budget < 2x model).  One buffer per unit, kept from
       the forward to the backward; re-gathered for the next micro-step right after the unit's
-      backward.  The next forward waits for whatever of those gathers did not fit in the
-      backward, so at N=2 it exposes ~comm - backward; pipelined exposes only comm - step.
+      backward.  The first ``LUMEN_ZERO3_LEAD`` units (embedding + first layer) are double
+      buffered like ``pipelined``: their re-gather would otherwise be issued at the very end of
+      the backward and exposed at the next step's start.  The next forward waits for whatever
+      of the other gathers did not fit in the backward (~comm - backward at N=2, hence
+      ``pipelined`` there; ``auto_schedule`` has the rule).
   ``release`` (budget < model: the reference's ``stage3_max_live_parameters: 1e9``).  A
       preallocated ring of ``P = budget / unit`` gather buffers (no allocator churn); prefetch
       depth from ``stage3_prefetch_bucket_size``; the last units of the forward stay live across
@@ -110,6 +113,7 @@ class _Unit:
         self.works: List[Optional[object]] = []
         self.states: List[str] = []                    # per slot: empty | inflight | ready
         self.bound = -1                                # slot the params currently view, or -1
+        self.slot = 0                                  # slot of the current micro-step
         self.dtype = None
         # W^T copies made off the critical path (keep / pipelined): (param idx, off, wt_off)
         self.tn: List[tuple] = []
@@ -202,15 +206,25 @@ class ParamCoordinator:
         self.total_numel = total
         self.elem_bytes = units_dtype_bytes(self.units)
         self.max_live = max_live if max_live >= 0 else self._hbm_live_budget(self.elem_bytes)
+        self.schedule_reason = ("world size 1: the one-rank partition is the whole unit"
+                                if schedule == "identity" else
+                                "forced (LUMEN_ZERO3_SCHEDULE or caller)")
         if schedule is None:
-            schedule = ("pipelined" if 2 * total <= self.max_live else
-                        "keep" if total <= self.max_live else "release")
+            schedule, self.schedule_reason = self.auto_schedule(total, self.max_live, W)
         assert schedule in self.SCHEDULES, schedule
         self.schedule = schedule
         self.identity = schedule == "identity"
         self.keep = schedule in ("keep", "pipelined")
-        n_slots = 2 if schedule == "pipelined" else 1
-        for u in self.units:
+        # "lead" units own a second buffer: their NEXT micro-step gather is issued when the
+        # current one starts (a full step of compute hides it).  pipelined: every unit.  keep:
+        # the first ``LUMEN_ZERO3_LEAD`` units (default 2: the embedding and the first decoder
+        # layer) -- the ones the next forward needs first, whose single-buffer re-gather after
+        # their own backward would otherwise be exposed at the step boundary.
+        n_lead = (len(self.units) if schedule == "pipelined" else
+                  int(os.environ.get("LUMEN_ZERO3_LEAD", "2")) if schedule == "keep" else 0)
+        self.lead = set(range(min(n_lead, len(self.units))))
+        for i, u in enumerate(self.units):
+            n_slots = 2 if i in self.lead else 1
             u.bufs = [None] * n_slots
             u.works = [None] * n_slots
             u.states = ["empty"] * n_slots
@@ -219,7 +233,6 @@ class ParamCoordinator:
         self._tstream = None
         self._cstream = None
         self.transposed_numel = 0
-        self.slot = 0
         self.last = len(self.units) - 1
         self.device = env.device
         sizes = [u.padded for u in self.units if u.padded]
@@ -263,6 +276,25 @@ class ParamCoordinator:
         self.poison = zero3_poison_enabled() and not self.identity
 
     # ---- sizing -----------------------------------------------------------------------------
+    @staticmethod
+    def auto_schedule(total: int, max_live: int, world: int):
+        """(schedule, reason) from the live-parameter budget and the world size.
+
+        * budget < model: ``release`` (the only schedule that bounds live weights).
+        * world <= 3 with room for two copies: ``pipelined``.  At 2 GPUs each rank receives
+          half the model per step over ONE xGMI link (~6.75 GB for Llama-2-7B, about a step of
+          compute), so only a full step of lookahead hides it.
+        * otherwise ``keep``: from 4 GPUs each rank's (N-1)/N share arrives over N-1 links, in
+          well under the backward that precedes its use; one gathered copy (plus double buffers
+          for the first ``LUMEN_ZERO3_LEAD`` units) instead of two."""
+        if total > max_live:
+            return "release", f"model {total:.3g} elements > live budget {max_live:.3g}"
+        if world <= 3 and 2 * total <= max_live:
+            return "pipelined", (f"world {world} <= 3: gathers cross <= 2 xGMI links, a full "
+                                 "step of lookahead hides them (budget fits 2 copies)")
+        return "keep", (f"world {world}: gathers spread over {max(world - 1, 1)} xGMI links fit "
+                        "inside the backward; one gathered copy")
+
     def _hbm_live_budget(self, elem_bytes: int) -> int:
         """``stage3_max_live_parameters: "auto"``: elements of gathered weights that fit in the
         free HBM left after the shards, minus an activation reserve (max(48 GiB, 25% of the
@@ -281,6 +313,7 @@ class ParamCoordinator:
     def stats(self) -> Dict:
         return dict(schedule=self.schedule, world=self.world, units=len(self.units),
                     total_numel=self.total_numel, max_live=self.max_live, depth=self.depth,
+                    lead_units=len(self.lead), reason=self.schedule_reason,
                     pool_size=self.pool_size, turn_keep=self.turn_keep,
                     pool_overflows=self.pool_overflows, separate_group=self.group is not None,
                     offload=self.offload)
@@ -325,13 +358,17 @@ class ParamCoordinator:
         return k, st[:shard.numel()]
 
     # ---- gather / bind / release ------------------------------------------------------------
-    def _issue(self, i: int, slot: Optional[int] = None):
+    def _issue(self, i: int, nxt: bool = False):
+        """Gather unit i into its current slot, or (``nxt``, lead units) into the other one
+        for the next micro-step."""
         if self.identity or i < 0 or i > self.last:
             return
-        slot = self.slot if slot is None else slot
         u = self.units[i]
         for d in u.deps:
-            self._issue(d, slot)
+            self._issue(d, nxt and d in self.lead)
+        if nxt and i not in self.lead:
+            return
+        slot = 1 - u.slot if nxt else u.slot
         if not u.params or u.states[slot] != "empty":
             return
         buf = self._buffer(u, slot)
@@ -475,9 +512,9 @@ class ParamCoordinator:
             self._wait(d)
         if not u.params:
             return
-        s = self.slot
+        s = u.slot
         if u.states[s] == "empty":
-            self._issue(i, s)
+            self._issue(i)
         if u.states[s] == "inflight":
             self._wait_work(u.works[s])
             u.works[s] = None
@@ -511,7 +548,7 @@ class ParamCoordinator:
         u = self.units[i]
         if not u.params:
             return
-        s = self.slot
+        s = u.slot
         if u.states[s] == "inflight":
             u.works[s].wait()
             u.works[s] = None
@@ -526,7 +563,7 @@ class ParamCoordinator:
         if i < 0 or i > self.last:
             return
         u = self.units[i]
-        if not u.params or u.states[self.slot] != "empty":
+        if not u.params or u.states[u.slot] != "empty":
             return
         if self.schedule == "release" and not self._pool_free(u.dtype):
             return
@@ -535,10 +572,10 @@ class ParamCoordinator:
     def _refresh(self, i: int):
         """keep: unit i is done for this micro-step -> re-gather it for the next one into the
         same buffer (issued after the compute that read it)."""
-        if i < 1 or i > self.last:
-            return
+        if i < 1 or i > self.last or i in self.lead:
+            return  # lead units: the next micro-step's copy is already in the other slot
         u = self.units[i]
-        if not u.params or u.states[self.slot] != "ready":
+        if not u.params or u.states[u.slot] != "ready":
             return
         self._release(i)
         self._issue(i)
@@ -551,12 +588,13 @@ class ParamCoordinator:
             return
         if self.schedule == "pipelined":
             for i in range(self.last + 1):
-                self._issue(i, self.slot)
-            for i in range(self.last + 1):
-                self._issue(i, 1 - self.slot)  # next micro-step, behind this one's
+                self._issue(i)
         else:
             for i in range(min(self.depth, self.last + 1)):
                 self._prefetch(i)
+        for i in sorted(self.lead):
+            self._issue(i)             # (no-op when already in flight / ready)
+            self._issue(i, nxt=True)   # next micro-step, behind this one's
 
     def pre_forward(self, i: int):
         if i == 0 and not self._in_step:
@@ -616,17 +654,20 @@ class ParamCoordinator:
         self._in_step = False
         if self.identity:
             return
-        if self.schedule == "keep":
-            for i in range(self.last + 1):  # units without a backward, then unit 1
-                u = self.units[i]
-                if u.params and u.states[self.slot] == "ready":
-                    self._release(i)
+        if self.keep:
+            for i, u in enumerate(self.units):
+                if i in self.lead:
+                    # switch to the copy gathered for this next micro-step; this one's slot is
+                    # re-gathered (for micro-step t+2) at t+1's start
+                    self._unbind(u)
+                    if u.states[u.slot] == "inflight":
+                        u.works[u.slot].wait()
+                        u.works[u.slot] = None
+                    u.states[u.slot] = "empty"
+                    u.slot = 1 - u.slot
+                elif u.params and u.states[u.slot] == "ready":
+                    self._release(i)  # keep: units without a backward (head / norm)
                     self._issue(i)
-        elif self.schedule == "pipelined":
-            for u in self.units:
-                self._unbind(u)
-                u.states[self.slot] = "empty"   # re-gathered (for micro-step t+2) at t+1's start
-            self.slot = 1 - self.slot
         else:
             for i in range(self.last + 1):
                 self._release(i)

@@ -93,6 +93,9 @@ class ZeroEngine:
                 group=self.gather_group, max_reuse_distance=cfg.stage3_max_reuse_distance,
                 force_partition=single)
             model.coordinator = self.coordinator
+            if env.is_main:
+                c = self.coordinator
+                print(f"[lumen] ZeRO-3 schedule '{c.schedule}': {c.schedule_reason}", flush=True)
         if self.device.type == "cuda":
             from ..models.layers import configure_backward_layout
 

@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU suite, default bench (now with the serving half), then TunableOp tuning of the fp16
+# training shapes (reference precision) merged into a copy of the shipped table
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3b_tune}; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1
+rc=$?; grep -E "FAILED|ERROR" $O/gpu_tests.txt | head -20; tail -1 $O/gpu_tests.txt
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench.json'));print('bench', d['ms_per_step'], d['value']);print('serve', d['extra']['serve'])"
+cp configs/tunableop/mi355x_gemms.csv $O/table.csv
+for mb in 8 1; do
+  timeout -k 10 600 python bench.py --dtype fp16 --micro_batch $mb --steps 2 --warmup 2 --no_serve --tune_gemms $O/table.csv > $O/tune_fp16_mb$mb.log 2>&1 || { tail -20 $O/tune_fp16_mb$mb.log; exit 1; }
+  echo "tuned fp16 mb=$mb: $(grep -c Half $O/table.csv) Half entries"
+done
+for dt in bf16 fp16; do
+  LUMEN_ZERO3_SINGLE=1 LUMEN_ZERO3_SCHEDULE=keep timeout -k 10 600 python bench.py --dtype $dt --steps 2 --warmup 2 --no_serve --tune_gemms $O/table.csv > $O/tune_keep_$dt.log 2>&1 || { tail -20 $O/tune_keep_$dt.log; exit 1; }
+  echo "tuned keep $dt: $(grep -c _NN $O/table.csv) NN entries"
+done
+for dt in bf16 fp16; do
+  LUMEN_GEMM_TABLE=$O/table.csv timeout -k 10 300 python bench.py --dtype $dt --steps 10 --warmup 3 --no_serve > $O/bench_$dt.json 2> $O/bench_$dt.err || exit 1
+  python -c "import json;d=json.load(open('$O/bench_$dt.json'));print('$dt identity', d['ms_per_step'], d['value'], 'skipped', d['extra']['timed_steps_skipped_nonfinite'])"
+done
+LUMEN_GEMM_TABLE=$O/table.csv timeout -k 10 300 python bench.py --config configs/ds_config_zero2.json --micro_batch 1 --steps 20 --warmup 5 --no_serve > $O/bench_zero2_bs1_fp16.json 2> $O/z2.err || exit 1
+python -c "import json;d=json.load(open('$O/bench_zero2_bs1_fp16.json'));print('zero2 fp16 bs1', d['ms_per_step'], 'samples/s', d['extra']['samples_per_second'], d['dtype'])"
