@@ -79,8 +79,11 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--save_strategy", default=v["save"], choices=["steps", "epoch", "no"])
     ap.add_argument("--warmup_steps", type=int, default=0)
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--gradient_checkpointing", default="auto", choices=["auto", "true", "false"],
+                    help="per-layer recompute (the reference always enables it).  auto: on only "
+                         "when the estimated activations do not fit in free HBM (logged)")
     ap.add_argument("--no_gradient_checkpointing", action="store_true",
-                    help="disable per-layer recompute (288 GB HBM rarely needs it)")
+                    help="same as --gradient_checkpointing false")
     ap.add_argument("--metrics_csv", default="results/training_metrics.csv")
     return ap
 
@@ -135,7 +138,8 @@ def main(variant: str, argv=None) -> dict:
         max_length=args.max_length, seed=args.seed, logging_steps=args.logging_steps,
         save_strategy=args.save_strategy, save_steps=args.save_steps,
         save_total_limit=args.save_total_limit,
-        gradient_checkpointing=not args.no_gradient_checkpointing,
+        gradient_checkpointing=("false" if args.no_gradient_checkpointing
+                                else args.gradient_checkpointing),
         resume_from_checkpoint=args.resume_from_checkpoint, max_steps=args.max_steps,
         warmup_steps=args.warmup_steps, synthetic=args.synthetic,
         synthetic_samples=args.synthetic_samples, init=args.init, experiment=experiment,

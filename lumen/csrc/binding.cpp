@@ -944,6 +944,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("car_signal_bytes", &lumen_car_signal_bytes);
   m.def("car_max_blocks", &lumen_car_max_blocks);
   m.def("car_max_ranks", &lumen_car_max_ranks);
-  m.def("cpu_adamw", &cpu_adamw);
+  // the GIL is released: the async ZeRO-Offload step runs this on a host thread while the
+  // main thread keeps launching the next forward
+  m.def("cpu_adamw", &cpu_adamw, py::call_guard<py::gil_scoped_release>());
   m.def("cpu_has_avx512", &lumen_cpu_has_avx512);
 }

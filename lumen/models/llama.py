@@ -134,6 +134,7 @@ class LlamaForCausalLM(nn.Module):
         self.norm = RMSNorm(H, cfg.rms_norm_eps, dtype, device)
         self.lm_head = Linear(H, V, dtype=dtype, device=device, seg_names=["lm_head"])
         self.gradient_checkpointing = False
+        self.unit_gate = None    # engine hook run before each unit (async optimizer offload)
         self.coordinator = None  # ZeRO-3 parameter coordinator (lumen.parallel.zero)
 
     # --- ZeRO-3 units, in execution order ------------------------------------------------------
@@ -152,6 +153,9 @@ class LlamaForCausalLM(nn.Module):
         init_normal_(self, std, seed)
 
     def _run_unit(self, idx, fn, *args):
+        g = self.unit_gate
+        if g is not None:  # async ZeRO-Offload step: this unit's adapters must have landed
+            g(idx)
         c = self.coordinator
         if c is None:
             return fn(*args)

@@ -83,6 +83,7 @@ class OPTForCausalLM(nn.Module):
         for p in self.parameters():
             p.requires_grad_(False)
         self.gradient_checkpointing = False
+        self.unit_gate = None    # engine hook run before each unit (async optimizer offload)
         self.coordinator = None
 
     def zero_units(self) -> List[List[nn.Module]]:
@@ -98,6 +99,9 @@ class OPTForCausalLM(nn.Module):
         init_normal_(self, std, seed)
 
     def _run_unit(self, idx, fn, *args):
+        g = self.unit_gate
+        if g is not None:  # async ZeRO-Offload step: this unit's adapters must have landed
+            g(idx)
         c = self.coordinator
         if c is None:
             return fn(*args)

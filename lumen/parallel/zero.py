@@ -227,6 +227,21 @@ class ShardAdamW:
             return self._host_skipped + int(self.state[1].item())
         return self._host_skipped
 
+    def host_coef(self, norm_sq: torch.Tensor, inv_scale: float, max_norm: float):
+        """Host-path step preamble (reads the norm: syncs): (grad coefficient, bc1, bc2) with
+        clipping folded in and the step counted, or None for a non-finite norm (skipped)."""
+        nsq = float(norm_sq.item())
+        if not math.isfinite(nsq):
+            self._host_skipped += 1
+            return None
+        coef = inv_scale
+        gn = math.sqrt(nsq) * inv_scale
+        if max_norm > 0 and gn > max_norm:
+            coef *= max_norm / (gn + 1e-6)
+        self._host_step += 1
+        t = self._host_step
+        return coef, 1 - self.b1 ** t, 1 - self.b2 ** t
+
     def step(self, grad: torch.Tensor, lr: float, inv_scale: float,
              norm_sq: Optional[torch.Tensor], max_norm: float) -> None:
         if self.state is not None and use_native(self.master):
@@ -281,6 +296,153 @@ class ShardAdamW:
             self.state[1] = 0.0
         else:
             self._host_step = int(d["step"])
+
+
+class AsyncOffloadStep:
+    """ZeRO-Offload optimizer step overlapped with the next forward (exact semantics: no stale
+    parameters; reference ``offload_optimizer: cpu``, configs/ds_config_zero3.json:19-22).
+
+    The step is cut into ``n_chunks`` slices of the flat shard, processed in FORWARD order (the
+    flat buffer is laid out backward-first, so from its end):
+
+    * copy stream: D2H of every gradient slice into pinned host memory (event per slice), then
+      the gradient buffer is zeroed there -- the compute stream only waits for that before its
+      next backward;
+    * host thread: per slice, wait for its D2H, C++ AVX-512 AdamW (GIL released), H2D of the
+      updated master slice into the device parameters (event per slice);
+    * the model calls ``gate(unit)`` before each unit's forward: the host waits until the
+      slices holding that unit's adapters are updated and the compute stream waits on their
+      H2D events.  Layer 1's adapters are ready after 1/n of the CPU step; the rest of the CPU
+      work runs under the forward of the layers before it.
+
+    Sharded ranks (world > 1) update their shard the same way into a device staging shard; the
+    first gate of the step joins the host thread and issues the publish all-gathers from the
+    main thread (collectives stay on one thread, in program order on every rank)."""
+
+    def __init__(self, opt: "ShardAdamW", flat: "FlatTrainable", device: torch.device,
+                 sharded: bool, n_chunks: int = 16):
+        import threading
+
+        self.opt, self.flat, self.device, self.sharded = opt, flat, device, sharded
+        n = opt.master.numel()
+        k = max(1, min(n_chunks, n // 4096))
+        step = _round_up((n + k - 1) // k, ALIGN)
+        bounds = [(a, min(a + step, n)) for a in range(0, n, step)]
+        self.chunks = bounds[::-1]          # forward order: the flat layout is backward-first
+        self.stream = torch.cuda.Stream(device=device)
+        self.g_host = torch.empty(n, dtype=torch.float32).pin_memory()
+        self.dst_shard = torch.empty(n, dtype=torch.float32, device=device) if sharded else None
+        self._thread: Optional[threading.Thread] = None
+        self._done = [threading.Event() for _ in self.chunks]
+        self._h2d: List[Optional[torch.cuda.Event]] = [None] * len(self.chunks)
+        self._grad_free: Optional[torch.cuda.Event] = None
+        self._err: Optional[BaseException] = None
+        self.pending = False
+        self.unit_chunks: Dict[int, List[int]] = {}
+
+    def map_units(self, model: nn.Module) -> None:
+        """unit index -> chunks holding its trainable parameters (world-1 flat offsets)."""
+        if self.sharded or not hasattr(model, "zero_units"):
+            return
+        for i, mods in enumerate(model.zero_units()):
+            ks = set()
+            for m in mods:
+                for p in m.parameters():
+                    if not p.requires_grad or id(p) not in self.flat.index:
+                        continue
+                    _, o, n = self.flat.index[id(p)]
+                    ks.update(j for j, (a, b) in enumerate(self.chunks) if a < o + n and o < b)
+            self.unit_chunks[i] = sorted(ks)
+
+    def launch(self, grad: torch.Tensor, lr: float, coef: float, bc1: float, bc2: float) -> None:
+        """Start the step for an already-reduced gradient (``grad`` = the flat gradient at world
+        1, the reduced shard otherwise).  Returns at once."""
+        import threading
+
+        self.join()
+        o = self.opt
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        d2h = []
+        with torch.cuda.stream(self.stream):
+            for a, b in self.chunks:
+                self.g_host[a:b].copy_(grad[a:b], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+                d2h.append(ev)
+            grad.zero_()
+            self._grad_free = torch.cuda.Event()
+            self._grad_free.record(self.stream)
+        for e in self._done:
+            e.clear()
+        self._h2d = [None] * len(self.chunks)
+        self._err = None
+        dst = self.dst_shard if self.sharded else self.flat.param
+        C = native()
+
+        def work():
+            try:
+                torch.cuda.set_device(self.device)
+                for j, (a, b) in enumerate(self.chunks):
+                    d2h[j].synchronize()
+                    C.cpu_adamw(o.master[a:b], self.g_host[a:b], o.m[a:b], o.v[a:b], lr, o.b1,
+                                o.b2, o.eps, o.wd, bc1, bc2, coef)
+                    with torch.cuda.stream(self.stream):
+                        dst[a:b].copy_(o.master[a:b], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(self.stream)
+                    self._h2d[j] = ev
+                    self._done[j].set()
+            except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
+                self._err = e
+                for ev in self._done:
+                    ev.set()
+
+        self.pending = True
+        self._thread = threading.Thread(target=work, name="lumen-offload-adam", daemon=True)
+        self._thread.start()
+
+    def _check(self):
+        if self._err is not None:
+            err, self._err = self._err, None
+            raise RuntimeError("async offloaded AdamW step failed") from err
+
+    def gate(self, unit: int) -> None:
+        if not self.pending:
+            return
+        if self.sharded or unit not in self.unit_chunks:
+            self.finish()
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for j in self.unit_chunks[unit]:
+            self._done[j].wait()
+            self._check()
+            cur.wait_event(self._h2d[j])
+
+    def finish(self) -> None:
+        """Everything of the pending step is on the device (and published when sharded)."""
+        if not self.pending:
+            return
+        self.join()
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(self.stream)
+        if self.sharded:
+            for b in self.flat.buckets:
+                dist.all_gather_into_tensor(self.flat.param[b.off:b.off + b.size],
+                                            self.flat.shard_view(self.dst_shard, b))
+        self.pending = False
+
+    def join(self) -> None:
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        self._check()
+
+    def before_backward(self) -> None:
+        """The next backward accumulates into the gradient buffer: after its zeroing."""
+        if self._grad_free is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._grad_free)
+            self._grad_free = None
 
 
 def _adamw_torch(p, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, coef):

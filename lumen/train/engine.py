@@ -23,8 +23,8 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..parallel.dist import DistEnv
-from ..parallel.zero import (DynamicLossScaler, FlatTrainable, ParamCoordinator, ShardAdamW,
-                             grad_norm_sq)
+from ..parallel.zero import (AsyncOffloadStep, DynamicLossScaler, FlatTrainable,
+                             ParamCoordinator, ShardAdamW, grad_norm_sq)
 from .config import DSConfig, warmup_lr
 
 
@@ -139,6 +139,16 @@ class ZeroEngine:
             cfg.warmup_type == "linear", W, self.scaler,
             cfg.decay_total_steps if cfg.lr_schedule == "hf_linear" else 0)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+        # ZeRO-Offload optimizer: the CPU step overlaps the next forward (exact semantics)
+        self.async_off: Optional[AsyncOffloadStep] = None
+        if (self.opt.offload and self.device.type == "cuda" and not self.device_sched
+                and os.environ.get("LUMEN_OFFLOAD_ASYNC", "1") != "0"):
+            from ..ops._native import native
+
+            if native() is not None:
+                self.async_off = AsyncOffloadStep(self.opt, self.flat, self.device, self.sharded)
+                self.async_off.map_units(model)
+                model.unit_gate = self.async_off.gate
         self._gscale = torch.ones(1, dtype=torch.float32, device=self.device)
         self._works: List = []
         for prm in trainable:  # .grad is a view of flat.grad: kernels may accumulate into it
@@ -223,6 +233,8 @@ class ZeroEngine:
 
     def backward(self, loss: torch.Tensor):
         self.timers.start("bwd")
+        if self.async_off is not None:
+            self.async_off.before_backward()
         if self.device_sched and self.scaler is not None:
             # fp16: scale by the device loss scale / accum (no host read of it); the same tensor
             # the forward handed the CE kernel as its gradient-scale hint
@@ -286,12 +298,24 @@ class ZeroEngine:
                 nsq = float(self._norm_buf.item())
                 overflow = not math.isfinite(nsq)
                 self.scaler.update(overflow)
+            launched = None
             if overflow:
                 self._scaler_skipped += 1
+            elif self.async_off is not None:
+                hp = self.opt.host_coef(self._norm_buf, inv_scale, self.cfg.gradient_clipping)
+                if hp is not None:  # None: non-finite norm, counted as skipped
+                    self.async_off.launch(grad, lr, *hp)
+                    launched = grad  # zeroed by the offload stream after its D2H
             else:
                 self.opt.step(grad, lr, inv_scale, self._norm_buf, self.cfg.gradient_clipping)
                 self._publish_params()
             self.last_grad_norm = self._norm_buf.sqrt() * inv_scale
+            if launched is not None:
+                if launched is not self.flat.grad:
+                    self.flat.grad.zero_()
+                self.global_step += 1
+                self.timers.stop("step")
+                return True
         self.flat.grad.zero_()
         if self.grad_shard is not None:
             self.grad_shard.zero_()
@@ -325,15 +349,23 @@ class ZeroEngine:
         bf16 NaN/Inf steps the fused AdamW kernel skipped on the device (reading that syncs)."""
         return self._scaler_skipped + self.opt.skipped
 
+    def sync_params(self) -> None:
+        """Finish a pending asynchronous (offloaded) optimizer step: params current."""
+        if self.async_off is not None:
+            self.async_off.finish()
+
     def close(self):
         """Complete in-flight ZeRO-3 gathers (the pipelined schedule keeps the next micro-step's
         in flight) so the process groups can be torn down cleanly."""
+        self.sync_params()
         if self.coordinator is not None:
             self.coordinator.drain()
 
     # ---- checkpoint state ----------------------------------------------------------------------
     def state_dict(self) -> Dict:
         from .reshard import engine_layout
+
+        self.sync_params()
 
         return dict(optimizer=self.opt.state_dict(), global_step=self.global_step,
                     micro_step=self.micro_step, skipped_steps=self.skipped_steps,
@@ -342,6 +374,7 @@ class ZeroEngine:
                     shard_numel=self.opt.master.numel(), layout=engine_layout(self))
 
     def load_state_dict(self, d: Dict):
+        self.sync_params()
         if d["shard_numel"] != self.opt.master.numel():
             raise ValueError("checkpoint shard layout does not match (world size / stage changed): "
                              "load it through lumen.train.reshard.load_engine_state")
