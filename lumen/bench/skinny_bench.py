@@ -48,51 +48,9 @@ def m1_forms():
                 row[f"form{form}_us"] = _time(lambda w: native().skinny_gemm(x, w, y), ws)
                 row[f"form{form}_TBps"] = round(N * K * 2 / (row[f"form{form}_us"] * 1e-6) / 1e12, 2)
             row["hipblaslt_us"] = _time(lambda w: torch.matmul(x, w.t()), ws)
-            if name == "down" and M == 1:
-                gu = torch.randn(1, 2 * K, device=dev).to(torch.bfloat16)
-                for form in (0, 1):
-                    native().set_gemv_form(form)
-                    row[f"swiglu_fused_form{form}_us"] = _time(
-                        lambda w: native().gemv_swiglu(gu, w, y), ws)
-                    row[f"swiglu_then_gemv_form{form}_us"] = _time(
-                        lambda w: native().skinny_gemm(swiglu(gu), w, y), ws)
             native().set_gemv_form(1)
             print(json.dumps(row), flush=True)
             del ws
-
-
-def dgemm_sweep():
-    """Decode-batch MFMA GEMM (kernels/decode_gemm.hip) vs hipBLASLt (tuned table) per M."""
-    import torch
-
-    from lumen.ops import gemm as G
-    from lumen.utils.gemm_tuning import load_tuned_gemms
-
-    load_tuned_gemms()
-    dev = "cuda"
-    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096),
-              "down": (4096, 11008), "lm_head": (32000, 4096)}
-    Ms = (2, 4, 8, 16, 32, 64, 128, 256)
-    if "--splits" in sys.argv:
-        Ms = (2, 8, 16, 32)
-    for M in Ms:
-        row = {"M": M}
-        for name, (N, K) in shapes.items():
-            copies = max(2, int(600e6 // (N * K * 2)))
-            ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
-            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
-            if "--splits" in sys.argv:
-                row[name] = {f"s{sp}": _time(lambda w: G.dgemm(x, w, splits=sp), ws)
-                             for sp in (1, 2, 4, 8, 16)}
-                row[name]["hipblaslt"] = _time(lambda w: torch.matmul(x, w.t()), ws)
-                del ws
-                continue
-            dg = _time(lambda w: G.dgemm(x, w), ws)
-            bl = _time(lambda w: torch.matmul(x, w.t()), ws)
-            row[name] = {"dgemm": dg, "hipblaslt": bl, "splits": G.dgemm_plan(M, N, K)[0],
-                         "dgemm_TBps": round(N * K * 2 / (dg * 1e-6) / 1e12, 2)}
-            del ws
-        print(json.dumps(row), flush=True)
 
 
 def main():
@@ -100,8 +58,6 @@ def main():
 
     if "--m1-forms" in sys.argv:
         return m1_forms()
-    if "--dgemm" in sys.argv:
-        return dgemm_sweep()
 
     from lumen.ops._native import native
     from lumen.utils.gemm_tuning import load_tuned_gemms

@@ -57,21 +57,14 @@ hipError_t lumen_lora3_up(int, int, void*, long long, const float*, long long, c
                           int, hipStream_t);
 hipError_t lumen_lora3_dy(int, const void*, long long, const float*, int, const float*, long long,
                           float*, long long, float*, int, int, float, int, const long long*,
-                          const long long*, const long long*, const int*, float*, long long,
-                          float*, long long, hipStream_t);
-hipError_t lumen_lora3_dy_reduce(const float*, int, long long, float*, long long, const float*, int,
-                                 long long, float*, long long, hipStream_t);
+                          const long long*, const long long*, const int*, hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, const float*, void*,
                             void*, const long long*, int, int, int, int, int, int, hipStream_t);
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
-hipError_t lumen_gemv_swiglu(int, const void*, const void*, void*, int, int, long long, long long,
-                             hipStream_t);
 void lumen_set_gemv_form(int);
 void lumen_set_rms_lds(int, int);
-hipError_t lumen_dgemm(int, const void*, const void*, void*, int, int, int, long long, long long, int,
-                       float*, unsigned*, hipStream_t);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
                                         float, float*, float*, void*, int, unsigned*, int, int,
@@ -214,47 +207,6 @@ void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
                           static_cast<int>(x.size(0)), static_cast<int>(w.size(0)),
                           static_cast<int>(w.size(1)), x.stride(0), y.stride(0), cur_stream()),
         "skinny_gemm");
-}
-
-// y[M, N] = x[M, K] @ w[N, K]^T on the matrix cores for decode batches (kernels/decode_gemm.hip)
-void dgemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, int64_t splits,
-           const std::optional<at::Tensor>& ws, const std::optional<at::Tensor>& cnt) {
-  if (!x.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: dgemm needs GPU tensors");
-  need_cuda(w, "w");
-  if (x.dim() != 2 || w.dim() != 2 || y.dim() != 2 || x.stride(1) != 1 || y.stride(1) != 1 ||
-      x.size(1) != w.size(1) || y.size(0) != x.size(0) || y.size(1) != w.size(0) ||
-      x.stride(0) % 8 != 0 || y.stride(0) % 4 != 0 || x.scalar_type() != w.scalar_type() ||
-      y.scalar_type() != w.scalar_type())
-    throw std::invalid_argument("lumen: dgemm shape/layout mismatch");
-  float* wsp = nullptr;
-  unsigned* cp = nullptr;
-  if (splits > 1) {
-    if (!ws.has_value() || !cnt.has_value() || ws->scalar_type() != at::kFloat ||
-        cnt->scalar_type() != at::kInt)
-      throw std::invalid_argument("lumen: dgemm split-K needs f32 workspace and int32 counters");
-    wsp = ws->data_ptr<float>();
-    cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
-  }
-  check(lumen_dgemm(dcode(w), x.data_ptr(), w.data_ptr(), y.data_ptr(), static_cast<int>(x.size(0)),
-                    static_cast<int>(w.size(0)), static_cast<int>(w.size(1)), x.stride(0),
-                    y.stride(0), static_cast<int>(splits), wsp, cp, cur_stream()),
-        "dgemm");
-}
-
-// y[1, N] = swiglu(gu[1, 2F]) @ w[N, F]^T with the activation formed inside the weight stream
-void gemv_swiglu(const at::Tensor& gu, const at::Tensor& w, at::Tensor& y) {
-  if (!gu.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: gemv_swiglu needs GPU tensors");
-  need_cuda(w, "w");
-  if (gu.dim() != 2 || w.dim() != 2 || y.dim() != 2 || gu.size(0) != 1 || y.size(0) != 1 ||
-      gu.stride(1) != 1 || y.stride(1) != 1 || !w.is_contiguous() ||
-      gu.size(1) != 2 * w.size(1) || y.size(1) != w.size(0) || w.size(0) % 4 != 0 ||
-      w.size(1) % 8 != 0 || gu.scalar_type() != w.scalar_type() ||
-      y.scalar_type() != w.scalar_type())
-    throw std::invalid_argument("lumen: gemv_swiglu shape/layout mismatch");
-  check(lumen_gemv_swiglu(dcode(w), gu.data_ptr(), w.data_ptr(), y.data_ptr(),
-                          static_cast<int>(w.size(0)), static_cast<int>(w.size(1)), gu.stride(0),
-                          y.stride(0), cur_stream()),
-        "gemv_swiglu");
 }
 
 void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
@@ -438,26 +390,8 @@ void lora3_up(int64_t fwd, at::Tensor& out, int64_t ldo, const at::Tensor& s1, i
 // segs: (n_off, r_off, b_off, n_len)
 void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r, const at::Tensor& Z,
               int64_t ldz, at::Tensor& dZ, int64_t lddz, at::Tensor& dB, int64_t T, int64_t tw,
-              double alpha, const std::vector<std::vector<int64_t>>& segs,
-              const c10::optional<at::Tensor>& pz, const c10::optional<at::Tensor>& pb) {
+              double alpha, const std::vector<std::vector<int64_t>>& segs) {
   if (!dy.is_cuda()) throw std::invalid_argument("lumen: lora3_dy needs GPU tensors");
-  float* pzp = nullptr;
-  float* pbp = nullptr;
-  long long pzs = 0, pbs = 0;
-  if (pz && pz->defined()) {
-    // partial mode: pz [column blocks, T, ldz], pb [row blocks, dB rows, r] f32 (see kernel)
-    if (!pb || !pb->defined()) throw std::invalid_argument("lumen: lora3_dy partial mode needs pz and pb");
-    need_cuda_f32(*pz, "lora3_dy pz");
-    need_cuda_f32(*pb, "lora3_dy pb");
-    if (!pz->is_contiguous() || !pb->is_contiguous() || pz->dim() != 3 || pb->dim() != 3 ||
-        pz->size(1) < T || pz->size(2) != lddz || pb->size(1) < dB.size(0) || pb->size(2) != r ||
-        tw <= 0 || pb->size(0) < (T + tw - 1) / tw)
-      throw std::invalid_argument("lumen: lora3_dy partial buffers: pz [gx, T, ldz], pb [gy, NB, r]");
-    pzp = pz->data_ptr<float>();
-    pbp = pb->data_ptr<float>();
-    pzs = pz->stride(0);
-    pbs = pb->stride(0);
-  }
   need_cuda_f32(B, "lora3_dy B");
   need_cuda_f32(Z, "lora3_dy Z");
   need_cuda_f32(dZ, "lora3_dy dZ");
@@ -470,34 +404,11 @@ void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r,
     if (segs[i].size() != 4) throw std::invalid_argument("lumen: lora3_dy segment = (n_off, r_off, b_off, n_len)");
     no[i] = segs[i][0]; ro[i] = segs[i][1]; bo[i] = segs[i][2]; nl[i] = static_cast<int>(segs[i][3]);
   }
-  if (pzp != nullptr) {
-    // every dZ slot of every segment must be written: equal segment widths, gx column blocks
-    const int gx = (nl[0] + 255) / 256;
-    for (int i = 1; i < nseg; ++i)
-      if (nl[i] != nl[0]) throw std::invalid_argument("lumen: lora3_dy partial mode needs equal segment widths");
-    if (pz->size(0) != gx) throw std::invalid_argument("lumen: lora3_dy pz needs ceil(n_len / 256) slots");
-  }
   check(lumen_lora3_dy(dcode(dy), dy.data_ptr(), ldy, B.data_ptr<float>(), static_cast<int>(r),
                        Z.data_ptr<float>(), ldz, dZ.data_ptr<float>(), lddz, dB.data_ptr<float>(),
                        static_cast<int>(T), static_cast<int>(tw), static_cast<float>(alpha), nseg,
-                       no, ro, bo, nl, pzp, pzs, pbp, pbs, cur_stream()),
+                       no, ro, bo, nl, cur_stream()),
         "lora3_dy");
-}
-
-void lora3_dy_reduce(const at::Tensor& pz, at::Tensor& dZ, const at::Tensor& pb, at::Tensor& dB) {
-  need_cuda_f32(pz, "lora3_dy_reduce pz");
-  need_cuda_f32(pb, "lora3_dy_reduce pb");
-  need_cuda_f32(dZ, "lora3_dy_reduce dZ");
-  need_cuda_f32(dB, "lora3_dy_reduce dB");
-  if (!pz.is_contiguous() || !pb.is_contiguous() || !dZ.is_contiguous() || !dB.is_contiguous() ||
-      pz.dim() != 3 || pb.dim() != 3 || pz.size(1) * pz.size(2) != dZ.numel() ||
-      pb.size(1) * pb.size(2) != dB.numel())
-    throw std::invalid_argument("lumen: lora3_dy_reduce: pz [S, T, R] -> dZ [T, R], pb [S, NB, r] -> dB [NB, r]");
-  check(lumen_lora3_dy_reduce(pz.data_ptr<float>(), static_cast<int>(pz.size(0)), pz.stride(0),
-                              dZ.data_ptr<float>(), dZ.numel(), pb.data_ptr<float>(),
-                              static_cast<int>(pb.size(0)), pb.stride(0), dB.data_ptr<float>(),
-                              dB.numel(), cur_stream()),
-        "lora3_dy_reduce");
 }
 
 // out[t, :] = W[ids[t], :]  (16-bit table, int64 ids; out of range ids -> zero rows)
@@ -895,9 +806,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding", &embedding);
   m.def("lora3_dy", &lora3_dy, py::arg("dy"), py::arg("ldy"), py::arg("B"), py::arg("r"),
         py::arg("Z"), py::arg("ldz"), py::arg("dZ"), py::arg("lddz"), py::arg("dB"), py::arg("T"),
-        py::arg("tw"), py::arg("alpha"), py::arg("segs"), py::arg("pz") = py::none(),
-        py::arg("pb") = py::none());
-  m.def("lora3_dy_reduce", &lora3_dy_reduce);
+        py::arg("tw"), py::arg("alpha"), py::arg("segs"));
   m.def("lora3_dxa", &lora3_dxa, py::arg("x"), py::arg("dx"), py::arg("dZ"), py::arg("A"),
         py::arg("dA"), py::arg("tw"), py::arg("seed"), py::arg("thresh"), py::arg("drop_scale"),
         py::arg("drop_ld"), py::arg("drop_col0"), py::arg("delta") = py::none());
@@ -916,8 +825,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora2", &lora2);
   m.def("transpose2d", &transpose2d);
   m.def("skinny_gemm", &skinny_gemm);
-  m.def("gemv_swiglu", &gemv_swiglu);
-  m.def("dgemm", &dgemm);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
   m.def("set_rms_lds", [](int64_t f, int64_t b) {
     lumen_set_rms_lds(static_cast<int>(f), static_cast<int>(b));

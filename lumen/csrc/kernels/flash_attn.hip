@@ -1718,167 +1718,8 @@ __global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
   }
 }
 
-// ---- backward dK/dV, 8 waves x 16 keys = 128 keys per workgroup ----------------------------
-// Same per-wave math as bwd_dkdv_kernel (16x16x32 MFMA, K / V fragments in registers, S and dP
-// with the queries as MFMA rows so P^T / dS^T feed dV / dK from registers), restructured:
-//  * the Q / dO / lse / delta tile of a step is shared by 8 waves (128 keys) instead of 4, so
-//    the LDS-DMA bytes and staging instructions per MFMA halve;
-//  * a 3-deep ring of (Q | dO | lse | delta) stages in three separately declared LDS objects,
-//    DMA issued two steps ahead, ONE barrier per step (it both publishes stage j and frees the
-//    buffer step j-1 read, which is where stage j+2 goes);
-//  * causal: waves whose 16 keys lie entirely after the step's 64 queries skip the step's math.
-// LDS 3 x 32.5 KiB (one workgroup, 2 waves per SIMD, per CU).
-template <typename T, bool CAUSAL, bool WDS>
-__global__ void __launch_bounds__(512) bwd_dkdv8_kernel(Args a) {
-  constexpr int STAGE = 2 * IMG + 512;  // Q image | dO image | lse[64] | delta[64]
-  __shared__ __attribute__((aligned(16))) char buf0[STAGE];
-  __shared__ __attribute__((aligned(16))) char buf1[STAGE];
-  __shared__ __attribute__((aligned(16))) char buf2[STAGE];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int seq = a.tiles[2 * blockIdx.x], k0 = a.tiles[2 * blockIdx.x + 1];
-  const int kvh = blockIdx.y;
-  const int grp = a.nh / a.nkv;
-  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
-  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
-  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
-  const int wk0 = k0 + wid * 16;  // this wave's 16 keys
-  const int krow = wk0 + lr;      // the key of this lane's accumulator column
-  uint4 kf[4], vf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    kf[ks] = gload16(K + (long long)krow * a.ldk + (4 * ks + lg) * 8, krow < L);
-    vf[ks] = gload16(V + (long long)krow * a.ldv + (4 * ks + lg) * 8, krow < L);
-  }
-  const int ds_base = WDS ? a.ds_off[seq] : 0;
-  wait_vm_all();
-  f32x4 dk[8], dv[8];
-#pragma unroll
-  for (int n = 0; n < 8; ++n) { dk[n] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[n] = dk[n]; }
-  const int qstart = CAUSAL ? k0 : 0;
-  const int nq = qstart < L ? (L - qstart + 63) / 64 : 0;
-  const int nsteps = grp * nq;  // (group head, query tile) pairs
-  const int ns = (L + 63) / 64;
-  const int wkt = (k0 >> 6) + (wid >> 2);  // this wave's 64-key tile (dS hand-off)
-  // stage: Q / dO tiles = 2 + 2 DMA instructions per wave, lse / delta one more on waves 0 / 1
-  auto stage = [&](int j, char* st) {
-    const int hh = j / nq, q0 = qstart + (j % nq) * 64;
-    const int head = kvh * grp + hh;
-    stage64_async8_o<T, 1>(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D,
-                           a.ldq, q0, L);
-    stage64_async8_o<T, 1>(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo +
-                           head * D, a.lddo, q0, L);
-    if (wid < 2) {
-      const float* src = (wid == 0 ? a.lse : a.delta) + (long long)head * a.T + s0;
-      int qr = q0 + lane;
-      qr = qr < L ? qr : L - 1;
-      dma4_o(src + qr, st + 2 * IMG + wid * 256);
-    }
-  };
-  uint4 pend[2];
-  long long pend_off = -1;
-  auto store_pend = [&]() {
-    if (pend_off < 0) return;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      char* dst = reinterpret_cast<char*>(a.ds) + pend_off + ((wid & 3) * 2 + ks) * 1024 + ds_slot(lg, lr);
-      *reinterpret_cast<uint4*>(dst) = pend[ks];
-    }
-  };
-  auto step = [&](int j, char* st, char* nx2) {
-    // stage j is complete once only stage j+1's loads remain younger (loads retire in order;
-    // the dS stores of step j-1 are not counted, so an early-retiring store cannot satisfy it)
-    if (j + 1 < nsteps) {
-      if (wid < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      wait_vm_all();
-    }
-    lds_fence_barrier();  // stage j visible to all; every wave is past step j-1 (nx2's reader)
-    if (j + 2 < nsteps) stage(j + 2, nx2);
-    if constexpr (WDS) {
-      store_pend();
-      pend_off = -1;
-    }
-    const int q0 = qstart + (j % nq) * 64;
-    if (CAUSAL && wk0 > q0 + 63) return;  // wave-uniform: every key after every query
-    const char* qimg = st;
-    const char* oimg = st + IMG;
-    const float* s_lse = reinterpret_cast<const float*>(st + 2 * IMG);
-    const float* s_del = s_lse + 64;
-    f32x4 sc[4], dp[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) { sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[nt] = sc[nt]; }
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        sc[nt] = Mfma<T>::run(row_read<1>(qimg, nt * 16 + lr, 4 * ks + lg), kf[ks], sc[nt]);
-        dp[nt] = Mfma<T>::run(row_read<1>(oimg, nt * 16 + lr, 4 * ks + lg), vf[ks], dp[nt]);
-      }
-    }
-    const bool need_mask = (q0 + 64 > L) || (CAUSAL && wk0 + 15 > q0) || (wk0 + 16 > L);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const float4 l4 = *reinterpret_cast<const float4*>(s_lse + nt * 16 + 4 * lg);
-      const float4 d4 = *reinterpret_cast<const float4*>(s_del + nt * 16 + 4 * lg);
-      const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qc = nt * 16 + 4 * lg + r;
-        float pv = fexp2(sc[nt][r] * a.scale_log2 - lq[r]);
-        if (need_mask && (krow >= L || q0 + qc >= L || (CAUSAL && krow > q0 + qc))) pv = 0.f;
-        sc[nt][r] = pv;
-        dp[nt][r] = pv * (dp[nt][r] - dq4[r]);
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint4 pa = pack_p<T>(sc[2 * ks], sc[2 * ks + 1]);
-      const uint4 da = pack_p<T>(dp[2 * ks], dp[2 * ks + 1]);
-      if constexpr (WDS) pend[ks] = da;
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        dv[n] = Mfma<T>::run(pa, tr_read_img2<1>(oimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dv[n]);
-        dk[n] = Mfma<T>::run(da, tr_read_img2<1>(qimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dk[n]);
-      }
-    }
-    if constexpr (WDS) {
-      if (wkt < ns)  // this wave's 64-key tile exists (keys past L belong to no tile)
-        pend_off = ds_tile(a, kvh * grp + j / nq, ds_base, q0 / 64, wkt, ns, CAUSAL);
-    }
-  };
-  if (nsteps > 0) stage(0, buf0);
-  if (nsteps > 1) stage(1, buf1);
-  for (int j = 0; j < nsteps; j += 3) {
-    step(j, buf0, buf2);
-    if (j + 1 < nsteps) step(j + 1, buf1, buf0);
-    if (j + 2 < nsteps) step(j + 2, buf2, buf1);
-  }
-  if constexpr (WDS) store_pend();
-  // write dK (x softmax scale), dV : rows wk0 + 4lg + r, cols 16n + lr
-  T* dK = reinterpret_cast<T*>(a.dk) + (long long)s0 * a.lddk + kvh * D;
-  T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int kr = wk0 + 4 * lg + r;
-    if (kr >= L) continue;
-    float kv[8];
-#pragma unroll
-    for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
-    if (a.rope_pos != nullptr) {  // column 16n + lr pairs with 16(n + 4) + lr: same lane
-      const long long pb = (long long)a.rope_pos[s0 + kr] * 64 + lr;
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        rope_inv_pair(kv[n], kv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
-    }
-#pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      dK[(long long)kr * a.lddk + n * 16 + lr] = from_f32<T>(kv[n]);
-      dV[(long long)kr * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
-    }
-  }
-}
+// (An 8-wave, 128-key dK/dV variant with a 3-deep DMA ring measured slower than the 4-wave
+// kernel above -- 117.6 vs 108.0 us at B=8 S=512, gpurun r2_36 -- and was removed.)
 
 static int cu_count() {
   static int n = [] {
@@ -1946,15 +1787,6 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     if (a.nitems > 0) grid = dim3(std::min(a.nitems, 2 * cu_count()), 1);
     if (causal) hipLaunchKernelGGL((bwd_dkdv_kernel<T, true, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dkdv_kernel<T, false, true>), grid, block, 0, st, a);
-  } else if (which == 9 || which == 10) {  // dK/dV, 8 waves, 128-key tiles (10: + dS hand-off)
-    dim3 grid(ntiles, a.nkv), block8(512);
-    if (which == 10) {
-      if (causal) hipLaunchKernelGGL((bwd_dkdv8_kernel<T, true, true>), grid, block8, 0, st, a);
-      else hipLaunchKernelGGL((bwd_dkdv8_kernel<T, false, true>), grid, block8, 0, st, a);
-    } else {
-      if (causal) hipLaunchKernelGGL((bwd_dkdv8_kernel<T, true, false>), grid, block8, 0, st, a);
-      else hipLaunchKernelGGL((bwd_dkdv8_kernel<T, false, false>), grid, block8, 0, st, a);
-    }
   } else if (which == 8) {  // dQ from the dS hand-off (64-query tiles)
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
     if (a.nitems > 0) grid = dim3(std::min(a.nitems, 3 * cu_count()), 1);  // 48 KiB LDS: 3 / CU
@@ -2008,7 +1840,6 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   const int tiles3 = (which >> 8) & 1;  // 0x100: (seq, row, head) triples, 1-D grid
   which &= 0xff;
   if (tiles3 && which != 0 && which != 2 && which != 5) return hipErrorInvalidValue;
-  if (which == 9 && tiles3) return hipErrorInvalidValue;
   // the fused inverse RoPE exists in the dK/dV kernel (which 2) and the 32x32 dQ kernel (which 5)
   if (rope_pos != nullptr && which != 2 && which != 5) return hipErrorInvalidValue;
   if (which != 1 && ntiles == 0) return hipSuccess;
@@ -2067,8 +1898,8 @@ extern "C" hipError_t lumen_flash_attn_ds(int dtype, int which, int causal, cons
                                           const int* ds_off, int ds_total, hipStream_t st) {
   const int tiles3 = (which >> 8) & 1;
   which &= 0xff;
-  if (nkv <= 0 || nh % nkv != 0 || (which != 7 && which != 8 && which != 10) || ds == nullptr ||
-      ds_off == nullptr || (tiles3 && which == 10))
+  if (nkv <= 0 || nh % nkv != 0 || (which != 7 && which != 8) || ds == nullptr ||
+      ds_off == nullptr)
     return hipErrorInvalidValue;
   if (ntiles == 0) return hipSuccess;
   lumen::fa::Args a{};

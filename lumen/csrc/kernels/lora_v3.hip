@@ -387,12 +387,6 @@ struct DyArgs {
   float alpha;
   DySeg seg;
   int probe;  // cost probes (0 in production): 16 dZ atomics, 32 dB atomics only when v == 1234.5
-  // partial mode (pz != nullptr): instead of f32 atomics into dZ / dB, every workgroup stores
-  // its partial sums into its own slot -- dZ partials by column block (pz[blockIdx.x][t][ldz]),
-  // dB partials by row block (pb[blockIdx.y][b][r]) -- and dy_reduce_kernel sums the slots.
-  // (The atomics' memory-side rate cost ~10 us per call, profiles/r2_lora.)
-  float* pz; long long pz_slot;
-  float* pb; long long pb_slot;
 };
 
 constexpr int kDyCC = 2;
@@ -522,11 +516,7 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int t = t0 + wid * 16 + g * 4 + r;
-          if (a.pz) {
-            if (t < te)
-              a.pz[blockIdx.x * a.pz_slot + a.seg.r_off[seg] + (long long)t * a.lddz + jt * 16 + L] =
-                  a.alpha * dzacc[jt][r];
-          } else if (t < te && (!(a.probe & 16) || dzacc[jt][r] == 1234.5f))
+          if (t < te && (!(a.probe & 16) || dzacc[jt][r] == 1234.5f))
             atomicAdd(dZ + (long long)t * a.lddz + jt * 16 + L, a.alpha * dzacc[jt][r]);
         }
     }
@@ -541,40 +531,11 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = cb + cc * 128 + wid * 32 + m * 16 + g * 4 + r;
-          if (a.pb) {
-            if (c < NL)
-              a.pb[blockIdx.y * a.pb_slot + (a.seg.b_off[seg] + c) * a.r + jt * 16 + L] =
-                  a.alpha * dbacc[cc][m][jt][r];
-          } else if (c < NL && (!(a.probe & 32) || dbacc[cc][m][jt][r] == 1234.5f))
+          if (c < NL && (!(a.probe & 32) || dbacc[cc][m][jt][r] == 1234.5f))
             atomicAdd(dB + (long long)c * a.r + jt * 16 + L, a.alpha * dbacc[cc][m][jt][r]);
         }
       }
   }
-}
-
-// dZ[i] += sum_s pz[s][i] (i < nz),  dB[i] += sum_s pb[s][i] (i < nb); 4 floats per thread
-__global__ void __launch_bounds__(256) dy_reduce_kernel(const float* __restrict__ pz, int nsz,
-                                                        long long pz_slot, float* __restrict__ dZ,
-                                                        long long nz, const float* __restrict__ pb,
-                                                        int nsb, long long pb_slot,
-                                                        float* __restrict__ dB, long long nb) {
-  long long i = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 4;
-  const float* p;
-  float* out;
-  int ns;
-  long long slot;
-  if (i < nz) { p = pz + i; out = dZ + i; ns = nsz; slot = pz_slot; }
-  else {
-    i -= nz;
-    if (i >= nb) return;
-    p = pb + i; out = dB + i; ns = nsb; slot = pb_slot;
-  }
-  float4 acc = *reinterpret_cast<const float4*>(out);
-  for (int s = 0; s < ns; ++s) {
-    const float4 v = *reinterpret_cast<const float4*>(p + s * slot);
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-  }
-  *reinterpret_cast<float4*>(out) = acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -924,15 +885,12 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
                                      const float* Z, long long ldz, float* dZ, long long lddz,
                                      float* dB, int T, int tw, float alpha, int nseg,
                                      const long long* n_off, const long long* r_off,
-                                     const long long* b_off, const int* n_len, float* pz,
-                                     long long pz_slot, float* pb, long long pb_slot,
-                                     hipStream_t st) {
+                                     const long long* b_off, const int* n_len, hipStream_t st) {
   if (T <= 0 || nseg < 1 || nseg > 4 || (r != 16 && r != 32 && r != 64) || tw < 64 || (tw & 63) ||
-      (ldy & 7) || ((pz == nullptr) != (pb == nullptr)))
+      (ldy & 7))
     return hipErrorInvalidValue;
   lv3::DyArgs a;
   a.probe = lv3_probe();
-  a.pz = pz; a.pz_slot = pz_slot; a.pb = pb; a.pb_slot = pb_slot;
   a.dy = dy; a.ldy = ldy; a.B = B; a.r = r; a.Z = Z; a.ldz = ldz; a.dZ = dZ; a.lddz = lddz;
   a.dB = dB; a.T = T; a.TW = tw; a.alpha = alpha;
   a.seg.nseg = nseg;
@@ -956,20 +914,6 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
   else if (dtype == kF16) { LV3_DY(fp16) }
   else return hipErrorInvalidValue;
 #undef LV3_DY
-  return hipGetLastError();
-}
-
-// partial-mode epilogue of lumen_lora3_dy: dZ += sum of nsz slots, dB += sum of nsb slots
-extern "C" hipError_t lumen_lora3_dy_reduce(const float* pz, int nsz, long long pz_slot, float* dZ,
-                                            long long nz, const float* pb, int nsb,
-                                            long long pb_slot, float* dB, long long nb,
-                                            hipStream_t st) {
-  if ((nz & 3) || (nb & 3) || (pz_slot & 3) || (pb_slot & 3) || nsz < 1 || nsb < 1)
-    return hipErrorInvalidValue;
-  const long long n4 = (nz + nb) / 4;
-  if (n4 == 0) return hipSuccess;
-  hipLaunchKernelGGL(lv3::dy_reduce_kernel, dim3(static_cast<unsigned>((n4 + 255) / 256)), dim3(256),
-                     0, st, pz, nsz, pz_slot, dZ, nz, pb, nsb, pb_slot, dB, nb);
   return hipGetLastError();
 }
 

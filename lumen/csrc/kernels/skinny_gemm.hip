@@ -324,24 +324,6 @@ hipError_t launch_gemv(const void* x, const void* W, void* y, int M, int N, int 
 
 // y[1, N] = (silu(gu[:, :K]) * gu[:, K:]) @ W[N, K]^T: the batch-1 down projection with the
 // SwiGLU activation formed on the fly (gu row stride ldgu >= 2K).
-extern "C" hipError_t lumen_gemv_swiglu(int dtype, const void* gu, const void* W, void* y, int N,
-                                        int K, long long ldgu, long long ldy, hipStream_t st) {
-  if (N % 4 != 0 || K % 8 != 0) return hipErrorInvalidValue;
-  dim3 grid(N / 4), block(256);
-#define LUMEN_GEMV_SW(TT)                                                                       \
-  if (g_gemv_form == 1)                                                                         \
-    hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<TT, true, 1>), grid, block, 0, st,           \
-                       (const TT*)gu, (const TT*)W, (TT*)y, N, K, 1, ldgu, ldy);                \
-  else                                                                                          \
-    hipLaunchKernelGGL((lumen::sk::gemv_kernel<TT, 1, true>), grid, block, 0, st, (const TT*)gu, \
-                       (const TT*)W, (TT*)y, 1, N, K, ldgu, ldy)
-  if (dtype == lumen::kBF16) { LUMEN_GEMV_SW(lumen::bf16); }
-  else if (dtype == lumen::kF16) { LUMEN_GEMV_SW(lumen::fp16); }
-  else return hipErrorInvalidValue;
-#undef LUMEN_GEMV_SW
-  return hipGetLastError();
-}
-
 // M == 1 kernel form: 1 = rows-per-lane (gemv_r4_kernel), 0 = row-group form (gemv_kernel)
 extern "C" void lumen_set_gemv_form(int form) { g_gemv_form = form; }
 

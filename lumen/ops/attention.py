@@ -40,9 +40,8 @@ def causal_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
 
 
 _merge_counters: dict = {}
-# Fused split-context merge: measured neutral in decode steps (batch 1: 3.857 vs 3.865 ms ITL,
-# profiles/r02_serve), so the two-kernel merge stays the default.
-PA_FUSED_MERGE = os.environ.get("LUMEN_PA_FUSED_MERGE", "0") == "1"
+# Fused split-context merge (two-pass kernel only): measured neutral in decode steps (batch 1:
+# 3.857 vs 3.865 ms ITL, profiles/r02_serve); callers may still ask for it (``fused_merge``).
 # single-pass decode kernel (K and V streamed together, online softmax per row group)
 PA_ONE_PASS = os.environ.get("LUMEN_PA_1PASS", "1") == "1"
 
@@ -83,7 +82,7 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
             tm = torch.empty(1, 1, 1, device=q.device, dtype=torch.float32)
             tl, to = tm, tm
         one = PA_ONE_PASS if one_pass is None else one_pass
-        fused = (PA_FUSED_MERGE if fused_merge is None else fused_merge) and not one
+        fused = bool(fused_merge) and not one
         cnt = (_pa_counters(q.device, num_seqs * nkv) if fused and max_parts > 1
                else None)
         native().paged_attention_decode(out, q.contiguous(), k_cache, v_cache, block_tables,
@@ -266,47 +265,6 @@ def _tiles(cu: tuple, rows: int, device, heavy_first: bool = True,
     return t
 
 
-N_XCD = 8  # MI355X: 8 XCDs, each with its own L2; workgroups go to XCDs round-robin by id
-
-
-def _xcd_tiles(cu: tuple, rows: int, nheads: int, device, heavy_low: bool) -> torch.Tensor:
-    """(seq, row start, head) triples for a 1-D launch, ordered so that all row tiles of one
-    (sequence, head) run on ONE XCD at the same time: group g goes to XCD g % 8 and takes
-    consecutive slots of that XCD's share of the block ids (id = slot * 8 + xcd), so the group's
-    Q / dO (dK/dV kernel) or K / V (forward, dQ) tiles are fetched from HBM once into that L2
-    instead of once per tile.  Longest sequences first; inside a group the heaviest causal tile
-    first (heavy_low: low row starts carry the most work, as in dK/dV).  Unequal XCD queues are
-    padded with seq = -1 entries (empty workgroups)."""
-    key = ("xcd", cu, rows, nheads, str(device), heavy_low)
-    t = _TILE_CACHE.get(key)
-    if t is None:
-        seqs = sorted(range(len(cu) - 1), key=lambda s: -(cu[s + 1] - cu[s]))
-        queues = [[] for _ in range(N_XCD)]
-        g = 0
-        for s in seqs:
-            L = cu[s + 1] - cu[s]
-            if L <= 0:
-                continue
-            starts = list(range(0, L, rows))
-            if not heavy_low:
-                starts.reverse()
-            for h in range(nheads):
-                queues[g % N_XCD] += [(s, r, h) for r in starts]
-                g += 1
-        n = max(len(q) for q in queues)
-        flat = []
-        for slot in range(n):
-            for x in range(N_XCD):
-                flat += queues[x][slot] if slot < len(queues[x]) else (-1, 0, 0)
-        t = torch.tensor(flat if flat else [0], dtype=torch.int32, device=device)
-        if not flat:
-            t = t[:0]
-        if len(_TILE_CACHE) > 256:
-            _TILE_CACHE.clear()
-        _TILE_CACHE[key] = t
-    return t
-
-
 def _cu_tensor(cu: tuple, device) -> torch.Tensor:
     key = ("cu", cu, str(device))
     t = _TILE_CACHE.get(key)
@@ -365,21 +323,12 @@ FA_FWD_ROWS = _fwd_rows(FA_FWD_MT)
 # backward kernels: "v16" = 16x16x32 dK/dV (64-key tiles) + dQ (64-query tiles);
 # "v32" = 32x32x16 kernels with 128-row tiles; "mix" = 16x16x32 dK/dV + 32x32x16 dQ
 FA_BWD = _os.environ.get("LUMEN_FA_BWD", "mix")
-# LUMEN_FA_DQ_DELTA=1: the 32x32 dQ kernel forms delta itself and runs before dK/dV (opt-in:
-# measured neutral end to end and +0.22 ms/step of kernel time, profiles/r04_train)
-FA_DQ_DELTA = _os.environ.get("LUMEN_FA_DQ_DELTA", "0") == "1"
 # dS hand-off (mix kernels): the dK/dV kernel stores dS per 64x64 tile and the dQ kernel forms
 # dQ = dS K from it, instead of recomputing S = Q K^T and dP = dO V^T (2 of its 3 products).
 # Used while the [nh, tiles, 64, 64] 16-bit buffer stays under LUMEN_FA_DS_MB (0 = off).
 FA_DS_MB = float(_os.environ.get("LUMEN_FA_DS_MB", "2048"))
-# dK/dV kernel of the dS hand-off path: "8" = 8 waves x 16 keys (128-key tiles, 3-stage DMA ring,
-# one barrier per step; opt-in: 117.6 vs 108.0 us at B=8 S=512, gpurun r2_36), "4" = the 4-wave
-# 64-key kernel
-FA_DKDV = _os.environ.get("LUMEN_FA_DKDV", "4")
-FA_DKDV_HEAVY = _os.environ.get("LUMEN_FA_DKDV_HEAVY", "1") == "1"  # A/B switch of that order
-# XCD-grouped 1-D launches (_xcd_tiles) for the forward and the dS hand-off backward: opt-in,
-# measured neutral at B=8 S=512 (dK/dV 108 -> 110 us, dQ 30 -> 31 us, gpurun r2_34)
-FA_XCD = _os.environ.get("LUMEN_FA_XCD", "0") == "1"
+# (Measured and removed: an 8-wave 128-key dK/dV kernel, 117.6 vs 108.0 us at B=8 S=512; XCD-
+# grouped 1-D tile orders, neutral; the 32x32 dQ kernel forming delta itself, neutral.)
 
 
 def _ds_offsets(cu: tuple, causal: bool, device):
@@ -414,11 +363,8 @@ class _FlashAttn(torch.autograd.Function):
         lse = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
         cut = _cu_tensor(cu, qkv.device)
         scale = 1.0 / math.sqrt(D) if scale is None else scale
-        if FA_XCD and FA_FWD_MT == 20:
-            tl, w = _xcd_tiles(cu, FA_FWD_ROWS, nh, qkv.device, False), 0x100
-        else:
-            tl, w = _tiles(cu, FA_FWD_ROWS, qkv.device), 0
-        C.flash_attn(w, causal, FA_FWD_MT, q, k, v, o, lse, cut, tl, nh, nkv, scale, None, None,
+        tl = _tiles(cu, FA_FWD_ROWS, qkv.device)
+        C.flash_attn(0, causal, FA_FWD_MT, q, k, v, o, lse, cut, tl, nh, nkv, scale, None, None,
                      None, None, None, None, None, None)
         ctx.save_for_backward(qkv, o, lse)
         ctx.meta = (cu, nh, nkv, D, causal, scale)
@@ -468,28 +414,13 @@ class _FlashAttn(torch.autograd.Function):
             if not handed:
                 C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh,
                              nkv, scale, do, None, None, None, delta, None, None, None)
-            if FA_DKDV == "8":
-                t7, w7 = _tiles(cu, 128, qkv.device, heavy_low=causal), 10
-                t8, w8 = ((_xcd_tiles(cu, 64, nh, qkv.device, False), 0x108) if FA_XCD
-                          else (_tiles(cu, 64, qkv.device), 8))
-            elif FA_XCD:
-                t7, w7 = _xcd_tiles(cu, 64, nkv, qkv.device, causal), 0x107
-                t8, w8 = _xcd_tiles(cu, 64, nh, qkv.device, False), 0x108
-            else:
-                # dK/dV: low key tiles carry the most (causal) query steps -> launched first
-                t7 = _tiles(cu, 64, qkv.device, heavy_low=causal and FA_DKDV_HEAVY)
-                t8 = _tiles(cu, 64, qkv.device)
-                w7, w8 = 7, 8
-            C.flash_attn_ds(w7, causal, q, k, v, lse, cut, t7, nh, nkv,
+            # dK/dV: low key tiles carry the most (causal) query steps -> launched first
+            t7 = _tiles(cu, 64, qkv.device, heavy_low=causal)
+            t8 = _tiles(cu, 64, qkv.device)
+            C.flash_attn_ds(7, causal, q, k, v, lse, cut, t7, nh, nkv,
                             scale, do, dq, dk, dv, delta, ds, ds_off, ds_total, pos, cos, sin)
-            C.flash_attn_ds(w8, causal, q, k, v, lse, cut, t8, nh, nkv,
+            C.flash_attn_ds(8, causal, q, k, v, lse, cut, t8, nh, nkv,
                             scale, do, dq, dk, dv, delta, ds, ds_off, ds_total, pos, cos, sin)
-        elif wq == 5 and FA_DQ_DELTA:
-            # the 32x32 dQ kernel forms delta = rowsum(dO * O) itself and runs first
-            C.flash_attn(wq, causal, 2, q, k, v, o, lse, cut, qtiles, nh, nkv,
-                         scale, do, dq, dk, dv, delta, pos, cos, sin)
-            C.flash_attn(wkv, causal, 1, q, k, v, o, lse, cut, _tiles(cu, rkv, qkv.device), nh,
-                         nkv, scale, do, dq, dk, dv, delta, pos, cos, sin)
         else:
             if not handed:
                 C.flash_attn(1, causal, 1, q, k, v, o, lse, cut, _tiles(cu, 64, qkv.device), nh,

@@ -23,9 +23,6 @@ from ._native import native, use_native
 SKINNY_MAX_M = int(os.environ.get("LUMEN_SKINNY_MAX_M", "4"))
 SKINNY_MAX_N = int(os.environ.get("LUMEN_SKINNY_MAX_N", str(1 << 30)))
 SKINNY_WIDE_MAX_M = 2  # above this M only N <= 4096 projections take the GEMV
-# SwiGLU formed inside the batch-1 down projection: measured 21.4 us vs 18.5 us for the swiglu
-# kernel + GEMV (every workgroup re-activates the whole gate|up vector), so off by default.
-SWIGLU_GEMV = os.environ.get("LUMEN_SWIGLU_GEMV", "0") == "1"
 
 
 def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -38,60 +35,10 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
                  if x.shape[0] <= 4 else w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0))
 
 
-# Decode-batch MFMA GEMM (kernels/decode_gemm.hip) for DGEMM_MIN_M <= M <= DGEMM_MAX_M.  Opt-in:
-# measured against hipBLASLt with the tuned table (profiles/r02_serve/dgemm_*.jsonl) it only ties
-# or wins by a few percent at M <= 16 without split-K (gate_up 35.7 vs 37.4 us, lm_head 56.4 vs
-# 58.7 us at M = 2), loses on o / down (too few column tiles; its split-K reduction costs more
-# than it recovers) and loses 2x at M >= 64, where re-reading x per 64-column tile from L2
-# dominates.  The M = 1 rows-per-lane VALU kernel above is the batch-1 path.
-DGEMM = os.environ.get("LUMEN_DGEMM", "0") == "1"
-DGEMM_MIN_M = int(os.environ.get("LUMEN_DGEMM_MIN_M", "2"))
-DGEMM_MAX_M = int(os.environ.get("LUMEN_DGEMM_MAX_M", "256"))
-DGEMM_WGS = int(os.environ.get("LUMEN_DGEMM_WGS", "256"))  # split-K until this many workgroups
-
-_dg_counters: dict = {}
-
-
-def dgemm_plan(M: int, N: int, K: int):
-    """(splits, M tiles, tile rows) as the kernel computes them: a workgroup is ceil(M / 32) <= 4
-    waves (3 rounds up to 4) of 32 rows; K is split in powers of two while the grid is under
-    DGEMM_WGS workgroups and every split keeps >= 4 stages of 128 columns."""
-    nw = -(-M // 32)
-    bm = 128 if nw >= 3 else 32 * nw
-    mt = -(-M // bm)
-    base, nst, s = (N // 64) * mt, K // 128, 1
-    while base * s < DGEMM_WGS and nst // (2 * s) >= 4:
-        s *= 2
-    return s, mt, bm
-
-
-def dgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (DGEMM and use_native(x) and x.dim() == 2 and w.dim() == 2
-            and DGEMM_MIN_M <= x.shape[0] <= min(DGEMM_MAX_M, 256)
-            and x.dtype == w.dtype and x.dtype in (torch.bfloat16, torch.float16)
-            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()
-            and x.shape[1] == w.shape[1] and w.shape[0] % 64 == 0 and w.shape[1] % 128 == 0)
-
-
-def dgemm(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None) -> torch.Tensor:
-    M, K = x.shape
-    N = w.shape[0]
-    s, mt, bm = dgemm_plan(M, N, K)
-    if splits is not None:
-        s = splits
-    y = torch.empty(M, N, device=x.device, dtype=x.dtype)
-    ws = cnt = None
-    if s > 1:
-        ws = torch.empty(s * mt * bm * N, device=x.device, dtype=torch.float32)
-        key = (x.device.type, x.device.index)
-        cnt = _dg_counters.get(key)
-        if cnt is None or cnt.numel() < mt * (N // 64):
-            # zeroed once; the kernel leaves every counter at zero again.  First use happens in
-            # the eager warm-up steps, before any HIP-graph capture.
-            cnt = torch.zeros(max(mt * (N // 64), 1 << 12), device=x.device, dtype=torch.int32)
-            _dg_counters[key] = cnt
-    native().dgemm(x, w, y, s, ws, cnt)
-    return y
+# Decode batches 5..256: hipBLASLt with the tuned table.  A hand-written decode-batch MFMA GEMM
+# (scripts/probes/decode_gemm.hip, no longer built) only tied it at M <= 16 and lost 2x from
+# M = 64 (profiles/r02_serve/dgemm_*.jsonl): at 256 sequences the decode step is bound by the
+# paged-attention KV reads, not by these GEMMs.
 
 
 # Training-shape GEMMs run 256 x 256 macro tiles, one per CU at a time, so a GEMM with 5.375 or
@@ -179,21 +126,13 @@ def linear_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
         native().skinny_gemm(x, w, y)
         return y
-    if dgemm_ok(x, w):
-        return dgemm(x, w)
     return torch.matmul(x, w.t())
 
 
 def swiglu_linear_nt(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """(silu(gu[:, :F]) * gu[:, F:]) @ w[N, F]^T, the MLP down projection.  At batch 1, where the
-    weight-streaming kernel runs it, the activation is formed inside that kernel (no separate
-    SwiGLU launch); otherwise SwiGLU kernel + ``linear_nt``."""
+    """(silu(gu[:, :F]) * gu[:, F:]) @ w[N, F]^T, the MLP down projection: SwiGLU kernel +
+    ``linear_nt`` (forming the activation inside the batch-1 weight stream measured slower:
+    21.4 vs 18.5 us, every workgroup re-activates the whole gate|up vector)."""
     from .activation import swiglu
 
-    F = gu.shape[1] // 2
-    if (SWIGLU_GEMV and gu.shape[0] == 1 and gu.shape[1] == 2 * F and skinny_ok(gu[:, :F], w)
-            and gu.stride(0) % 8 == 0):
-        y = torch.empty(1, w.shape[0], device=gu.device, dtype=gu.dtype)
-        native().gemv_swiglu(gu, w, y)
-        return y
     return linear_nt(swiglu(gu), w)

@@ -178,13 +178,11 @@ def _zeros(*shape, device, train: bool = False):
 
 USE_V3 = _os.environ.get("LUMEN_LORA_V3", "1") != "0"
 DY_TW = int(_os.environ.get("LUMEN_LORA_DY_TW", "0"))  # dY rows per block of lora3_dy (0 = auto)
-# lora3_dy writes per-workgroup partial dZ / dB sums and one reduce kernel adds them up, instead
-# of f32 atomics into dZ / dB (LUMEN_LORA_DY_PARTIAL=1; measured neutral, profiles/r2_lora)
-DY_PARTIAL = _os.environ.get("LUMEN_LORA_DY_PARTIAL", "0") == "1"
-# per-call A/B (scripts/probes/lora_kernels.py, us): the v3 UP write-back is on par with v2
-# without RoPE (o_proj 15.0 vs 14.3) and slower with it (q|k|v 55.7 vs 45.6), so v2 stays the
-# forward UP; v3's DOWN (17.3 vs 21.9), fused dY pass (32.5 vs 53.3) and dx update win
-UP_V3 = _os.environ.get("LUMEN_LORA_UP_V3", "0") == "1"
+# per-call A/B (scripts/probes/lora_kernels.py, us): the v3 UP write-back was on par with v2
+# without RoPE (o_proj 15.0 vs 14.3) and slower with it (q|k|v 55.7 vs 45.6), so v2 is the
+# forward UP; v3's DOWN (17.3 vs 21.9), fused dY pass (32.5 vs 53.3) and dx update win.  A
+# partial-sum + reduce variant of the dY pass (instead of f32 atomics) measured neutral and was
+# removed (profiles/r2_lora).
 # fused x-side backward (dA + dx in one pass over the activation rows, lora3_dxa)
 DXA = _os.environ.get("LUMEN_LORA_DXA", "1") != "0"
 # flash-attention delta hand-off: when this linear's input is a flash-attention output O (it
@@ -203,78 +201,28 @@ def _v3_ok(r: int, R: int, segs, *mats) -> bool:
             and all(m.stride(1) == 1 and m.stride(0) % 8 == 0 for m in mats))
 
 
-# fold: the DOWN kernel's last-arriving K-block writes the 16-bit Z tail of the extended operand
-# itself (no z_tail launch per adapted linear); LUMEN_LORA_FUSED_TAIL=0 keeps the separate kernel
-FUSED_TAIL = _os.environ.get("LUMEN_LORA_FUSED_TAIL", "0") == "1"
-_tail_counters: dict = {}
-
-
-def _tail_cnt(T: int, device) -> torch.Tensor:
-    """Arrival counters of the fused tail, one per 64-row tile: zeroed once, and the kernel
-    leaves them at zero (first use is in an eager step, before any graph capture)."""
-    key = (device.type, device.index)
-    c = _tail_counters.get(key)
-    need = (T + 63) // 64
-    if c is None or c.numel() < need:
-        c = torch.zeros(max(need, 1024), device=device, dtype=torch.int32)
-        _tail_counters[key] = c
-    return c
-
-
-def _lora3_down(x2d, A, Z, p, seed, xe=None, KP=0):
-    """Z += drop(x) A^T; with ``xe`` (the [T, K + KP] fold operand) also writes its Z tail."""
+def _lora3_down(x2d, A, Z, p, seed):
+    """Z += drop(x) A^T (f32 [T, R])."""
     T, K = x2d.shape
     R = A.shape[0]
     native().lora3_down(x2d, x2d.stride(0), A, Z, R, T, K, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
                         drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0,
-                        xe, K if xe is not None else 0, KP,
-                        _tail_cnt(T, x2d.device) if xe is not None else None)
+                        None, 0, 0, None)
 
 
-def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope, gemm=None):
-    """``gemm`` (overlap mode): callable producing y; the DOWN product runs on the side stream
-    while it executes, and the UP write-back joins both.  Returns (y, rope fused)."""
-    T, K = x2d.shape
-    R = A.shape[0]
-    nat = native()
-    if gemm is not None:
-        cur = torch.cuda.current_stream(x2d.device)
-        side = _side_stream(x2d.device)
-        side.wait_stream(cur)      # x and the zeroed Z are ready
-        with torch.cuda.stream(side):
-            _lora3_down(x2d, A, Z, p, seed)
-        y = gemm()
-        cur.wait_stream(side)
-    else:
-        _lora3_down(x2d, A, Z, p, seed)
+def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope):
+    """v3 DOWN, then the v2 UP write-back (its write-back issues the RoPE table loads with the
+    output loads).  Returns (y, rope fused).  (Running the memory-bound adapter products on a
+    side stream under the frozen-weight GEMM measured +1.7 ms/step and was removed.)"""
+    _lora3_down(x2d, A, Z, p, seed)
     fuse = rope is not None and len(segs) <= 4 and _rope_covered(segs, rope[3])
     for i in range(0, len(segs), 4):
         ch = segs[i:i + 4]
         mask = sum(1 << j for j, sg in enumerate(ch) if sg[0] + sg[1] <= rope[3]) if fuse else 0
-        if UP_V3:
-            rp = (rope[1], rope[2], rope[0]) if fuse else (None, None, None)
-            nat.lora3_up(1, y, y.stride(0), Z, R, B, r, T, r, scale, 0, 0, 1.0, 0, 0,
-                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
-                         *rp, mask)
-        else:  # v2 UP: its write-back issues the RoPE table loads with the output loads
-            _lora2(2, 1, B, Z, y, y.stride(0), 1, scale, T, r, 1,
-                   [(b_off * r, r_off, n_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
-                   rope=(rope[1], rope[2], rope[0], mask) if fuse else None)
+        _lora2(2, 1, B, Z, y, y.stride(0), 1, scale, T=x2d.shape[0], J=r, split=1,
+               segs4=[(b_off * r, r_off, n_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
+               rope=(rope[1], rope[2], rope[0], mask) if fuse else None)
     return y, fuse
-
-
-# LUMEN_LORA_OVERLAP=1: the memory-bound adapter products that depend only on the layer input
-# (forward DOWN) or only on the output gradient (backward dZ / dB pass) run on a side stream
-# concurrently with the compute-bound frozen-weight GEMM of the same linear
-OVERLAP = _os.environ.get("LUMEN_LORA_OVERLAP", "0") == "1"
-_SIDE = {}
-
-
-def _side_stream(device) -> "torch.cuda.Stream":
-    s = _SIDE.get(device)
-    if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device=device)
-    return s
 
 
 # LUMEN_LORA_FOLD (default on): the forward UP product is folded into the frozen-weight GEMM as
@@ -304,7 +252,7 @@ def _dy_tw(segs, T: int) -> int:
 
 
 def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train: bool = False,
-                    rope=None, gemm=None):
+                    rope=None):
     """Z = drop(x) A^T (f32 [T,R]); y[:, seg] += scale * Z[:, rseg] B_seg^T (in place).
 
     ``rope`` = (pos int32 [T], cos, sin, ncols): also rotate columns [0, ncols) of y (q|k heads,
@@ -312,17 +260,14 @@ def lora_fwd_native(x2d, y, A, B, segs: Sequence[Seg], r, scale, p, seed, train:
     (Z, rope_done)."""
     T, K = x2d.shape
     R = A.shape[0]
-    v3 = (_v3_ok(r, R, segs, x2d, *(() if y is None else (y,))) and K % 8 == 0
+    v3 = (_v3_ok(r, R, segs, x2d, y) and K % 8 == 0
           and A.is_contiguous() and B.is_contiguous() and A.dtype == B.dtype == torch.float32)
-    if gemm is not None and not v3:
-        y = gemm()
-        return lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed, train, rope) + (y,)
-    Ntot = y.shape[1] if y is not None else 0
+    Ntot = y.shape[1]
     act = DTYPE_CODE[x2d.dtype]
     Z = _zeros(T, R, device=x2d.device, train=train)
     if v3:
-        y, fuse = _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope, gemm)
-        return (Z, fuse, y) if gemm is not None else (Z, fuse)
+        y, fuse = _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope)
+        return Z, fuse
     if _v2_ok(r, R, x2d):
         _lora2(0, 1, x2d, A, Z, R, 1, 1.0, T, R, _split(math.ceil(T / 64), K, 256),
                [(0, 0, 0, K)], seed, p, K)
@@ -369,11 +314,6 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
     v2 = _v2_ok(r, R, x2d, dy)
     v3 = (v2 and _v3_ok(r, R, segs, x2d, dy) and K % 8 == 0 and A.is_contiguous()
           and B.is_contiguous() and A.dtype == B.dtype == torch.float32)
-    if callable(dx):
-        if v3 and dy.is_cuda:
-            return _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB,
-                              v2 and DIRECT_GRAD and _direct_ok(A) and _direct_ok(B))
-        dx = dx()
     v3 = v3 and (dx is None or _v3_ok(r, R, segs, dx))
     # dA / dB accumulate straight into the parameters' .grad (views of the engine's flat f32
     # gradient buffer) when they exist: no zero-filled temporaries and no autograd add kernels
@@ -446,35 +386,10 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     dZ = ws[:T * R].view(T, R)
     dB = B.grad if (direct and need_dB) else ws[T * R + nA:].view(B.shape[0], r)
 
-    def dy_pass():
-        if DY_PARTIAL and len(segs) <= 4 and len({sg[1] for sg in segs}) == 1:
-            # per-workgroup partial sums + one reduce launch instead of contended f32 atomics
-            tw = _dy_tw(segs, T)
-            pz = torch.empty(math.ceil(segs[0][1] / 256), T, R, device=dev, dtype=torch.float32)
-            pb = torch.empty(math.ceil(T / tw), B.shape[0], r, device=dev, dtype=torch.float32)
-            nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, tw, scale,
-                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in segs],
-                         pz, pb)
-            nat.lora3_dy_reduce(pz, dZ, pb, dB)
-            return
-        for i in range(0, len(segs), 4):
-            ch = segs[i:i + 4]
-            nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
-                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
-
-    if callable(dx):
-        # overlap: the dY pass (memory-bound) on the side stream under the dX GEMM
-        cur = torch.cuda.current_stream(dev)
-        side = _side_stream(dev)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            dy_pass()
-        dx = dx()
-        cur.wait_stream(side)
-        if dx is not None and not _v3_ok(r, R, segs, dx):
-            dx = dx.contiguous()
-    else:
-        dy_pass()
+    for i in range(0, len(segs), 4):  # one pass over dY: dZ and dB (f32 atomics)
+        ch = segs[i:i + 4]
+        nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
+                     [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
     dA = None
     if need_dA:
         dA = A.grad if direct else ws[T * R:T * R + nA].view(R, K)
@@ -539,18 +454,12 @@ class _LoraLinear(torch.autograd.Function):
             R = A.shape[0]
             xe = fold_operand(x2d, K)
             Z = _zeros(T, R, device=x2d.device, train=ctx.train)
-            if FUSED_TAIL:
-                _lora3_down(x2d, A, Z, p, seed, xe, FOLD_KP)
-            else:
-                _lora3_down(x2d, A, Z, p, seed)
-                native().lora3_z_tail(Z, xe, K, FOLD_KP)
+            _lora3_down(x2d, A, Z, p, seed)
+            native().lora3_z_tail(Z, xe, K, FOLD_KP)
             y = torch.matmul(xe, fold.t())
             if bias is not None:
                 y.add_(bias)
             rope_done = False
-        elif OVERLAP and x2d.is_cuda:
-            Z, rope_done, y = lora_fwd_native(x2d, None, A, B, segs, r, scale, p, seed,
-                                              train=ctx.train, rope=rope, gemm=gemm)
         else:
             y = gemm()
             Z, rope_done = lora_fwd_native(x2d, y, A, B, segs, r, scale, p, seed,
@@ -580,13 +489,7 @@ class _LoraLinear(torch.autograd.Function):
             if not getattr(dy, "_lumen_scratch", False):
                 dy = dy.clone()
             _rope_(dy, ctx.rope, inverse=True)
-        held = {}
-        if OVERLAP and dy.is_cuda and ctx.needs_input_grad[0]:
-            def dx():  # runs while the side-stream dY pass is in flight
-                held["dx"] = _input_grad(ctx, dy)
-                return held["dx"]
-        else:
-            dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
+        dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
         _IN_BACKWARD[0] = True
         _DELTA_SLOT[0] = ctx.delta_slot
         try:
@@ -595,9 +498,7 @@ class _LoraLinear(torch.autograd.Function):
         finally:
             _IN_BACKWARD[0] = False
             _DELTA_SLOT[0] = None
-        if callable(dx):
-            dx = held["dx"]
-        dw = torch.matmul(dy.t(), x2d) if ctx.w_grad else None
+        dw =torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
         return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None, None, None
 

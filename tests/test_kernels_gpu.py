@@ -223,19 +223,17 @@ def test_adamw_device_hf_linear_schedule():
 
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
-@pytest.mark.parametrize("impl", ["v3", "v3-atomic", "v3-nodxa", "v2", "f32"])
+@pytest.mark.parametrize("impl", ["v3", "v2", "f32"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch, dtype):
-    """impl v3: one-shot DOWN / lane-local UP / fused dY pass (lora_v3.hip) with the opt-in
-    partial-sum dZ / dB slots + reduce (v3-atomic: the default f32 atomics); v2: 16-bit MFMA kernels (lora_v2.hip); f32:
-    exact-f32 MFMA kernel (lora.hip)."""
+    """impl v3 (shipped default): one-shot DOWN / fused dY pass / fused dA + dx (lora_v3.hip)
+    with the v2 UP write-back; v2: 16-bit MFMA kernels (lora_v2.hip, the fallback for
+    unaligned segments); f32: exact-f32 MFMA kernel (lora.hip, other ranks)."""
     import lumen.ops.lora as lora_mod
     from lumen.ops.lora import lora_linear, lora_linear_ref
 
     monkeypatch.setattr(lora_mod, "USE_V2", impl != "f32")
-    monkeypatch.setattr(lora_mod, "USE_V3", impl.startswith("v3"))
-    monkeypatch.setattr(lora_mod, "DXA", impl in ("v3", "v3-atomic"))
-    monkeypatch.setattr(lora_mod, "DY_PARTIAL", impl == "v3")
+    monkeypatch.setattr(lora_mod, "USE_V3", impl == "v3")
 
     T, K, r = 512 + 64, 1024, 16
     if segs_kind == "qkv":
@@ -354,18 +352,18 @@ def test_sampling_greedy_and_topk():
 @pytest.mark.parametrize("nh,nkv,lens", [(8, 8, [512, 512]), (8, 2, [512, 300, 77]),
                                          (4, 4, [1000, 64, 129])])
 @pytest.mark.parametrize("fwd,bwd", [("t1", "v16"), ("t2", "v16"), ("old", "v16"),
-                                     ("v32", "v32"), ("v32", "mix"), ("v32", "mix-sep")])
+                                     ("v32", "v32"), ("v32", "mix")])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch, dtype):
-    """bwd "mix-sep": mix kernels with the separate delta pass instead of the dQ kernel's own."""
+    """Forward variants (t1 / t2 / old / v32 = default) and recompute backward kernels
+    (v16 / v32 / mix = default when the dS hand-off buffer does not fit) vs the f32 reference."""
     import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
 
     mt = {"t1": 11, "t2": 12, "old": 1, "v32": 20}[fwd]
     monkeypatch.setattr(att, "FA_FWD_MT", mt)
     monkeypatch.setattr(att, "FA_FWD_ROWS", att._fwd_rows(mt))
-    monkeypatch.setattr(att, "FA_DQ_DELTA", bwd != "mix-sep")
-    monkeypatch.setattr(att, "FA_BWD", "mix" if bwd == "mix-sep" else bwd)
+    monkeypatch.setattr(att, "FA_BWD", bwd)
     monkeypatch.setattr(att, "FA_DS_MB", 0)  # the recompute dQ kernels (dS hand-off: below)
 
     D = 128
@@ -393,15 +391,11 @@ def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch, dtype):
                                          (4, 4, [1000, 64, 129])])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("dkdv", ["8", "4"])
-def test_flash_attention_ds_handoff(nh, nkv, lens, causal, monkeypatch, dtype, dkdv):
+def test_flash_attention_ds_handoff(nh, nkv, lens, causal, monkeypatch, dtype):
     """dS hand-off backward (dK/dV kernel stores dS tiles, dQ = dS K from them) vs the fp32
-    reference, and dQ vs the recompute kernel (same bf16 dS operand: near-identical); dkdv = the
-    8-wave 128-key or the 4-wave 64-key dK/dV kernel."""
+    reference, and dQ vs the recompute kernel (same bf16 dS operand: near-identical)."""
     import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
-
-    monkeypatch.setattr(att, "FA_DKDV", dkdv)
 
     D = 128
     cu = [0]
@@ -425,10 +419,8 @@ def test_flash_attention_ds_handoff(nh, nkv, lens, causal, monkeypatch, dtype, d
     assert rel(g[:, qs:qs + ks], g2[:, qs:qs + ks]) < 3e-2, "dk"
     assert rel(g[:, qs + ks:], g2[:, qs + ks:]) < 3e-2, "dv"
     assert rel(g[:, :qs], grads[0][:, :qs].float()) < 1e-2, "dq vs recompute"
-    if dkdv == "4":  # same dK/dV kernel with and without the dS store
-        assert torch.equal(grads[2048][:, qs:], grads[0][:, qs:]), "dk/dv unchanged"
-    else:
-        assert rel(g[:, qs:], grads[0][:, qs:].float()) < 1e-2, "dk/dv vs 4-wave kernel"
+    # same dK/dV kernel with and without the dS store
+    assert torch.equal(grads[2048][:, qs:], grads[0][:, qs:]), "dk/dv unchanged"
 
 
 @pytest.mark.parametrize("nh,nkv", [(8, 8), (8, 2)])
@@ -669,61 +661,17 @@ def test_skinny_gemm(M, N, K):
     assert rel(yv, xv.float() @ w.float().t()) < 1e-2
 
 
-@pytest.mark.parametrize("M", [2, 5, 16, 32, 33, 64, 96, 128, 200, 256])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (1024, 11008)])
-def test_dgemm(M, N, K, monkeypatch):
-    """Decode-batch MFMA GEMM (kernels/decode_gemm.hip) vs an f32 reference: planned split,
-    forced single / split-K (last-arriving split reduces), deterministic, counters left zeroed,
-    row-strided x."""
-    from lumen.ops import gemm as G
-
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
-    ref = x.float() @ w.float().t()
-    y = G.dgemm(x, w)
-    assert y.shape == (M, N) and rel(y, ref) < 1e-2
-    assert torch.equal(G.dgemm(x, w), y)  # fixed-order split reduction: bitwise repeatable
-    for s in (1, 2, 8):
-        assert rel(G.dgemm(x, w, splits=s), ref) < 1e-2
-    assert all(int(c.abs().sum()) == 0 for c in G._dg_counters.values())
-    xb = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)
-    xv = xb[:, :K]
-    assert rel(G.dgemm(xv, w, splits=2), xv.float() @ w.float().t()) < 1e-2
-    monkeypatch.setattr(G, "DGEMM", True)  # opt-in dispatch (LUMEN_DGEMM=1)
-    monkeypatch.setattr(G, "SKINNY_MAX_M", 0)  # (the batch <= 4 GEMV would take M = 2..4)
-    assert G.dgemm_ok(x, w)
-    assert torch.equal(G.linear_nt(x, w), G.dgemm(x, w))
-
-
-@pytest.mark.parametrize("N,F", [(4096, 11008), (1024, 2752), (4096, 1000)])
-def test_gemv_swiglu(N, F):
-    """Batch-1 down projection with SwiGLU formed inside the weight stream == swiglu kernel +
-    GEMM (the activation rounds to bf16 identically, so only summation order differs)."""
-    from lumen.ops.activation import swiglu
+@pytest.mark.parametrize("N,F", [(4096, 11008), (1024, 2752)])
+def test_swiglu_down_projection(N, F):
+    """Batch-1 MLP down projection of the serving path: SwiGLU kernel + weight-streaming GEMV ==
+    the f32 reference (silu in f32, product rounded to bf16 as the kernel does)."""
     from lumen.ops.gemm import swiglu_linear_nt
-    from lumen.ops._native import native
 
     gu = torch.randn(1, 2 * F, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, F, device=DEV) * 0.02).to(torch.bfloat16)
-    act = swiglu(gu)
-    ref = act.float() @ w.float().t()
-    y = torch.empty(1, N, device=DEV, dtype=torch.bfloat16)
-    # f32 reference of the whole op (silu in f32, product rounded to bf16 as the kernel does)
     g, u = gu.float().chunk(2, -1)
     ref32 = (F_silu(g) * u).to(torch.bfloat16).float() @ w.float().t()
-    for form in (0, 1):
-        native().set_gemv_form(form)
-        native().gemv_swiglu(gu, w, y)
-        assert rel(y, ref) < 1e-2
-        assert rel(y, ref32) < 1e-2
-    native().set_gemv_form(1)
-    assert rel(swiglu_linear_nt(gu, w), ref) < 1e-2
-    # row-strided gate|up buffer (a view into a wider allocation)
-    gb = torch.randn(1, 2 * F + 64, device=DEV).to(torch.bfloat16)
-    gv = gb[:, :2 * F]
-    yv = torch.empty(1, N, device=DEV, dtype=torch.bfloat16)
-    native().gemv_swiglu(gv, w, yv)
-    assert rel(yv, swiglu(gv.contiguous()).float() @ w.float().t()) < 1e-2
+    assert rel(swiglu_linear_nt(gu, w), ref32) < 1e-2
 
 
 def F_silu(x):
@@ -972,42 +920,6 @@ def test_llama_lora_fold_matches_unfolded(p_drop, monkeypatch):
     assert torch.equal(w1[:, :K], w2[:, :K]) and not torch.equal(w1[:, K:], w2[:, K:])
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("T,R", [(4096, 48), (1000, 16), (64, 64)])
-def test_lora3_down_fused_fold_tail(T, R):
-    """The DOWN kernel's last-arriving K-block writes the 16-bit Z tail of the fold operand:
-    bit-identical to the separate z_tail kernel, x columns untouched, counters back at zero."""
-    from lumen.ops import lora as L
-    from lumen.ops._native import native
-
-    dev = torch.device("cuda")
-    K, KP = 4096, L.FOLD_KP
-    g = torch.Generator(device=dev).manual_seed(3)
-    xe = torch.randn(T, K + KP, device=dev, generator=g).bfloat16()
-    A = torch.randn(R, K, device=dev, generator=g) * 0.02
-    x2d = xe[:, :K]
-    outs = []
-    for fused in (True, False):
-        buf = xe.clone()
-        Z = torch.zeros(T, R, device=dev)
-        if fused:
-            L._lora3_down(buf[:, :K], A, Z, 0.05, 1234, buf, KP)
-        else:
-            L._lora3_down(buf[:, :K], A, Z, 0.05, 1234)
-            native().lora3_z_tail(Z, buf, K, KP)
-        torch.cuda.synchronize()
-        outs.append((buf, Z))
-    (b1, z1), (b2, z2) = outs
-    assert torch.equal(b1[:, :K], x2d)
-    assert torch.allclose(z1, z2, atol=1e-4, rtol=1e-4)  # f32 atomics: order may differ
-    ref = torch.zeros(T, KP, device=dev)
-    ref[:, :R] = z1
-    assert torch.equal(b1[:, K:].float(), ref.bfloat16().float())
-    assert torch.allclose(b1[:, K:].float(), b2[:, K:].float(), atol=1e-2, rtol=1e-2)
-    assert int(L._tail_cnt(T, dev).abs().sum()) == 0
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
 def test_lora3_dxa_delta_handoff_kernel(p_drop):
     """The o_proj fused dA + dx kernel's delta output == rowsum(dO * O) per 128-column head,

@@ -61,6 +61,7 @@ def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_
         eng.backward(loss)
         eng.step()
         losses.append(float(loss))
+    eng.sync_params()  # an offloaded optimizer step may still be in flight (async offload)
     torch.cuda.synchronize()
     return adapter_state_dict(m), losses, eng.coordinator
 
