@@ -241,6 +241,17 @@ def rope_write_kv(qkv: torch.Tensor, positions: torch.Tensor, nh: int, nkv: int,
 _TILE_CACHE = {}
 
 
+def _upload_i32(vals, device) -> torch.Tensor:
+    """Small int32 host list -> device without a stream synchronise: a blocking
+    ``torch.tensor(..., device=gpu)`` copy waits for every kernel queued before it, which would
+    serialise the serving engine's host work (a new chunk layout every step) with the GPU.  The
+    pinned staging block is recycled by torch's caching host allocator once the copy is done."""
+    h = torch.tensor(vals, dtype=torch.int32)
+    if torch.device(device).type != "cuda":
+        return h
+    return h.pin_memory().to(device, non_blocking=True)
+
+
 def _tiles(cu: tuple, rows: int, device, heavy_first: bool = True,
            heavy_low: bool = False) -> torch.Tensor:
     """(seq, row start) pairs; heavy_first: causal query tiles (last rows = most keys) first;
@@ -256,7 +267,7 @@ def _tiles(cu: tuple, rows: int, device, heavy_first: bool = True,
             lst.sort(key=lambda x: (x[1], -(cu[x[0] + 1] - cu[x[0]])))
         elif heavy_first:  # causal: the last tiles of a sequence carry the most keys
             lst.sort(key=lambda x: -x[1])
-        t = torch.tensor(lst if lst else [(0, 0)], dtype=torch.int32, device=device).reshape(-1)
+        t = _upload_i32(lst if lst else [(0, 0)], device).reshape(-1)
         if not lst:
             t = t[:0]
         if len(_TILE_CACHE) > 256:
@@ -269,7 +280,7 @@ def _cu_tensor(cu: tuple, device) -> torch.Tensor:
     key = ("cu", cu, str(device))
     t = _TILE_CACHE.get(key)
     if t is None:
-        t = torch.tensor(cu, dtype=torch.int32, device=device)
+        t = _upload_i32(list(cu), device)
         _TILE_CACHE[key] = t
     return t
 

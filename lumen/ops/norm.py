@@ -13,21 +13,9 @@ import torch
 
 from ._native import native, use_native
 
-_LDS_SET = [False]
-
-
 def _occupancy_cap(C) -> None:
-    """``LUMEN_RMS_LDS=fwd,bwd``: dynamic LDS bytes reserved per workgroup, which caps how many
-    RMSNorm workgroups share a CU (lumen/bench/rmsnorm_probe.py measures the effect)."""
-    if _LDS_SET[0]:
-        return
-    _LDS_SET[0] = True
-    import os
-
-    v = os.environ.get("LUMEN_RMS_LDS")
-    if v:
-        f, _, b = v.partition(",")
-        C.set_rms_lds(int(f or 0), int(b or f or 0))
+    """(No-op.)  An occupancy cap through reserved dynamic LDS per workgroup measured no gain;
+    the knob stays reachable for lumen/bench/rmsnorm_probe.py via ``C.set_rms_lds``."""
 
 
 def rms_norm_ref(x, w, eps, residual=None):

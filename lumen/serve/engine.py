@@ -291,6 +291,15 @@ class LLMEngine:
         rows = np.concatenate([np.asarray(done_rows, dtype=np.int64),
                                np.arange(Tp, T, dtype=np.int64)])
         extra.append(rows)
+        R = len(rows)
+        if R:
+            # sampling parameters of the sampled rows ride in the same async copy: building them
+            # with torch.tensor(list, device=...) is a blocking copy -- a stream synchronise per
+            # step that would serialise the host with the GPU and undo async scheduling
+            ps = [s.params for s in batch.sampled]
+            extra += [np.fromiter((p.temperature for p in ps), np.float64, R).view(np.int64),
+                      np.fromiter((p.top_p for p in ps), np.float64, R).view(np.int64),
+                      np.fromiter((p.top_k for p in ps), np.int64, R)]
         if use_lora:
             extra.append(np.concatenate(lora))
         host = np.concatenate([np.concatenate(parts)] + extra)
@@ -316,8 +325,13 @@ class LLMEngine:
             o += N
             prev = self._inflight["toks"]
             inp.tokens[Tp:] = torch.where(s_dev >= 0, prev[s_dev.clamp(min=0)], inp.tokens[Tp:])
-        inp.sample_rows = dev[o:o + len(rows)]
-        o += len(rows)
+        inp.sample_rows = dev[o:o + R]
+        o += R
+        if R:
+            inp.temps = dev[o:o + R].view(torch.float64).float()
+            inp.top_ps = dev[o + R:o + 2 * R].view(torch.float64).float()
+            inp.top_ks = dev[o + 2 * R:o + 3 * R].int()
+            o += 3 * R
         if use_lora:
             inp.lora_ids = dev[o:o + T].int()
         return inp
@@ -406,8 +420,7 @@ class LLMEngine:
             seed = self.cfg.seed if ps[0].seed is None else ps[0].seed
             if any(p.has_penalties for p in ps):
                 logits = apply_penalties(logits, sampled)
-            t, lp = self.runner.sample(logits, [p.temperature for p in ps],
-                                       [p.top_p for p in ps], [p.top_k for p in ps], seed,
+            t, lp = self.runner.sample(logits, inp.temps, inp.top_ps, inp.top_ks, seed,
                                        self.step_count, want_logprobs=True)
             R = t.shape[0]
             th = torch.empty(R, dtype=torch.long, pin_memory=self.device.type == "cuda")
@@ -479,8 +492,7 @@ class LLMEngine:
             seed = self.cfg.seed if ps[0].seed is None else ps[0].seed
             if any(p.has_penalties for p in ps):
                 logits = apply_penalties(logits, sampled)
-            t, lp = self.runner.sample(logits, [p.temperature for p in ps],
-                                       [p.top_p for p in ps], [p.top_k for p in ps], seed,
+            t, lp = self.runner.sample(logits, inp.temps, inp.top_ps, inp.top_ks, seed,
                                        self.step_count, want_logprobs=True)
             toks = t.tolist()
             lps = lp.tolist() if lp is not None else [None] * len(toks)

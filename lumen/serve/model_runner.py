@@ -104,6 +104,9 @@ class StepInput:
     kv_lens_t: Optional[torch.Tensor] = None     # ... on the device, int32 [P]
     prefill_tables: Optional[torch.Tensor] = None  # prefill chunks [P, maxb] int32
     sample_rows: Optional[torch.Tensor] = None   # rows whose logits are sampled, int64 [R]
+    temps: Optional[torch.Tensor] = None         # [R] f32 sampling temperature per sampled row
+    top_ps: Optional[torch.Tensor] = None        # [R] f32
+    top_ks: Optional[torch.Tensor] = None        # [R] int32
 
     @property
     def num_prefill_rows(self) -> int:
@@ -207,7 +210,7 @@ class ModelRunner:
             gu = linear_nt(y2, L.gate_up)
             if ml is not None:
                 ml.apply(i, "gate_up", y2, gu, masks)
-            if ml is None:  # batch 1: SwiGLU formed inside the down-projection weight stream
+            if ml is None:  # SwiGLU kernel + down projection (GEMV at batch <= 4)
                 h = self._allreduce(swiglu_linear_nt(gu, L.down))
             else:
                 act = swiglu(gu)
@@ -354,9 +357,12 @@ class ModelRunner:
                top_ks: Seq[int], seed: int, offset: int, want_logprobs: bool = True):
         R = logits.shape[0]
         dev = logits.device
-        t = torch.tensor(temps, dtype=torch.float32, device=dev)
-        p = torch.tensor(top_ps, dtype=torch.float32, device=dev)
-        k = torch.tensor(top_ks, dtype=torch.int32, device=dev)
+        # device tensors (the engine ships them in its packed step copy); lists are converted
+        # here with a blocking copy
+        t = temps if torch.is_tensor(temps) else torch.tensor(temps, dtype=torch.float32, device=dev)
+        p = top_ps if torch.is_tensor(top_ps) else torch.tensor(top_ps, dtype=torch.float32,
+                                                                device=dev)
+        k = top_ks if torch.is_tensor(top_ks) else torch.tensor(top_ks, dtype=torch.int32, device=dev)
         if use_native(logits):
             out = torch.empty(R, dtype=torch.long, device=dev)
             lp = torch.empty(R, dtype=torch.float32, device=dev) if want_logprobs else None

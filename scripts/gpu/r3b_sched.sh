@@ -12,6 +12,9 @@ run() {  # name, env..., -- bench args
   env "$@" > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; return 1; }
   summ $O/$name.json $name
 }
+timeout -k 10 400 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1
+rc=$?; grep -E "FAILED|ERROR" $O/gpu_tests.txt | head -20; tail -1 $O/gpu_tests.txt
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 B="timeout -k 10 400 python bench.py --no_serve"
 run identity $B --steps 20 --warmup 5 || exit 1
 run keep LUMEN_ZERO3_SINGLE=1 LUMEN_ZERO3_SCHEDULE=keep $B --steps 20 --warmup 5 || exit 1
