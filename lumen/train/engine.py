@@ -93,9 +93,12 @@ class ZeroEngine:
                 group=self.gather_group, max_reuse_distance=cfg.stage3_max_reuse_distance,
                 force_partition=single)
             model.coordinator = self.coordinator
-            if env.is_main:
+            if env.is_main:  # stderr: bench.py's stdout is exactly one JSON line
+                import sys
+
                 c = self.coordinator
-                print(f"[lumen] ZeRO-3 schedule '{c.schedule}': {c.schedule_reason}", flush=True)
+                print(f"[lumen] ZeRO-3 schedule '{c.schedule}': {c.schedule_reason}",
+                      file=sys.stderr, flush=True)
         if self.device.type == "cuda":
             from ..models.layers import configure_backward_layout
 

@@ -288,6 +288,8 @@ def test_bench_contract_torchrun(world):
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
+    # the driver contract: rank 0's stdout is exactly that one JSON line (logs go to stderr)
+    assert [l for l in out.stdout.splitlines() if l.strip()] == lines, out.stdout[-2000:]
     j = json.loads(lines[0])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
