@@ -159,8 +159,9 @@ class LLMEngine:
         self._pin_i = 0
         self.async_sched = bool(cfg.async_scheduling and self.tp == 1)
         self._inflight: Optional[dict] = None
-        self.scheduler = Scheduler(SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,
-                                                   cfg.max_model_len), self.blocks)
+        self.scheduler = Scheduler(SchedulerConfig(
+            cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
+            decode_outside_budget=self.runner.overlaps_mixed_steps()), self.blocks)
         if tokenizer is None:
             from ..data.tokenizer import load_tokenizer
 
