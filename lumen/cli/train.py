@@ -84,6 +84,8 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
                          "when the estimated activations do not fit in free HBM (logged)")
     ap.add_argument("--no_gradient_checkpointing", action="store_true",
                     help="same as --gradient_checkpointing false")
+    ap.add_argument("--no_fuse_accumulation", action="store_true",
+                    help="run every accumulation micro-batch as its own forward / backward")
     ap.add_argument("--metrics_csv", default="results/training_metrics.csv")
     return ap
 
@@ -144,7 +146,8 @@ def main(variant: str, argv=None) -> dict:
         warmup_steps=args.warmup_steps, synthetic=args.synthetic,
         synthetic_samples=args.synthetic_samples, init=args.init, experiment=experiment,
         synthetic_min_len=args.synthetic_min_len, pack_sequences=not args.no_packing,
-        prefetch=args.prefetch, pack_tokens=args.pack_tokens)
+        prefetch=args.prefetch, pack_tokens=args.pack_tokens,
+        fuse_accumulation=not args.no_fuse_accumulation)
     t0 = time.time()
     trainer = Trainer(targs, ds, env)
     result = trainer.train()

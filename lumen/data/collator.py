@@ -62,6 +62,40 @@ class CausalLMCollator:
                 "n_valid": n_valid, "n_tokens": n_tokens}
 
 
+def fuse_collated(cbs: Sequence[Dict]) -> Dict:
+    """Concatenate collated micro-batches into one batch (gradient-accumulation fusion).
+
+    Packed batches join end to end (``cu_seqlens`` shifted; every part is already padded to the
+    tuned multiple, so the sum stays on the grid); padded batches are re-padded to the longest
+    row and stacked.  ``micro_steps`` tells the engine how many accumulation micro-steps the
+    batch stands for."""
+    if len(cbs) == 1:
+        return dict(cbs[0], micro_steps=1)
+    out: Dict = {"n_valid": sum(c["n_valid"] for c in cbs),
+                 "n_tokens": sum(c["n_tokens"] for c in cbs), "micro_steps": len(cbs)}
+    if cbs[0].get("cu_seqlens") is not None:
+        cu, o = [0], 0
+        for c in cbs:
+            cu += [o + x for x in c["cu_seqlens"][1:]]
+            o += c["input_ids"].shape[1]
+        out.update(input_ids=torch.cat([c["input_ids"] for c in cbs], 1),
+                   labels=torch.cat([c["labels"] for c in cbs], 1),
+                   pos=torch.cat([c["pos"] for c in cbs]), cu_seqlens=tuple(cu),
+                   n_padded=o, n_seqs=sum(c.get("n_seqs", 0) for c in cbs))
+        return out
+    L = max(c["input_ids"].shape[1] for c in cbs)
+
+    def pad(t, v):
+        return torch.nn.functional.pad(t, (0, L - t.shape[1]), value=v)
+
+    # right padding under causal attention: the filler id is never attended to by a real token
+    # and never a target, so any id works
+    out.update(input_ids=torch.cat([pad(c["input_ids"], 0) for c in cbs]),
+               labels=torch.cat([pad(c["labels"], IGNORE) for c in cbs]),
+               attention_mask=torch.cat([pad(c["attention_mask"], 0) for c in cbs]))
+    return out
+
+
 class PackedCollator:
     """Sequence packing for the varlen flash-attention path (no padding compute).
 

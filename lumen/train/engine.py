@@ -142,6 +142,7 @@ class ZeroEngine:
             cfg.warmup_type == "linear", W, self.scaler,
             cfg.decay_total_steps if cfg.lr_schedule == "hf_linear" else 0)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._k = 1  # accumulation micro-steps fused into the current forward / backward
         # ZeRO-Offload optimizer: the CPU step overlaps the next forward (exact semantics)
         self.async_off: Optional[AsyncOffloadStep] = None
         if (self.opt.offload and self.device.type == "cuda" and not self.device_sched
@@ -183,7 +184,7 @@ class ZeroEngine:
             self.opt.sched[9] = float(n)
 
     def is_boundary(self) -> bool:
-        return (self.micro_step + 1) % self.cfg.grad_accum == 0
+        return (self.micro_step + self._k) % self.cfg.grad_accum == 0
 
     def lr(self) -> float:
         """LR for the next update (host path): WarmupLR at the applied-step count."""
@@ -213,14 +214,19 @@ class ZeroEngine:
 
     # ----------------------------------------------------------------------------------------
     def forward(self, batch: Dict) -> torch.Tensor:
+        """``batch["micro_steps"]`` = k > 1: the batch is k accumulation micro-batches fused
+        into one (the trainer does this when they hold equal valid-token counts, so the fused
+        mean loss IS the mean of their means): backward scales by k / grad_accum and the step
+        counts k micro-steps."""
         self.timers.start("fwd")
+        self._k = int(batch.get("micro_steps", 1))
         fp16_dev = self.device_sched and self.scaler is not None
         if fp16_dev:
             # the fused LM-head CE writes dlogits already multiplied by the scale the backward
             # will apply (device scalar: no host read of the loss scale)
             from ..ops import loss as loss_ops
 
-            torch.div(self.opt.state[2:3], self.cfg.grad_accum, out=self._gscale)
+            torch.div(self.opt.state[2:3], self.cfg.grad_accum / self._k, out=self._gscale)
             loss_ops.GRAD_SCALE_HINT[0] = self._gscale
         try:
             kw = {"cu_seqlens": batch["cu_seqlens"]} if batch.get("cu_seqlens") is not None else {}
@@ -243,7 +249,7 @@ class ZeroEngine:
             # the forward handed the CE kernel as its gradient-scale hint
             (loss * self._gscale[0]).backward()
         else:
-            scale = self.loss_scale / self.cfg.grad_accum
+            scale = self.loss_scale * self._k / self.cfg.grad_accum
             (loss * scale if scale != 1.0 else loss).backward()
         if self.coordinator is not None:
             self.coordinator.end_micro_step()
@@ -264,7 +270,8 @@ class ZeroEngine:
     def step(self) -> bool:
         """Call after every backward; updates only at the accumulation boundary."""
         boundary = self.is_boundary()
-        self.micro_step += 1
+        self.micro_step += self._k
+        self._k = 1
         if not boundary:
             return False
         self.timers.start("step")

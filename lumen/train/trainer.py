@@ -64,6 +64,7 @@ class TrainArgs:
     save_final: bool = True
     log_file: Optional[str] = None
     async_save: bool = True
+    fuse_accumulation: bool = True  # equal-size accumulation micro-batches as one forward
 
 
 def model_flops_per_token(cfg, seq_len: int, lora: bool = True) -> float:
@@ -136,6 +137,8 @@ class Trainer:
         if env.device.type != "cuda":
             return False
         tokens = max(a.pack_tokens, self.ds.micro_batch * a.max_length)
+        if a.fuse_accumulation:
+            tokens *= self.ds.grad_accum
         est = tokens * cfg.num_hidden_layers * 16 * cfg.hidden_size * 2
         free, _ = torch.cuda.mem_get_info(env.device)
         on = 2 * est > free
@@ -195,7 +198,8 @@ class Trainer:
         d = self.env.device
         out = {"input_ids": b["input_ids"].to(d, non_blocking=True),
                "labels": b["labels"].to(d, non_blocking=True),
-               "n_valid": b["n_valid"], "n_tokens": b["n_tokens"]}
+               "n_valid": b["n_valid"], "n_tokens": b["n_tokens"],
+               "micro_steps": b.get("micro_steps", 1)}
         if b.get("cu_seqlens") is not None:
             out["cu_seqlens"] = b["cu_seqlens"]
             out["pos"] = b["pos"].to(d, non_blocking=True)
@@ -208,6 +212,39 @@ class Trainer:
         ld = PrefetchLoader(self._batches(epoch, skip), self.collator, depth=self.args.prefetch,
                             pin=self.env.device.type == "cuda")
         return ld, iter(ld)
+
+    def _fused(self, stream):
+        """(raw examples, collated batch, micro-steps) per engine forward.  Gradient-accumulation
+        fusion: the ``grad_accum`` micro-batches of one optimizer step run as ONE forward /
+        backward when they hold the same number of valid labels -- then the fused mean loss is
+        exactly the mean of the per-micro-batch means the reference accumulates (HF Trainer
+        divides each micro-batch loss by the accumulation steps).  Bigger GEMMs (M = 4096 for
+        the ZeRO-3 defaults 2 x 4 x 512 instead of 1024), a quarter of the launches and, under
+        ZeRO-3, a quarter of the weight gathers.  Groups start only on an optimizer-step
+        boundary; unequal groups run micro-batch by micro-batch."""
+        from ..data.collator import fuse_collated
+
+        k = self.ds.grad_accum
+        if k <= 1 or not self.args.fuse_accumulation:
+            for raw, cb in stream:
+                yield raw, cb, 1
+            return
+        buf = []
+        for raw, cb in stream:
+            if not buf and self.engine.micro_step % k:
+                yield raw, cb, 1          # not at a step boundary (epoch tail): no fusion
+                continue
+            buf.append((raw, cb))
+            if len(buf) < k:
+                continue
+            if len({c["n_valid"] for _, c in buf}) == 1:
+                yield [e for r, _ in buf for e in r], fuse_collated([c for _, c in buf]), k
+            else:
+                for r, c in buf:
+                    yield r, c, 1
+            buf = []
+        for r, c in buf:
+            yield r, c, 1
 
     def steps_per_epoch(self) -> int:
         if self.token_budget:
@@ -270,17 +307,17 @@ class Trainer:
             self._batches_in_epoch = skip_b
             produced = 0
             loader, stream = self._batch_stream(epoch, skip_b)
-            for raw, cb in stream:
-                produced += 1
-                self._batches_in_epoch += 1
+            for raw, cb, k in self._fused(stream):
+                produced += k
+                self._batches_in_epoch += k
                 if wd is not None:
                     wd.kick()
                 b = self._to_device(cb)
                 loss = eng.forward(b)
                 check_finite("loss", loss, eng.global_step, env.rank)
                 eng.backward(loss)
-                loss_acc += loss.detach().float()
-                loss_n += 1
+                loss_acc += loss.detach().float() * k  # a fused batch = k micro-step losses
+                loss_n += k
                 tokens += b["n_tokens"]
                 samples += len(raw)
                 samples_in_epoch += len(raw)

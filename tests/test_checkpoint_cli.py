@@ -168,3 +168,34 @@ def test_async_checkpoint_layout_and_resume(tmp_path):
     got = adapter_state_dict(second.model)
     for k in ref:
         assert torch.allclose(ref[k], got[k], atol=1e-6), k
+
+
+def test_accumulation_fusion_matches_micro_steps(tmp_path):
+    """grad_accum micro-batches with equal valid-token counts run as ONE forward/backward
+    (trainer ``fuse_accumulation``): same adapters and logged losses as accumulating them one by
+    one (dropout off: the fused forward draws its masks differently)."""
+    env = init(device="cpu")
+    res = {}
+    for fuse in (False, True):
+        ds = load_ds_config({"zero_optimization": {"stage": 2}}, 2, 4, 1, 5e-3,
+                            dtype_override="fp32")
+        a = TrainArgs(model_name="tiny-llama", synthetic=True, synthetic_samples=64, max_length=16,
+                      per_device_train_batch_size=2, gradient_accumulation_steps=4, max_steps=3,
+                      logging_steps=1, lora_r=4, lora_dropout=0.0, save_strategy="no",
+                      output_dir=str(tmp_path / str(fuse)), seed=3, save_final=False,
+                      fuse_accumulation=fuse)
+        tr = Trainer(a, ds, env, printer=lambda *x, **k: None)
+        calls = []
+        orig = tr.engine.forward
+        tr.engine.forward = lambda b: (calls.append(b.get("micro_steps", 1)), orig(b))[1]
+        tr.train()
+        res[fuse] = (adapter_state_dict(tr.model), [r["loss"] for r in tr.log_history], calls)
+    (a0, l0, c0), (a1, l1, c1) = res[False], res[True]
+    assert c0 == [1] * 12 and c1 == [4] * 3
+    assert l0 == l1
+    # f32 summation order differs (one batch vs four); Adam turns a rounding difference in a
+    # near-zero gradient into an update of up to ~lr, so bound outliers by lr and the bulk tightly
+    for k in a0:
+        d = (a0[k] - a1[k]).abs()
+        assert d.max().item() < 5e-3, (k, d.max().item())
+        assert (d > 1e-5 + 1e-3 * a0[k].abs()).float().mean().item() < 0.02, k
