@@ -238,3 +238,17 @@ def test_zero_to_fp32_consolidation(tmp_path):
         assert torch.equal(got[k], r["sd"][k]), k
     st = torch.load(os.path.join(out, "optimizer_fp32.pt"), weights_only=True)
     assert all(set(v) == {"exp_avg", "exp_avg_sq"} for v in st.values())
+
+
+def test_zero3_auto_schedule_rule():
+    """``stage3_max_live_parameters: "auto"``: release below the model size, pipelined at 2-3
+    ranks (one xGMI link per peer pair: a whole step of lookahead), keep from 4 ranks."""
+    from lumen.parallel.zero3 import ParamCoordinator as PC
+
+    assert PC.auto_schedule(100, 99, 8)[0] == "release"
+    assert PC.auto_schedule(100, 250, 2)[0] == "pipelined"
+    assert PC.auto_schedule(100, 250, 3)[0] == "pipelined"
+    assert PC.auto_schedule(100, 150, 2)[0] == "keep"      # two copies do not fit
+    for w in (4, 8):
+        s, why = PC.auto_schedule(100, 250, w)
+        assert s == "keep" and "xGMI" in why
