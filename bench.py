@@ -67,7 +67,18 @@ def run_serve_bench(args) -> dict:
     return out
 
 
+def _claim_stdout():
+    """The driver contract: stdout carries exactly one JSON line.  Keep a private handle on the
+    real stdout for it and point fd 1 at stderr, so chatter from native libraries (gloo's
+    connection messages, RCCL/HIP diagnostics) and from any Python print lands in stderr."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
+    json_out = _claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -303,6 +314,8 @@ def main():
                 "gather_group_world": gather_world,
                 "backend": env.backend,
                 "zero3": zstats,
+                # keep schedule: the frozen weights are gathered once (warm-up), 0 per timed step
+                "zero3_gathered_mb_total": round(coord.gathered_bytes / 1e6, 1) if coord else 0.0,
                 "zero3_gathered_mb_per_step": round(gathered_mb, 1),
                 "zero3_received_mb_per_step_per_rank": round(gathered_mb * (world - 1) / world, 1),
                 "zero3_exposed_wait_ms_per_step_max_rank": round(exposed_ms / args.steps, 2),
@@ -312,7 +325,7 @@ def main():
                 "serve": serve,
             },
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if engine is not None:
         engine.close()  # drain in-flight (next-step) gathers before teardown
     if dist.is_initialized():

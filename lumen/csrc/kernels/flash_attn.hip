@@ -109,6 +109,27 @@ __device__ __forceinline__ void stage64_async(char* img, const T* base, long lon
   }
 }
 
+// stage64_async with a wave-uniform 64-bit base (the tile's first row, SGPRs) and 32-bit per-lane
+// byte offsets (< 64 rows x ld): the DMA takes the saddr + voffset form, one VGPR per address
+// instead of a 64-bit VGPR pair -- fwd32_kernel's eight K / V addresses per tile otherwise pushed
+// it over its 256-VGPR budget and spilled them to scratch inside the key loop.
+template <typename T>
+__device__ __forceinline__ void stage64_async_s(char* img, const T* base, long long ld, int r0,
+                                                int rmax) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const char* tile = reinterpret_cast<const char*>(base + (long long)r0 * ld);
+  const int last = rmax - 1 - r0;  // >= 0: callers stage only tiles that start inside the range
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ swz(row);
+    const unsigned off = (unsigned)((row < last ? row : last) * (int)ld + ch * 8) * sizeof(T);
+    __builtin_amdgcn_global_load_lds(
+        (const void*)(tile + off),
+        (__attribute__((address_space(3))) void*)(img + (wid * 4 + i) * 1024), 16, 0, 0);
+  }
+}
+
 // Opaque LDS-DMA: the same global_load_lds as the builtin, as inline asm.  hipcc's wait
 // insertion cannot tell an in-flight LDS-DMA into one ping-pong buffer from the ds_reads of the
 // other and puts s_waitcnt vmcnt(0) before them (seen after the barrier of every step in the
@@ -129,7 +150,7 @@ __device__ __forceinline__ void dma4_o(const void* g, const char* lds_wave_base)
 template <typename T, int SW>
 __device__ __forceinline__ void stage64_async_o(char* img, const T* base, long long ld, int r0,
                                                 int rmax) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (wid * 4 + i) * 4 + (lane >> 4);
@@ -703,7 +724,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   // tell the in-flight prefetch from the tile being read), serialising the DMA ring
   __shared__ __attribute__((aligned(16))) char bufA[STAGE];
   __shared__ __attribute__((aligned(16))) char bufB[STAGE];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lr = lane & 15, lg = lane >> 4;
   // persistent (a.nitems > 0): a grid of ~2 workgroups per CU walks the (key tile, kv head)
   // items in the host's heaviest-first order.  One workgroup's dK/dV stores (and dS flush) are
@@ -719,13 +740,12 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   const int krow = wk0 + lr;      // the key of this lane's accumulator column
   const int qstart = CAUSAL ? (k0 / 64) * 64 : 0;
   const int nq = qstart < L ? (L - qstart + 63) / 64 : 0;
-  const int nsteps = (a.probe & 128) ? 0 : grp * nq;  // (group head, query tile) pairs
+  const int nsteps = grp * nq;  // (group head, query tile) pairs
   // stage step j: Q / dO tiles via 8 DMA instructions per wave, lse / delta via one 4-byte DMA
   // instruction on waves 0 / 1 (the DMA ring stays the only in-loop global traffic, so the
   // counted vmcnt waits below stay exact: every wave keeps the same count per step, waves 0/1
   // issue one more, waited with vmcnt(0) on the last step only)
   auto stage = [&](int j, char* st) {
-    if ((a.probe & 1) && j >= 2) return;
     const int hh = j / nq, q0 = qstart + (j % nq) * 64;
     const int head = kvh * grp + hh;
     stage64_async_o<T, 1>(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
@@ -745,7 +765,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
   uint4 pend[2];
   long long pend_off = -1;
   auto store_pend = [&]() {
-    if (pend_off < 0 || (a.probe & 16)) return;
+    if (pend_off < 0) return;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       char* dst = reinterpret_cast<char*>(a.ds) + pend_off + (wid * 2 + ks) * 1024 + ds_slot(lg, lr);
@@ -785,7 +805,6 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     f32x4 sc[4], dp[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) { sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[nt] = sc[nt]; }
-    if (!(a.probe & 2)) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
@@ -793,7 +812,6 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
         sc[nt] = Mfma<T>::run(row_read<1>(qimg, nt * 16 + lr, 4 * ks + lg), kf[ks], sc[nt]);
         dp[nt] = Mfma<T>::run(row_read<1>(oimg, nt * 16 + lr, 4 * ks + lg), vf[ks], dp[nt]);
       }
-    }
     }
     // lane: key krow, queries q0 + 16nt + 4lg + r
     // (WDS: keys past the end must also store dS = 0 -- dQ multiplies it by the clamped K rows;
@@ -838,15 +856,10 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
       const uint4 pa = pack_p<T>(sc[2 * ks], sc[2 * ks + 1]);
       const uint4 da = pack_p<T>(dp[2 * ks], dp[2 * ks + 1]);
       if constexpr (WDS) pend[ks] = da;
-      if (!(a.probe & 4)) {
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
         dv[n] = Mfma<T>::run(pa, tr_read_img2<1>(oimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dv[n]);
         dk[n] = Mfma<T>::run(da, tr_read_img2<1>(qimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dk[n]);
-      }
-      } else {
-        dv[0][0] += __builtin_bit_cast(float, pa.x);  // keep P / dS live
-        dk[0][0] += __builtin_bit_cast(float, da.y);
       }
     }
     if constexpr (WDS)
@@ -864,7 +877,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int kr = wk0 + 4 * lg + r;
-    if (kr >= L || ((a.probe & 32) && dk[0][r] != 1234.5f)) continue;
+    if (kr >= L) continue;
     float kv[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
@@ -1251,8 +1264,8 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
       stage64_paged(img, K, kvh, a.nkv, bt, a.block_size, r0, Lk);
       stage64_paged(img + IMG, V, kvh, a.nkv, bt, a.block_size, r0, Lk);
     } else {
-      stage64_async(img, K, a.ldk, r0, L);
-      stage64_async(img + IMG, V, a.ldv, r0, L);
+      stage64_async_s(img, K, a.ldk, r0, L);
+      stage64_async_s(img + IMG, V, a.ldv, r0, L);
     }
   };
   wait_vm_all();  // Q fragments in registers before the DMA ring starts (exact vmcnt below)
@@ -1628,7 +1641,7 @@ __global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
   constexpr int TILE = IMG + 8192;  // K image | dS tile
   __shared__ __attribute__((aligned(16))) char bufA[TILE];  // ping-pong as in bwd_dkdv_kernel
   __shared__ __attribute__((aligned(16))) char bufB[TILE];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lr = lane & 15, lg = lane >> 4;
   // persistent (a.nitems > 0, as bwd_dkdv_kernel) over (query tile, head) items
   auto run = [&](const int seq, const int q0, const int head) {

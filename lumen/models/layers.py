@@ -148,8 +148,8 @@ class Linear(nn.Module):
         if W.stride(0) == K + KP and W.stride(1) == 1:
             # the weight itself lives in [N, K + KP] rows (ZeRO-3 layout): fold in place
             wext = W.as_strided((W.shape[0], K + KP), (K + KP, 1))
-            if getattr(W, "_lumen_gathered", False):
-                return wext  # tail filled by the coordinator when the unit was bound
+            # (ZeRO-3: a fresh gather clears the key, invalidate_fold_tail; a resident unit
+            # keeps its tail until the optimizer's publish bumps lora_B's version)
             tkey = (W.data_ptr(), lo.lora_B.data_ptr(), lo.lora_B._version, lo.scale)
             if self._tail_key != tkey:
                 self._fill_tail(wext)
@@ -177,12 +177,10 @@ class Linear(nn.Module):
                               [(n_off, b_off, n_len, r_off)
                                for (n_off, n_len, r_off, b_off) in lo.segs], lo.scale)
 
-    def fill_fold_tail(self) -> None:
-        """ZeRO-3: write s * lora_B into the tail of the freshly gathered [N, K + KP] weight."""
-        W = self.weight
-        K, KP = self.in_features, lora_ops.FOLD_KP
-        if self.lora is not None and W.numel() and W.stride(0) == K + KP:
-            self._fill_tail(W.as_strided((W.shape[0], K + KP), (K + KP, 1)))
+    def invalidate_fold_tail(self) -> None:
+        """ZeRO-3: the unit was just gathered, so the tail columns of its [N, K + KP] rows hold
+        the shard's padding; the next ``fold_weight()`` writes s * lora_B there."""
+        self._tail_key = None
 
     def seg_offset(self, name: str) -> Tuple[int, int]:
         i = self.seg_names.index(name)

@@ -17,8 +17,8 @@ MI355X-first design (not a DeepSpeed translation):
 * The fused AdamW kernel (kernels/adamw.hip) reads the global grad-norm from device memory and
   folds unscale, averaging and clipping into the update: a bf16 step has no host sync.
 * ZeRO-3 partitions the frozen base weights per unit (embedding, each decoder layer, head):
-  see lumen/parallel/zero3.py (own RCCL communicator for the weight gathers, pipelined / keep /
-  release / identity schedules, offloaded shards on a copy stream).
+  see lumen/parallel/zero3.py (own RCCL communicator for the weight gathers, keep (gathered once,
+  resident) / release / identity schedules, offloaded shards on a copy stream).
 """
 from __future__ import annotations
 
@@ -135,6 +135,15 @@ class FlatTrainable:
                 p.grad = self.grad[o:o + n].view_as(p)
                 self.index[id(p)] = (b, o, n)
                 o += n
+
+    def mark_updated(self) -> None:
+        """The flat buffer was rewritten (optimizer publish): bump every parameter's autograd
+        version counter.  The params are views installed with ``p.data = ...``, whose counters
+        do not see writes through ``self.param`` -- and caches keyed on ``_version`` (the LoRA
+        fold's [W | s B] tail, lumen.models.layers.Linear.fold_weight) must."""
+        from torch.autograd.graph import increment_version
+
+        increment_version([p for b in self.buckets for p in b.params])
 
     def _close(self, params, n, W):
         off = self.buckets[-1].off + self.buckets[-1].size if self.buckets else 0

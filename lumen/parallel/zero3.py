@@ -18,17 +18,17 @@ MI355X-first design (not a DeepSpeed translation):
 * Schedules, picked from the live-parameter budget (``stage3_max_live_parameters``; ``"auto"``
   sizes it from free HBM):
 
-  ``pipelined`` (budget >= 2x model: Llama-2-7B on 288 GB).  Two buffers per unit; the NEXT
-      micro-step's gathers are issued, in forward order, when the current one starts.  One step
-      of compute hides one step of xGMI traffic: at 2 GPUs each rank receives 6.75 GB per step
-      over ONE ~77 GB/s link (~90 ms), against a ~96 ms step.
-  ``keep`` (auto from 4 GPUs, or model <= budget < 2x model).  One buffer per unit, kept from
-      the forward to the backward; re-gathered for the next micro-step right after the unit's
-      backward.  The first ``LUMEN_ZERO3_LEAD`` units (embedding + first layer) are double
-      buffered like ``pipelined``: their re-gather would otherwise be issued at the very end of
-      the backward and exposed at the next step's start.  The next forward waits for whatever
-      of the other gathers did not fit in the backward (~comm - backward at N=2, hence
-      ``pipelined`` there; ``auto_schedule`` has the rule).
+  ``keep`` (budget >= model: Llama-2-7B on 288 GB at any world size, Llama-2-70B from 8
+      GPUs).  One buffer per unit, gathered on first use (prefetched ``depth`` units ahead)
+      and then RESIDENT: the partitioned weights are the frozen base model -- LoRA never writes
+      them -- so a gathered buffer can never go stale, and re-gathering it every micro-step (as
+      DeepSpeed does, to free the memory) would move 13.5 GB per step over xGMI to rebuild
+      bytes already in HBM.  The adapter tail of the K-extended (folded) weights is rewritten
+      in place whenever ``lora_B`` changes.  W^T of the projections, when enabled, is also
+      written once.  Steady-state traffic: the LoRA gradient reduce-scatter and the adapter
+      publish only.  (Until round 3 this schedule re-gathered after every unit's backward, and
+      a ``pipelined`` variant double-buffered every unit: 102-103 ms/step forced at world 1
+      against 91-93 ms for no gathers, profiles/r3_zero3.)
   ``release`` (budget < model: the reference's ``stage3_max_live_parameters: 1e9``).  A
       preallocated ring of ``P = budget / unit`` gather buffers (no allocator churn); prefetch
       depth from ``stage3_prefetch_bucket_size``; the last units of the forward stay live across
@@ -109,20 +109,19 @@ class _Unit:
         self.numel = 0
         self.padded = 0
         self.shard: Optional[torch.Tensor] = None      # [padded / W] (device, or pinned host)
-        self.bufs: List[Optional[torch.Tensor]] = []   # per slot: [>= padded] gathered (device)
-        self.works: List[Optional[object]] = []
-        self.states: List[str] = []                    # per slot: empty | inflight | ready
-        self.bound = -1                                # slot the params currently view, or -1
-        self.slot = 0                                  # slot of the current micro-step
+        self.buf: Optional[torch.Tensor] = None        # [>= padded] gathered (device)
+        self.work: Optional[object] = None
+        self.state = "empty"                           # empty | inflight | ready
+        self.bound = False                             # params view ``buf``
         self.dtype = None
-        # W^T copies made off the critical path (keep / pipelined): (param idx, off, wt_off)
+        # W^T copies made off the critical path (keep): (param idx, off, wt_off)
         self.tn: List[tuple] = []
         # LoRA-folded linears of this unit: their weights are stored as [N, K + KP] rows (the
-        # adapter tail of the K-extended GEMM); the tail is filled at every bind
+        # adapter tail of the K-extended GEMM); a bind marks the tail for a refill
         self.folds: List[nn.Module] = []
         self.wt_numel = 0
-        self.wt_bufs: List[Optional[torch.Tensor]] = []
-        self.wt_events: List[Optional[object]] = []
+        self.wt_buf: Optional[torch.Tensor] = None
+        self.wt_event: Optional[object] = None
 
 
 class ParamCoordinator:
@@ -132,7 +131,7 @@ class ParamCoordinator:
     call ``pre_backward(i)`` (before unit i's backward runs); the engine calls
     ``end_micro_step()`` after ``loss.backward()``.  See the module docstring for schedules."""
 
-    SCHEDULES = ("release", "keep", "pipelined", "identity")
+    SCHEDULES = ("release", "keep", "identity")
 
     def __init__(self, model: nn.Module, env: DistEnv, persistence_threshold: int,
                  max_live: int, prefetch_numel: int, offload_param: bool = False,
@@ -214,22 +213,7 @@ class ParamCoordinator:
         assert schedule in self.SCHEDULES, schedule
         self.schedule = schedule
         self.identity = schedule == "identity"
-        self.keep = schedule in ("keep", "pipelined")
-        # "lead" units own a second buffer: their NEXT micro-step gather is issued when the
-        # current one starts (a full step of compute hides it).  pipelined: every unit.  keep:
-        # the first ``LUMEN_ZERO3_LEAD`` units (default 2: the embedding and the first decoder
-        # layer) -- the ones the next forward needs first, whose single-buffer re-gather after
-        # their own backward would otherwise be exposed at the step boundary.
-        n_lead = (len(self.units) if schedule == "pipelined" else
-                  int(os.environ.get("LUMEN_ZERO3_LEAD", "2")) if schedule == "keep" else 0)
-        self.lead = set(range(min(n_lead, len(self.units))))
-        for i, u in enumerate(self.units):
-            n_slots = 2 if i in self.lead else 1
-            u.bufs = [None] * n_slots
-            u.works = [None] * n_slots
-            u.states = ["empty"] * n_slots
-            u.wt_bufs = [None] * n_slots
-            u.wt_events = [None] * n_slots
+        self.keep = schedule == "keep"
         self._tstream = None
         self._cstream = None
         self.transposed_numel = 0
@@ -280,26 +264,20 @@ class ParamCoordinator:
     def auto_schedule(total: int, max_live: int, world: int):
         """(schedule, reason) from the live-parameter budget and the world size.
 
-        * budget < model: ``release`` (the only schedule that bounds live weights).
-        * world <= 3 with room for two copies: ``pipelined``.  At 2 GPUs each rank receives
-          half the model per step over ONE xGMI link (~6.75 GB for Llama-2-7B, about a step of
-          compute), so only a full step of lookahead hides it.
-        * otherwise ``keep``: from 4 GPUs each rank's (N-1)/N share arrives over N-1 links, in
-          well under the backward that precedes its use; one gathered copy (plus double buffers
-          for the first ``LUMEN_ZERO3_LEAD`` units) instead of two."""
+        * budget < model: ``release`` (the only schedule that bounds live weights; every unit
+          is gathered again at each use).
+        * otherwise ``keep``: one gathered copy of the frozen weights, gathered once and kept
+          resident (the world size only sets how fast that first gather is)."""
         if total > max_live:
             return "release", f"model {total:.3g} elements > live budget {max_live:.3g}"
-        if world <= 3 and 2 * total <= max_live:
-            return "pipelined", (f"world {world} <= 3: gathers cross <= 2 xGMI links, a full "
-                                 "step of lookahead hides them (budget fits 2 copies)")
-        return "keep", (f"world {world}: gathers spread over {max(world - 1, 1)} xGMI links fit "
-                        "inside the backward; one gathered copy")
+        return "keep", (f"model {total:.3g} elements <= live budget {max_live:.3g}: frozen "
+                        f"weights gathered once (world {world}) and kept resident")
 
     def _hbm_live_budget(self, elem_bytes: int) -> int:
         """``stage3_max_live_parameters: "auto"``: elements of gathered weights that fit in the
         free HBM left after the shards, minus an activation reserve (max(48 GiB, 25% of the
-        device)).  On MI355X (288 GB) that is both buffers of the pipelined schedule for
-        Llama-2-7B and one full copy (keep) for Llama-2-70B.  Unlimited off-GPU."""
+        device)).  On MI355X (288 GB) that holds one full gathered copy (keep) of Llama-2-7B at
+        any world size and of Llama-2-70B from 8 ranks.  Unlimited off-GPU."""
         if self.env.device.type != "cuda":
             return 1 << 62
         free, total = torch.cuda.mem_get_info(self.env.device)
@@ -313,17 +291,17 @@ class ParamCoordinator:
     def stats(self) -> Dict:
         return dict(schedule=self.schedule, world=self.world, units=len(self.units),
                     total_numel=self.total_numel, max_live=self.max_live, depth=self.depth,
-                    lead_units=len(self.lead), reason=self.schedule_reason,
+                    reason=self.schedule_reason,
                     pool_size=self.pool_size, turn_keep=self.turn_keep,
                     pool_overflows=self.pool_overflows, separate_group=self.group is not None,
                     offload=self.offload)
 
     # ---- buffers ----------------------------------------------------------------------------
-    def _buffer(self, u: _Unit, slot: int) -> torch.Tensor:
+    def _buffer(self, u: _Unit) -> torch.Tensor:
         if self.schedule != "release":
-            if u.bufs[slot] is None:
-                u.bufs[slot] = torch.empty(u.padded, dtype=u.dtype, device=self.device)
-            return u.bufs[slot]
+            if u.buf is None:
+                u.buf = torch.empty(u.padded, dtype=u.dtype, device=self.device)
+            return u.buf
         free = self._pool.setdefault(u.dtype, [])
         if free:
             buf = free.pop()
@@ -332,7 +310,7 @@ class ParamCoordinator:
                 self.pool_overflows += 1  # schedule bug or a model whose units re-enter
             self._pool_alloc += 1
             buf = torch.empty(self.max_unit, dtype=u.dtype, device=self.device)
-        u.bufs[slot] = buf
+        u.buf = buf
         return buf
 
     def _pool_free(self, dtype) -> bool:
@@ -358,34 +336,30 @@ class ParamCoordinator:
         return k, st[:shard.numel()]
 
     # ---- gather / bind / release ------------------------------------------------------------
-    def _issue(self, i: int, nxt: bool = False):
-        """Gather unit i into its current slot, or (``nxt``, lead units) into the other one
-        for the next micro-step."""
+    def _issue(self, i: int):
+        """Gather unit i (and the units it shares parameters with) into its buffer."""
         if self.identity or i < 0 or i > self.last:
             return
         u = self.units[i]
         for d in u.deps:
-            self._issue(d, nxt and d in self.lead)
-        if nxt and i not in self.lead:
+            self._issue(d)
+        if not u.params or u.state != "empty":
             return
-        slot = 1 - u.slot if nxt else u.slot
-        if not u.params or u.states[slot] != "empty":
-            return
-        buf = self._buffer(u, slot)
+        buf = self._buffer(u)
         if self.poison:  # race detector: stale reads of this buffer now see NaN
             buf.fill_(float("nan"))
         if self.offload and buf.is_cuda:
-            u.works[slot] = self._issue_offloaded(u, buf)
+            u.work = self._issue_offloaded(u, buf)
         elif self.local:
-            u.works[slot] = _LocalGather(buf, u.shard)
+            u.work = _LocalGather(buf, u.shard)
         else:
-            u.works[slot] = dist.all_gather_into_tensor(buf[:u.padded], u.shard,
-                                                        group=self.group, async_op=True)
+            u.work = dist.all_gather_into_tensor(buf[:u.padded], u.shard, group=self.group,
+                                                 async_op=True)
         self.gathered_bytes += u.padded * buf.element_size()
         self.gathers += 1
-        u.states[slot] = "inflight"
+        u.state = "inflight"
         if u.tn:
-            self._transpose_after_gather(u, slot)
+            self._transpose_after_gather(u)
 
     def _issue_offloaded(self, u: _Unit, buf: torch.Tensor):
         """H2D copy of the pinned shard and the gather, both on the copy stream: ordered after
@@ -408,7 +382,7 @@ class ParamCoordinator:
             self._staging_work[k] = work
             return work
 
-    def _transpose_after_gather(self, u: _Unit, slot: int):
+    def _transpose_after_gather(self, u: _Unit):
         """On a side stream: wait for the gather, write W^T of the unit's projections (for the
         backward's TN input-gradient GEMMs).  The compute stream waits on the event only when it
         binds the unit."""
@@ -418,12 +392,12 @@ class ParamCoordinator:
         if self._tstream is None:
             self._tstream = torch.cuda.Stream(device=self.device)
         side = self._tstream
-        if u.wt_bufs[slot] is None:
-            u.wt_bufs[slot] = torch.empty(u.wt_numel, dtype=u.dtype, device=self.device)
-        side.wait_stream(cur)      # earlier readers of this slot's W^T are done
+        if u.wt_buf is None:
+            u.wt_buf = torch.empty(u.wt_numel, dtype=u.dtype, device=self.device)
+        side.wait_stream(cur)      # earlier readers of this W^T are done
         with torch.cuda.stream(side):
-            u.works[slot].wait()   # side stream waits on the collective
-            full, wt = u.bufs[slot], u.wt_bufs[slot]
+            u.work.wait()          # side stream waits on the collective
+            full, wt = u.buf, u.wt_buf
             for k, off, wt_off in u.tn:
                 rows, cols = u.params[k]._zero_shape
                 kp = getattr(u.params[k], "_lumen_fold_kp", 0)
@@ -431,12 +405,12 @@ class ParamCoordinator:
                 transpose_2d(src, out=wt[wt_off:wt_off + rows * cols].view(cols, rows))
             ev = torch.cuda.Event()
             ev.record(side)
-        u.wt_events[slot] = ev
+        u.wt_event = ev
 
     def enable_transposes(self, params: Sequence[nn.Parameter]) -> int:
-        """Keep W^T of these gathered weights next to the gathered buffer (keep / pipelined
-        schedules, when HBM allows: one more copy of the projections per slot).  Returns the
-        number of weights covered."""
+        """Keep W^T of these gathered weights next to the gathered buffer (keep schedule, when
+        HBM allows: one more copy of the projections, written once).  Returns the number of
+        weights covered."""
         if not self.keep or self.device.type != "cuda":
             return 0
         want = {id(p) for p in params}
@@ -453,10 +427,10 @@ class ParamCoordinator:
                     wo += n
                 o += _store_numel(p)
             plan.append((u, tn, wo))
-            need += wo * (u.dtype.itemsize if u.dtype is not None else 2) * len(u.bufs)
+            need += wo * (u.dtype.itemsize if u.dtype is not None else 2)
         free, total = torch.cuda.mem_get_info(self.device)
-        gathered = sum(u.padded * u.dtype.itemsize for u in self.units if u.params) * len(
-            self.units[0].bufs)
+        gathered = sum(u.padded * u.dtype.itemsize for u in self.units
+                       if u.params and u.buf is None)
         if need + gathered > free - max(48 * 2**30, 0.25 * total):
             return 0
         n = 0
@@ -504,7 +478,7 @@ class ParamCoordinator:
         return ms
 
     def _wait(self, i: int):
-        """Make unit i's params view the current slot's gathered buffer."""
+        """Make unit i's params view its gathered buffer."""
         if self.identity:
             return
         u = self.units[i]
@@ -512,72 +486,58 @@ class ParamCoordinator:
             self._wait(d)
         if not u.params:
             return
-        s = u.slot
-        if u.states[s] == "empty":
+        if u.state == "empty":
             self._issue(i)
-        if u.states[s] == "inflight":
-            self._wait_work(u.works[s])
-            u.works[s] = None
-            u.states[s] = "ready"
-        if u.bound != s:
-            self._bind_views(u, u.bufs[s])
-            for lin in u.folds:  # freshly gathered: the adapter tail comes from lora_B
-                lin.fill_fold_tail()
+        if u.state == "inflight":
+            self._wait_work(u.work)
+            u.work = None
+            u.state = "ready"
+        if not u.bound:
+            self._bind_views(u, u.buf)
+            for lin in u.folds:  # freshly gathered: the adapter tail is refilled from lora_B
+                lin.invalidate_fold_tail()
             if u.tn:
-                if u.wt_events[s] is not None:
-                    torch.cuda.current_stream(self.device).wait_event(u.wt_events[s])
-                    u.wt_events[s] = None
-                wt = u.wt_bufs[s]
+                if u.wt_event is not None:
+                    torch.cuda.current_stream(self.device).wait_event(u.wt_event)
+                    u.wt_event = None
                 for k, off, wt_off in u.tn:
                     rows, cols = u.params[k]._zero_shape
-                    u.params[k]._lumen_wt = wt[wt_off:wt_off + rows * cols].view(cols, rows)
-            u.bound = s
+                    u.params[k]._lumen_wt = u.wt_buf[wt_off:wt_off + rows * cols].view(cols, rows)
+            u.bound = True
 
     def _unbind(self, u: _Unit):
-        if u.bound >= 0:
+        if u.bound:
             for p in u.params:
                 p.data = torch.empty(0, dtype=u.dtype, device=p.device)
                 p._lumen_wt = None
-            u.bound = -1
+            u.bound = False
 
     def _release(self, i: int):
-        """Drop unit i's current-slot contents (release schedule: the buffer returns to the ring;
-        reuse is stream-ordered because the next gather is issued after this point)."""
+        """Drop unit i's contents (release schedule: the buffer returns to the ring; reuse is
+        stream-ordered because the next gather is issued after this point)."""
         if self.identity or i < 0 or i > self.last:
             return
         u = self.units[i]
         if not u.params:
             return
-        s = u.slot
-        if u.states[s] == "inflight":
-            u.works[s].wait()
-            u.works[s] = None
+        if u.state == "inflight":
+            u.work.wait()
+            u.work = None
         self._unbind(u)
-        if self.schedule == "release" and u.bufs[s] is not None:
-            self._pool.setdefault(u.dtype, []).append(u.bufs[s])
-            u.bufs[s] = None
-        u.states[s] = "empty"
+        if self.schedule == "release" and u.buf is not None:
+            self._pool.setdefault(u.dtype, []).append(u.buf)
+            u.buf = None
+        u.state = "empty"
 
     def _prefetch(self, i: int):
         """release: gather unit i ahead of use if a ring buffer is free (never grows the ring)."""
         if i < 0 or i > self.last:
             return
         u = self.units[i]
-        if not u.params or u.states[u.slot] != "empty":
+        if not u.params or u.state != "empty":
             return
         if self.schedule == "release" and not self._pool_free(u.dtype):
             return
-        self._issue(i)
-
-    def _refresh(self, i: int):
-        """keep: unit i is done for this micro-step -> re-gather it for the next one into the
-        same buffer (issued after the compute that read it)."""
-        if i < 1 or i > self.last or i in self.lead:
-            return  # lead units: the next micro-step's copy is already in the other slot
-        u = self.units[i]
-        if not u.params or u.states[u.slot] != "ready":
-            return
-        self._release(i)
         self._issue(i)
 
     # ---- model hooks ------------------------------------------------------------------------
@@ -586,15 +546,8 @@ class ParamCoordinator:
         self._in_step = True
         if self.identity:
             return
-        if self.schedule == "pipelined":
-            for i in range(self.last + 1):
-                self._issue(i)
-        else:
-            for i in range(min(self.depth, self.last + 1)):
-                self._prefetch(i)
-        for i in sorted(self.lead):
-            self._issue(i)             # (no-op when already in flight / ready)
-            self._issue(i, nxt=True)   # next micro-step, behind this one's
+        for i in range(min(self.depth, self.last + 1)):
+            self._prefetch(i)          # (keep: no-op once the units are resident)
 
     def pre_forward(self, i: int):
         if i == 0 and not self._in_step:
@@ -602,9 +555,8 @@ class ParamCoordinator:
         if self.identity:
             return
         self._wait(i)
-        if self.schedule != "pipelined":
-            for j in range(i + 1, min(i + 1 + self.depth, self.last + 1)):
-                self._prefetch(j)
+        for j in range(i + 1, min(i + 1 + self.depth, self.last + 1)):
+            self._prefetch(j)
 
     def post_forward(self, i: int, out):
         # release: the head (last) and the ``turn_keep`` units before it are consumed by the
@@ -639,8 +591,6 @@ class ParamCoordinator:
             return
         if self.schedule == "release":
             self._release(i + 1)
-        elif self.schedule == "keep":
-            self._refresh(i + 1)
         self._wait(i)
         if self.schedule == "release":
             for j in range(i - 1, max(i - 1 - self.depth, 0), -1):
@@ -652,25 +602,10 @@ class ParamCoordinator:
         if not self._in_step:
             return
         self._in_step = False
-        if self.identity:
-            return
-        if self.keep:
-            for i, u in enumerate(self.units):
-                if i in self.lead:
-                    # switch to the copy gathered for this next micro-step; this one's slot is
-                    # re-gathered (for micro-step t+2) at t+1's start
-                    self._unbind(u)
-                    if u.states[u.slot] == "inflight":
-                        u.works[u.slot].wait()
-                        u.works[u.slot] = None
-                    u.states[u.slot] = "empty"
-                    u.slot = 1 - u.slot
-                elif u.params and u.states[u.slot] == "ready":
-                    self._release(i)  # keep: units without a backward (head / norm)
-                    self._issue(i)
-        else:
-            for i in range(self.last + 1):
-                self._release(i)
+        if self.identity or self.keep:
+            return  # keep: the gathered frozen weights stay resident
+        for i in range(self.last + 1):
+            self._release(i)
 
     def gather_all_full(self) -> None:
         """Materialise every unit (checkpoint save with gather_16bit_weights_on_model_save).
@@ -689,13 +624,12 @@ class ParamCoordinator:
                 self._pool_alloc -= 1
 
     def drain(self):
-        """Complete every in-flight gather (all slots): before process-group teardown."""
+        """Complete every in-flight gather: before process-group teardown."""
         for u in self.units:
-            for s, w in enumerate(u.works):
-                if w is not None:
-                    w.wait()
-                    u.works[s] = None
-                    u.states[s] = "ready"
+            if u.work is not None:
+                u.work.wait()
+                u.work = None
+                u.state = "ready"
 
 
 def units_dtype_bytes(units: Sequence[_Unit]) -> int:

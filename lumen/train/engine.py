@@ -103,12 +103,10 @@ class ZeroEngine:
             from ..models.layers import configure_backward_layout
 
             configure_backward_layout(model)  # TN input-gradient GEMMs for persistent weights
-            # ... and, opt-in, for gathered ones: W^T written on a side stream after each gather.
-            # Measured on one GPU (forced partitioning, profiles/r02_zero3): the side-stream
-            # transposes' HBM traffic costs the compute stream about what the TN GEMMs save
-            # (110.3 vs 109.8 ms/step), so the default keeps on-the-fly q|k|v / down transposes.
-            if (self.coordinator is not None
-                    and os.environ.get("LUMEN_ZERO3_OFFPATH_WT", "0") == "1"):
+            # ... and for resident (keep) gathered ones: W^T written once, on a side stream right
+            # after the unit's first gather, when HBM allows (release re-gathers every use and
+            # keeps the on-the-fly q|k|v / down transposes, Linear.transpose_gathered)
+            if self.coordinator is not None and self.coordinator.keep:
                 from ..models.layers import Linear
 
                 self.coordinator.enable_transposes(
@@ -315,6 +313,7 @@ class ZeroEngine:
                 hp = self.opt.host_coef(self._norm_buf, inv_scale, self.cfg.gradient_clipping)
                 if hp is not None:  # None: non-finite norm, counted as skipped
                     self.async_off.launch(grad, lr, *hp)
+                    self.flat.mark_updated()  # params land under the next forward's unit gates
                     launched = grad  # zeroed by the offload stream after its D2H
             else:
                 self.opt.step(grad, lr, inv_scale, self._norm_buf, self.cfg.gradient_clipping)
@@ -338,6 +337,7 @@ class ZeroEngine:
         master = self.opt.master
         if master.device != self.device:
             master = master.to(self.device, non_blocking=True)
+        self.flat.mark_updated()
         if not self.sharded:
             self.flat.param.copy_(master)
             return
@@ -365,8 +365,8 @@ class ZeroEngine:
             self.async_off.finish()
 
     def close(self):
-        """Complete in-flight ZeRO-3 gathers (the pipelined schedule keeps the next micro-step's
-        in flight) so the process groups can be torn down cleanly."""
+        """Complete in-flight ZeRO-3 gathers (prefetches issued ahead of their use) so the process
+        groups can be torn down cleanly."""
         self.sync_params()
         if self.coordinator is not None:
             self.coordinator.drain()

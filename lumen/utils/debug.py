@@ -18,9 +18,10 @@ pays nothing when they are off:
 ``LUMEN_ZERO3_POISON=1``   race detector for the ZeRO-3 gather schedules (also on under
                            ``LUMEN_DEBUG``): every gathered-weight buffer is filled with NaN on the
                            compute stream right before it is (re-)gathered, so a kernel that reads
-                           a buffer outside its live window -- the refresh of the keep schedule, the
-                           next-step slot of the pipelined one -- turns the loss NaN at once
-                           instead of silently reading identical-looking stale weights.
+                           a buffer outside its live window -- a release-ring buffer already
+                           handed to the next unit, a keep unit read before its first gather
+                           landed -- turns the loss NaN at once instead of silently reading
+                           identical-looking stale weights.
 ``LUMEN_FAULT_STEP=k``     fault injection: the rank(s) in ``LUMEN_FAULT_RANK`` (default 0) exit
                            with code 17 right after optimizer step k (after any checkpoint of
                            that step).  Used by the kill-and-resume equality test.
@@ -180,7 +181,7 @@ class StepWatchdog:
                f"(limit {self.timeout_s:.0f} s); a collective or kernel is hung.")
         c = self.coordinator
         if c is not None and not getattr(c, "identity", True):
-            inflight = sum(st == "inflight" for u in c.units for st in u.states)
+            inflight = sum(u.state == "inflight" for u in c.units)
             msg += (f" ZeRO-3 schedule '{c.schedule}', {inflight} weight gather(s) in flight on "
                     f"{'a separate' if c.group is not None else 'the default'} communicator.")
             if c.group is not None:

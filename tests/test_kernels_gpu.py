@@ -920,6 +920,52 @@ def test_llama_lora_fold_matches_unfolded(p_drop, monkeypatch):
     assert torch.equal(w1[:, :K], w2[:, :K]) and not torch.equal(w1[:, K:], w2[:, K:])
 
 
+@pytest.mark.parametrize("stage", [2, 3])
+def test_engine_steps_refresh_fold_tail(stage):
+    """The optimizer writes the adapters through the engine's flat buffer (views installed with
+    ``p.data``, whose version counters do not see those writes): every publish must still
+    refresh the folded weights' [s B] tail, so the forward after step k uses step k's lora_B
+    (stage 2: the cached [W | s B] copy; stage 3 at world 1: the tail of the unit's own rows)."""
+    import lumen.ops.lora as lora_mod
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+    from lumen.parallel.dist import init
+    from lumen.train.config import load_ds_config
+    from lumen.train.engine import ZeroEngine
+
+    assert lora_mod.FOLD
+    torch.manual_seed(0)
+    m = build_model("small-llama", dtype=torch.bfloat16, device=torch.device("cuda"), seed=3)
+    apply_lora(m, LoraConfig(r=16, lora_dropout=0.0))
+    m.train()
+    eng = ZeroEngine(m, load_ds_config({"zero_optimization": {"stage": stage}}, 2, 1, 1, 1e-2),
+                     init())
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(3, m.config.vocab_size, (2, 64), generator=g).cuda()
+    for _ in range(3):
+        loss = eng.forward({"input_ids": ids, "labels": torch.roll(ids, -1, 1)})
+        eng.backward(loss)
+        eng.step()
+    loss = eng.forward({"input_ids": ids, "labels": torch.roll(ids, -1, 1)})
+    eng.backward(loss)
+    torch.cuda.synchronize()
+    KP = lora_mod.FOLD_KP
+    n = 0
+    for _, mod in m.lora_modules():
+        W, K = mod.weight, mod.in_features
+        wext = (W.as_strided((W.shape[0], K + KP), (K + KP, 1)) if W.stride(0) == K + KP
+                else mod._wext)
+        if wext is None:
+            continue
+        want = torch.zeros(W.shape[0], K + KP, dtype=W.dtype, device=W.device)
+        mod._fill_tail(want)
+        assert want[:, K:].abs().sum() > 0  # lora_B moved off its zero init
+        torch.testing.assert_close(wext[:, K:], want[:, K:], rtol=0, atol=0)
+        n += 1
+    assert n > 0
+    eng.close()
+
+
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
 def test_lora3_dxa_delta_handoff_kernel(p_drop):
     """The o_proj fused dA + dx kernel's delta output == rowsum(dO * O) per 128-column head,

@@ -1,8 +1,8 @@
 """ZeRO-3 parameter coordinator on the GPU path (native kernels read the gathered weights at
 backward time through ``weight_fn``), on a one-GPU box: ``LUMEN_ZERO3_SINGLE=1`` partitions at
 world size 1, where a gather is an async copy on a side stream with the same stream ordering
-as RCCL's.  Every schedule (release / keep / pipelined), with accumulation and activation
-checkpointing, must give the stage-0 trajectory."""
+as RCCL's.  Every schedule (release / keep), with accumulation and activation checkpointing,
+must give the stage-0 trajectory."""
 import math
 
 import pytest
@@ -67,8 +67,7 @@ def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_
 
 
 @pytest.mark.parametrize("schedule,ckpt", [("release", False), ("keep", False),
-                                           ("pipelined", False), ("keep", True),
-                                           ("pipelined", True), ("release", True)])
+                                           ("keep", True), ("release", True)])
 def test_zero3_schedules_match_stage0_on_gpu(schedule, ckpt, monkeypatch):
     ref, ref_losses, _ = _train(monkeypatch, 0, ckpt=ckpt)
     # release: a live budget of one unit -> a ring of 2 buffers, nothing kept across the turn,
@@ -82,23 +81,19 @@ def test_zero3_schedules_match_stage0_on_gpu(schedule, ckpt, monkeypatch):
         # forward: every unit; backward: every layer (the head is consumed at the turn)
         assert coord.gathers == 8 * (n_units + n_units - 2)
     else:
-        # every micro-step re-gathers every unit (the shards are the only persistent copy);
-        # pipelined has the next micro-step's gathers issued already
-        extra = n_units if schedule == "pipelined" else 0
-        assert coord.gathers >= 8 * (n_units - 1) + extra
+        # keep: every unit gathered once, then resident (frozen weights never go stale)
+        assert coord.gathers == n_units
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 2e-2 * max(1.0, abs(b))
     for k in ref:
         torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)
 
 
-@pytest.mark.parametrize("schedule", ["keep", "pipelined"])
-def test_zero3_offpath_transposes_match_persistent_layout(schedule, monkeypatch):
-    """keep / pipelined: W^T of every gathered projection is written on a side stream right
-    after its gather, so the backward runs the same TN GEMMs as with persistent weights."""
-    monkeypatch.setenv("LUMEN_ZERO3_OFFPATH_WT", "1")
+def test_zero3_offpath_transposes_match_persistent_layout(monkeypatch):
+    """keep: W^T of every gathered projection is written once, on a side stream right after its
+    gather, so the backward runs the same TN GEMMs as with persistent weights."""
     ref, _, _ = _train(monkeypatch, 0, bwd_wt="all", ckpt=True)
-    got, _, coord = _train(monkeypatch, 3, schedule, bwd_wt="all", ckpt=True)
+    got, _, coord = _train(monkeypatch, 3, "keep", bwd_wt="all", ckpt=True)
     assert coord.transposed_numel > 0
     assert sum(len(u.tn) for u in coord.units) == 4 * sum(1 for u in coord.units[1:-1])
     for k in ref:
@@ -130,7 +125,7 @@ def test_reference_zero3_config_with_cpu_offload(monkeypatch):
         assert (d > 3e-4 + 5e-3 * ref[k].abs()).float().mean().item() < 5e-3, k
 
 
-@pytest.mark.parametrize("schedule", ["keep", "pipelined", "release"])
+@pytest.mark.parametrize("schedule", ["keep", "release"])
 def test_zero3_schedules_race_free_under_nan_poison(schedule, monkeypatch):
     """Race detector: with LUMEN_ZERO3_POISON every buffer is NaN-filled right before each
     (re-)gather.  A read outside a buffer's live window would make the loss NaN; the run must
@@ -149,12 +144,13 @@ def test_zero3_schedules_race_free_under_nan_poison(schedule, monkeypatch):
         torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)
 
 
-@pytest.mark.parametrize("schedule", ["pipelined", "release"])
+@pytest.mark.parametrize("schedule", ["keep", "release"])
 def test_zero3_gathered_lora_fold(schedule, monkeypatch):
     """LoRA fold on ZeRO-3-gathered weights: the partitioned layout reserves the [N, K + 64]
-    adapter tail, the coordinator fills it (s * lora_B) at every bind, and one micro-step's loss
-    and adapter gradients equal the unfolded UP write-back's (gradients compared before any
-    optimizer step, where bf16 rounding is not amplified)."""
+    adapter tail, it is (re)filled with s * lora_B after every gather and whenever lora_B
+    changes, and one micro-step's loss and adapter gradients equal the unfolded UP write-back's
+    (gradients compared before any optimizer step, where bf16 rounding is not amplified).
+    keep: after an optimizer step the resident weights' tails hold the NEW lora_B."""
     import lumen.ops.lora as lora_mod
     from lumen.lora import LoraConfig, apply_lora
     from lumen.models import build_model
@@ -191,6 +187,22 @@ def test_zero3_gathered_lora_fold(schedule, monkeypatch):
         grads = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.requires_grad}
         out.append((float(loss), grads))
         eng.step()
+        if fold:
+            eng.sync_params()
+            loss = eng.forward({"input_ids": ids, "labels": torch.roll(ids, -1, 1)})
+            eng.backward(loss)
+            torch.cuda.synchronize()
+            KP = lora_mod.FOLD_KP
+            for u in coord.units[1:-1]:
+                for lin in u.folds:
+                    W = lin.weight
+                    if W.numel() == 0:   # release: unit handed back to the ring
+                        continue
+                    K = lin.in_features
+                    tail = W.as_strided((W.shape[0], K + KP), (K + KP, 1))[:, K:]
+                    want = torch.zeros(W.shape[0], K + KP, dtype=W.dtype, device=W.device)
+                    lin._fill_tail(want)
+                    torch.testing.assert_close(tail, want[:, K:], rtol=0, atol=0)
         eng.close()
     (l1, g1), (l2, g2) = out
     assert abs(l1 - l2) < 2e-3 * abs(l2)
