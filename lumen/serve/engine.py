@@ -160,8 +160,7 @@ class LLMEngine:
         self.async_sched = bool(cfg.async_scheduling and self.tp == 1)
         self._inflight: Optional[dict] = None
         self.scheduler = Scheduler(SchedulerConfig(
-            cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
-            decode_outside_budget=self.runner.overlaps_mixed_steps()), self.blocks)
+            cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len), self.blocks)
         if tokenizer is None:
             from ..data.tokenizer import load_tokenizer
 

@@ -113,7 +113,6 @@ class StepInput:
         return self.cu_seqlens[-1] if self.cu_seqlens else 0
 
 
-SERVE_OVERLAP = os.environ.get("LUMEN_SERVE_OVERLAP", "1") != "0"
 
 
 def kv_bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2, tp_size: int = 1) -> int:
@@ -175,7 +174,6 @@ class ModelRunner:
         # cost no LDS
         self.partition = int(os.environ.get("LUMEN_PA_PARTITION", "2048"))
         self.lora = None  # serve.multi_lora.MultiLoRA when adapters are served un-merged
-        self._dstream = None  # decode-row stream of overlapped mixed steps
 
     # ------------------------------------------------------------------------------------------
     def check_collectives(self) -> None:
@@ -247,48 +245,12 @@ class ModelRunner:
     # ---- mixed step: prefill chunks (whole prompts or pieces of long ones) + decode rows -----
     @torch.no_grad()
     def execute(self, inp: StepInput) -> torch.Tensor:
-        """Logits [len(sample_rows), V] of one mixed step (see StepInput).
-
-        With decode rows and a captured decode graph (TP = 1, no multi-LoRA), the decode rows
-        run as that graph on a second stream WHILE the prefill chunk runs on the current one:
-        the chunk's GEMMs are compute-bound, the decode rows' paged attention streams the whole
-        KV cache (memory-bound), so the two overlap on the chip instead of taking turns inside
-        one forward (``LUMEN_SERVE_OVERLAP=0``: one merged forward)."""
-        T = inp.tokens.shape[0]
-        Tp = inp.num_prefill_rows
-        N = T - Tp
-        if (SERVE_OVERLAP and Tp and N and self.use_graphs and self.tp == 1
-                and inp.lora_ids is None and N <= self.graph_buckets[-1]
-                and inp.tokens.is_cuda and inp.sample_rows is not None):
-            return self._execute_overlapped(inp, Tp, N)
+        """Logits [len(sample_rows), V] of one mixed step (see StepInput): prefill chunk and
+        decode rows in ONE forward (every weight read once for both).  (Running the decode rows
+        as their graph on a second stream concurrently with the chunk measured worse: 7.46k vs
+        7.55k tok/s and ITL p99 64 vs 40 ms at 256 x 512 / 128, profiles/r3_serve -- the chunk's
+        GEMMs already fill the chip, and the decode rows then waited for a full-budget chunk.)"""
         return self._execute(inp)
-
-    def overlaps_mixed_steps(self) -> bool:
-        """Mixed steps run their decode rows concurrently with the prefill chunk (the engine's
-        scheduler then budgets the prefill chunk alone).  Not with un-merged multi-LoRA."""
-        return (SERVE_OVERLAP and self.use_graphs and self.tp == 1 and self.lora is None
-                and self.device.type == "cuda")
-
-    def _execute_overlapped(self, inp: StepInput, Tp: int, N: int) -> torch.Tensor:
-        n_done = inp.sample_rows.numel() - N   # completing prefills come first in sample_rows
-        cur = torch.cuda.current_stream(self.device)
-        if self._dstream is None:
-            self._dstream = torch.cuda.Stream(device=self.device)
-        ds = self._dstream
-        ds.wait_stream(cur)    # step inputs (incl. device-gathered decode tokens) are ready
-        dec = StepInput("decode", inp.tokens[Tp:], inp.positions[Tp:], inp.slots[Tp:], [0],
-                        block_tables=inp.block_tables, context_lens=inp.context_lens,
-                        max_context=inp.max_context)
-        with torch.cuda.stream(ds):
-            dlog = self.decode(dec)
-        pre = StepInput("mixed", inp.tokens[:Tp], inp.positions[:Tp], inp.slots[:Tp],
-                        inp.cu_seqlens, kv_lens=inp.kv_lens, kv_lens_t=inp.kv_lens_t,
-                        prefill_tables=inp.prefill_tables, sample_rows=inp.sample_rows[:n_done])
-        plog = self._execute(pre)
-        cur.wait_stream(ds)
-        # (the graph's static output is read here, on the current stream, before the next
-        # replay: the next step's decode stream waits for this stream first)
-        return torch.cat([plog, dlog], 0)
 
     def _execute(self, inp: StepInput) -> torch.Tensor:
         h = embedding(inp.tokens, self.w.embed)

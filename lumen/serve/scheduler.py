@@ -34,10 +34,6 @@ class SchedulerConfig:
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 2048
     max_model_len: int = 4096
-    # the runner executes decode rows concurrently with the prefill chunk (overlapped mixed
-    # steps): the token budget then bounds the PREFILL chunk alone, which also keeps the chunk's
-    # GEMMs at the tuned M = budget instead of a different M every step
-    decode_outside_budget: bool = False
 
 
 @dataclass
@@ -112,8 +108,7 @@ class Scheduler:
                         batch.decodes.remove(victim)
                     if victim is s:
                         break
-        if not self.cfg.decode_outside_budget:
-            budget -= len(batch.decodes)
+        budget -= len(batch.decodes)
         # 2) continue partially cached prompts, then admit waiting requests (FCFS)
         for s in self.running:
             if budget <= 0:

@@ -111,45 +111,3 @@ def test_multi_lora_graph_decode_matches_merged(tmp_path):
         ref = full[len(p) - 1:].argmax(-1).tolist()
         agree = sum(int(a == b) for a, b in zip(ref, s.output_ids)) / len(ref)
         assert agree >= 0.85, (i, agree)
-
-
-def test_overlapped_mixed_steps_match_merged(monkeypatch):
-    """Mixed steps with the decode rows as a graph on a second stream, concurrent with the
-    prefill chunk (LUMEN_SERVE_OVERLAP, default) vs one merged forward: same greedy tokens
-    (teacher-forced check against the full forward), and the overlapped path really ran."""
-    import lumen.serve.model_runner as mr
-    from lumen.models import build_model
-    from lumen.serve.engine import EngineConfig, LLMEngine
-    from lumen.serve.sequence import SamplingParams
-
-    dev = torch.device("cuda", 0)
-    m = build_model("tiny-llama-gqa", dtype=torch.bfloat16, device=dev, init="random", seed=3)
-    m.eval()
-    prompts = [[5, 9, 33, 7] * 10, list(range(3, 60)), [42, 43], list(range(100, 190))]
-    outs = {}
-    for ov in (False, True):
-        monkeypatch.setattr(mr, "SERVE_OVERLAP", ov)
-        eng = LLMEngine(EngineConfig(model="tiny-llama-gqa", device="cuda", max_model_len=512,
-                                     block_size=16, num_blocks=128, use_graphs=True,
-                                     max_num_batched_tokens=40), model=m)
-        calls = []
-        orig = eng.runner._execute_overlapped
-        eng.runner._execute_overlapped = lambda *a: (calls.append(1), orig(*a))[1]
-        seqs = []
-        for p in prompts:  # staggered arrivals: chunks of new prompts ride with decode rows
-            seqs.append(eng.add_request(p, SamplingParams(max_tokens=12, temperature=0.0,
-                                                          ignore_eos=True)))
-            eng.step()
-        while eng.has_work:
-            eng.step()
-        outs[ov] = [s.output_ids for s in seqs]
-        assert bool(calls) == ov
-        for p, s in zip(prompts, seqs):
-            ids = torch.tensor([p + s.output_ids[:-1]], device=dev)
-            with torch.no_grad():
-                full = m(ids).float().view(ids.shape[1], -1)
-            ref = full[len(p) - 1:].argmax(-1).tolist()
-            agree = sum(int(a == b) for a, b in zip(ref, s.output_ids)) / len(ref)
-            assert agree >= 0.9, (ov, agree)
-    same = sum(a == b for x, y in zip(outs[False], outs[True]) for a, b in zip(x, y))
-    assert same >= 0.9 * sum(len(x) for x in outs[False])
