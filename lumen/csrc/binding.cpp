@@ -63,8 +63,6 @@ hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, con
                             void*, const long long*, int, int, int, int, int, int, hipStream_t);
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
-hipError_t lumen_batch_gemm(int, const void*, const void*, void*, int, int, int, long long,
-                            long long, hipStream_t);
 void lumen_set_gemv_form(int);
 void lumen_set_rms_lds(int, int);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
@@ -209,20 +207,6 @@ void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
                           static_cast<int>(x.size(0)), static_cast<int>(w.size(0)),
                           static_cast<int>(w.size(1)), x.stride(0), y.stride(0), cur_stream()),
         "skinny_gemm");
-}
-
-void batch_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
-  if (!x.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: batch_gemm needs GPU tensors");
-  need_cuda(w, "w");  // x / y may be row-strided views (unit column stride checked below)
-  if (x.dim() != 2 || w.dim() != 2 || y.dim() != 2 || x.stride(1) != 1 || y.stride(1) != 1 ||
-      !w.is_contiguous() || x.size(1) != w.size(1) || y.size(0) != x.size(0) ||
-      y.size(1) != w.size(0) || x.scalar_type() != w.scalar_type() ||
-      y.scalar_type() != w.scalar_type())
-    throw std::invalid_argument("lumen: batch_gemm shape/layout mismatch");
-  check(lumen_batch_gemm(dcode(w), x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                         static_cast<int>(x.size(0)), static_cast<int>(w.size(0)),
-                         static_cast<int>(w.size(1)), x.stride(0), y.stride(0), cur_stream()),
-        "batch_gemm");
 }
 
 void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
@@ -841,7 +825,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora2", &lora2);
   m.def("transpose2d", &transpose2d);
   m.def("skinny_gemm", &skinny_gemm);
-  m.def("batch_gemm", &batch_gemm);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
   m.def("set_rms_lds", [](int64_t f, int64_t b) {
     lumen_set_rms_lds(static_cast<int>(f), static_cast<int>(b));

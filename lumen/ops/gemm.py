@@ -2,8 +2,8 @@
 
 At decode batch 1-4 the projection is a pure stream of the weight matrix; for the shapes where it
 measured faster the HIP weight-streaming kernel (``kernels/skinny_gemm.hip``) runs it instead
-of a library GEMM.  Batches 5-256 run the MFMA batch GEMM (``kernels/batch_gemm.hip``); larger
-batches (prefill, training) and CPU tensors go to ``torch.matmul`` (hipBLASLt, tuned table)."""
+of a library GEMM.  Larger batches (and CPU tensors) go to ``torch.matmul`` (hipBLASLt with the
+tuned table)."""
 from __future__ import annotations
 
 import os
@@ -35,21 +35,11 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
                  if x.shape[0] <= 4 else w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0))
 
 
-# Decode batches 5..256: the MFMA batch GEMM (kernels/batch_gemm.hip: all M rows per workgroup,
-# ~one workgroup per CU, W streamed once through LDS) where it measured faster than hipBLASLt
-# with the tuned table (lumen/bench/batch_gemm_bench.py, profiles/r3_serve).  (An earlier
-# decode-batch kernel with 32-row M tiles, scripts/probes/decode_gemm.hip, lost 2x from M = 64:
-# each of its column tiles re-read x from L2 once per M tile.)
-BATCH_GEMM = os.environ.get("LUMEN_BATCH_GEMM", "0") != "0"
-BATCH_MIN_M = int(os.environ.get("LUMEN_BATCH_GEMM_MIN_M", "5"))
-
-
-def batch_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (BATCH_GEMM and BATCH_MIN_M <= x.shape[0] <= 256 and use_native(x) and x.dim() == 2
-            and w.dim() == 2 and x.dtype == w.dtype and x.dtype in (torch.bfloat16, torch.float16)
-            and x.stride(1) == 1 and w.is_contiguous() and x.shape[1] == w.shape[1]
-            and w.shape[0] % 16 == 0 and w.shape[1] % 256 == 0 and x.stride(0) % 8 == 0
-            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+# Decode batches 5..256: hipBLASLt with the tuned table.  Two hand-written decode-batch MFMA GEMMs
+# measured slower (scripts/probes/): decode_gemm.hip (32-row M tiles) lost 2x from M = 64, and
+# batch_gemm.hip (all M rows per workgroup, ~one workgroup per CU, W through LDS) reached only
+# 3.7-4.7 TB/s at M <= 64 and fell to 1.5 TB/s at M = 256 as every workgroup re-reads x
+# (profiles/r3_serve/batch_gemm_sweep.jsonl; serving 6.6k vs 7.6k tok/s with it).
 
 
 # Training-shape GEMMs run 256 x 256 macro tiles, one per CU at a time, so a GEMM with 5.375 or
@@ -136,10 +126,6 @@ def linear_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if skinny_ok(x, w):
         y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
         native().skinny_gemm(x, w, y)
-        return y
-    if batch_ok(x, w):
-        y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
-        native().batch_gemm(x, w, y)
         return y
     return torch.matmul(x, w.t())
 

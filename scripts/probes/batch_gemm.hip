@@ -1,3 +1,7 @@
+// PROBE, NOT BUILT (moved out of lumen/csrc/kernels after measuring it against hipBLASLt):
+// 3.7-4.7 TB/s at M <= 64 (hipBLASLt with the tuned table ties or wins), 1.5 TB/s at M = 256 where
+// every workgroup re-reads all of x from L2 (q|k|v 68 vs 38 us); serving 6.6k vs 7.6k tok/s
+// with it (profiles/r3_serve/batch_gemm_sweep.jsonl).  Kept for the record of what was tried.
 // Decode-batch GEMM on the matrix cores: y[M, N] = x[M, K] @ W[N, K]^T for 5 <= M <= 256.
 //
 // Reference behaviour: vLLM's decode projections (the serving stack the reference declares,

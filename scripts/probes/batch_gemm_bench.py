@@ -1,4 +1,7 @@
-"""Decode-batch projections: the MFMA batch GEMM (kernels/batch_gemm.hip) vs hipBLASLt with the
+"""(Probe: needs scripts/probes/batch_gemm.hip built into the extension with a `batch_gemm`
+binding; it is not part of the shipped build.)
+
+Decode-batch projections: the MFMA batch GEMM (kernels/batch_gemm.hip) vs hipBLASLt with the
 tuned table, Llama-2-7B shapes (q|k|v, o, gate|up, down, lm_head) at M = 8..256.
 
     python -m lumen.bench.batch_gemm_bench [--ms 8,16,...] > out.jsonl

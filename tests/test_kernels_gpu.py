@@ -661,35 +661,6 @@ def test_skinny_gemm(M, N, K):
     assert rel(yv, xv.float() @ w.float().t()) < 1e-2
 
 
-@pytest.mark.parametrize("M", [5, 17, 64, 100, 200, 256])
-@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (22016, 256), (4112, 512),
-                                 (32000, 4096)])
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_batch_gemm(M, N, K, dtype, monkeypatch):
-    """Decode-batch MFMA GEMM (kernels/batch_gemm.hip) vs an f32 reference: every M-block count
-    (1-4 x 64 rows, ragged M), the column-block widths the launcher picks (N = 4096 / 12288 /
-    22016 / 32000; 4112 = a ragged last tile), strided x / y views, and the linear_nt dispatch."""
-    from lumen.ops._native import native
-    from lumen.ops.gemm import batch_ok, linear_nt
-
-    g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
-    xb = torch.randn(M, K + 64, device=DEV, generator=g).to(dtype)
-    x = xb[:, :K]                                    # row stride K + 64
-    w = (torch.randn(N, K, device=DEV, generator=g) * 0.02).to(dtype)
-    ref = x.float() @ w.float().t()
-    yb = torch.full((M, N + 32), 7.0, device=DEV, dtype=dtype)
-    y = yb[:, :N]
-    native().batch_gemm(x, w, y)
-    assert rel(y, ref) < 1e-2
-    assert torch.all(yb[:, N:] == 7.0)               # nothing written past the view
-    import lumen.ops.gemm as gemm_mod
-
-    monkeypatch.setattr(gemm_mod, "BATCH_GEMM", True)
-    assert batch_ok(x.contiguous(), w)
-    y2 = linear_nt(x.contiguous(), w)
-    assert rel(y2, ref) < 1e-2
-
-
 @pytest.mark.parametrize("N,F", [(4096, 11008), (1024, 2752)])
 def test_swiglu_down_projection(N, F):
     """Batch-1 MLP down projection of the serving path: SwiGLU kernel + weight-streaming GEMV ==
