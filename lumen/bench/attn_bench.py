@@ -24,9 +24,7 @@ def main():
     ap.add_argument("--only", default="all")
     a = ap.parse_args()
     D = 128
-    res = {"fwd_kernel": os.environ.get("LUMEN_FA_FWD", "v32"),
-           "bwd_kernel": os.environ.get("LUMEN_FA_BWD", "mix"), "B": a.B, "S": a.S, "nh": a.nh,
-           "nkv": a.nkv}
+    res = {"B": a.B, "S": a.S, "nh": a.nh, "nkv": a.nkv}
     dev = "cuda"
     T = a.B * a.S
     qkv = (torch.randn(T, (a.nh + 2 * a.nkv) * D, device=dev) * 0.5).to(torch.bfloat16)

@@ -331,9 +331,6 @@ struct Args {
   int tiles3;
   int nitems;  // > 0: persistent dK/dV launch over nitems = ntiles * nkv items (1-D grid)
   int snake;   // persistent item order: 1 snake rounds, 0 plain strided
-  int probe;  // cost probes (0 in production; LUMEN_FA_PROBE, dK/dV kernel only): 1 no DMA after
-              // step 1, 2 no S / dP products, 4 no dV / dK products, 8 no exp, 16 no dS
-              // stores, 32 no dK / dV epilogue stores, 128 no steps (prologue + epilogue only)
 };
 
 struct Work { int seq, r0, head; };
@@ -353,166 +350,8 @@ __device__ __forceinline__ void rope_inv_pair(float& lo, float& hi, float c, flo
   hi = h * c - l * s;
 }
 
-// =============================================================================================
-// forward
-// =============================================================================================
-template <typename T, bool CAUSAL, int MT>
-__global__ void __launch_bounds__(256, 2) fwd_kernel(Args a) {
-  constexpr int QW = 16 * MT;        // query rows per wave
-  constexpr int BM = 4 * QW;         // query rows per workgroup
-  constexpr int YCOLS = QW;          // P^T scratch: [64 keys][QW queries]
-  constexpr int YB = BN * (YCOLS + 4) * 2;  // bytes of one wave's Y scratch
-  // [K0 | V0 | K1 | V1 | Y x 4]: K/V double-buffered, filled by LDS-DMA one tile ahead
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 4 * YB];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
-  char* y = smem + 4 * IMG + wid * YB;
-  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
-  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
-  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
-  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
-  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
-  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
-  const int wq0 = q0 + wid * QW;     // first query row of this wave
-
-  uint4 qf[MT][4];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = wq0 + mt * 16 + lr;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      qf[mt][ks] = gload16(Q + (long long)row * a.ldq + (4 * ks + lg) * 8, row < L);
-  }
-  f32x4 acc[MT][8];
-  float m_i[MT][4], l_i[MT][4];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-    for (int n = 0; n < 8; ++n) acc[mt][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { m_i[mt][r] = -INFINITY; l_i[mt][r] = 0.f; }
-  }
-  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
-  if (kv_end > 0) {
-    stage64_async(smem, K, a.ldk, 0, L);
-    stage64_async(smem + IMG, V, a.ldv, 0, L);
-  }
-  int it = 0;
-  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
-    char* kimg = smem + (it & 1) * 2 * IMG;
-    char* vimg = kimg + IMG;
-    if (kv0 + BN < kv_end) {  // prefetch the next tile into the other buffer, then wait for this one
-      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
-      stage64_async(nk, K, a.ldk, kv0 + BN, L);
-      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
-      wait_vm_8();
-    } else {
-      wait_vm_all();
-    }
-    lds_fence_barrier();
-    // S = Q K^T   [QW x 64] per wave
-    f32x4 s[MT][4];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) s[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const uint4 b = row_read(kimg, nt * 16 + lr, 4 * ks + lg);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) s[mt][nt] = Mfma<T>::run(qf[mt][ks], b, s[mt][nt]);
-      }
-    }
-    // online softmax (exp2 domain); rows of this lane: wq0 + 16mt + 4lg + r
-    // masking only where a key can be past the sequence end or above this wave's first row
-    const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      float pr[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qrow = wq0 + mt * 16 + 4 * lg + r;
-        float mx = -INFINITY;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          float x = s[mt][nt][r] * a.scale_log2;
-          if (need_mask) {
-            const int kpos = kv0 + nt * 16 + lr;
-            if (kpos >= L || (CAUSAL && kpos > qrow)) x = -INFINITY;
-          }
-          pr[nt][r] = x;
-          mx = fmaxf(mx, x);
-        }
-        mx = red16_max(mx);
-        const float m_new = fmaxf(m_i[mt][r], mx);
-        const float alpha = (m_new == -INFINITY) ? 1.f : fexp2(m_i[mt][r] - m_new);
-        float rs = 0.f;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const float p = (m_new == -INFINITY) ? 0.f : fexp2(pr[nt][r] - m_new);
-          pr[nt][r] = p;
-          rs += p;
-        }
-        rs = red16_sum(rs);
-        l_i[mt][r] = l_i[mt][r] * alpha + rs;
-        m_i[mt][r] = m_new;
-#pragma unroll
-        for (int n = 0; n < 8; ++n) acc[mt][n][r] *= alpha;
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        y_store<T>(y, YCOLS, nt * 16, mt * 16, lane, pr[nt][0], pr[nt][1], pr[nt][2], pr[nt][3]);
-    }
-    // Y is per-wave: the wave's own LDS writes must land before its transposed reads
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // O += P V
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      uint4 pa[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) pa[mt] = tr_read_y(y, YCOLS, 32 * ks, mt * 16, lane);
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const uint4 b = tr_read_img(vimg, 32 * ks, n * 16, lane);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt][n] = Mfma<T>::run(pa[mt], b, acc[mt][n]);
-      }
-    }
-    lds_fence_barrier();  // every wave is done with this K/V buffer before it is refilled
-  }
-  // epilogue: O /= l ; LSE (log2) per row
-  T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qrow = wq0 + mt * 16 + 4 * lg + r;
-      if (qrow >= L) continue;
-      const float inv = l_i[mt][r] > 0.f ? 1.f / l_i[mt][r] : 0.f;
-#pragma unroll
-      for (int n = 0; n < 8; ++n)
-        O[(long long)qrow * a.ldo + n * 16 + lr] = from_f32<T>(acc[mt][n][r] * inv);
-      if (lr == 0 && a.lse)
-        a.lse[(long long)head * a.T + s0 + qrow] =
-            l_i[mt][r] > 0.f ? m_i[mt][r] + __log2f(l_i[mt][r]) : INFINITY;
-    }
-  }
-}
-
-// =============================================================================================
-// forward, transposed formulation
-// =============================================================================================
-// S^T = K Q^T puts one query per lane column: lane (L, g) holds 16 scores of query L (keys
-// nt*16 + 4g + r), so the row max / sum are 15 in-register ops plus two cross-lane steps, the
-// online-softmax rescale is a per-lane scalar, and P never leaves registers: it is directly the
-// B operand of O^T += V^T P^T once V's transposed LDS reads use the same key order
-// (k-slot 8g + e <-> key 32ks + 4g + e for e < 4, 32ks + 16 + 4g + (e - 4) otherwise).
-// Removes the P round trip through LDS and ~3/4 of the softmax VALU work of fwd_kernel.
-
-// V^T operand rows for the permuted key order: lane (L, g) gets column n0 + L of rows
-// rlo + 0..3 (lo) and rhi + 0..3 (hi)
+// V^T operand rows for the permuted key order (the dK/dV kernel): lane (L, g) gets column
+// n0 + L of rows rlo + 0..3 (lo) and rhi + 0..3 (hi)
 template <int SW = 0>
 __device__ __forceinline__ uint4 tr_read_img2(const char* img, int rlo, int rhi, int n0, int lane) {
   const int L = lane & 15;
@@ -526,144 +365,6 @@ __device__ __forceinline__ uint4 tr_read_img2(const char* img, int rlo, int rhi,
 template <typename T>
 __device__ __forceinline__ uint4 pack_p(const f32x4& a, const f32x4& b) {
   return make_uint4(pk2<T>(a[0], a[1]), pk2<T>(a[2], a[3]), pk2<T>(b[0], b[1]), pk2<T>(b[2], b[3]));
-}
-
-template <typename T, bool CAUSAL, int QG>
-__global__ void __launch_bounds__(256, 2) fwd_t_kernel(Args a) {
-  constexpr int BM = 64 * QG;        // query rows per workgroup (16 * QG per wave)
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [K0 | V0 | K1 | V1]
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
-  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
-  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
-  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
-  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
-  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
-  const int wq0 = q0 + wid * 16 * QG;  // first query row of this wave
-
-  uint4 qf[QG][4];
-  int qrow[QG];
-#pragma unroll
-  for (int qg = 0; qg < QG; ++qg) {
-    qrow[qg] = wq0 + qg * 16 + lr;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      qf[qg][ks] = gload16(Q + (long long)qrow[qg] * a.ldq + (4 * ks + lg) * 8, qrow[qg] < L);
-  }
-  f32x4 acc[QG][8];
-  float m_i[QG], l_i[QG];
-#pragma unroll
-  for (int qg = 0; qg < QG; ++qg) {
-#pragma unroll
-    for (int n = 0; n < 8; ++n) acc[qg][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    m_i[qg] = -INFINITY;
-    l_i[qg] = 0.f;
-  }
-  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
-  if (kv_end > 0) {
-    stage64_async(smem, K, a.ldk, 0, L);
-    stage64_async(smem + IMG, V, a.ldv, 0, L);
-  }
-  int it = 0;
-  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
-    char* kimg = smem + (it & 1) * 2 * IMG;
-    char* vimg = kimg + IMG;
-    if (kv0 + BN < kv_end) {
-      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
-      stage64_async(nk, K, a.ldk, kv0 + BN, L);
-      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
-      wait_vm_8();
-    } else {
-      wait_vm_all();
-    }
-    lds_fence_barrier();
-    // S^T = K Q^T: per query group 4 key tiles of 16
-    f32x4 st[QG][4];
-#pragma unroll
-    for (int qg = 0; qg < QG; ++qg)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) st[qg][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const uint4 kf = row_read(kimg, nt * 16 + lr, 4 * ks + lg);
-#pragma unroll
-        for (int qg = 0; qg < QG; ++qg) st[qg][nt] = Mfma<T>::run(kf, qf[qg][ks], st[qg][nt]);
-      }
-    }
-    const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
-    uint4 pf[QG][2];
-#pragma unroll
-    for (int qg = 0; qg < QG; ++qg) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = st[qg][nt][r] * a.scale_log2;
-          if (need_mask) {
-            const int kpos = kv0 + nt * 16 + 4 * lg + r;
-            if (kpos >= L || (CAUSAL && kpos > qrow[qg])) x = -INFINITY;
-          }
-          st[qg][nt][r] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_i[qg], mx);
-      const float mref = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = fexp2(m_i[qg] - mref);
-      float rs = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = fexp2(st[qg][nt][r] - mref);
-          st[qg][nt][r] = p;
-          rs += p;
-        }
-      rs += __shfl_xor(rs, 16);
-      rs += __shfl_xor(rs, 32);
-      l_i[qg] = l_i[qg] * alpha + rs;
-      m_i[qg] = m_new;
-      if (__any(alpha != 1.f)) {
-#pragma unroll
-        for (int n = 0; n < 8; ++n) acc[qg][n] *= alpha;
-      }
-      pf[qg][0] = pack_p<T>(st[qg][0], st[qg][1]);
-      pf[qg][1] = pack_p<T>(st[qg][2], st[qg][3]);
-    }
-    // O^T += V^T P^T
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const uint4 vf = tr_read_img2(vimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane);
-#pragma unroll
-        for (int qg = 0; qg < QG; ++qg) acc[qg][n] = Mfma<T>::run(vf, pf[qg][ks], acc[qg][n]);
-      }
-    }
-    lds_fence_barrier();  // every wave is done with this K/V buffer before it is refilled
-  }
-  // epilogue: lane (L, g) holds O[query L][d = 16n + 4g + r]
-  T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D;
-#pragma unroll
-  for (int qg = 0; qg < QG; ++qg) {
-    if (qrow[qg] >= L) continue;
-    const float inv = l_i[qg] > 0.f ? 1.f / l_i[qg] : 0.f;
-#pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      struct alignas(8) O4 { T v[4]; } o4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o4.v[r] = from_f32<T>(acc[qg][n][r] * inv);
-      *reinterpret_cast<O4*>(O + (long long)qrow[qg] * a.ldo + n * 16 + 4 * lg) = o4;
-    }
-    if (lg == 0 && a.lse)
-      a.lse[(long long)head * a.T + s0 + qrow[qg]] =
-          l_i[qg] > 0.f ? m_i[qg] + __log2f(l_i[qg]) : INFINITY;
-  }
 }
 
 // =============================================================================================
@@ -908,97 +609,6 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     const Work wk = work_item(a);
     if (wk.seq < 0) return;
     run(wk.seq, wk.r0, wk.head);
-  }
-}
-
-// =============================================================================================
-// backward: dQ  (workgroup = 64 queries of one head; loops over key tiles)
-// =============================================================================================
-template <typename T, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2) bwd_dq_kernel(Args a) {
-  // S^T = K Q^T and dP^T = V dO^T with the keys as MFMA rows: lane (query L, keys 4g + r) holds
-  // its query's dS row in the permuted-k order, the A operand of dQ += dS K without LDS.
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int seq = a.tiles[2 * blockIdx.x], q0 = a.tiles[2 * blockIdx.x + 1];
-  const int head = blockIdx.y, kvh = head / (a.nh / a.nkv);
-  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
-  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
-  const T* dO = reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D;
-  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
-  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
-  const int wq0 = q0 + wid * 16;
-  const int qrow = wq0 + lr;  // this lane's query
-  uint4 qf[4], of[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    qf[ks] = gload16(Q + (long long)qrow * a.ldq + (4 * ks + lg) * 8, qrow < L);
-    of[ks] = gload16(dO + (long long)qrow * a.lddo + (4 * ks + lg) * 8, qrow < L);
-  }
-  const float lse_q = qrow < L ? a.lse[(long long)head * a.T + s0 + qrow] : INFINITY;
-  const float del_q = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
-  f32x4 dq[8];
-#pragma unroll
-  for (int n = 0; n < 8; ++n) dq[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kv_end = CAUSAL ? min(L, q0 + 64) : L;
-  wait_vm_all();  // Q / dO fragments and row statistics are in registers before the DMA ring starts
-  if (kv_end > 0) {
-    stage64_async(smem, K, a.ldk, 0, L);
-    stage64_async(smem + IMG, V, a.ldv, 0, L);
-  }
-  int it = 0;
-  for (int kv0 = 0; kv0 < kv_end; kv0 += BN, ++it) {
-    char* kimg = smem + (it & 1) * 2 * IMG;
-    char* vimg = kimg + IMG;
-    if (kv0 + BN < kv_end) {
-      char* nk = smem + ((it + 1) & 1) * 2 * IMG;
-      stage64_async(nk, K, a.ldk, kv0 + BN, L);
-      stage64_async(nk + IMG, V, a.ldv, kv0 + BN, L);
-      wait_vm_8();
-    } else {
-      wait_vm_all();
-    }
-    lds_fence_barrier();
-    f32x4 s[4], dp[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) { s[nt] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[nt] = s[nt]; }
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        s[nt] = Mfma<T>::run(row_read(kimg, nt * 16 + lr, 4 * ks + lg), qf[ks], s[nt]);
-        dp[nt] = Mfma<T>::run(row_read(vimg, nt * 16 + lr, 4 * ks + lg), of[ks], dp[nt]);
-      }
-    }
-    const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kpos = kv0 + nt * 16 + 4 * lg + r;
-        float pv = fexp2(s[nt][r] * a.scale_log2 - lse_q);
-        if (need_mask && (kpos >= L || qrow >= L || (CAUSAL && kpos > qrow))) pv = 0.f;
-        s[nt][r] = pv * (dp[nt][r] - del_q);
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint4 da = pack_p<T>(s[2 * ks], s[2 * ks + 1]);
-#pragma unroll
-      for (int n = 0; n < 8; ++n)
-        dq[n] = Mfma<T>::run(da, tr_read_img2(kimg, 32 * ks + 4 * lg, 32 * ks + 16 + 4 * lg, n * 16, lane), dq[n]);
-    }
-    lds_fence_barrier();
-  }
-  T* dQ = reinterpret_cast<T*>(a.dq) + (long long)s0 * a.lddq + head * D;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qr = wq0 + 4 * lg + r;
-    if (qr >= L) continue;
-#pragma unroll
-    for (int n = 0; n < 8; ++n)
-      dQ[(long long)qr * a.lddq + n * 16 + lr] = from_f32<T>(dq[n][r] * a.scale);
   }
 }
 
@@ -1329,150 +939,6 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
 }
 
 template <typename T, bool CAUSAL, bool MASK>
-__device__ __forceinline__ void dkdv32_block(const char* qimg, const char* oimg,
-                                             const float* s_lse, const float* s_del,
-                                             const Off32& off, const uint4 (&kf)[8],
-                                             const uint4 (&vf)[8], f32x16 (&dk)[4],
-                                             f32x16 (&dv)[4], int qb, int q0, int L, int krow,
-                                             int hi, float scale_log2) {
-  f32x16 sc = zero16(), dp = zero16();
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    sc = Mfma32<T>::run(lds16(qimg + qb * 8192 + off.row[ks]), kf[ks], sc);
-    dp = Mfma32<T>::run(lds16(oimg + qb * 8192 + off.row[ks]), vf[ks], dp);
-  }
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const int qc = qb * 32 + 8 * jj + 4 * hi;  // rows qc + 0..3 of the staged tile
-    const float4 l4 = *reinterpret_cast<const float4*>(s_lse + qc);
-    const float4 d4 = *reinterpret_cast<const float4*>(s_del + qc);
-    const float lq4[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * jj + i;
-      float pv = fexp2(fmaf(sc[r], scale_log2, -lq4[i]));
-      if (MASK) {
-        const int qpos = q0 + qc + i;
-        const bool out = (krow >= L) | (qpos >= L) | (CAUSAL & (krow > qpos));
-        pv = out ? 0.f : pv;
-      }
-      sc[r] = pv;
-      dp[r] = pv * (dp[r] - dq4[i]);
-    }
-  }
-  // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T += Q^T dS   (q in the register order)
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const uint4 pb = pack8<T>(sc, s);
-    const uint4 db = pack8<T>(dp, s);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      dv[n] = Mfma32<T>::run(tr32(oimg, off, qb * 32 + 16 * s, n), pb, dv[n]);
-      dk[n] = Mfma32<T>::run(tr32(qimg, off, qb * 32 + 16 * s, n), db, dk[n]);
-    }
-  }
-}
-
-// ---- backward dK/dV: 32 keys per wave, 128 per workgroup ------------------------------------
-// S = Q K^T and dP = dO V^T with the queries on the accumulator rows and lane = key: P and dS
-// are the B operands of dV^T += dO^T P and dK^T += Q^T dS straight from registers.
-template <typename T, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) bwd_dkdv32_kernel(Args a) {
-  constexpr int STAGE = 2 * IMG + 512;  // Q image | dO image | lse[64] | delta[64]
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int lk = lane & 31, hi = lane >> 5;
-  const int seq = a.tiles[2 * blockIdx.x], k0 = a.tiles[2 * blockIdx.x + 1];
-  const int kvh = blockIdx.y;
-  const int grp = a.nh / a.nkv;
-  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
-  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
-  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
-  const int wk0 = k0 + wid * 32;
-  const int krow = wk0 + lk;
-  uint4 kf[8], vf[8];  // B operands: K[krow][16ks + 8hi ..], V[krow][...]
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    kf[ks] = gload16(K + (long long)krow * a.ldk + 16 * ks + 8 * hi, krow < L);
-    vf[ks] = gload16(V + (long long)krow * a.ldv + 16 * ks + 8 * hi, krow < L);
-  }
-  wait_vm_all();
-  f32x16 dk[4], dv[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) { dk[n] = zero16(); dv[n] = zero16(); }
-  const int qstart = CAUSAL ? (k0 / 64) * 64 : 0;
-  const int nq = qstart < L ? (L - qstart + 63) / 64 : 0;
-  const int nsteps = grp * nq;
-  auto stage = [&](int j, char* st) {
-    const int hh = j / nq, qq = qstart + (j % nq) * 64;
-    const int head = kvh * grp + hh;
-    stage64_async(st, reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D, a.ldq,
-                  qq, L);
-    stage64_async(st + IMG, reinterpret_cast<const T*>(a.dout) + (long long)s0 * a.lddo + head * D,
-                  a.lddo, qq, L);
-    if (wid < 2) {
-      const float* src = (wid == 0 ? a.lse : a.delta) + (long long)head * a.T + s0;
-      int qr = qq + lane;
-      qr = qr < L ? qr : L - 1;
-      __builtin_amdgcn_global_load_lds((const void*)(src + qr),
-                                       (__attribute__((address_space(3))) void*)(st + 2 * IMG + wid * 256),
-                                       4, 0, 0);
-    }
-  };
-  Off32 off;
-  make_off32(off, lane);
-  if (nsteps > 0) stage(0, smem);
-  for (int j = 0; j < nsteps; ++j) {
-    char* st = smem + (j & 1) * STAGE;
-    char* qimg = st;
-    char* oimg = st + IMG;
-    const float* s_lse = reinterpret_cast<const float*>(st + 2 * IMG);
-    const float* s_del = s_lse + 64;
-    const int q0 = qstart + (j % nq) * 64;
-    if (j + 1 < nsteps) {
-      stage(j + 1, smem + ((j + 1) & 1) * STAGE);
-      if (wid < 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      wait_vm_all();
-    }
-    lds_fence_barrier();
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int qb0 = q0 + qb * 32;
-      if (CAUSAL && qb0 + 31 < wk0) continue;  // every query of the block is before every key
-      // wave-uniform (the MFMAs read every lane's operands: never branch per lane around them)
-      const bool need_mask = (qb0 + 32 > L) || (wk0 + 32 > L) || (CAUSAL && wk0 + 31 > qb0);
-      if (need_mask)
-        dkdv32_block<T, CAUSAL, true>(qimg, oimg, s_lse, s_del, off, kf, vf, dk, dv, qb, q0, L,
-                                      krow, hi, a.scale_log2);
-      else
-        dkdv32_block<T, CAUSAL, false>(qimg, oimg, s_lse, s_del, off, kf, vf, dk, dv, qb, q0, L,
-                                       krow, hi, a.scale_log2);
-    }
-    lds_fence_barrier();
-  }
-  // lane holds dK^T / dV^T column krow, rows (dims) 32n + 8j + 4hi + i
-  if (krow < L) {
-    T* dK = reinterpret_cast<T*>(a.dk) + (long long)s0 * a.lddk + kvh * D + (long long)krow * a.lddk;
-    T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D + (long long)krow * a.lddv;
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        struct alignas(8) O4 { T v[4]; } k4, v4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          k4.v[i] = from_f32<T>(dk[n][4 * jj + i] * a.scale);
-          v4.v[i] = from_f32<T>(dv[n][4 * jj + i]);
-        }
-        *reinterpret_cast<O4*>(dK + 32 * n + 8 * jj + 4 * hi) = k4;
-        *reinterpret_cast<O4*>(dV + 32 * n + 8 * jj + 4 * hi) = v4;
-      }
-  }
-}
-
-template <typename T, bool CAUSAL, bool MASK>
 __device__ __forceinline__ void dq32_tile(const char* kimg, const char* vimg, const Off32& off,
                                           const uint4 (&qf)[8], const uint4 (&of)[8],
                                           f32x16 (&dq)[4], int kv0, int L, int qrow, int hi,
@@ -1509,11 +975,10 @@ __device__ __forceinline__ void dq32_tile(const char* kimg, const char* vimg, co
 }
 
 // ---- backward dQ: 32 queries per wave, 128 per workgroup ------------------------------------
-// S^T = K Q^T, dP^T = V dO^T (keys on rows, lane = query); dQ^T += K^T dS^T.
-// FUSE_DELTA: the kernel also forms delta = rowsum(dO * O) for its own 128 queries (from L2-warm
-// rows it is loading anyway) and writes it for the dK/dV kernel, which then runs after it --
-// this replaces the separate delta pass over O and dO.
-template <typename T, bool CAUSAL, bool FUSE_DELTA = false>
+// S^T = K Q^T, dP^T = V dO^T (keys on rows, lane = query); dQ^T += K^T dS^T.  The recompute
+// path, used when the dS hand-off buffer does not fit (LUMEN_FA_DS_MB).  (A variant that also
+// formed delta from the rows it loads measured neutral and was removed.)
+template <typename T, bool CAUSAL>
 __global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
   constexpr int BM = 128;
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
@@ -1530,38 +995,20 @@ __global__ void __launch_bounds__(256, 2) bwd_dq32_kernel(Args a) {
   const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
   const int wq0 = q0 + wid * 32;
   const int qrow = wq0 + lq;
-  uint4 qf[8], of[8], ob[8];
-  // FUSE_DELTA: this lane's O fragments, issued with the Q / dO loads so one latency covers all
-  const T* orow = reinterpret_cast<const T*>(a.o) + (long long)(s0 + qrow) * a.ldo + head * D;
+  uint4 qf[8], of[8];
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) {
     qf[ks] = gload16(Q + (long long)qrow * a.ldq + 16 * ks + 8 * hi, qrow < L);
     of[ks] = gload16(dO + (long long)qrow * a.lddo + 16 * ks + 8 * hi, qrow < L);
-    if constexpr (FUSE_DELTA) ob[ks] = gload16(orow + 16 * ks + 8 * hi, qrow < L);
   }
   const float lse_q = qrow < L ? a.lse[(long long)head * a.T + s0 + qrow] : INFINITY;
-  float del_q = 0.f;
-  if constexpr (!FUSE_DELTA) del_q = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
+  const float del_q = qrow < L ? a.delta[(long long)head * a.T + s0 + qrow] : 0.f;
   f32x16 dq[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) dq[n] = zero16();
   const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
   const int w_end = CAUSAL ? min(kv_end, wq0 + 32) : kv_end;
   wait_vm_all();
-  if constexpr (FUSE_DELTA) {
-    // delta = rowsum(dO * O): lanes q and q + 32 hold the two halves of every 16-column chunk
-    float sd = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const T* x = reinterpret_cast<const T*>(&of[ks]);
-      const T* y = reinterpret_cast<const T*>(&ob[ks]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sd += to_f32(x[e]) * to_f32(y[e]);
-    }
-    sd += __shfl_xor(sd, 32, 64);
-    del_q = sd;  // 0 for rows past the end (their fragments were zero-filled)
-    if (hi == 0 && qrow < L) const_cast<float*>(a.delta)[(long long)head * a.T + s0 + qrow] = sd;
-  }
   if (kv_end > 0) {
     stage64_async(smem, K, a.ldk, 0, L);
     stage64_async(smem + IMG, V, a.ldv, 0, L);
@@ -1748,53 +1195,23 @@ static int cu_count() {
 template <typename T>
 static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& a, hipStream_t st) {
   dim3 block(256);
-  if (which == 0) {
+  if (which == 0) {  // forward: 32x32x16 kernel, 128-row tiles
+    if (mt != 20) return hipErrorInvalidValue;
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
-    if (mt == 20) {  // 32x32x16 kernel, 128-row tiles
-      if (a.nitems > 0) grid = dim3(std::min(a.nitems, (causal ? 2 : 1) * cu_count()), 1);
-      if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
-      else hipLaunchKernelGGL((fwd32_kernel<T, false>), grid, block, 0, st, a);
-    } else if (mt >= 10) {  // transposed-formulation kernel, QG = mt - 10 query groups per wave
-      const int qg = mt - 10;
-      if (causal) {
-        if (qg == 2) hipLaunchKernelGGL((fwd_t_kernel<T, true, 2>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((fwd_t_kernel<T, true, 1>), grid, block, 0, st, a);
-      } else {
-        if (qg == 2) hipLaunchKernelGGL((fwd_t_kernel<T, false, 2>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((fwd_t_kernel<T, false, 1>), grid, block, 0, st, a);
-      }
-    } else if (causal) {
-      if (mt == 2) hipLaunchKernelGGL((fwd_kernel<T, true, 2>), grid, block, 0, st, a);
-      else hipLaunchKernelGGL((fwd_kernel<T, true, 1>), grid, block, 0, st, a);
-    } else {
-      if (mt == 2) hipLaunchKernelGGL((fwd_kernel<T, false, 2>), grid, block, 0, st, a);
-      else hipLaunchKernelGGL((fwd_kernel<T, false, 1>), grid, block, 0, st, a);
-    }
+    if (a.nitems > 0) grid = dim3(std::min(a.nitems, (causal ? 2 : 1) * cu_count()), 1);
+    if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((fwd32_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 1) {
     dim3 grid((unsigned)((a.T + 3) / 4));
     hipLaunchKernelGGL(delta_kernel<T>, grid, block, 0, st, a);
-  } else if (which == 2) {
+  } else if (which == 2) {  // dK/dV (64-key tiles), dS recomputed by which 5
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nkv);
     if (causal) hipLaunchKernelGGL((bwd_dkdv_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((bwd_dkdv_kernel<T, false>), grid, block, 0, st, a);
-  } else if (which == 3) {
-    dim3 grid(ntiles, a.nh);
-    if (causal) hipLaunchKernelGGL((bwd_dq_kernel<T, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((bwd_dq_kernel<T, false>), grid, block, 0, st, a);
-  } else if (which == 4) {  // dK/dV, 32x32x16 kernel, 128-key tiles
-    dim3 grid(ntiles, a.nkv);
-    if (causal) hipLaunchKernelGGL((bwd_dkdv32_kernel<T, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((bwd_dkdv32_kernel<T, false>), grid, block, 0, st, a);
-  } else if (which == 5) {  // dQ, 32x32x16 kernel, 128-query tiles (mt == 2: + delta)
+  } else if (which == 5) {  // dQ, 32x32x16 kernel, 128-query tiles
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
-    if (mt == 2) {
-      if (causal) hipLaunchKernelGGL((bwd_dq32_kernel<T, true, true>), grid, block, 0, st, a);
-      else hipLaunchKernelGGL((bwd_dq32_kernel<T, false, true>), grid, block, 0, st, a);
-    } else if (causal) {
-      hipLaunchKernelGGL((bwd_dq32_kernel<T, true>), grid, block, 0, st, a);
-    } else {
-      hipLaunchKernelGGL((bwd_dq32_kernel<T, false>), grid, block, 0, st, a);
-    }
+    if (causal) hipLaunchKernelGGL((bwd_dq32_kernel<T, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((bwd_dq32_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 7) {  // dK/dV (64-key tiles) + dS hand-off
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nkv);
     if (a.nitems > 0) grid = dim3(std::min(a.nitems, 2 * cu_count()), 1);
@@ -1829,16 +1246,11 @@ static int fa_persist() {
   static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 9; }();
   return v;
 }
-static int fa_probe() {
-  static int v = [] { const char* e = std::getenv("LUMEN_FA_PROBE"); return e ? std::atoi(e) : 0; }();
-  return v;
-}
 
-// which: 0 = forward (tiles of 64*mt query rows; mt >= 10 selects the transposed-formulation
-//        kernel with 64*(mt-10)-row tiles; mt == 20 the 32x32x16 kernel, 128-row tiles),
-//        1 = delta, 2 = dK/dV (64-key tiles), 3 = dQ (64-query tiles),
-//        4 = dK/dV (32x32x16, 128-key tiles), 5 = dQ (32x32x16, 128-query tiles; mt == 2: it
-//        also writes delta, so it runs before dK/dV and replaces which 1)
+// which: 0 = forward (mt must be 20: the 32x32x16 kernel, 128-row tiles), 1 = delta,
+//        2 = dK/dV (64-key tiles), 5 = dQ (32x32x16, 128-query tiles).  (Measured-slower
+//        variants -- a 16x16x32 forward, the transposed-formulation forward, 16x16x32 dQ and a
+//        32x32x16 dK/dV -- were removed, profiles/r02_fa and profiles/r2_fa.)
 extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
                                        const void* q, const void* k, const void* v,
                                        long long ldq, long long ldk, long long ldv, void* o,
@@ -1864,7 +1276,7 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.lddv = lddv; a.delta = delta;
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
-  a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3; a.probe = 0;
+  a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3;
   a.nitems = (which == 0 && mt == 20 && !tiles3 && (fa_persist() & 2)) ? ntiles * nh : 0;
   a.snake = (fa_persist() >> 3) & 1;
   if (which == 6 || which == 7 || which == 8) return hipErrorInvalidValue;  // other entries
@@ -1923,7 +1335,6 @@ extern "C" hipError_t lumen_flash_attn_ds(int dtype, int which, int causal, cons
   a.lddv = lddv; a.delta = delta;
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   a.ds = ds; a.ds_off = ds_off; a.ds_total = ds_total; a.tiles3 = tiles3;
-  a.probe = fa_probe();
   a.snake = (fa_persist() >> 3) & 1;
   a.nitems = tiles3 ? 0 : (which == 7 && (fa_persist() & 1)) ? ntiles * nkv
                         : (which == 8 && (fa_persist() & 4)) ? ntiles * nh : 0;

@@ -318,23 +318,12 @@ def prepare_varlen(cu: tuple, device) -> None:
 
 
 import os as _os
-FA_MT = int(_os.environ.get("LUMEN_FA_MT", "1"))  # query m-tiles (16 rows) per wave (old fwd)
-# forward kernel: "v32" = 32x32x16 MFMA, 32 queries per wave, 128-row tiles (default: 56 vs 71
-# us at B8 S512, 524 vs 668 us at B2 S4096, profiles/r02_fa); "t1"/"t2" = 16x16x32 transposed
-# formulation with 1/2 query groups per wave (P stays in registers), "old" = fwd_kernel
-_FWD = _os.environ.get("LUMEN_FA_FWD", "v32")
-FA_FWD_MT = {"t1": 11, "t2": 12, "v32": 20}.get(_FWD, FA_MT)
-
-
-def _fwd_rows(mt: int) -> int:
-    return 128 if mt == 20 else 64 * (mt - 10 if mt >= 10 else mt)
-
-
-FA_FWD_ROWS = _fwd_rows(FA_FWD_MT)
-# backward kernels: "v16" = 16x16x32 dK/dV (64-key tiles) + dQ (64-query tiles);
-# "v32" = 32x32x16 kernels with 128-row tiles; "mix" = 16x16x32 dK/dV + 32x32x16 dQ
-FA_BWD = _os.environ.get("LUMEN_FA_BWD", "mix")
-# dS hand-off (mix kernels): the dK/dV kernel stores dS per 64x64 tile and the dQ kernel forms
+# forward: the 32x32x16 MFMA kernel, 32 queries per wave, 128-row tiles (56 vs 71 us for the
+# 16x16x32 forms at B8 S512, profiles/r02_fa; those variants were removed)
+FA_FWD_MT, FA_FWD_ROWS = 20, 128
+# backward: 16x16x32 dK/dV (64-key tiles) + 32x32x16 dQ (128-query tiles), or -- while the buffer
+# fits -- the dS hand-off pair below
+# dS hand-off: the dK/dV kernel stores dS per 64x64 tile and the dQ kernel forms
 # dQ = dS K from it, instead of recomputing S = Q K^T and dP = dO V^T (2 of its 3 products).
 # Used while the [nh, tiles, 64, 64] 16-bit buffer stays under LUMEN_FA_DS_MB (0 = off).
 FA_DS_MB = float(_os.environ.get("LUMEN_FA_DS_MB", "2048"))
@@ -409,16 +398,14 @@ class _FlashAttn(torch.autograd.Function):
         DELTA_HANDOFFS[0] += int(handed)
         slot.clear()
         cut = _cu_tensor(cu, qkv.device)
-        # dK/dV and dQ kernels per FA_BWD: "v16" both 16x16x32 (64-row tiles), "v32" both
-        # 32x32x16 (128-row tiles), "mix" = 16x16x32 dK/dV + 32x32x16 dQ
-        wkv, rkv = (4, 128) if FA_BWD == "v32" else (2, 64)
-        wq, rq = (5, 128) if FA_BWD in ("v32", "mix") else (3, 64)
-        # the mix kernels undo the forward's RoPE in their dQ / dK epilogues (d(pre-rotation)
-        # written directly): the producer of q|k then skips its own inverse-rotation pass
-        rp = ctx.rope if (ctx.rope is not None and wkv == 2 and wq == 5) else None
+        # dK/dV (which 2, 64-key tiles) and dQ (which 5, 128-query tiles); both undo the
+        # forward's RoPE in their dQ / dK epilogues (d(pre-rotation) written directly): the
+        # producer of q|k then skips its own inverse-rotation pass
+        wkv, rkv, wq, rq = 2, 64, 5, 128
+        rp = ctx.rope
         pos, cos, sin = rp if rp is not None else (None, None, None)
         qtiles = _tiles(cu, rq, qkv.device)
-        ds_off, ds_total = (_ds_offsets(cu, causal, qkv.device) if wkv == 2 and FA_DS_MB > 0
+        ds_off, ds_total = (_ds_offsets(cu, causal, qkv.device) if FA_DS_MB > 0
                             else (None, 0))
         if ds_off is not None and nh * ds_total * 8192 <= FA_DS_MB * 2 ** 20:
             ds = torch.empty(nh, ds_total, 4096, device=qkv.device, dtype=qkv.dtype)

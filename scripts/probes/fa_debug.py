@@ -20,9 +20,8 @@ q2 = qkv0.detach().float().requires_grad_(True)
 o2 = att.flash_attention_ref(q2, tuple(cu), nh, nkv, D, True)
 do = torch.randn_like(o2).to(torch.bfloat16)
 o2.backward(do.float())
-for fwd, bwd in [("t1", "v16"), ("v32", "v16"), ("t1", "v32"), ("v32", "v32")]:
-    mt = {"t1": 11, "v32": 20}[fwd]
-    att.FA_FWD_MT, att.FA_FWD_ROWS, att.FA_BWD = mt, att._fwd_rows(mt), bwd
+for fwd, bwd in [("v32", "ds"), ("v32", "recompute")]:
+    att.FA_DS_MB = 2048 if bwd == "ds" else 0
     x = qkv0.clone().requires_grad_(True)
     o = att.flash_attention_qkv(x, cu, nh, nkv, D, True)
     o.backward(do)

@@ -351,19 +351,13 @@ def test_sampling_greedy_and_topk():
 
 @pytest.mark.parametrize("nh,nkv,lens", [(8, 8, [512, 512]), (8, 2, [512, 300, 77]),
                                          (4, 4, [1000, 64, 129])])
-@pytest.mark.parametrize("fwd,bwd", [("t1", "v16"), ("t2", "v16"), ("old", "v16"),
-                                     ("v32", "v32"), ("v32", "mix")])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_flash_attention_fwd_bwd(nh, nkv, lens, fwd, bwd, monkeypatch, dtype):
-    """Forward variants (t1 / t2 / old / v32 = default) and recompute backward kernels
-    (v16 / v32 / mix = default when the dS hand-off buffer does not fit) vs the f32 reference."""
+def test_flash_attention_fwd_bwd(nh, nkv, lens, monkeypatch, dtype):
+    """Forward kernel and the recompute backward (dK/dV + 32x32 dQ: the path when the dS
+    hand-off buffer does not fit) vs the f32 reference."""
     import lumen.ops.attention as att
     from lumen.ops.attention import flash_attention_qkv, flash_attention_ref
 
-    mt = {"t1": 11, "t2": 12, "old": 1, "v32": 20}[fwd]
-    monkeypatch.setattr(att, "FA_FWD_MT", mt)
-    monkeypatch.setattr(att, "FA_FWD_ROWS", att._fwd_rows(mt))
-    monkeypatch.setattr(att, "FA_BWD", bwd)
     monkeypatch.setattr(att, "FA_DS_MB", 0)  # the recompute dQ kernels (dS hand-off: below)
 
     D = 128
