@@ -93,6 +93,12 @@ class ZeroEngine:
                 group=self.gather_group, max_reuse_distance=cfg.stage3_max_reuse_distance,
                 force_partition=single)
             model.coordinator = self.coordinator
+            if self.gather_group is not None and self.coordinator.keep:
+                # keep gathers each unit once (warm-up): a second communicator would buy no
+                # overlap, only a second RCCL communicator per GPU (never initialised: RCCL
+                # communicators are created at their first collective)
+                self.coordinator.group = None
+                self.gather_group = None
             if env.is_main:  # stderr: bench.py's stdout is exactly one JSON line
                 import sys
 

@@ -157,7 +157,8 @@ def test_zero3_world4_split_groups(case, deep_reference, tmp_path):
     _close(r["sd"], deep_reference["sd"])
     z = r["zero3"]
     assert z["schedule"] == case["schedule"] and z["world"] == 4
-    assert z["gather_group_separate"]
+    # release re-gathers every use on its own communicator; keep gathers once, on the default
+    assert z["gather_group_separate"] == (case["schedule"] == "release")
     assert z["pool_overflows"] == 0
     n_units = 8
     if case["schedule"] == "release":
@@ -188,7 +189,8 @@ def test_zero3_world8_split_groups(schedule, tmp_path):
              extra=extra)
     _close(r["sd"], ref["sd"])
     z = r["zero3"]
-    assert z["schedule"] == schedule and z["world"] == 8 and z["gather_group_separate"]
+    assert z["schedule"] == schedule and z["world"] == 8
+    assert z["gather_group_separate"] == (schedule == "release")
     assert z["pool_overflows"] == 0
 
 
