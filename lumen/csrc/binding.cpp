@@ -41,6 +41,7 @@ hipError_t lumen_lora2(int, int, int, const void*, long long, const float*, long
 hipError_t lumen_rmsnorm_fwd_ld(int, const void*, const void*, const void*, void*, void*, float*,
                                 int, int, float, long long, hipStream_t);
 hipError_t lumen_lora3_z_tail(int, const float*, int, void*, long long, int, int, int, hipStream_t);
+hipError_t lumen_lora3_w_tail_batch(int, const long long*, int, long long, hipStream_t);
 hipError_t lumen_lora3_w_tail(int, void*, long long, int, const float*, int, int, const long long*,
                               const long long*, const int*, const int*, float, hipStream_t);
 hipError_t lumen_lora3_dxa(int, const void*, long long, void*, long long, const float*, const float*,
@@ -456,6 +457,19 @@ void lora3_w_tail(at::Tensor& w, int64_t K, const at::Tensor& B, int64_t r,
         "lora3_w_tail");
 }
 
+// every folded linear's tail in one launch: desc [n, 24] int64 on the GPU (built by
+// lumen.models.layers.FoldTails, which also validates the pointers / shapes it encodes)
+void lora3_w_tail_batch(const at::Tensor& desc, int64_t dtype, int64_t max_chunks) {
+  need_cuda(desc, "lora3_w_tail_batch desc");
+  if (desc.scalar_type() != at::kLong || desc.dim() != 2 || desc.size(1) != 24 ||
+      !desc.is_contiguous())
+    throw std::invalid_argument("lumen: lora3_w_tail_batch: desc [n, 24] int64");
+  check(lumen_lora3_w_tail_batch(static_cast<int>(dtype),
+                                 reinterpret_cast<const long long*>(desc.data_ptr<int64_t>()),
+                                 static_cast<int>(desc.size(0)), max_chunks, cur_stream()),
+        "lora3_w_tail_batch");
+}
+
 // fused x-side LoRA backward (kernels/lora_v3.hip dxa3_kernel)
 void lora3_dxa(const at::Tensor& x, at::Tensor& dx, const at::Tensor& dZ, const at::Tensor& A,
                at::Tensor& dA, int64_t tw, int64_t seed, int64_t thresh, double drop_scale,
@@ -825,6 +839,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora2", &lora2);
   m.def("transpose2d", &transpose2d);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("lora3_w_tail_batch", &lora3_w_tail_batch);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
   m.def("set_rms_lds", [](int64_t f, int64_t b) {
     lumen_set_rms_lds(static_cast<int>(f), static_cast<int>(b));

@@ -786,10 +786,50 @@ __global__ void __launch_bounds__(256) w_tail_kernel(T* __restrict__ w, long lon
   store8(w + (sg.n_off[seg] + n) * ldw + K + sg.r_off[seg] + c, v);
 }
 
+// All folded linears of a model in ONE launch after an optimizer publish (64 single-linear
+// launches of w_tail_kernel cost ~0.3 ms per Llama-2-7B step, almost all launch overhead: a
+// linear's tail is only N x 16 16-bit values per segment).  desc: per linear 24 int64 =
+// {w, ldw, B, K, r, nseg, float bits of scale, dtype, n_off[4], n_len[4], r_off[4], b_off[4]};
+// blockIdx.y = linear * 4 + segment.
+template <typename T>
+__global__ void __launch_bounds__(256) w_tail_batch_kernel(const long long* __restrict__ desc) {
+  const long long* d = desc + (blockIdx.y >> 2) * 24;
+  const int seg = blockIdx.y & 3;
+  if (seg >= static_cast<int>(d[5])) return;
+  const int r = static_cast<int>(d[4]), K = static_cast<int>(d[3]);
+  const int nch = r / 8;
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const long long n_len = d[12 + seg];
+  if (i >= n_len * nch) return;
+  const long long n = i / nch;
+  const int c = static_cast<int>(i % nch) * 8;
+  const float scale = __builtin_bit_cast(float, static_cast<unsigned>(d[6]));
+  const float* B = reinterpret_cast<const float*>(d[2]);
+  T* w = reinterpret_cast<T*>(d[0]);
+  float v[8];
+  load8(B + (d[20 + seg] + n) * r + c, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= scale;
+  store8(w + (d[8 + seg] + n) * d[1] + K + d[16 + seg] + c, v);
+}
+
 }  // namespace lv3
 }  // namespace lumen
 
 using namespace lumen;
+
+// desc: n linears x 24 int64 on the device (see w_tail_batch_kernel), all of one 16-bit dtype;
+// max_chunks = the largest n_len * r / 8 over all segments
+extern "C" hipError_t lumen_lora3_w_tail_batch(int dtype, const long long* desc, int n,
+                                               long long max_chunks, hipStream_t st) {
+  if (n <= 0 || max_chunks <= 0) return hipSuccess;
+  if (n > 16383) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>((max_chunks + 255) / 256), 4 * n), block(256);
+  if (dtype == kBF16) hipLaunchKernelGGL(lv3::w_tail_batch_kernel<bf16>, grid, block, 0, st, desc);
+  else if (dtype == kF16) hipLaunchKernelGGL(lv3::w_tail_batch_kernel<fp16>, grid, block, 0, st, desc);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
 
 #include <cstdlib>
 static int lv3_probe() {

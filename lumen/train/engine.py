@@ -157,6 +157,9 @@ class ZeroEngine:
                 self.async_off = AsyncOffloadStep(self.opt, self.flat, self.device, self.sharded)
                 self.async_off.map_units(model)
                 model.unit_gate = self.async_off.gate
+        from ..models.layers import FoldTails
+
+        self.fold_tails = FoldTails(model) if self.device.type == "cuda" else None
         self._gscale = torch.ones(1, dtype=torch.float32, device=self.device)
         self._works: List = []
         for prm in trainable:  # .grad is a view of flat.grad: kernels may accumulate into it
@@ -346,10 +349,12 @@ class ZeroEngine:
         self.flat.mark_updated()
         if not self.sharded:
             self.flat.param.copy_(master)
-            return
-        for b in self.flat.buckets:
-            dist.all_gather_into_tensor(self.flat.param[b.off:b.off + b.size],
-                                        self.flat.shard_view(master, b))
+        else:
+            for b in self.flat.buckets:
+                dist.all_gather_into_tensor(self.flat.param[b.off:b.off + b.size],
+                                            self.flat.shard_view(master, b))
+        if self.fold_tails is not None:
+            self.fold_tails.refresh()  # every folded linear's [s B] tail, one launch
 
     def _scaler_state(self):
         if self.scaler is None:

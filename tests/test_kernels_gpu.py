@@ -957,6 +957,8 @@ def test_engine_steps_refresh_fold_tail(stage):
         torch.testing.assert_close(wext[:, K:], want[:, K:], rtol=0, atol=0)
         n += 1
     assert n > 0
+    # the engine's one-launch refresh (FoldTails, run at every publish) covers every folded linear
+    assert eng.fold_tails.refresh() == n
     eng.close()
 
 
