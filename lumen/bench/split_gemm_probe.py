@@ -11,7 +11,7 @@ two parts into column views of one buffer (ldc = full width, no copy) lets the t
 own, separately tuned GEMM.  This probe times one-piece vs split back to back (power-capped, as
 in a step) and prints the kernels a split call launches (no copy kernels expected).
 
-    python -m lumen.bench.split_gemm_probe --tune OUT.csv
+    python -m lumen.bench.split_gemm_probe --tune OUT.csv [--dtype fp16]
 """
 from __future__ import annotations
 
@@ -40,7 +40,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tune", default=None, help="tune new shapes into this table copy")
     ap.add_argument("--T", type=int, default=4096)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     args = ap.parse_args()
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
     from lumen.utils.gemm_tuning import DEFAULT_TABLE, load_tuned_gemms, start_gemm_tuning
 
     if args.tune:
@@ -52,11 +54,11 @@ def main():
     dev = torch.device("cuda")
     T, H, I = args.T, 4096, 11008
     g = torch.Generator(device=dev).manual_seed(0)
-    x = torch.randn(T, H, device=dev, generator=g).bfloat16()
-    Wgu = (torch.randn(2 * I, H, device=dev, generator=g) * 0.02).bfloat16()
-    WdnT = (torch.randn(I, H, device=dev, generator=g) * 0.02).bfloat16()  # cached W_down^T
-    y = torch.empty(T, 2 * I, device=dev, dtype=torch.bfloat16)
-    dx = torch.empty(T, I, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(T, H, device=dev, generator=g).to(dt)
+    Wgu = (torch.randn(2 * I, H, device=dev, generator=g) * 0.02).to(dt)
+    WdnT = (torch.randn(I, H, device=dev, generator=g) * 0.02).to(dt)  # cached W_down^T
+    y = torch.empty(T, 2 * I, device=dev, dtype=dt)
+    dx = torch.empty(T, I, device=dev, dtype=dt)
     res = {}
 
     def gu_one():
@@ -90,9 +92,9 @@ def main():
         res[name] = {"us": round(timeit(fn), 1), "max_err": float(err)}
         print(name, res[name], flush=True)
     # sustained interleaved with a filler GEMM (power state of a training step)
-    filler_w = (torch.randn(H, I, device=dev, generator=g) * 0.02).bfloat16()
-    h = torch.randn(T, I, device=dev, generator=g).bfloat16()
-    out_f = torch.empty(T, H, device=dev, dtype=torch.bfloat16)
+    filler_w = (torch.randn(H, I, device=dev, generator=g) * 0.02).to(dt)
+    h = torch.randn(T, I, device=dev, generator=g).to(dt)
+    out_f = torch.empty(T, H, device=dev, dtype=dt)
 
     def filler():
         torch.mm(h, filler_w.t(), out=out_f)

@@ -157,7 +157,10 @@ class LLMEngine:
         self._pinned: List[Optional[torch.Tensor]] = [None, None]
         self._pinned_ready: List[Optional[object]] = [None, None]
         self._pin_i = 0
-        self.async_sched = bool(cfg.async_scheduling and self.tp == 1)
+        # TP > 1 too: a step is broadcast when it is launched, its decode tokens straight from
+        # the device (gathered from the previous step's samples), so workers never wait for
+        # rank 0's host to see the tokens
+        self.async_sched = bool(cfg.async_scheduling)
         self._inflight: Optional[dict] = None
         self.scheduler = Scheduler(SchedulerConfig(
             cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len), self.blocks)
@@ -407,6 +410,8 @@ class LLMEngine:
 
     def _launch(self, batch: Batch) -> None:
         inp = self._build_input(batch)
+        if self.tp > 1:
+            self._broadcast(inp)
         sampled = batch.sampled
         if batch.kind == "decode":
             logits = self.runner.decode(inp)

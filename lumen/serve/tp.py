@@ -1,11 +1,13 @@
 """Tensor-parallel serving plumbing: step broadcast from rank 0 and the worker loop.
 
-Rank 0 (scheduler + API) sends each step as a fixed 12-int64 header and one int64 payload
-(tokens | positions | slots | prefill cu / kv lens / block tables | decode block tables /
-context lens | sampled rows | LoRA slots) with two RCCL
-broadcasts -- no pickled Python objects on the hot path.  Workers rebuild the
-StepInput and run the same model step; the row-parallel all-reduces inside the layers keep the
-ranks in lock-step.
+Rank 0 (scheduler + API) sends each step as ONE fixed-size int64 broadcast: a 12-int64 header
+followed by the payload (tokens | positions | slots | prefill cu / kv lens / block tables |
+decode block tables / context lens | sampled rows | LoRA slots) -- no pickled Python objects on
+the hot path.  A payload larger than the inline capacity (CAP, 16384 values: a
+256-sequence decode step with ~40 blocks per sequence fits) sends its remainder in a second
+broadcast.  Workers rebuild the StepInput and run the same model step; the row-parallel
+all-reduces inside the layers keep the ranks in lock-step.  With async scheduling (default)
+rank 0 broadcasts a step when it LAUNCHES it, decode tokens straight from the device.
 """
 from __future__ import annotations
 
@@ -18,13 +20,14 @@ from .model_runner import StepInput
 
 KIND = {"mixed": 0, "decode": 1, "shutdown": 2}
 HDR = 12  # kind, T, P, maxb_p, N, maxb_d, max_context, R, lora, payload numel, -, -
+CAP = 16384  # payload values carried inline with the header
 
 
 def pack_step(inp: Optional[StepInput], device) -> None:
-    hdr = torch.zeros(HDR, dtype=torch.long, device=device)
     if inp is None:
-        hdr[0] = KIND["shutdown"]
-        dist.broadcast(hdr, src=0)
+        msg = torch.zeros(HDR + CAP, dtype=torch.long, device=device)
+        msg[0] = KIND["shutdown"]
+        dist.broadcast(msg, src=0)
         return
     T = inp.tokens.numel()
     P = len(inp.cu_seqlens) - 1
@@ -42,20 +45,29 @@ def pack_step(inp: Optional[StepInput], device) -> None:
     if inp.lora_ids is not None:  # multi-LoRA: per-token adapter slots ride at the end
         parts.append(inp.lora_ids.long())
     payload = torch.cat(parts)
-    hdr[:10] = torch.tensor([KIND[inp.kind], T, P, maxb_p, N, maxb_d, inp.max_context, R,
-                             int(inp.lora_ids is not None), payload.numel()])
-    dist.broadcast(hdr, src=0)
-    dist.broadcast(payload, src=0)
+    n = payload.numel()
+    hdr = torch.tensor([KIND[inp.kind], T, P, maxb_p, N, maxb_d, inp.max_context, R,
+                        int(inp.lora_ids is not None), n, 0, 0], dtype=torch.long)
+    msg = torch.zeros(HDR + CAP, dtype=torch.long, device=device)
+    msg[:HDR].copy_(hdr, non_blocking=False)
+    msg[HDR:HDR + min(n, CAP)] = payload[:CAP]
+    dist.broadcast(msg, src=0)
+    if n > CAP:
+        dist.broadcast(payload[CAP:].contiguous(), src=0)
 
 
 def recv_step(device) -> Optional[StepInput]:
-    hdr = torch.zeros(HDR, dtype=torch.long, device=device)
-    dist.broadcast(hdr, src=0)
-    kind, T, P, maxb_p, N, maxb_d, maxc, R, has_lora, n = hdr.tolist()[:10]
+    msg = torch.empty(HDR + CAP, dtype=torch.long, device=device)
+    dist.broadcast(msg, src=0)
+    kind, T, P, maxb_p, N, maxb_d, maxc, R, has_lora, n = msg[:10].tolist()
     if kind == KIND["shutdown"]:
         return None
-    payload = torch.empty(n, dtype=torch.long, device=device)
-    dist.broadcast(payload, src=0)
+    if n <= CAP:
+        payload = msg[HDR:HDR + n]
+    else:
+        rest = torch.empty(n - CAP, dtype=torch.long, device=device)
+        dist.broadcast(rest, src=0)
+        payload = torch.cat([msg[HDR:], rest])
     inp = StepInput("mixed" if kind == KIND["mixed"] else "decode", payload[:T],
                     payload[T:2 * T].int(), payload[2 * T:3 * T], [0])
     o = 3 * T

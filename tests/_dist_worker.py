@@ -70,7 +70,7 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
     shutdown()
 
 
-def serve_tp_worker(rank, world, port, outdir, loras=None):
+def serve_tp_worker(rank, world, port, outdir, loras=None, async_sched=True, cap=None):
     """TP serving on gloo: rank 0 runs the engine, rank 1 the worker loop; greedy outputs of
     rank 0 are saved for comparison with a single-process engine."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -81,12 +81,17 @@ def serve_tp_worker(rank, world, port, outdir, loras=None):
     from lumen.parallel.dist import init, shutdown
     from lumen.serve.engine import EngineConfig, LLMEngine
     from lumen.serve.sequence import SamplingParams
+    import lumen.serve.tp as tp_mod
     from lumen.serve.tp import worker_loop
+
+    if cap is not None:  # small inline capacity: every step takes the two-broadcast path
+        tp_mod.CAP = cap
 
     init(device="cpu")
     model = _tp_test_model()
     cfg = EngineConfig(model="tiny-llama-gqa", device="cpu", max_model_len=128, block_size=4,
-                       use_graphs=False, num_blocks=128, tp_size=world, lora_modules=loras)
+                       use_graphs=False, num_blocks=128, tp_size=world, lora_modules=loras,
+                       async_scheduling=async_sched)
     eng = LLMEngine(cfg, model=model)
     if rank == 0:
         prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
@@ -97,6 +102,7 @@ def serve_tp_worker(rank, world, port, outdir, loras=None):
         while any(not s.finished for s in seqs):
             eng.step()
         eng.shutdown()
+        assert eng.async_sched == async_sched
         torch.save([s.output_ids for s in seqs], os.path.join(outdir, "tp_out.pt"))
     else:
         worker_loop(eng.runner)
@@ -240,7 +246,11 @@ def serve_tp_gpu_worker(rank, world, port, outdir):
     from lumen.parallel.dist import init, shutdown
     from lumen.serve.engine import EngineConfig, LLMEngine
     from lumen.serve.sequence import SamplingParams
+    import lumen.serve.tp as tp_mod
     from lumen.serve.tp import worker_loop
+
+    if cap is not None:  # small inline capacity: every step takes the two-broadcast path
+        tp_mod.CAP = cap
 
     init(backend="gloo", device="cuda")
     model = _tp_test_model().to("cuda")

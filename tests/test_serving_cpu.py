@@ -128,9 +128,12 @@ def test_openai_api_surface(model):
     assert llama2_chat_prompt([{"role": "user", "content": "q"}]) == "[INST] q [/INST]"
 
 
-def test_tensor_parallel_serving_gloo(tmp_path):
+@pytest.mark.parametrize("async_sched,cap", [(True, None), (False, None), (True, 16)])
+def test_tensor_parallel_serving_gloo(tmp_path, async_sched, cap):
     """TP=2 over gloo (head/FFN-sharded layers, row-parallel all-reduce, vocab-parallel LM head,
-    step broadcast to the worker) reproduces single-process greedy decoding."""
+    step broadcast to the worker) reproduces single-process greedy decoding, with the async
+    scheduler (steps broadcast at launch, tokens gathered on the device) and without, and with a
+    payload larger than the inline capacity of the step message."""
     import socket
 
     import torch.multiprocessing as mp
@@ -141,8 +144,8 @@ def test_tensor_parallel_serving_gloo(tmp_path):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    mp.start_processes(serve_tp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
-                       start_method="spawn")
+    mp.start_processes(serve_tp_worker, args=(2, port, str(tmp_path), None, async_sched, cap),
+                       nprocs=2, join=True, start_method="spawn")
     got = torch.load(tmp_path / "tp_out.pt", weights_only=True)
     ref_model = _tp_test_model()
     prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
