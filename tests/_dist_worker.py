@@ -246,11 +246,7 @@ def serve_tp_gpu_worker(rank, world, port, outdir):
     from lumen.parallel.dist import init, shutdown
     from lumen.serve.engine import EngineConfig, LLMEngine
     from lumen.serve.sequence import SamplingParams
-    import lumen.serve.tp as tp_mod
     from lumen.serve.tp import worker_loop
-
-    if cap is not None:  # small inline capacity: every step takes the two-broadcast path
-        tp_mod.CAP = cap
 
     init(backend="gloo", device="cuda")
     model = _tp_test_model().to("cuda")
