@@ -263,6 +263,7 @@ def main():
     else:
         par = f"dp{world}-zero{ds.stage}"
     gathered_mb = ((coord.gathered_bytes - gb0) / 1e6 / args.steps) if coord else 0.0
+    gathered_total_mb = coord.gathered_bytes / 1e6 if coord else 0.0
     zstats = coord.stats() if coord else None
     if wd is not None:
         wd.close()
@@ -315,7 +316,7 @@ def main():
                 "backend": env.backend,
                 "zero3": zstats,
                 # keep schedule: the frozen weights are gathered once (warm-up), 0 per timed step
-                "zero3_gathered_mb_total": round(coord.gathered_bytes / 1e6, 1) if coord else 0.0,
+                "zero3_gathered_mb_total": round(gathered_total_mb, 1),
                 "zero3_gathered_mb_per_step": round(gathered_mb, 1),
                 "zero3_received_mb_per_step_per_rank": round(gathered_mb * (world - 1) / world, 1),
                 "zero3_exposed_wait_ms_per_step_max_rank": round(exposed_ms / args.steps, 2),
