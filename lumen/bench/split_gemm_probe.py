@@ -113,10 +113,7 @@ def main():
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
     res["split_kernels"] = names
     print(json.dumps(res))
-    if args.tune:
-        import torch.cuda.tunable as tn
-
-        tn.write_file()
+    # (with --tune, TunableOp writes the table named by start_gemm_tuning at process exit)
 
 
 if __name__ == "__main__":
