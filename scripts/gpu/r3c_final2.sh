@@ -5,6 +5,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3c_final2}; mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
 summ() { python3 -c "import json;d=json.load(open('$1'));e=d['extra'];print('$2', d['ms_per_step'], 'ms/step', d['value'], 'tok/s', 'peak GB', e['peak_hbm_gb_max_rank'], 'sched', (e['zero3'] or {}).get('schedule'), 'gathered total MB', e.get('zero3_gathered_mb_total'))"; }
 for v in bf16 fp16 bf16b fp16b; do
   dt=${v%b}
