@@ -572,28 +572,52 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     if (j + 1 < nsteps) step(j + 1, bufB, bufA);
   }
   if constexpr (WDS) store_pend();
-  // write dK (x softmax scale), dV : rows wk0 + 4lg + r, cols 16n + lr
+  // write dK (x softmax scale), dV : rows wk0 + 4lg + r, cols 16n + lr.  Each wave's two 16 x 128
+  // tiles go through LDS (bufA is free after the loop's last barrier: wave w owns 8 KiB of it)
+  // and leave as whole 256-byte rows instead of 64 two-byte stores per lane.
   T* dK = reinterpret_cast<T*>(a.dk) + (long long)s0 * a.lddk + kvh * D;
   T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D;
+  {
+    int ln = threadIdx.x;  // opaque: keep the tile addresses below out of the query loop
+    asm volatile("" : "+v"(ln));
+    const int lr2 = ln & 15, lg2 = (ln >> 4) & 3;
+    char* kt = bufA + wid * 8192;
+    char* vt = kt + 4096;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int kr = wk0 + 4 * lg + r;
-    if (kr >= L) continue;
-    float kv[8];
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * lg2 + r;
+      const int kr = wk0 + row;
+      float kv[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
-    if (a.rope_pos != nullptr) {  // column 16n + lr pairs with 16(n + 4) + lr: same lane
-      const long long pb = (long long)a.rope_pos[s0 + kr] * 64 + lr;
+      for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
+      if (a.rope_pos != nullptr && kr < L) {  // column 16n + lr pairs with 16(n + 4) + lr
+        const long long pb = (long long)a.rope_pos[s0 + kr] * 64 + lr2;
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-        rope_inv_pair(kv[n], kv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
+        for (int n = 0; n < 4; ++n)
+          rope_inv_pair(kv[n], kv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
+      }
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const int o = img_off(row, 2 * n + (lr2 >> 3)) + 2 * (lr2 & 7);
+        *reinterpret_cast<T*>(kt + o) = from_f32<T>(kv[n]);
+        *reinterpret_cast<T*>(vt + o) = from_f32<T>(dv[n][r]);
+      }
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back its own tiles only
+    const int ch = ln & 15;
 #pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      dK[(long long)kr * a.lddk + n * 16 + lr] = from_f32<T>(kv[n]);
-      dV[(long long)kr * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
+    for (int it = 0; it < 4; ++it) {
+      const int row = 4 * it + ((ln >> 4) & 3);
+      const int kr = wk0 + row;
+      const uint4 kv4 = *reinterpret_cast<const uint4*>(kt + img_off(row, ch));
+      const uint4 vv4 = *reinterpret_cast<const uint4*>(vt + img_off(row, ch));
+      if (kr < L) {
+        *reinterpret_cast<uint4*>(dK + (long long)kr * a.lddk + ch * 8) = kv4;
+        *reinterpret_cast<uint4*>(dV + (long long)kr * a.lddv + ch * 8) = vv4;
+      }
     }
   }
+  if (a.nitems > 0) lds_fence_barrier();  // the next item's first DMA refills bufA
   };
   if (a.nitems > 0) {
     // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
@@ -771,6 +795,17 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
       for (int kb = 0; kb < 2; ++kb) st[kb] = Mfma32<T>::run(as_u4(kr[kb][ks]), qf[ks], st[kb]);
     }
   }
+  // V^T operands for the P V product, read while the S MFMAs drain and the softmax runs (they
+  // take the K fragments' registers): the 32 transposed LDS reads' latency leaves the PV phase
+  const unsigned vb = lds_off(vimg);
+  u32x4v vr[4][4];  // [16-key slice kb * 2 + s][output block n]
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    vr[0][n] = tr32a<0>(vb, off, n);
+    vr[1][n] = tr32a<1>(vb, off, n);
+    vr[2][n] = tr32a<2>(vb, off, n);
+    vr[3][n] = tr32a<3>(vb, off, n);
+  }
   float mx = -INFINITY;
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb)
@@ -810,15 +845,6 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
     }
   l_i += xor32_sum(rs);
   // O^T[d][q] += V^T[d][key] P^T[key][q], keys in the register order
-  const unsigned vb = lds_off(vimg);
-  u32x4v vr[4][4];  // [16-key slice kb * 2 + s][output block n]
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    vr[0][n] = tr32a<0>(vb, off, n);
-    vr[1][n] = tr32a<1>(vb, off, n);
-    vr[2][n] = tr32a<2>(vb, off, n);
-    vr[3][n] = tr32a<3>(vb, off, n);
-  }
   const uint4 pb[4] = {pack8<T>(st[0], 0), pack8<T>(st[0], 1), pack8<T>(st[1], 0),
                        pack8<T>(st[1], 1)};
 #pragma unroll
@@ -859,10 +885,6 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   const int qpos = qrow + qoff;  // key position of this lane's query (causal limit)
   Off32 off;
   make_off32(off, lane);
-  uint4 qf[8];  // B operand of S^T: Q[qrow][16ks + 8hi .. +7]
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks)
-    qf[ks] = gload16(Q + (long long)qrow * a.ldq + 16 * ks + 8 * hi, qrow < L);
   f32x16 acc[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) acc[n] = zero16();
@@ -878,8 +900,29 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
       stage64_async_s(img + IMG, V, a.ldv, r0, L);
     }
   };
-  wait_vm_all();  // Q fragments in registers before the DMA ring starts (exact vmcnt below)
-  if (kv_end > 0) stage(bufA, 0);
+  // Q tile by LDS-DMA into bufB (free until the first tile prefetches into it), in flight
+  // together with the first K / V tile: one memory round trip before the key loop instead of
+  // two, and whole 256-byte rows per wave-instruction instead of 32 strided 16-byte pieces.
+  // Rows >= L are clamped duplicates (their outputs are never stored).
+  uint4 qf[8];  // B operand of S^T: Q[qrow][16ks + 8hi .. +7]
+  {
+    const bool two = q0 + 64 < L;
+    stage64_async_s(bufB, Q, a.ldq, q0, L);
+    if (two) stage64_async_s(bufB + IMG, Q, a.ldq, q0 + 64, L);
+    if (kv_end > 0) {
+      stage(bufA, 0);
+      wait_vm_8();  // this wave's Q pieces landed (the newest 8 are the K / V tile)
+    } else {
+      wait_vm_all();
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's Q pieces landed
+    asm volatile("" ::: "memory");
+    const int r = 32 * wid + lq;   // row of the 128-row Q block
+    const char* qi = bufB + (r >> 6) * IMG;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = row_read(qi, r & 63, 2 * ks + hi);
+    lds_fence_barrier();  // bufB is the first prefetch target
+  }
   // one K/V tile: prefetch the next into `nxt`, wait for `cur`, compute, release `cur`
   auto tile = [&](char* cur, char* nxt, int kv0) {
     if (kv0 + BN < kv_end) {
@@ -904,10 +947,18 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
     tile(bufA, bufB, kv0);
     if (kv0 + BN < kv_end) tile(bufB, bufA, kv0 + BN);
   }
-  // epilogue: lane holds O[qrow][32n + 8j + 4hi + i] in acc[n][4j + i]
-  if (qrow < L) {
-    T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D + (long long)qrow * a.ldo;
+  // epilogue: lane holds O[qrow][32n + 8j + 4hi + i] in acc[n][4j + i].  The wave's 32 x 128
+  // tile goes through LDS (bufA is free after the loop's last barrier; wave w owns 8 KiB of it)
+  // and leaves as whole 256-byte rows: 8 wave-instructions of 4 rows each instead of 16 per-lane
+  // 8-byte stores that touch 32 rows apiece.
+  {
+    // lane index made opaque here: the tile addresses below must not be hoisted above the key
+    // loop (they would stay live across it and push it over the 256-VGPR budget)
+    int ln = threadIdx.x;
+    asm volatile("" : "+v"(ln));
+    const int lq2 = ln & 31, hi2 = (ln >> 5) & 1;
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+    char* ot = bufA + wid * 8192;
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -915,11 +966,22 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
         struct alignas(8) O4 { T v[4]; } o4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o4.v[i] = from_f32<T>(acc[n][4 * j + i] * inv);
-        *reinterpret_cast<O4*>(O + 32 * n + 8 * j + 4 * hi) = o4;
+        *reinterpret_cast<O4*>(ot + img_off(lq2, 4 * n + j) + 8 * hi2) = o4;
       }
-    if (hi == 0 && a.lse)
+    if (hi == 0 && a.lse && qrow < L)
       a.lse[(long long)head * a.T + s0 + qrow] = l_i > 0.f ? m_i + __log2f(l_i) : INFINITY;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back its own tile only
+    T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D;
+    const int ch = ln & 15;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int r = 4 * it + ((ln >> 4) & 3);
+      const uint4 v = *reinterpret_cast<const uint4*>(ot + img_off(r, ch));
+      if (wq0 + r < L) *reinterpret_cast<uint4*>(O + (long long)(wq0 + r) * a.ldo + ch * 8) = v;
+    }
   }
+  // the next item (persistent launch) refills bufA: every wave's read-back is done first
+  if (a.nitems > 0) lds_fence_barrier();
   };
   if (a.nitems > 0) {
     // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
@@ -1142,24 +1204,44 @@ __global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
     step(kt, bufA, bufB);
     if (kt + 1 < nkt) step(kt + 1, bufB, bufA);
   }
-  // lane: queries q0 + 16 wid + 4lg + r, columns 16n + lr
+  // lane: queries q0 + 16 wid + 4lg + r, columns 16n + lr.  The wave's 16 x 128 tile goes
+  // through LDS (bufA is free after the loop's last barrier; wave w owns 4 KiB of it) and leaves
+  // as whole 256-byte rows (4 wave-instructions) instead of 32 two-byte stores per lane.
   T* dQ = reinterpret_cast<T*>(a.dq) + (long long)s0 * a.lddq + head * D;
+  {
+    int ln = threadIdx.x;  // opaque: keep the tile addresses below out of the key loop
+    asm volatile("" : "+v"(ln));
+    const int lr2 = ln & 15, lg2 = (ln >> 4) & 3;
+    char* ot = bufA + wid * 4096;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qr = q0 + wid * 16 + 4 * lg + r;
-    if (qr >= L) continue;
-    float qv[8];
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * lg2 + r;
+      float qv[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) qv[n] = dq[n][r] * a.scale;
-    if (a.rope_pos != nullptr) {  // column 16n + lr pairs with 16(n + 4) + lr: same lane
-      const long long pb = (long long)a.rope_pos[s0 + qr] * 64 + lr;
+      for (int n = 0; n < 8; ++n) qv[n] = dq[n][r] * a.scale;
+      const int qr = q0 + wid * 16 + row;
+      if (a.rope_pos != nullptr && qr < L) {  // column 16n + lr pairs with 16(n + 4) + lr
+        const long long pb = (long long)a.rope_pos[s0 + qr] * 64 + lr2;
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-        rope_inv_pair(qv[n], qv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
+        for (int n = 0; n < 4; ++n)
+          rope_inv_pair(qv[n], qv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
+      }
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        *reinterpret_cast<T*>(ot + img_off(row, 2 * n + (lr2 >> 3)) + 2 * (lr2 & 7)) =
+            from_f32<T>(qv[n]);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back its own tile only
+    const int ch = ln & 15;
 #pragma unroll
-    for (int n = 0; n < 8; ++n) dQ[(long long)qr * a.lddq + n * 16 + lr] = from_f32<T>(qv[n]);
+    for (int it = 0; it < 4; ++it) {
+      const int row = 4 * it + ((ln >> 4) & 3);
+      const int qr = q0 + wid * 16 + row;
+      const uint4 v = *reinterpret_cast<const uint4*>(ot + img_off(row, ch));
+      if (qr < L) *reinterpret_cast<uint4*>(dQ + (long long)qr * a.lddq + ch * 8) = v;
+    }
   }
+  if (a.nitems > 0) lds_fence_barrier();  // the next item's first DMA refills bufA
   };
   if (a.nitems > 0) {
     // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
