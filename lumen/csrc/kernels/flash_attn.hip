@@ -572,52 +572,30 @@ __global__ void __launch_bounds__(256, 2) bwd_dkdv_kernel(Args a) {
     if (j + 1 < nsteps) step(j + 1, bufB, bufA);
   }
   if constexpr (WDS) store_pend();
-  // write dK (x softmax scale), dV : rows wk0 + 4lg + r, cols 16n + lr.  Each wave's two 16 x 128
-  // tiles go through LDS (bufA is free after the loop's last barrier: wave w owns 8 KiB of it)
-  // and leave as whole 256-byte rows instead of 64 two-byte stores per lane.
+  // write dK (x softmax scale), dV : rows wk0 + 4lg + r, cols 16n + lr.  (Staging these tiles
+  // through LDS for whole-row stores, as the forward's O, measured slower here and in the dQ
+  // kernel: 88.9 -> 92.8 us and 32.6 -> 33.7 us, profiles/r3d/fa)
   T* dK = reinterpret_cast<T*>(a.dk) + (long long)s0 * a.lddk + kvh * D;
   T* dV = reinterpret_cast<T*>(a.dv) + (long long)s0 * a.lddv + kvh * D;
-  {
-    int ln = threadIdx.x;  // opaque: keep the tile addresses below out of the query loop
-    asm volatile("" : "+v"(ln));
-    const int lr2 = ln & 15, lg2 = (ln >> 4) & 3;
-    char* kt = bufA + wid * 8192;
-    char* vt = kt + 4096;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * lg2 + r;
-      const int kr = wk0 + row;
-      float kv[8];
+  for (int r = 0; r < 4; ++r) {
+    const int kr = wk0 + 4 * lg + r;
+    if (kr >= L) continue;
+    float kv[8];
 #pragma unroll
-      for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
-      if (a.rope_pos != nullptr && kr < L) {  // column 16n + lr pairs with 16(n + 4) + lr
-        const long long pb = (long long)a.rope_pos[s0 + kr] * 64 + lr2;
+    for (int n = 0; n < 8; ++n) kv[n] = dk[n][r] * a.scale;
+    if (a.rope_pos != nullptr) {  // column 16n + lr pairs with 16(n + 4) + lr: same lane
+      const long long pb = (long long)a.rope_pos[s0 + kr] * 64 + lr;
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-          rope_inv_pair(kv[n], kv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
-      }
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const int o = img_off(row, 2 * n + (lr2 >> 3)) + 2 * (lr2 & 7);
-        *reinterpret_cast<T*>(kt + o) = from_f32<T>(kv[n]);
-        *reinterpret_cast<T*>(vt + o) = from_f32<T>(dv[n][r]);
-      }
+      for (int n = 0; n < 4; ++n)
+        rope_inv_pair(kv[n], kv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back its own tiles only
-    const int ch = ln & 15;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int row = 4 * it + ((ln >> 4) & 3);
-      const int kr = wk0 + row;
-      const uint4 kv4 = *reinterpret_cast<const uint4*>(kt + img_off(row, ch));
-      const uint4 vv4 = *reinterpret_cast<const uint4*>(vt + img_off(row, ch));
-      if (kr < L) {
-        *reinterpret_cast<uint4*>(dK + (long long)kr * a.lddk + ch * 8) = kv4;
-        *reinterpret_cast<uint4*>(dV + (long long)kr * a.lddv + ch * 8) = vv4;
-      }
+    for (int n = 0; n < 8; ++n) {
+      dK[(long long)kr * a.lddk + n * 16 + lr] = from_f32<T>(kv[n]);
+      dV[(long long)kr * a.lddv + n * 16 + lr] = from_f32<T>(dv[n][r]);
     }
   }
-  if (a.nitems > 0) lds_fence_barrier();  // the next item's first DMA refills bufA
   };
   if (a.nitems > 0) {
     // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
@@ -1204,44 +1182,24 @@ __global__ void __launch_bounds__(256) bwd_dq_ds_kernel(Args a) {
     step(kt, bufA, bufB);
     if (kt + 1 < nkt) step(kt + 1, bufB, bufA);
   }
-  // lane: queries q0 + 16 wid + 4lg + r, columns 16n + lr.  The wave's 16 x 128 tile goes
-  // through LDS (bufA is free after the loop's last barrier; wave w owns 4 KiB of it) and leaves
-  // as whole 256-byte rows (4 wave-instructions) instead of 32 two-byte stores per lane.
+  // lane: queries q0 + 16 wid + 4lg + r, columns 16n + lr
   T* dQ = reinterpret_cast<T*>(a.dq) + (long long)s0 * a.lddq + head * D;
-  {
-    int ln = threadIdx.x;  // opaque: keep the tile addresses below out of the key loop
-    asm volatile("" : "+v"(ln));
-    const int lr2 = ln & 15, lg2 = (ln >> 4) & 3;
-    char* ot = bufA + wid * 4096;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * lg2 + r;
-      float qv[8];
+  for (int r = 0; r < 4; ++r) {
+    const int qr = q0 + wid * 16 + 4 * lg + r;
+    if (qr >= L) continue;
+    float qv[8];
 #pragma unroll
-      for (int n = 0; n < 8; ++n) qv[n] = dq[n][r] * a.scale;
-      const int qr = q0 + wid * 16 + row;
-      if (a.rope_pos != nullptr && qr < L) {  // column 16n + lr pairs with 16(n + 4) + lr
-        const long long pb = (long long)a.rope_pos[s0 + qr] * 64 + lr2;
+    for (int n = 0; n < 8; ++n) qv[n] = dq[n][r] * a.scale;
+    if (a.rope_pos != nullptr) {  // column 16n + lr pairs with 16(n + 4) + lr: same lane
+      const long long pb = (long long)a.rope_pos[s0 + qr] * 64 + lr;
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-          rope_inv_pair(qv[n], qv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
-      }
-#pragma unroll
-      for (int n = 0; n < 8; ++n)
-        *reinterpret_cast<T*>(ot + img_off(row, 2 * n + (lr2 >> 3)) + 2 * (lr2 & 7)) =
-            from_f32<T>(qv[n]);
+      for (int n = 0; n < 4; ++n)
+        rope_inv_pair(qv[n], qv[n + 4], a.rope_cos[pb + 16 * n], a.rope_sin[pb + 16 * n]);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back its own tile only
-    const int ch = ln & 15;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int row = 4 * it + ((ln >> 4) & 3);
-      const int qr = q0 + wid * 16 + row;
-      const uint4 v = *reinterpret_cast<const uint4*>(ot + img_off(row, ch));
-      if (qr < L) *reinterpret_cast<uint4*>(dQ + (long long)qr * a.lddq + ch * 8) = v;
-    }
+    for (int n = 0; n < 8; ++n) dQ[(long long)qr * a.lddq + n * 16 + lr] = from_f32<T>(qv[n]);
   }
-  if (a.nitems > 0) lds_fence_barrier();  // the next item's first DMA refills bufA
   };
   if (a.nitems > 0) {
     // snake order over the heaviest-first item list: round r takes items r*G + w (even r) or
