@@ -111,7 +111,8 @@ def build_rank_envs(a, env: Optional[Dict[str, str]] = None) -> List[Dict[str, s
     vis = visible_device_count(env)
     if nproc is None:
         nproc = int(env.get("SLURM_GPUS_ON_NODE", 0)) or vis or 1
-    if vis > 0 and nproc > vis:
+    # (LUMEN_SHARED_GPU_REHEARSAL=1: ranks deliberately share devices, lumen.parallel.dist)
+    if vis > 0 and nproc > vis and env.get("LUMEN_SHARED_GPU_REHEARSAL") != "1":
         raise SystemExit(f"lumen.launch: {nproc} ranks per node requested but only {vis} GPU(s) "
                          f"are visible to this job; refusing to widen the device set")
     nnodes = a.nnodes or int(env.get("SLURM_NNODES", 1))

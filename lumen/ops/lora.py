@@ -575,7 +575,9 @@ def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: tor
     of a [T, K + 64] buffer, see ``fold_operand``)."""
     shp = x.shape
     x2d = x if x.dim() == 2 else x.reshape(-1, shp[-1])
-    if use_native(x2d):
+    # the adapter kernels take 16-bit activations (the training / serving dtypes); an fp32
+    # model on the GPU (--dtype fp32) runs the adapter products in torch
+    if use_native(x2d) and x2d.dtype != torch.float32:
         if fold is not None and fold_operand(x2d, x2d.shape[1]) is None:
             fold = None
         y = _LoraLinear.apply(x2d if fold is not None else x2d.contiguous(), weight_fn, bias, A,

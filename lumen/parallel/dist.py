@@ -63,9 +63,18 @@ def init(backend: Optional[str] = None, device: Optional[str] = None,
         timeout_s = int(os.environ.get("LUMEN_DIST_TIMEOUT", "1800"))
     rank, world, local, local_world = env_ints()
     want_gpu = device != "cpu" and (device == "cuda" or torch.cuda.is_available())
+    shared = os.environ.get("LUMEN_SHARED_GPU_REHEARSAL", "0") == "1" and world > 1
     if want_gpu:
         ndev = torch.cuda.device_count()
-        if local >= ndev:
+        if shared:
+            # rehearsal of the multi-rank RCCL path on fewer GPUs than ranks (testing only):
+            # ranks share devices round-robin, and each rank claims its own RCCL "host" so
+            # RCCL's duplicate-device check passes and the ranks talk over its socket transport
+            # (loopback).  Collective semantics are RCCL's; timings mean nothing.
+            os.environ["NCCL_HOSTID"] = f"lumen-rehearsal-{rank}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            local = local % max(ndev, 1)
+        elif local >= ndev:
             raise RuntimeError(
                 f"LOCAL_RANK={local} but only {ndev} GPU(s) are visible "
                 f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')}, "
@@ -98,7 +107,7 @@ def barrier():
     if dist.is_initialized():
         e = get_env()
         if e.backend == "nccl":
-            dist.barrier(device_ids=[e.local_rank])
+            dist.barrier(device_ids=[e.device.index])
         else:
             dist.barrier()
 

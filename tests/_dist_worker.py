@@ -23,7 +23,9 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
         os.environ["LUMEN_ZERO3_SCHEDULE"] = extra["schedule"]
     if extra and extra.get("single"):
         os.environ["LUMEN_ZERO3_SINGLE"] = "1"
-    env = init(device="cpu")
+    if (extra or {}).get("device") == "cuda" and world > 1:
+        os.environ["LUMEN_SHARED_GPU_REHEARSAL"] = "1"  # RCCL ranks share the one GPU
+    env = init(device=(extra or {}).get("device", "cpu"))
     raw = {"zero_optimization": {"stage": stage, "reduce_bucket_size": 3000,
                                  "stage3_param_persistence_threshold": 100,
                                  "stage3_max_live_parameters": (extra or {}).get("max_live", 1e9)},
@@ -36,7 +38,8 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
         raw["zero_optimization"]["stage3_prefetch_bucket_size"] = extra["prefetch"]
     if extra and extra.get("reuse") is not None:
         raw["zero_optimization"]["stage3_max_reuse_distance"] = extra["reuse"]
-    ds = load_ds_config(raw, micro, accum, world, 1e-2, dtype_override="fp32")
+    ds = load_ds_config(raw, micro, accum, world, 1e-2,
+                        dtype_override=(extra or {}).get("dtype", "fp32"))
     ex = extra or {}
     a = TrainArgs(model_name=model, synthetic=True, synthetic_samples=64, max_length=16,
                   per_device_train_batch_size=micro, gradient_accumulation_steps=accum,
@@ -235,12 +238,15 @@ def car_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def serve_tp_gpu_worker(rank, world, port, outdir):
-    """TP=2 serving with both ranks on the ONE GPU (gloo carries the step broadcast and the
-    vocab gather; the row-parallel sums take the custom IPC all-reduce, so decode buckets run
-    as hipGraphs).  Rank 0 saves greedy outputs + which paths were active."""
+def serve_tp_gpu_worker(rank, world, port, outdir, backend="gloo"):
+    """TP=2 serving with both ranks on the ONE GPU (``backend`` carries the step broadcast and
+    the vocab gather -- gloo, or RCCL under LUMEN_SHARED_GPU_REHEARSAL; the row-parallel sums
+    take the custom IPC all-reduce, so decode buckets run as hipGraphs).  Rank 0 saves greedy
+    outputs + which paths were active."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
+    if backend == "nccl":
+        os.environ["LUMEN_SHARED_GPU_REHEARSAL"] = "1"
     import torch
 
     from lumen.parallel.dist import init, shutdown
@@ -248,7 +254,7 @@ def serve_tp_gpu_worker(rank, world, port, outdir):
     from lumen.serve.sequence import SamplingParams
     from lumen.serve.tp import worker_loop
 
-    init(backend="gloo", device="cuda")
+    init(backend=backend, device="cuda")
     model = _tp_test_model().to("cuda")
     model = model.to(torch.bfloat16)  # the paged-KV kernels are 16-bit
     cfg = EngineConfig(model="tiny-llama-gqa", device="cuda:0", dtype="bf16", max_model_len=128,
@@ -266,6 +272,7 @@ def serve_tp_gpu_worker(rank, world, port, outdir):
         info["captured"] = sorted(eng.runner._graphs)
         info["car_calls"] = eng.runner.car.calls if eng.runner.car is not None else 0
         eng.runner.car.check()
+        info["backend"] = torch.distributed.get_backend()
         torch.save({"out": [s.output_ids for s in seqs], "info": info},
                    os.path.join(outdir, "tp_gpu_out.pt"))
     else:
@@ -356,3 +363,17 @@ def car_timeout_worker(rank, world, port, outdir):
         with open(os.path.join(outdir, "car_timeout.json"), "w") as f:
             json.dump(res, f)
     dist.destroy_process_group()
+
+
+def rccl_probe_worker(rank, world, port, outdir):
+    """scripts/probes/rccl_probe.py as a spawned rank: RCCL collectives with every rank on the
+    box's one GPU (LUMEN_SHARED_GPU_REHEARSAL)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      LUMEN_SHARED_GPU_REHEARSAL="1")
+    sys.path.insert(0, os.path.join(ROOT, "scripts", "probes"))
+    import rccl_probe
+
+    rccl_probe.main()
+    with open(os.path.join(outdir, f"probe_ok_{rank}"), "w") as f:
+        f.write("ok")
