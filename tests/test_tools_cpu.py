@@ -116,6 +116,42 @@ def test_launch_refuses_to_widen_visible_devices(tmp_path):
     assert "should not run" not in out.stdout
 
 
+def test_shared_gpu_rehearsal_mapping(monkeypatch):
+    """LUMEN_SHARED_GPU_REHEARSAL: the launcher allows more ranks than GPUs, and dist.init maps
+    ranks onto the visible devices round-robin with a per-rank RCCL host id (mocked HIP)."""
+    import argparse
+
+    import lumen.parallel.dist as D
+    from lumen.launch import build_rank_envs
+
+    a = argparse.Namespace(nproc_per_node=4, num_gpus=None, nnodes=None, node_rank=None,
+                           master_addr=None, master_port=29700)
+    envs = build_rank_envs(a, {"HIP_VISIBLE_DEVICES": "0", "LUMEN_SHARED_GPU_REHEARSAL": "1"})
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    with pytest.raises(SystemExit):
+        build_rank_envs(a, {"HIP_VISIBLE_DEVICES": "0"})
+    seen = {}
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: seen.setdefault("dev", d))
+    monkeypatch.setattr(D.dist, "is_initialized", lambda: False)
+    monkeypatch.setattr(D.dist, "init_process_group", lambda **kw: seen.setdefault("kw", kw))
+    monkeypatch.setattr(D, "_ENV", None)
+    for k, v in dict(RANK="3", WORLD_SIZE="4", LOCAL_RANK="3", LOCAL_WORLD_SIZE="4",
+                     LUMEN_SHARED_GPU_REHEARSAL="1").items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.delenv("NCCL_HOSTID", raising=False)
+    try:
+        env = D.init()
+        assert env.device == torch.device("cuda", 1) and seen["dev"] == 1
+        assert seen["kw"]["backend"] == "nccl" and seen["kw"]["device_id"] == env.device
+        assert os.environ["NCCL_HOSTID"] == "lumen-rehearsal-3"
+    finally:
+        D._ENV = None
+        os.environ.pop("NCCL_HOSTID", None)
+        os.environ.pop("NCCL_SOCKET_IFNAME", None)
+
+
 def test_launch_fail_fast(tmp_path):
     script = _write(tmp_path / "w.py", """
         import os, sys, time
