@@ -150,17 +150,53 @@ class IncrementalDetokenizer:
         self.tok = tok
         self.prefix = 0
         self.read = 0
+        self._prefix_text = ""   # decode(ids[prefix:read]), kept across steps (one decode/token)
 
     def step(self, ids: List[int]) -> str:
-        prefix_text = self.tok.decode(ids[self.prefix:self.read])
+        prefix_text = self._prefix_text
         new_text = self.tok.decode(ids[self.prefix:])
         if len(new_text) > len(prefix_text) and not new_text.endswith("\ufffd"):
             self.prefix, self.read = self.read, len(ids)
+            self._prefix_text = self.tok.decode(ids[self.prefix:self.read])
             return new_text[len(prefix_text):]
         return ""
 
     def flush(self, ids: List[int]) -> str:
         return self.tok.decode(ids[self.prefix:])[len(self.tok.decode(ids[self.prefix:self.read])):]
+
+
+def stream_chunk(rid: str, chat: bool, created: int, model: str, delta_text: str,
+                 finish: Optional[str], index: int = 0) -> Dict[str, Any]:
+    """One OpenAI streaming chunk (``chat.completion.chunk`` / ``text_completion``)."""
+    if chat:
+        d = {"content": delta_text} if delta_text else {}
+        ch = {"index": index, "delta": d, "finish_reason": finish}
+        o = "chat.completion.chunk"
+    else:
+        ch = {"index": index, "text": delta_text, "logprobs": None, "finish_reason": finish}
+        o = "text_completion"
+    return {"id": rid, "object": o, "created": created, "model": model, "choices": [ch]}
+
+
+def sse_head(rid: str, chat: bool, created: int, model: str) -> str:
+    """The constant part of a stream's chunks, serialised once per request."""
+    return json.dumps({"id": rid, "object": "chat.completion.chunk" if chat else
+                       "text_completion", "created": created, "model": model})[:-1]
+
+
+def sse_event(head: str, chat: bool, delta_text: str, finish: Optional[str],
+              index: int = 0) -> str:
+    """``data: <json.dumps(stream_chunk(...))>`` built from the pre-serialised head: at 256
+    concurrent streams the API process formats ~13k events per second, and a nested-dict dumps
+    per event was a visible share of its time."""
+    f = "null" if finish is None else json.dumps(finish)
+    if chat:
+        d = '{"content": %s}' % json.dumps(delta_text) if delta_text else "{}"
+        ch = '{"index": %d, "delta": %s, "finish_reason": %s}' % (index, d, f)
+    else:
+        ch = ('{"index": %d, "text": %s, "logprobs": null, "finish_reason": %s}'
+              % (index, json.dumps(delta_text), f))
+    return 'data: %s, "choices": [%s]}\n\n' % (head, ch)
 
 
 def create_app(aengine, served_model_name: Optional[str] = None):
@@ -211,28 +247,37 @@ def create_app(aengine, served_model_name: Optional[str] = None):
         ]
         return PlainTextResponse("\n".join(lines) + "\n")
 
-    async def _one(prompt, params, rid, lora, stops, include_stop, on_delta=None):
-        """Drive one engine stream through the detokenizer and the stop-string check.  Calls
-        ``on_delta(text, finish_reason, seq)`` per engine step (streaming); returns
-        (text, seq, finish_reason)."""
+    async def _deltas(prompt, params, rid, lora, stop):
+        """One engine stream through the detokenizer and the stop-string check: yields
+        (text delta, finish_reason | None, seq) per engine step that produced tokens."""
         detok = IncrementalDetokenizer(tok)
+        last = None
+        try:
+            async for seq in aengine.stream(prompt, params, rid, lora):
+                last = seq
+                fin = seq.finish_reason if seq.finished else None
+                d = detok.step(seq.output_ids)
+                if fin:
+                    d += detok.flush(seq.output_ids)
+                out = stop.feed(d, final=fin is not None)
+                if stop.stopped:
+                    fin = "stop"
+                yield out, fin, seq
+                if fin is not None:
+                    break   # a stop string ends the stream early: the engine request is aborted
+        finally:
+            if last is not None:
+                stats.observe(last)
+
+    async def _one(prompt, params, rid, lora, stops, include_stop, on_delta=None):
+        """Drive one engine stream to completion.  Calls ``on_delta(text, finish_reason, seq)``
+        per engine step (streaming); returns (text, seq, finish_reason)."""
         stop = StopChecker(stops, include_stop)
         last, fin = None, None
-        async for seq in aengine.stream(prompt, params, rid, lora):
+        async for out, fin, seq in _deltas(prompt, params, rid, lora, stop):
             last = seq
-            fin = seq.finish_reason if seq.finished else None
-            d = detok.step(seq.output_ids)
-            if fin:
-                d += detok.flush(seq.output_ids)
-            out = stop.feed(d, final=fin is not None)
-            if stop.stopped:
-                fin = "stop"
             if on_delta is not None:
                 await on_delta(out, fin, seq)
-            if fin is not None:
-                break   # a stop string ends the stream early: the engine request is aborted
-        if last is not None:
-            stats.observe(last)
         return stop.text, last, fin
 
     async def _run(prompt, params, chat: bool, stream: bool, model: str, body: Dict[str, Any]):
@@ -254,16 +299,30 @@ def create_app(aengine, served_model_name: Optional[str] = None):
                 p.seed = p.seed + i     # distinct choices under a fixed seed
             return p
 
-        def chunk(delta_text, finish, index=0):
-            if chat:
-                d = {"content": delta_text} if delta_text else {}
-                ch = {"index": index, "delta": d, "finish_reason": finish}
-                o = "chat.completion.chunk"
-            else:
-                ch = {"index": index, "text": delta_text, "logprobs": None,
-                      "finish_reason": finish}
-                o = "text_completion"
-            return {"id": rid, "object": o, "created": created, "model": model, "choices": [ch]}
+        head = sse_head(rid, chat, created, model)
+
+        def sse(delta_text, finish, index=0):
+            return sse_event(head, chat, delta_text, finish, index)
+
+        if stream and n == 1:
+            async def gen1():
+                # one choice: the engine stream drives the response directly (no per-token
+                # queue hop or task switch)
+                if chat:
+                    first = {"id": rid, "object": "chat.completion.chunk", "created": created,
+                             "model": model, "choices": [{"index": 0,
+                                                          "delta": {"role": "assistant"},
+                                                          "finish_reason": None}]}
+                    yield f"data: {json.dumps(first)}\n\n"
+                stop = StopChecker(stops, include_stop)
+                try:
+                    async for out, fin, _seq in _deltas(prompt, sub_params(0), rid, lora, stop):
+                        yield sse(out, fin)
+                except ValueError as e:
+                    stats.errors += 1
+                    yield f"data: {json.dumps({'error': {'message': str(e)}})}\n\n"
+                yield "data: [DONE]\n\n"
+            return StreamingResponse(gen1(), media_type="text/event-stream")
 
         if stream:
             async def gen():
@@ -274,7 +333,7 @@ def create_app(aengine, served_model_name: Optional[str] = None):
                         # one event per engine step that produced tokens, even when the text
                         # delta is still empty (incomplete UTF-8 / held-back stop prefix):
                         # clients see token timing (TTFT, inter-token latency)
-                        await q.put(f"data: {json.dumps(chunk(text, fin, i))}\n\n")
+                        await q.put(sse(text, fin, i))
                     try:
                         await _one(prompt, sub_params(i), f"{rid}-{i}" if n > 1 else rid, lora,
                                    stops, include_stop, on_delta)

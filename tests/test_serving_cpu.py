@@ -523,3 +523,19 @@ def test_fp8_kv_cache_engine_cpu(model):
     out = _engine(model, num_blocks=200, kv_cache_dtype="fp8").generate(
         [[5, 17, 33, 9]], SamplingParams(max_tokens=8, temperature=0.0))
     assert len(out[0].output_ids) == 8
+
+
+def test_sse_event_template_matches_chunk_json():
+    """The pre-serialised SSE event is exactly json.dumps of the chunk dict."""
+    import json
+
+    from lumen.serve.api_server import sse_event, sse_head, stream_chunk
+
+    for chat in (False, True):
+        head = sse_head("cmpl-x\"y", chat, 1700000000, "m/é")
+        for text, fin, idx in (("hi", None, 0), ("", None, 1), ("a\"b\n中", "stop", 2),
+                               ("x", "length", 0)):
+            ev = sse_event(head, chat, text, fin, idx)
+            assert ev.startswith("data: ") and ev.endswith("\n\n")
+            want = stream_chunk("cmpl-x\"y", chat, 1700000000, "m/é", text, fin, idx)
+            assert ev[6:-2] == json.dumps(want)
