@@ -34,14 +34,18 @@ template <> __device__ __forceinline__ fp16 from_f32<fp16>(float x) { return __f
 // two f32 -> one packed 16-bit pair (element 0 in the low half), round to nearest even.  For
 // bf16 this is ONE v_cvt_pk_bf16_f32; converting the elements one at a time compiles to two
 // conversions plus a shift and an or per pair (4x the VALU in the attention / LoRA inner loops).
+// fp16 likewise: ONE v_cvt_pk_f16_f32 (gfx950).  __floats2half2_rn compiled to two
+// v_cvt_f16_f32 + v_perm per pair, and the compiler then waited for each feeding load on its
+// own (lora3_dy: 116 vs 39 s_waitcnt, 58 vs 36 us per call; profiles/r3d/fp16).
 typedef float lumen_f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 lumen_bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 lumen_f16x2 __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ unsigned pk2(float a, float b);
 template <> __device__ __forceinline__ unsigned pk2<bf16>(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(lumen_f32x2{a, b}, lumen_bf16x2));
 }
 template <> __device__ __forceinline__ unsigned pk2<fp16>(float a, float b) {
-  return __builtin_bit_cast(unsigned, __floats2half2_rn(a, b));
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(lumen_f32x2{a, b}, lumen_f16x2));
 }
 
 // 16-byte vector of 8 half-precision elements.
