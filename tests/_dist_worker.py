@@ -25,6 +25,7 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
         os.environ["LUMEN_ZERO3_SINGLE"] = "1"
     if (extra or {}).get("device") == "cuda" and world > 1:
         os.environ["LUMEN_SHARED_GPU_REHEARSAL"] = "1"  # RCCL ranks share the one GPU
+        os.environ.setdefault("LUMEN_DIST_TIMEOUT", "120")  # a hung collective fails the test
     env = init(device=(extra or {}).get("device", "cpu"))
     raw = {"zero_optimization": {"stage": stage, "reduce_bucket_size": 3000,
                                  "stage3_param_persistence_threshold": 100,
@@ -247,6 +248,7 @@ def serve_tp_gpu_worker(rank, world, port, outdir, backend="gloo"):
                       WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
     if backend == "nccl":
         os.environ["LUMEN_SHARED_GPU_REHEARSAL"] = "1"
+        os.environ.setdefault("LUMEN_DIST_TIMEOUT", "120")
     import torch
 
     from lumen.parallel.dist import init, shutdown
@@ -370,7 +372,7 @@ def rccl_probe_worker(rank, world, port, outdir):
     box's one GPU (LUMEN_SHARED_GPU_REHEARSAL)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
-                      LUMEN_SHARED_GPU_REHEARSAL="1")
+                      LUMEN_SHARED_GPU_REHEARSAL="1", LUMEN_DIST_TIMEOUT="120")
     sys.path.insert(0, os.path.join(ROOT, "scripts", "probes"))
     import rccl_probe
 
