@@ -48,7 +48,8 @@ def run_serve_bench(args) -> dict:
 
     a = types.SimpleNamespace(
         model=args.serve_model or args.model, max_model_len=1024, max_num_seqs=256,
-        max_batched_tokens=2048, no_graphs=False, sync_scheduling=False, kv_cache_dtype="auto",
+        max_batched_tokens=2048, prefill_boost=int(os.environ.get("LUMEN_PREFILL_BOOST", "1")),
+        no_graphs=False, sync_scheduling=False, kv_cache_dtype="auto",
         num_requests=256, prompt_len=512, max_tokens=128, temperature=0.0, request_rate=None)
     t0 = time.time()
     try:
@@ -61,7 +62,8 @@ def run_serve_bench(args) -> dict:
     out["bench_s"] = round(time.time() - t0, 1)
     out["config"] = {"model": a.model, "tp": 1, "requests": a.num_requests,
                      "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
-                     "max_num_batched_tokens": a.max_batched_tokens, "kv_cache_dtype": "bf16",
+                     "max_num_batched_tokens": a.max_batched_tokens,
+                     "prefill_boost": a.prefill_boost, "kv_cache_dtype": "bf16",
                      "sampling": "greedy, ignore_eos", "arrival": "all at t=0",
                      "async_scheduling": r.get("async_scheduling"), "mode": "in-process engine"}
     return out

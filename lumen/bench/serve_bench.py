@@ -37,7 +37,7 @@ def bench_engine(a) -> dict:
 
     cfg = EngineConfig(model=a.model, dtype="bf16", max_model_len=a.max_model_len,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_batched_tokens,
-                       use_graphs=not a.no_graphs, init="random",
+                       prefill_boost=a.prefill_boost, use_graphs=not a.no_graphs, init="random",
                        async_scheduling=not a.sync_scheduling, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.time()
     eng = LLMEngine(cfg)
@@ -101,7 +101,8 @@ def bench_http(a) -> dict:
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "serve.py"), "--model", a.model,
            "--port", str(port), "--max-model-len", str(a.max_model_len),
            "--max-num-seqs", str(a.max_num_seqs),
-           "--max-num-batched-tokens", str(a.max_batched_tokens)]
+           "--max-num-batched-tokens", str(a.max_batched_tokens),
+           "--prefill-boost", str(a.prefill_boost)]
     if a.no_graphs:
         cmd.append("--no-graphs")
     if a.kv_cache_dtype != "auto":
@@ -150,6 +151,8 @@ def main():
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
+    ap.add_argument("--prefill-boost", type=int, default=1,
+                    help="x token budget while at most max-num-seqs/4 sequences decode (1: off)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     ap.add_argument("--sync-scheduling", action="store_true",

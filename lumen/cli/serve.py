@@ -29,6 +29,8 @@ def build_parser():
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-num-batched-tokens", type=int, default=2048,
                     help="tokens per engine step (running decodes + prefill chunks)")
+    ap.add_argument("--prefill-boost", type=int, default=1,
+                    help="x token budget while at most max-num-seqs/4 sequences decode (1: off)")
     ap.add_argument("--block-size", type=int, default=16)
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
     ap.add_argument("--no-graphs", action="store_true")
@@ -75,7 +77,7 @@ def main(argv=None):
                        max_model_len=a.max_model_len, block_size=a.block_size,
                        gpu_memory_utilization=a.gpu_memory_utilization,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_num_batched_tokens,
-                       tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs,
+                       prefill_boost=a.prefill_boost, tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs,
                        kv_cache_dtype=a.kv_cache_dtype,
                        lora_modules=dict(m.split("=", 1) for m in a.lora_modules)
                        if a.lora_modules else None, max_loras=a.max_loras)

@@ -4,7 +4,9 @@
 Every engine step spends a TOKEN BUDGET (``max_num_batched_tokens``):
 
 1. every running sequence that is past its prompt decodes one token (always: a prefill never
-   stalls the running streams, which is what bounds inter-token latency under load);
+   stalls the running streams, which is what bounds inter-token latency under load); while
+   only a few sequences decode, the budget is ``prefill_boost`` times larger (few streams pay
+   for the longer step; a burst of arrivals reaches its first tokens sooner);
 2. the rest of the budget goes to prefill CHUNKS, first to sequences whose prompt is already
    partly in the cache, then to waiting requests in arrival order.  A prompt longer than what
    is left is split: its first chunk runs now, the next chunks in later steps (its queries
@@ -34,6 +36,12 @@ class SchedulerConfig:
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 2048
     max_model_len: int = 4096
+    # prefill boost: while at most ``boost_max_decodes`` sequences are decoding, a step may
+    # batch ``prefill_boost`` x the token budget.  The budget exists to bound the inter-token
+    # latency of the running streams; with few of them, a longer step delays few tokens, and the
+    # waiting prompts get their first token sooner (a burst of arrivals).  1 disables it.
+    prefill_boost: int = 1
+    boost_max_decodes: int = 0   # 0: max_num_seqs // 4
 
 
 @dataclass
@@ -108,6 +116,9 @@ class Scheduler:
                         batch.decodes.remove(victim)
                     if victim is s:
                         break
+        if self.cfg.prefill_boost > 1 and len(batch.decodes) <= (
+                self.cfg.boost_max_decodes or self.cfg.max_num_seqs // 4):
+            budget *= self.cfg.prefill_boost
         budget -= len(batch.decodes)
         # 2) continue partially cached prompts, then admit waiting requests (FCFS)
         for s in self.running:

@@ -314,7 +314,7 @@ def test_chunked_prefill_and_mixed_steps_match_naive(model):
     """A 12-token step budget: prompts longer than it are prefilled in chunks over several
     steps (queries attend to the cached earlier chunks), and every step after the first mixes
     the running decodes with prefill chunks.  Greedy outputs == full-recompute decoding."""
-    eng = _engine(model, num_blocks=256, max_num_batched_tokens=12)
+    eng = _engine(model, num_blocks=256, max_num_batched_tokens=12, prefill_boost=1)
     prompts = [list(range(3, 40)), [5, 9, 33, 7], list(range(50, 80)), [42, 43]]
     params = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
     kinds, chunked = [], 0
@@ -539,3 +539,29 @@ def test_sse_event_template_matches_chunk_json():
             assert ev.startswith("data: ") and ev.endswith("\n\n")
             want = stream_chunk("cmpl-x\"y", chat, 1700000000, "m/é", text, fin, idx)
             assert ev[6:-2] == json.dumps(want)
+
+
+def test_prefill_boost_budget():
+    """The step budget doubles (prefill_boost = 2) only while at most max_num_seqs // 4
+    sequences decode; above that the plain budget bounds the step."""
+    from lumen.serve.block_manager import BlockManager
+    from lumen.serve.scheduler import Scheduler, SchedulerConfig
+    from lumen.serve.sequence import SamplingParams as SP
+    from lumen.serve.sequence import Sequence
+
+    def plan(n_dec, boost):
+        sch = Scheduler(SchedulerConfig(max_num_seqs=16, max_num_batched_tokens=64,
+                                        max_model_len=512, prefill_boost=boost),
+                        BlockManager(4096, 16))
+        for i in range(n_dec):          # sequences already past their prompt
+            s = Sequence(list(range(8)), SP(), f"d{i}")
+            sch.blocks.allocate(s.seq_id, s.length + 1)
+            s.num_cached, s.prefilled = s.length, True
+            sch.running.append(s)
+        for i in range(8):
+            sch.add(Sequence(list(range(40)), SP(), f"w{i}"))
+        return sch.schedule()
+
+    assert plan(2, 1).num_tokens == 64            # no boost: 2 decodes + 62 prefill tokens
+    assert plan(2, 2).num_tokens == 128           # 2 <= 16 // 4 decoding: budget x 2
+    assert plan(5, 2).num_tokens == 64            # 5 > 4 decoding: the plain budget
