@@ -1264,6 +1264,7 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     else hipLaunchKernelGGL((bwd_dq_ds_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 6) {  // forward over the paged KV cache (32x32x16, 128-row tiles)
     dim3 grid(ntiles, a.nh);
+    if (a.nitems > 0) grid = dim3(std::min(a.nitems, (causal ? 2 : 1) * cu_count()), 1);
     if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((fwd32_kernel<T, false, true>), grid, block, 0, st, a);
   } else {
@@ -1279,11 +1280,13 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 #include <cstdlib>
 // persistent launches (bit 0 dK/dV, 1 forward, 2 dQ-from-dS; bit 3 snake item order);
 // LUMEN_FA_PERSIST overrides.
-// Default 9 = dK/dV only, snake order (r2_55: 98.0 -> 96.3 us same box); same-box A/B at B=8
-// S=512 (gpurun r2_51) dK/dV 109.6 -> 91.6 us persistent, forward
-// 52.4 -> 55.6, dQ 35.2 -> 39.4 (those two lose the hardware's dynamic load balance)
+// Default 11 = dK/dV and forward, snake order.  dK/dV: 109.6 -> 91.6 us persistent (gpurun
+// r2_51), snake 98.0 -> 96.3 (r2_55).  Forward: slower persistent with its round-2 prologue
+// (52.4 -> 55.6), faster since Q arrives by LDS-DMA with the first K/V tile: 45.1 -> 41.0 us at
+// B=8 S=512 and 128 -> 95 us at B=2 S=2048 causal (profiles/r3d/fa).  dQ stays a one-shot grid
+// (35.2 -> 39.4 persistent, r2_51).
 static int fa_persist() {
-  static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 9; }();
+  static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 11; }();
   return v;
 }
 
@@ -1344,6 +1347,10 @@ extern "C" hipError_t lumen_flash_attn_paged(int dtype, int causal, const void* 
   a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
   a.kv_lens = kv_lens; a.block_tables = block_tables; a.bt_stride = bt_stride;
   a.block_size = block_size;
+  // one-shot grid: the persistent form measured neutral on the serving burst (7.54k / 7.51k vs
+  // 7.55k / 7.53k tok/s, profiles/r3d/fa) and its item loop keeps a scratch reload per key tile
+  // in this (PAGED) instantiation
+  a.nitems = 0;
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(6, causal, 20, ntiles, a, st);
   if (dtype == lumen::kF16) return lumen::fa::launch<lumen::fp16>(6, causal, 20, ntiles, a, st);
   return hipErrorInvalidValue;
