@@ -1280,13 +1280,14 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
 #include <cstdlib>
 // persistent launches (bit 0 dK/dV, 1 forward, 2 dQ-from-dS; bit 3 snake item order);
 // LUMEN_FA_PERSIST overrides.
-// Default 11 = dK/dV and forward, snake order.  dK/dV: 109.6 -> 91.6 us persistent (gpurun
-// r2_51), snake 98.0 -> 96.3 (r2_55).  Forward: slower persistent with its round-2 prologue
+// Default 15 = all three, snake order.  dK/dV: 109.6 -> 91.6 us persistent (gpurun r2_51),
+// snake 98.0 -> 96.3 (r2_55).  Forward: slower persistent with its round-2 prologue
 // (52.4 -> 55.6), faster since Q arrives by LDS-DMA with the first K/V tile: 45.1 -> 41.0 us at
-// B=8 S=512 and 128 -> 95 us at B=2 S=2048 causal (profiles/r3d/fa).  dQ stays a one-shot grid
-// (35.2 -> 39.4 persistent, r2_51).
+// B=8 S=512 and 128 -> 95 us at B=2 S=2048 causal.  dQ-from-dS: neutral at B=8 S=512, backward
+// 338 -> 320 us at B=2 S=2048 causal (profiles/r3d/fa; round 2 measured it slower, 35.2 -> 39.4,
+// before the dQ kernel's register fix).
 static int fa_persist() {
-  static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 11; }();
+  static int v = [] { const char* e = std::getenv("LUMEN_FA_PERSIST"); return e ? std::atoi(e) : 15; }();
   return v;
 }
 
