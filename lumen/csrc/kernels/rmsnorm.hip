@@ -218,7 +218,13 @@ static hipError_t launch_fwd(const void* x, const void* res, const void* w, void
                              float* rstd, int rows, int H, float eps, long long ldy,
                              hipStream_t st) {
   dim3 block(256);
-  if (rows < 1024 && H <= 8192) {  // under ~4 waves per CU: one workgroup per row
+  // LUMEN_RMS_FWD_WPR=4: the workgroup-per-row kernel at every row count (A/B switch; slower at
+  // the training shape, profiles/r3d/rmsnorm)
+  static const bool env_row = [] {
+    const char* e = getenv("LUMEN_RMS_FWD_WPR");
+    return e && atoi(e) == 4;
+  }();
+  if ((rows < 1024 || env_row) && H <= 8192) {  // under ~4 waves per CU: one workgroup per row
     dim3 grid(rows);
     const int vpt = (H + 2047) / 2048;
 #define LUMEN_RMS_ROW(V)                                                                          \
@@ -263,8 +269,15 @@ static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const
                              const void* ds_res, void* dx, float* dw, int rows, int H,
                              hipStream_t st) {
   dim3 block(256);
-  // two waves per row once a row needs more than 4 vectors per lane (H > 2048)
-  const int wpr = H > 2048 ? 2 : 1;
+  // four waves per row (one row per workgroup) once a row needs more than 4 vectors per lane
+  // (H > 2048): Llama-2-7B training rows 29.4 -> 26.0 us per call against two waves per row
+  // (profiles/r3d/rmsnorm; the forward measured the opposite way, 24.3 vs 25.9 us, and keeps
+  // two).  LUMEN_RMS_BWD_WPR=2: two.
+  static const int env_bwd_wpr = [] {
+    const char* e = getenv("LUMEN_RMS_BWD_WPR");
+    return e && atoi(e) == 2 ? 2 : 4;
+  }();
+  const int wpr = H > 2048 ? env_bwd_wpr : 1;
   dim3 grid((rows + 4 / wpr - 1) / (4 / wpr));
   const int vpl = (H + 512 * wpr - 1) / (512 * wpr);
 #define LUMEN_RMS_BWD(V, W)                                                                     \
@@ -274,10 +287,15 @@ static hipError_t launch_bwd(const void* dy, const void* s, const void* w, const
     if (vpl <= 1) LUMEN_RMS_BWD(1, 1);
     else if (vpl <= 2) LUMEN_RMS_BWD(2, 1);
     else LUMEN_RMS_BWD(4, 1);
-  } else {
+  } else if (wpr == 2) {
     if (vpl <= 4) LUMEN_RMS_BWD(4, 2);
     else if (vpl <= 8) LUMEN_RMS_BWD(8, 2);
     else if (vpl <= 16) LUMEN_RMS_BWD(16, 2);
+    else return hipErrorInvalidValue;
+  } else {
+    if (vpl <= 2) LUMEN_RMS_BWD(2, 4);
+    else if (vpl <= 4) LUMEN_RMS_BWD(4, 4);
+    else if (vpl <= 8) LUMEN_RMS_BWD(8, 4);
     else return hipErrorInvalidValue;
   }
 #undef LUMEN_RMS_BWD
