@@ -306,6 +306,9 @@ def _transpose_budget(model: nn.Module) -> float:
     if dev is None:
         return float("inf")
     free, total = torch.cuda.mem_get_info(dev)
+    # blocks the caching allocator holds but no tensor uses (e.g. init temporaries) are free
+    # for the W^T copies too (mem_get_info counts them as used)
+    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
     reserve = float(os.environ.get("LUMEN_BWD_WT_RESERVE_GB", "0")) * 2**30 or max(48 * 2**30, 0.25 * total)
     return max(0.0, free - reserve)
 
