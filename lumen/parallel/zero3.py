@@ -429,6 +429,9 @@ class ParamCoordinator:
             plan.append((u, tn, wo))
             need += wo * (u.dtype.itemsize if u.dtype is not None else 2)
         free, total = torch.cuda.mem_get_info(self.device)
+        # blocks the caching allocator holds but no tensor uses count as free (as in the live
+        # budget): after sharding it still caches the full weights' storage
+        free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         gathered = sum(u.padded * u.dtype.itemsize for u in self.units
                        if u.params and u.buf is None)
         if need + gathered > free - max(48 * 2**30, 0.25 * total):
