@@ -33,10 +33,16 @@ METRIC = "train tok/s Llama-2-7B ZeRO-3+LoRA at 1/2/4/8 GPUs; serve tok/s + p50 
 
 
 def run_serve_bench(args) -> dict:
-    """Engine-mode serving bench (lumen/bench/serve_bench.py): continuous batching, chunked
-    prefill (2048-token step budget), hipGraph decode, async scheduling, bf16 KV, greedy, all
-    256 requests arriving at once.  A failure is reported in the record, never fatal to the
-    training number already measured."""
+    """Serving half of the metric, after the timed training region (training model freed).
+
+    One LLMEngine (Llama-2-7B TP=1: continuous batching, chunked prefill with a 2048-token step
+    budget, hipGraph decode, async scheduling, bf16 KV, greedy), two measurements of the same
+    256-request burst (512 in / 128 out, all arriving at t=0):
+      * ``http`` -> ``extra.serve``: the reference's declared path -- the OpenAI HTTP server (a
+        spawned process, the production layout of scripts/serve.py) streaming
+        ``/v1/completions`` to the async load client (a third process; the Locust request shape);
+      * ``engine`` -> ``extra.serve_engine``: the same engine driven in-process (no HTTP).
+    A failure is reported in the record, never fatal to the training number already measured."""
     import gc
     import types
 
@@ -44,28 +50,141 @@ def run_serve_bench(args) -> dict:
 
     gc.collect()
     torch.cuda.empty_cache()
-    from lumen.bench.serve_bench import bench_engine
+    from lumen.bench.serve_bench import bench_engine, bench_http, make_engine
 
     a = types.SimpleNamespace(
         model=args.serve_model or args.model, max_model_len=1024, max_num_seqs=256,
         max_batched_tokens=2048, prefill_boost=int(os.environ.get("LUMEN_PREFILL_BOOST", "1")),
         no_graphs=False, sync_scheduling=False, kv_cache_dtype="auto",
-        num_requests=256, prompt_len=512, max_tokens=128, temperature=0.0, request_rate=None)
+        num_requests=256, concurrency=256, prompt_len=512, max_tokens=128, temperature=0.0,
+        request_rate=None)
+    keep = ("output_tok_s", "ttft_p50_ms", "ttft_p99_ms", "itl_p50_ms", "itl_p99_ms", "wall_s",
+            "total_tok_s", "output_tokens", "preemptions", "steps", "setup_s", "ok", "errors",
+            "http_section_s")
+    conf = {"model": a.model, "tp": 1, "requests": a.num_requests, "prompt_len": a.prompt_len,
+            "max_tokens": a.max_tokens, "max_num_batched_tokens": a.max_batched_tokens,
+            "prefill_boost": a.prefill_boost, "kv_cache_dtype": "bf16",
+            "sampling": "greedy, ignore_eos", "arrival": "all at t=0"}
     t0 = time.time()
     try:
-        r = bench_engine(a)
+        eng = make_engine(a)
+        r = bench_engine(a, eng)
     except Exception as e:  # noqa: BLE001 - keep the training result
-        return {"error": repr(e)[:500]}
-    keep = ("output_tok_s", "ttft_p50_ms", "ttft_p99_ms", "itl_p50_ms", "itl_p99_ms", "wall_s",
-            "total_tok_s", "output_tokens", "preemptions", "steps", "setup_s")
-    out = {k: r[k] for k in keep if k in r}
-    out["bench_s"] = round(time.time() - t0, 1)
-    out["config"] = {"model": a.model, "tp": 1, "requests": a.num_requests,
-                     "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
-                     "max_num_batched_tokens": a.max_batched_tokens,
-                     "prefill_boost": a.prefill_boost, "kv_cache_dtype": "bf16",
-                     "sampling": "greedy, ignore_eos", "arrival": "all at t=0",
-                     "async_scheduling": r.get("async_scheduling"), "mode": "in-process engine"}
+        return {"error": repr(e)[:500]}, None
+    e_out = {k: r[k] for k in keep if k in r}
+    e_out["bench_s"] = round(time.time() - t0, 1)
+    e_out["config"] = dict(conf, async_scheduling=r.get("async_scheduling"),
+                           mode="in-process engine")
+    t1 = time.time()
+    try:
+        h = bench_http(a, eng)
+    except Exception as e:  # noqa: BLE001 - the engine-mode number stands
+        return {"error": "http: " + repr(e)[:500], "engine_fallback": e_out}, e_out
+    finally:
+        eng.shutdown()
+    h_out = {k: h[k] for k in keep if k in h}
+    h_out["bench_s"] = round(time.time() - t1, 1)
+    h_out["vs_engine"] = round(h["output_tok_s"] / max(r["output_tok_s"], 1e-9), 3)
+    h_out["config"] = dict(conf, concurrency=a.concurrency,
+                           mode="OpenAI HTTP API (/v1/completions, SSE) + async load client")
+    return h_out, e_out
+
+
+def run_partitioned(args, env, ds_base, batches, schedule: str, max_live: float,
+                    steps: int = 5, warmup: int = 2) -> dict:
+    """Extra timed steps of a PARTITIONED ZeRO-3 schedule on a fresh model + engine (after the
+    headline engine is freed): ``release`` / ``hybrid`` re-gather frozen weights every use over
+    the weight-gather communicator -- the per-step xGMI traffic ``keep`` avoids.  At world size
+    1 the partitioning is forced (LUMEN_ZERO3_SINGLE: every gather is a device copy)."""
+    import copy
+    import gc
+
+    import torch
+    import torch.distributed as dist
+
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+    from lumen.train.engine import ZeroEngine
+
+    on_gpu = env.device.type == "cuda"
+    gc.collect()
+    if on_gpu:
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+    ds = copy.copy(ds_base)
+    ds.stage3_max_live_parameters = int(max_live)
+    saved = {k: os.environ.get(k) for k in ("LUMEN_ZERO3_SCHEDULE", "LUMEN_ZERO3_SINGLE")}
+    os.environ["LUMEN_ZERO3_SCHEDULE"] = schedule
+    if env.world_size == 1:
+        os.environ["LUMEN_ZERO3_SINGLE"] = "1"
+    try:
+        torch.manual_seed(1234)
+        model = build_model(args.model, dtype=ds.torch_dtype, device=env.device, init="random",
+                            seed=0)
+        apply_lora(model, LoraConfig(r=args.lora_r, lora_dropout=0.05))
+        model.train()
+        eng = ZeroEngine(model, ds, env)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    co = eng.coordinator
+
+    def run(n, off):
+        for s in range(n):
+            for a in range(ds.grad_accum):
+                b = batches[(off + s * ds.grad_accum + a) % len(batches)]
+                loss = eng.forward(b)
+                eng.backward(loss)
+                eng.step()
+        return loss
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            from lumen.parallel.dist import barrier
+
+            barrier()
+            if on_gpu:
+                torch.cuda.synchronize()
+
+    run(warmup, 0)
+    sync()
+    gb0 = co.gathered_bytes
+    co.pop_exposed_wait_ms()
+    co.track_waits = True
+    sk0 = eng.skipped_steps
+    t1 = time.perf_counter()
+    run(steps, warmup)
+    sync()
+    dt = time.perf_counter() - t1
+    exposed = co.pop_exposed_wait_ms()
+    t = torch.tensor([dt, exposed, torch.cuda.max_memory_allocated() / 1e9 if on_gpu else 0.0],
+                     dtype=torch.float32 if on_gpu else torch.float64, device=env.device)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, exposed, peak = (float(x) for x in t.tolist())
+    st = co.stats()
+    out = {"schedule": st["schedule"], "stage3_max_live_parameters": int(max_live),
+           "resident_units": st["resident_units"], "units": st["units"],
+           "ring_buffers": st["pool_size"], "turn_keep": st["turn_keep"],
+           "steps": steps, "warmup": warmup,
+           "ms_per_step": round(dt / steps * 1000, 2),
+           "tok_s": round(env.world_size * ds.micro_batch * ds.grad_accum * args.seq_len
+                          * steps / dt, 1),
+           "peak_hbm_gb_max_rank": round(peak, 2),
+           "gathered_mb_per_step": round((co.gathered_bytes - gb0) / 1e6 / steps, 1),
+           "exposed_gather_wait_ms_per_step_max_rank": round(exposed / steps, 2),
+           "skipped_nonfinite": eng.skipped_steps - sk0,
+           "forced_world1": env.world_size == 1}
+    eng.close()
+    del eng, model, co
+    gc.collect()
+    if on_gpu:
+        torch.cuda.empty_cache()
     return out
 
 
@@ -105,6 +224,11 @@ def main():
                          "bench (Llama-2-7B TP=1, 256 requests x 512 in / 128 out) -> extra.serve")
     ap.add_argument("--no_serve", dest="serve", action="store_false")
     ap.add_argument("--serve_model", default=None, help="serving model (default: --model)")
+    ap.add_argument("--partitioned", default="release,hybrid",
+                    help="after the timed steps: 5 timed steps of each listed partitioned ZeRO-3 "
+                         "schedule (release = the reference live budget 1e9 [configs/"
+                         "ds_config_zero3.json]; hybrid = half the model resident) -> "
+                         "extra.zero3_<schedule>; '' = none")
     args = ap.parse_args()
 
     import torch
@@ -262,21 +386,44 @@ def main():
         par = f"dp{world}-zero{ds.stage}"
     elif coord.identity:
         par = f"dp{world}-zero{ds.stage}(world-1 partition = whole model: no gathers)"
+    elif coord.keep:
+        # frozen base weights gathered once, then resident (replicated): per-step traffic is
+        # the LoRA gradient reduce-scatter + adapter publish; the partitioned schedules are
+        # timed separately (extra.zero3_release / extra.zero3_hybrid)
+        par = f"dp{world}-zero{ds.stage}-keep(frozen weights gathered once, resident)"
     else:
-        par = f"dp{world}-zero{ds.stage}"
+        par = f"dp{world}-zero{ds.stage}-{coord.schedule}"
     gathered_mb = ((coord.gathered_bytes - gb0) / 1e6 / args.steps) if coord else 0.0
     gathered_total_mb = coord.gathered_bytes / 1e6 if coord else 0.0
     zstats = coord.stats() if coord else None
     if wd is not None:
         wd.close()
-    serve = None
+    serve = serve_engine = None
+    parts = {}
+    want_parts = [x for x in args.partitioned.split(",") if x] if ds.stage == 3 else []
+    if want_parts or (args.serve and world == 1 and on_gpu):
+        engine.close()
+        del engine, model, coord
+        engine = None
+        import gc
+
+        gc.collect()
+        if on_gpu:
+            torch.cuda.empty_cache()
+    for sched in want_parts:
+        # the partitioned ZeRO-3 paths, timed after (and outside) the headline region
+        ml = 1e9 if sched == "release" else 0.5 * cfg.num_params()
+        try:
+            parts[sched] = run_partitioned(args, env, ds, batches, sched, ml)
+        except Exception as e:  # noqa: BLE001 - keep the headline result
+            parts[sched] = {"error": repr(e)[:300]}
+            if world > 1:
+                raise  # ranks may disagree on where they failed: do not continue collectives
     if args.serve and world == 1 and on_gpu:
         # second half of the BASELINE metric ("serve tok/s + p50 TTFT"), after the timed
         # training region: the training model and engine are freed first
-        engine.close()
-        del engine, model, coord, batches
-        serve = run_serve_bench(args)
-        engine = None
+        del batches
+        serve, serve_engine = run_serve_bench(args)
     if env.is_main:
         from lumen.train.trainer import model_flops_per_token
 
@@ -325,7 +472,9 @@ def main():
                 "baseline_tok_s": BASELINE_TOK_S,
                 "gemm_algos": gemm_table,
                 "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,
+                **{f"zero3_{k}": v for k, v in parts.items()},
                 "serve": serve,
+                "serve_engine": serve_engine,
             },
         }
         print(json.dumps(out), file=json_out, flush=True)

@@ -134,7 +134,12 @@ def main():
     ap.add_argument("--max-tokens", type=int, default=128)
     ap.add_argument("--vocab", type=int, default=32000)
     ap.add_argument("--model", default="lumen")
+    ap.add_argument("--warmup", type=int, default=0,
+                    help="first run this many short (4-token) requests, untimed")
     a = ap.parse_args()
+    if a.warmup:
+        asyncio.run(run_load(a.url, a.warmup, a.warmup, a.prompt_len, 4, a.vocab,
+                             model=a.model, seed=1))
     res = asyncio.run(run_load(a.url, a.num_requests, a.concurrency, a.prompt_len, a.max_tokens,
                                a.vocab, a.request_rate, a.model))
     print(json.dumps(res))

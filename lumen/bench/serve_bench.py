@@ -4,8 +4,9 @@ Metric: "serve tok/s + p50 TTFT".  Two modes:
   * ``--mode engine``: in-process LLMEngine, ``--num-requests`` requests arriving all at once (or
     at ``--request-rate``), continuous batching; output tokens/s over the wall time of the run
     and TTFT = first-token time - arrival per request.
-  * ``--mode http``: starts the OpenAI server in a subprocess and drives it with the async
-    client (lumen.bench.async_client) -- the API + load-generator path the reference declares.
+  * ``--mode http``: the production serving path -- engine core in this process, the OpenAI
+    server in a spawned process, the async client (lumen.bench.async_client) in a third: the
+    API + load-generator path the reference declares.
 Random-init weights, random token-id prompts (offline); ``ignore_eos`` so every request produces
 exactly ``--max-tokens`` tokens.
 """
@@ -29,11 +30,9 @@ def _pct(xs, q):
     return s[min(len(s) - 1, int(q * len(s)))] if s else 0.0
 
 
-def bench_engine(a) -> dict:
-    import torch
-
+def make_engine(a):
+    """The LLMEngine both modes serve from (Llama-2-7B preset, random init, bf16)."""
     from lumen.serve.engine import EngineConfig, LLMEngine
-    from lumen.serve.sequence import SamplingParams
 
     cfg = EngineConfig(model=a.model, dtype="bf16", max_model_len=a.max_model_len,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_batched_tokens,
@@ -41,17 +40,35 @@ def bench_engine(a) -> dict:
                        async_scheduling=not a.sync_scheduling, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.time()
     eng = LLMEngine(cfg)
-    setup = time.time() - t0
-    rng = random.Random(0)
+    eng._bench_setup_s = time.time() - t0
+    return eng
+
+
+def _warm(eng, a, rng):
+    """Warm-up: capture the decode-bucket graphs this run will touch."""
+    import torch
+
+    from lumen.serve.sequence import SamplingParams
+
     V = eng.model_config.vocab_size
-    mk = lambda n: [rng.randrange(3, V) for _ in range(n)]  # noqa: E731
-    # warm-up: compile graphs for the decode buckets this run will touch
-    warm = [eng.add_request(mk(a.prompt_len), SamplingParams(max_tokens=4, temperature=0,
-                                                              ignore_eos=True))
+    warm = [eng.add_request([rng.randrange(3, V) for _ in range(a.prompt_len)],
+                            SamplingParams(max_tokens=4, temperature=0, ignore_eos=True))
             for _ in range(min(a.num_requests, a.max_num_seqs))]
     while any(not s.finished for s in warm):
         eng.step()
     torch.cuda.synchronize()
+
+
+def bench_engine(a, eng=None) -> dict:
+    import torch
+
+    from lumen.serve.sequence import SamplingParams
+
+    eng = eng if eng is not None else make_engine(a)
+    rng = random.Random(0)
+    V = eng.model_config.vocab_size
+    mk = lambda n: [rng.randrange(3, V) for _ in range(n)]  # noqa: E731
+    _warm(eng, a, rng)
     params = dict(max_tokens=a.max_tokens, temperature=a.temperature, ignore_eos=True)
     prompts = [mk(a.prompt_len) for _ in range(a.num_requests)]
     seqs = []
@@ -88,59 +105,85 @@ def bench_engine(a) -> dict:
             "kv_blocks": eng.blocks.num_blocks, "preemptions": eng.scheduler.num_preemptions,
             "max_batched_tokens": a.max_batched_tokens, "steps": eng.stats["steps"],
             "async_scheduling": eng.async_sched, "kv_cache_dtype": a.kv_cache_dtype,
-            "setup_s": round(setup, 1), "graphs": sorted(eng.runner._graphs)}
+            "setup_s": round(getattr(eng, "_bench_setup_s", 0.0), 1),
+            "graphs": sorted(eng.runner._graphs)}
 
 
-def bench_http(a) -> dict:
-    from lumen.bench.async_client import run_load
+def bench_http(a, eng=None) -> dict:
+    """The production serving path (``scripts/serve.py``): the engine core loop in THIS (GPU)
+    process, the OpenAI HTTP server in a spawned process talking to it over two queues, and the
+    async client (the Locust request shape: streamed ``/v1/completions`` with ``ignore_eos``) in
+    a third process -- the client's SSE parsing never competes with the engine for a GIL.  With
+    ``eng`` (already warm, e.g. after ``bench_engine``) no model load or graph capture is paid
+    again."""
+    import multiprocessing as mp
+    import threading
+    import urllib.request
 
+    from lumen.serve.frontend import api_process_main, run_engine_core
+
+    t0 = time.time()
+    eng = eng if eng is not None else make_engine(a)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    cmd = [sys.executable, os.path.join(ROOT, "scripts", "serve.py"), "--model", a.model,
-           "--port", str(port), "--max-model-len", str(a.max_model_len),
-           "--max-num-seqs", str(a.max_num_seqs),
-           "--max-num-batched-tokens", str(a.max_batched_tokens),
-           "--prefill-boost", str(a.prefill_boost)]
-    if a.no_graphs:
-        cmd.append("--no-graphs")
-    if a.kv_cache_dtype != "auto":
-        cmd += ["--kv-cache-dtype", a.kv_cache_dtype]
-    proc = subprocess.Popen(cmd, env=dict(os.environ, PYTHONPATH=ROOT))
     url = f"http://127.0.0.1:{port}"
+    ctx = mp.get_context("spawn")
+    req_q, out_q = ctx.Queue(), ctx.Queue()
+    api = ctx.Process(target=api_process_main, name="lumen-api",
+                      args=(req_q, out_q, a.model, a.max_model_len, "127.0.0.1", port, "lumen",
+                            eng.model_config.vocab_size), daemon=True)
+    api.start()
+    client = None
     try:
-        import urllib.request
-
-        t0 = time.time()
         while True:
             try:
                 urllib.request.urlopen(url + "/health", timeout=2)
                 break
             except Exception:
-                if proc.poll() is not None or time.time() - t0 > 600:
-                    raise RuntimeError("server did not come up")
-                time.sleep(1)
-        # warm-up round (graph capture for the buckets)
-        asyncio.run(run_load(url, min(a.concurrency, a.num_requests), a.concurrency,
-                             a.prompt_len, 4))
-        res = asyncio.run(run_load(url, a.num_requests, a.concurrency, a.prompt_len,
-                                   a.max_tokens, request_rate=a.request_rate))
-        res["mode"] = "http"
-        res["prompt_len"], res["max_tokens"] = a.prompt_len, a.max_tokens
-        return res
+                if not api.is_alive() or time.time() - t0 > 300:
+                    raise RuntimeError("API server did not come up")
+                time.sleep(0.2)
+        cmd = [sys.executable, "-m", "lumen.bench.async_client", "--url", url,
+               "--num-requests", str(a.num_requests), "--concurrency", str(a.concurrency),
+               "--prompt-len", str(a.prompt_len), "--max-tokens", str(a.max_tokens),
+               "--vocab", str(eng.model_config.vocab_size),
+               "--warmup", str(min(a.concurrency, a.num_requests))]
+        if a.request_rate:
+            cmd += ["--request-rate", str(a.request_rate)]
+        client = subprocess.Popen(cmd, stdout=subprocess.PIPE, cwd=ROOT,
+                                  env=dict(os.environ, PYTHONPATH=ROOT))
+        out = {}
+
+        def watch():  # the engine core loop ends when the client has its numbers
+            out["stdout"] = client.communicate()[0]
+            req_q.put(("stop",))
+
+        w = threading.Thread(target=watch, daemon=True)
+        w.start()
+        run_engine_core(eng, req_q, out_q)
+        w.join()
+        if client.returncode != 0:
+            raise RuntimeError(f"load client exited with {client.returncode}")
+        lines = [x for x in out["stdout"].decode().splitlines() if x.startswith("{")]
+        res = json.loads(lines[-1])
     finally:
-        proc.terminate()
-        try:
-            proc.wait(30)
-        except subprocess.TimeoutExpired:
-            proc.kill()
+        out_q.put(None)
+        if client is not None and client.poll() is None:
+            client.kill()
+        api.terminate()
+        api.join(10)
+    res["mode"] = "http"
+    res["prompt_len"], res["max_tokens"] = a.prompt_len, a.max_tokens
+    res["http_section_s"] = round(time.time() - t0, 1)
+    return res
 
 
 def main():
     sys.path.insert(0, ROOT)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="engine", choices=["engine", "http"])
+    ap.add_argument("--mode", default="engine", choices=["engine", "http", "both"])
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--num-requests", type=int, default=256)
     ap.add_argument("--concurrency", type=int, default=256)
@@ -158,7 +201,12 @@ def main():
     ap.add_argument("--sync-scheduling", action="store_true",
                     help="engine mode: host waits for each step's tokens before the next step")
     a = ap.parse_args()
-    res = bench_engine(a) if a.mode == "engine" else bench_http(a)
+    if a.mode == "both":
+        eng = make_engine(a)
+        res = bench_http(a, eng)
+        res["engine"] = bench_engine(a, eng)
+    else:
+        res = bench_engine(a) if a.mode == "engine" else bench_http(a)
     res.update(metric="serve tok/s + p50 TTFT (Llama-2-7B, TP=1)", model=a.model, dtype="bf16",
                data="random token-id prompts; random-init weights")
     print(json.dumps(res), flush=True)

@@ -122,6 +122,31 @@ def all_reduce_scalar(x: float, op=dist.ReduceOp.SUM) -> float:
     return float(t.item())
 
 
+_HOST_GROUP = None
+
+
+def host_group():
+    """A gloo group over every rank for host-side agreements (values the host already holds,
+    e.g. a per-step scheduling decision): no device work, no stream sync.  On a gloo world this
+    is the default group (None).  Created on first use -- every rank must reach the first call
+    at the same point of its program (``new_group`` is collective)."""
+    global _HOST_GROUP
+    if not dist.is_initialized() or dist.get_backend() == "gloo":
+        return None
+    if _HOST_GROUP is None:
+        _HOST_GROUP = dist.new_group(backend="gloo")
+    return _HOST_GROUP
+
+
+def agree_all(flag: bool) -> bool:
+    """True only if ``flag`` is True on every rank (MIN all-reduce on the host group)."""
+    if not dist.is_initialized():
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group())
+    return bool(t.item())
+
+
 def broadcast_object(obj, src: int = 0):
     if not dist.is_initialized():
         return obj
@@ -131,10 +156,11 @@ def broadcast_object(obj, src: int = 0):
 
 
 def shutdown():
-    global _ENV
+    global _ENV, _HOST_GROUP
     if dist.is_initialized():
         try:
             barrier()
         finally:
             dist.destroy_process_group()
     _ENV = None
+    _HOST_GROUP = None

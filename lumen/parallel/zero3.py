@@ -29,14 +29,20 @@ MI355X-first design (not a DeepSpeed translation):
       publish only.  (Until round 3 this schedule re-gathered after every unit's backward, and
       a ``pipelined`` variant double-buffered every unit: 102-103 ms/step forced at world 1
       against 91-93 ms for no gathers, profiles/r3_zero3.)
-  ``release`` (budget < model: the reference's ``stage3_max_live_parameters: 1e9``).  A
-      preallocated ring of ``P = budget / unit`` gather buffers (no allocator churn); prefetch
-      depth from ``stage3_prefetch_bucket_size``; the last units of the forward stay live across
-      the forward->backward turn when they fall within ``stage3_max_reuse_distance`` (DeepSpeed's
-      reuse semantics), everything else is gathered twice per micro-step.
+  ``hybrid`` (budget < model but > a two-buffer ring plus one decoder unit: Llama-2-70B on 2-4
+      GPUs, or a user-set live budget, e.g. the reference's 1e9).  As many decoder units as the
+      budget holds beyond the ring are resident (gathered once, W^T once, like ``keep``); they
+      are spread evenly so each remaining unit's per-use all-gather overlaps the compute of the
+      resident units before it, and the look-ahead counts ring units only.  The cost scales
+      with the bytes that do not fit instead of jumping from ``keep`` to ``release``.
+  ``release`` (budget below even that).  A preallocated ring of ``P = budget / unit`` gather
+      buffers (no allocator churn); prefetch depth from ``stage3_prefetch_bucket_size``; the
+      last units of the forward stay live across the forward->backward turn when they fall
+      within ``stage3_max_reuse_distance`` (DeepSpeed's reuse semantics), everything else is
+      gathered twice per micro-step.  ``hybrid`` runs the same ring for its non-resident units.
   ``identity`` (world size 1).  The one-rank partition IS the unit: parameters view the shard
       permanently and no gather runs.  ``LUMEN_ZERO3_SINGLE=1`` instead forces real per-step
-      materialisation (a side-stream copy with RCCL's stream semantics) so the three schedules
+      materialisation (a side-stream copy with RCCL's stream semantics) so the schedules
       above run on a one-GPU box.
 
 * ``offload_param``: pinned host shards are copied H2D on a dedicated copy stream into a ring of
@@ -122,6 +128,9 @@ class _Unit:
         self.wt_numel = 0
         self.wt_buf: Optional[torch.Tensor] = None
         self.wt_event: Optional[object] = None
+        # gathered once and kept (keep: every unit; hybrid: the units the live budget holds
+        # beyond the ring); never released, W^T written once
+        self.resident = False
 
 
 class ParamCoordinator:
@@ -131,7 +140,7 @@ class ParamCoordinator:
     call ``pre_backward(i)`` (before unit i's backward runs); the engine calls
     ``end_micro_step()`` after ``loss.backward()``.  See the module docstring for schedules."""
 
-    SCHEDULES = ("release", "keep", "identity")
+    SCHEDULES = ("release", "hybrid", "keep", "identity")
 
     def __init__(self, model: nn.Module, env: DistEnv, persistence_threshold: int,
                  max_live: int, prefetch_numel: int, offload_param: bool = False,
@@ -208,12 +217,15 @@ class ParamCoordinator:
         self.schedule_reason = ("world size 1: the one-rank partition is the whole unit"
                                 if schedule == "identity" else
                                 "forced (LUMEN_ZERO3_SCHEDULE or caller)")
+        unit_sizes = [u.padded for u in self.units]
         if schedule is None:
-            schedule, self.schedule_reason = self.auto_schedule(total, self.max_live, W)
+            schedule, self.schedule_reason = self.auto_schedule(total, self.max_live, W,
+                                                                unit_sizes)
         assert schedule in self.SCHEDULES, schedule
         self.schedule = schedule
         self.identity = schedule == "identity"
         self.keep = schedule == "keep"
+        self.ring = schedule in ("release", "hybrid")   # some units re-gathered every use
         self._tstream = None
         self._cstream = None
         self.transposed_numel = 0
@@ -224,24 +236,35 @@ class ParamCoordinator:
         avg = (sum(sizes) / len(sizes)) if sizes else 1
         # prefetch depth: upcoming units whose gathered size fits the prefetch bucket
         self.depth = max(1, int(prefetch_numel // max(avg, 1)))
-        # release: ring of P gather buffers sized from the live budget; units kept across the
-        # forward->backward turn (those within the reuse distance that the ring can hold)
+        # release / hybrid: ring of P gather buffers sized from the live budget (hybrid: what
+        # the resident units leave of it); units kept across the forward->backward turn (those
+        # within the reuse distance that the ring can hold)
         self.pool_size = 0
         self.turn_keep = 0
         self._pool: Dict[torch.dtype, List[torch.Tensor]] = {}
         self._pool_alloc = 0
         self.pool_overflows = 0
-        if schedule == "release":
-            n_units = len(sizes)
-            P = int(self.max_live // max(self.max_unit, 1))
-            P = max(2, min(P, n_units))
+        if self.keep:
+            for u in self.units:
+                u.resident = bool(u.params)
+        elif schedule == "hybrid":
+            for i in self.resident_plan(unit_sizes, self.max_live):
+                self.units[i].resident = True
+        self.resident_numel = sum(u.padded for u in self.units if u.resident)
+        if self.ring:
+            ring_sizes = [u.padded for u in self.units if u.padded and not u.resident]
+            n_units = len(ring_sizes)
+            ring_avg = (sum(ring_sizes) / n_units) if n_units else 1
+            P = int((self.max_live - self.resident_numel) // max(self.max_unit, 1))
+            P = max(2, min(P, max(n_units, 2)))
             self.pool_size = P
             # DeepSpeed reuse distance: elements accessed between two uses of a unit.  Unit
             # last-k is reused after ~2k units (k more forward, k backward).  Reuse saves xGMI
             # bytes, prefetch depth only hides latency: the ring serves reuse first, then depth
             reuse_units = int(max_reuse_distance // max(2 * avg, 1))
             self.turn_keep = max(0, min(P - 2, reuse_units))
-            self.depth = max(1, min(self.depth, P - 1 - self.turn_keep))
+            self.depth = max(1, min(int(prefetch_numel // max(ring_avg, 1)),
+                                    P - 1 - self.turn_keep))
         elif self.keep:
             self.depth = max(self.depth, 2)
         # staging ring for offloaded shards (device side of the H2D copy)
@@ -261,17 +284,47 @@ class ParamCoordinator:
 
     # ---- sizing -----------------------------------------------------------------------------
     @staticmethod
-    def auto_schedule(total: int, max_live: int, world: int):
+    def auto_schedule(total: int, max_live: int, world: int,
+                      unit_sizes: Optional[Sequence[int]] = None):
         """(schedule, reason) from the live-parameter budget and the world size.
 
-        * budget < model: ``release`` (the only schedule that bounds live weights; every unit
-          is gathered again at each use).
-        * otherwise ``keep``: one gathered copy of the frozen weights, gathered once and kept
-          resident (the world size only sets how fast that first gather is)."""
-        if total > max_live:
-            return "release", f"model {total:.3g} elements > live budget {max_live:.3g}"
-        return "keep", (f"model {total:.3g} elements <= live budget {max_live:.3g}: frozen "
-                        f"weights gathered once (world {world}) and kept resident")
+        * budget >= model: ``keep``: one gathered copy of the frozen weights, gathered once and
+          kept resident (the world size only sets how fast that first gather is).
+        * budget < model, but above a two-buffer ring plus at least one decoder unit:
+          ``hybrid``: as many units resident as the budget holds beyond the ring, the rest
+          re-gathered at every use -- the cost moves smoothly from ``keep`` to ``release``
+          instead of falling off a cliff one element below the model size.
+        * otherwise ``release`` (every unit gathered again at each use)."""
+        if total <= max_live:
+            return "keep", (f"model {total:.3g} elements <= live budget {max_live:.3g}: frozen "
+                            f"weights gathered once (world {world}) and kept resident")
+        why = f"model {total:.3g} elements > live budget {max_live:.3g}"
+        if unit_sizes is not None:
+            res = ParamCoordinator.resident_plan(unit_sizes, max_live)
+            if res:
+                n = sum(1 for s in unit_sizes if s)
+                return "hybrid", (f"{why}: {len(res)} of {n} units resident, the rest through "
+                                  "a ring of gather buffers")
+        return "release", why
+
+    @staticmethod
+    def resident_plan(unit_sizes: Sequence[int], max_live: int) -> List[int]:
+        """Units kept resident under ``hybrid``: decoder units (1 .. last-1 -- each saves a
+        forward AND a backward gather per micro-step; the embedding has no backward and the head
+        is consumed at the turn anyway), as many as the budget holds after a two-buffer ring,
+        spread evenly so each re-gathered unit's all-gather overlaps resident units' compute."""
+        sizes = list(unit_sizes)
+        mx = max(sizes, default=0)
+        cand = [i for i in range(1, len(sizes) - 1) if sizes[i]]
+        if not cand or mx == 0:
+            return []
+        avail = max_live - 2 * mx
+        per = max(sizes[i] for i in cand)
+        n = int(min(len(cand), max(avail, 0) // per))
+        if n <= 0:
+            return []
+        m = len(cand)
+        return [cand[min(m - 1, int((k + 0.5) * m / n))] for k in range(n)]
 
     def _hbm_live_budget(self, elem_bytes: int) -> int:
         """``stage3_max_live_parameters: "auto"``: elements of gathered weights that fit in the
@@ -293,12 +346,34 @@ class ParamCoordinator:
                     total_numel=self.total_numel, max_live=self.max_live, depth=self.depth,
                     reason=self.schedule_reason,
                     pool_size=self.pool_size, turn_keep=self.turn_keep,
+                    resident_units=sum(1 for u in self.units if u.resident and u.params),
+                    resident_numel=self.resident_numel,
                     pool_overflows=self.pool_overflows, separate_group=self.group is not None,
                     offload=self.offload)
 
+    def pending_alloc_bytes(self) -> int:
+        """HBM this coordinator will still allocate at the first micro-steps: resident units not
+        gathered yet, their planned W^T copies, ring buffers not created yet (a memory estimate
+        made right after engine init -- e.g. ``--gradient_checkpointing auto`` -- must count
+        them: under ``keep`` that is a whole model copy plus W^T)."""
+        if self.identity:
+            return 0
+        n = 0
+        for u in self.units:
+            if not u.params:
+                continue
+            isz = u.dtype.itemsize
+            if u.resident and u.buf is None:
+                n += u.padded * isz
+            if u.tn and u.wt_buf is None:
+                n += u.wt_numel * isz
+        isz = units_dtype_bytes(self.units)
+        n += max(0, self.pool_size - self._pool_alloc) * self.max_unit * isz
+        return n
+
     # ---- buffers ----------------------------------------------------------------------------
     def _buffer(self, u: _Unit) -> torch.Tensor:
-        if self.schedule != "release":
+        if not self.ring or u.resident:
             if u.buf is None:
                 u.buf = torch.empty(u.padded, dtype=u.dtype, device=self.device)
             return u.buf
@@ -408,15 +483,17 @@ class ParamCoordinator:
         u.wt_event = ev
 
     def enable_transposes(self, params: Sequence[nn.Parameter]) -> int:
-        """Keep W^T of these gathered weights next to the gathered buffer (keep schedule, when
-        HBM allows: one more copy of the projections, written once).  Returns the number of
-        weights covered."""
-        if not self.keep or self.device.type != "cuda":
+        """Keep W^T of these gathered weights next to the gathered buffer (resident units of
+        keep / hybrid, when HBM allows: one more copy of the projections, written once).
+        Returns the number of weights covered."""
+        if self.device.type != "cuda" or not any(u.resident for u in self.units):
             return 0
         want = {id(p) for p in params}
         need = 0
         plan = []
         for u in self.units:
+            if not u.resident:
+                continue
             tn, o, wo = [], 0, 0
             for k, p in enumerate(u.params):
                 shape = p._zero_shape
@@ -433,7 +510,8 @@ class ParamCoordinator:
         # budget): after sharding it still caches the full weights' storage
         free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         gathered = sum(u.padded * u.dtype.itemsize for u in self.units
-                       if u.params and u.buf is None)
+                       if u.params and u.buf is None and u.resident)
+        gathered += self.pool_size * self.max_unit * units_dtype_bytes(self.units)
         if need + gathered > free - max(48 * 2**30, 0.25 * total):
             return 0
         n = 0
@@ -523,11 +601,13 @@ class ParamCoordinator:
         u = self.units[i]
         if not u.params:
             return
+        if u.resident:
+            return  # keep / hybrid resident unit: gathered once, frozen, never stale
         if u.state == "inflight":
             u.work.wait()
             u.work = None
         self._unbind(u)
-        if self.schedule == "release" and u.buf is not None:
+        if self.ring and u.buf is not None:
             self._pool.setdefault(u.dtype, []).append(u.buf)
             u.buf = None
         u.state = "empty"
@@ -539,9 +619,21 @@ class ParamCoordinator:
         u = self.units[i]
         if not u.params or u.state != "empty":
             return
-        if self.schedule == "release" and not self._pool_free(u.dtype):
+        if self.ring and not u.resident and not self._pool_free(u.dtype):
             return
         self._issue(i)
+
+    def _ahead(self, i: int, step: int, lo: int = 0):
+        """The ``depth`` units to prefetch after unit i in direction ``step`` (>= lo).  Resident
+        units of a hybrid schedule do not count: the look-ahead is over ring units, so a
+        re-gathered unit's all-gather starts while the resident units before it compute."""
+        j, n = i + step, 0
+        while lo <= j <= self.last and n < self.depth:
+            u = self.units[j]
+            if not (self.ring and u.resident):
+                yield j
+                n += 1
+            j += step
 
     # ---- model hooks ------------------------------------------------------------------------
     def begin_micro_step(self):
@@ -549,7 +641,7 @@ class ParamCoordinator:
         self._in_step = True
         if self.identity:
             return
-        for i in range(min(self.depth, self.last + 1)):
+        for i in self._ahead(-1, 1):
             self._prefetch(i)          # (keep: no-op once the units are resident)
 
     def pre_forward(self, i: int):
@@ -558,13 +650,13 @@ class ParamCoordinator:
         if self.identity:
             return
         self._wait(i)
-        for j in range(i + 1, min(i + 1 + self.depth, self.last + 1)):
+        for j in self._ahead(i, 1):
             self._prefetch(j)
 
     def post_forward(self, i: int, out):
-        # release: the head (last) and the ``turn_keep`` units before it are consumed by the
-        # backward right after the turn and stay live; everything else is freed
-        if self.schedule == "release" and i < self.last - self.turn_keep:
+        # release / hybrid: the head (last) and the ``turn_keep`` units before it are consumed
+        # by the backward right after the turn and stay live; every other ring unit is freed
+        if self.ring and i < self.last - self.turn_keep:
             self._release(i)
         if torch.is_grad_enabled():
             tensors = out if isinstance(out, (tuple, list)) else (out,)
@@ -592,11 +684,11 @@ class ParamCoordinator:
         self._bwd_seen.add(i)
         if self.identity:
             return
-        if self.schedule == "release":
+        if self.ring:
             self._release(i + 1)
         self._wait(i)
-        if self.schedule == "release":
-            for j in range(i - 1, max(i - 1 - self.depth, 0), -1):
+        if self.ring:
+            for j in self._ahead(i, -1, lo=1):
                 self._prefetch(j)  # unit 0 (embedding) has no backward
 
     def end_micro_step(self):
@@ -608,7 +700,7 @@ class ParamCoordinator:
         if self.identity or self.keep:
             return  # keep: the gathered frozen weights stay resident
         for i in range(self.last + 1):
-            self._release(i)
+            self._release(i)   # (hybrid: resident units stay)
 
     def gather_all_full(self) -> None:
         """Materialise every unit (checkpoint save with gather_16bit_weights_on_model_save).

@@ -109,10 +109,12 @@ class ZeroEngine:
             from ..models.layers import configure_backward_layout
 
             configure_backward_layout(model)  # TN input-gradient GEMMs for persistent weights
-            # ... and for resident (keep) gathered ones: W^T written once, on a side stream right
-            # after the unit's first gather, when HBM allows (release re-gathers every use and
-            # keeps the on-the-fly q|k|v / down transposes, Linear.transpose_gathered)
-            if self.coordinator is not None and self.coordinator.keep:
+            # ... and for resident (keep / hybrid) gathered ones: W^T written once, on a side
+            # stream right after the unit's first gather, when HBM allows (ring units are
+            # re-gathered every use and keep the on-the-fly q|k|v / down transposes,
+            # Linear.transpose_gathered)
+            if self.coordinator is not None and (self.coordinator.keep
+                                                 or self.coordinator.schedule == "hybrid"):
                 from ..models.layers import Linear
 
                 self.coordinator.enable_transposes(

@@ -21,7 +21,7 @@ from ..data import (CausalLMCollator, PackedCollator, PrefetchLoader, ShardedSam
                     build_dataset, load_tokenizer)
 from ..lora import LoraConfig, apply_lora, print_trainable_parameters, save_adapter
 from ..models import build_model, get_config
-from ..parallel.dist import DistEnv, all_reduce_scalar, barrier
+from ..parallel.dist import DistEnv, agree_all, all_reduce_scalar, barrier
 from ..utils.debug import StepProfiler, StepWatchdog, check_finite, maybe_inject_fault
 from .checkpoint import AsyncCheckpointer, latest_checkpoint, load_checkpoint, save_checkpoint
 from .config import DSConfig
@@ -123,6 +123,9 @@ class Trainer:
         self.ckpt = AsyncCheckpointer() if args.async_save else None
         self.flops_per_token = model_flops_per_token(cfg, args.max_length)
         self._plans: Dict[int, List[List[int]]] = {}
+        # accumulation groups: fused / run micro-batch by micro-batch / fusable here but not on
+        # every rank (vetoed by the cross-rank agreement)
+        self.fusion_stats = {"fused": 0, "unfused": 0, "vetoed": 0}
 
     # ---------------------------------------------------------------------------------------
     def _auto_checkpointing(self) -> bool:
@@ -141,6 +144,13 @@ class Trainer:
             tokens *= self.ds.grad_accum
         est = tokens * cfg.num_hidden_layers * 16 * cfg.hidden_size * 2
         free, _ = torch.cuda.mem_get_info(env.device)
+        # blocks the caching allocator holds but no tensor uses are free for activations
+        free += torch.cuda.memory_reserved(env.device) - torch.cuda.memory_allocated(env.device)
+        # ZeRO-3 allocates at the first micro-steps what is not there yet: the resident
+        # gathered units (keep: a whole model copy) with their W^T, and the ring buffers
+        co = self.engine.coordinator
+        if co is not None:
+            free = max(0, free - co.pending_alloc_bytes())
         on = 2 * est > free
         self.print(f"[lumen] activation checkpointing {'ON' if on else 'off'} (auto): "
                    f"~{est / 1e9:.1f} GB of activations per micro-step vs {free / 1e9:.1f} GB "
@@ -237,7 +247,16 @@ class Trainer:
             buf.append((raw, cb))
             if len(buf) < k:
                 continue
-            if len({c["n_valid"] for _, c in buf}) == 1:
+            local = len({c["n_valid"] for _, c in buf}) == 1
+            fuse = local
+            if self.env.world_size > 1:
+                # one decision for every rank: a fused rank runs ONE forward / backward (one set
+                # of ZeRO-3 gathers and bucket reduce-scatters) where an unfused one runs k --
+                # mismatched collectives would hang or cross.  Host-side (gloo) agreement: no
+                # device sync on the step path
+                fuse = agree_all(local)
+            self.fusion_stats["fused" if fuse else "vetoed" if local else "unfused"] += 1
+            if fuse:
                 yield [e for r, _ in buf for e in r], fuse_collated([c for _, c in buf]), k
             else:
                 for r, c in buf:
@@ -250,6 +269,16 @@ class Trainer:
         if self.token_budget:
             return len(self._plan(0)) // self.ds.grad_accum
         return len(self.sampler) // (self.ds.micro_batch * self.ds.grad_accum)
+
+    def planned_steps(self) -> int:
+        """Optimizer steps of the whole run (no ``max_steps``).  Token-budget plans differ in
+        length from epoch to epoch (each epoch packs its own permutation), so the total -- which
+        sets the HF-linear decay horizon -- sums every epoch's rank-agreed plan; the engine's
+        accumulation boundary runs across epochs, hence one floor over the sum."""
+        if not self.token_budget:
+            return max(self.steps_per_epoch(), 1) * self.args.num_train_epochs
+        n = sum(len(self._plan(e)) for e in range(self.args.num_train_epochs))
+        return max(n // self.ds.grad_accum, 1)
 
     def train(self) -> Dict:
         a, ds, env, eng = self.args, self.ds, self.env, self.engine
@@ -281,8 +310,7 @@ class Trainer:
                 self.print(f"[lumen] resumed from {ck} (step {eng.global_step})")
             else:
                 self.print("[lumen] no checkpoint found; starting fresh")
-        spe = max(self.steps_per_epoch(), 1)
-        total_steps = a.max_steps if a.max_steps > 0 else spe * a.num_train_epochs
+        total_steps = a.max_steps if a.max_steps > 0 else self.planned_steps()
         eng.set_total_steps(total_steps)  # HF linear decay (baseline: no DeepSpeed config)
         self.print(f"[lumen] ZeRO-{ds.stage} world={env.world_size} micro={ds.micro_batch} "
                    f"accum={ds.grad_accum} effective batch={ds.train_batch_size} "

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 4, first call: ZeRO-3 hybrid schedule + RCCL async-offload tests, then the driver's bench
+# (headline + partitioned release / hybrid timings + HTTP serving section)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4_1}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_zero3_gpu.py tests/test_rccl_gpu.py -v --timeout 180 --timeout-method thread > $O/gpu_tests.txt 2>&1
+rc=$?; grep -E "PASSED|FAILED|ERROR" $O/gpu_tests.txt | tail -40; tail -1 $O/gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 - <<EOF
+import json
+d = json.load(open("$O/bench.json"))
+e = d["extra"]
+print("train", d["value"], d["ms_per_step"], d["config"]["parallelism"])
+for k in ("zero3_release", "zero3_hybrid", "serve", "serve_engine"):
+    print(k, json.dumps(e.get(k)))
+EOF
+timeout -k 10 400 python -m lumen.bench.decode_gemm_probe > $O/decode_probe.jsonl 2> $O/decode_probe.err || { tail -5 $O/decode_probe.err; exit 1; }
+grep step_ms $O/decode_probe.jsonl

@@ -19,6 +19,8 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
     from lumen.train.trainer import TrainArgs, Trainer
 
     saved_env = {k: os.environ.get(k) for k in ("LUMEN_ZERO3_SCHEDULE", "LUMEN_ZERO3_SINGLE")}
+    saved_env.update({k: os.environ.get(k) for k in (extra or {}).get("env", {})})
+    os.environ.update((extra or {}).get("env", {}))
     if extra and extra.get("schedule"):
         os.environ["LUMEN_ZERO3_SCHEDULE"] = extra["schedule"]
     if extra and extra.get("single"):
@@ -50,7 +52,7 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
                       "resume", False), save_final=False,
                   output_dir=ex.get("ckdir") or os.path.join(outdir, "ck"),
                   seed=7, gradient_checkpointing=bool((extra or {}).get("gc", False)),
-                  fuse_accumulation=ex.get("fuse", True))
+                  fuse_accumulation=ex.get("fuse", True), synthetic_min_len=ex.get("min_len"))
     try:
         t = Trainer(a, ds, env, printer=lambda *x, **k: None)
         res = t.train()
@@ -69,7 +71,8 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
         if stats is not None:
             stats["gather_group_separate"] = t.engine.gather_group is not None
         torch.save({"sd": sd, "losses": [r["loss"] for r in t.log_history], "res": res,
-                    "zero3": stats},
+                    "zero3": stats, "fusion": dict(t.fusion_stats),
+                    "async_offload": t.engine.async_off is not None},
                    os.path.join(outdir, f"result_stage{stage}_w{world}.pt"))
     shutdown()
 

@@ -78,6 +78,27 @@ def test_zero_rccl_world2_matches_single_process(stage, schedule, dtype, tmp_pat
         assert r["zero3"]["gathers"] > 0
 
 
+@pytest.mark.parametrize("schedule", ["keep", "release"])
+def test_async_offloaded_optimizer_world2_rccl(schedule, tmp_path):
+    """ZeRO-Offload at world 2 on RCCL: the asynchronous host AdamW (D2H on a copy stream, C++
+    AdamW into the rank's shard, the publish all-gathers issued from the next forward's first
+    unit gate) == the synchronous offloaded step, for the resident (keep) and ring (release)
+    gather schedules -- the publish all-gathers share the default communicator with keep's
+    gathers and with the gradient reduce-scatters, so their cross-rank order is exercised."""
+    ex = {"device": "cuda", "dtype": "bf16", "fuse": False, "offload": True,
+          "schedule": schedule}
+    runs = {}
+    for mode in ("0", "1"):
+        runs[mode] = _run(2, 3, str(tmp_path / mode), model="tiny-llama", micro=1, accum=2,
+                          steps=3, extra=dict(ex, env={"LUMEN_OFFLOAD_ASYNC": mode}))
+    sync, asy = runs["0"], runs["1"]
+    assert asy["async_offload"] and not sync["async_offload"]
+    assert asy["zero3"]["schedule"] == schedule and asy["zero3"]["world"] == 2
+    for a, b in zip(asy["losses"], sync["losses"]):
+        assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (asy["losses"], sync["losses"])
+    _close(asy["sd"], sync["sd"])
+
+
 def test_tp2_serving_rccl_on_one_gpu(tmp_path):
     """TP=2 serving with the step broadcast and vocab gather on RCCL (custom IPC all-reduce for
     the row-parallel sums): same greedy tokens as the gloo-broadcast TP run."""

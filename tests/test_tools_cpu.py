@@ -333,8 +333,14 @@ def test_bench_contract_torchrun(world):
         assert k in j, k
     assert j["n_gpus"] == world and j["steps"] == 2 and j["scaling"] == "weak"
     assert j["config"]["global_batch"] == 2 * world
-    assert j["config"]["parallelism"] == f"dp{world}-zero3"
+    assert j["config"]["parallelism"].startswith(f"dp{world}-zero3-keep")
     x = j["extra"]
+    # the partitioned schedules, timed after the headline region on fresh engines
+    for sched in ("release", "hybrid"):
+        p = x[f"zero3_{sched}"]
+        assert p["schedule"] == sched and p["ms_per_step"] > 0, p
+        assert p["gathered_mb_per_step"] > 0 and p["steps"] == 5, p
+    assert x["zero3_release"]["stage3_max_live_parameters"] == int(1e9)
     # "auto" live budget: one gathered copy, gathered once (warm-up) and kept resident
     assert x["zero3"]["schedule"] == "keep", x["zero3"]
     # keep gathers once, on the default communicator (no second RCCL communicator per GPU)

@@ -66,20 +66,41 @@ def _train(monkeypatch, stage, schedule=None, ckpt=False, steps=4, accum=2, bwd_
     return adapter_state_dict(m), losses, eng.coordinator
 
 
+def _layer_numel(name="small-llama"):
+    from lumen.models import get_config
+
+    c = get_config(name)
+    H, D = c.hidden_size, c.head_dim
+    return (H * (c.num_attention_heads + 2 * c.num_key_value_heads) * D
+            + c.num_attention_heads * D * H + 3 * H * c.intermediate_size)
+
+
+# live budgets: release -> 1 element (a ring of 2 buffers); hybrid -> a 2-buffer ring + one of
+# the two decoder layers resident
+_LIVE = {"release": lambda: 1, "hybrid": lambda: int(3.02 * _layer_numel()), "keep": lambda: None}
+
+
 @pytest.mark.parametrize("schedule,ckpt", [("release", False), ("keep", False),
-                                           ("keep", True), ("release", True)])
+                                           ("keep", True), ("release", True),
+                                           ("hybrid", False), ("hybrid", True)])
 def test_zero3_schedules_match_stage0_on_gpu(schedule, ckpt, monkeypatch):
     ref, ref_losses, _ = _train(monkeypatch, 0, ckpt=ckpt)
     # release: a live budget of one unit -> a ring of 2 buffers, nothing kept across the turn,
     # every layer gathered twice per micro-step
-    got, losses, coord = _train(monkeypatch, 3, schedule, ckpt=ckpt,
-                                max_live=1 if schedule == "release" else None)
-    assert coord is not None and coord.schedule == schedule
+    got, losses, coord = _train(monkeypatch, 3, None if schedule == "hybrid" else schedule,
+                                ckpt=ckpt, max_live=_LIVE[schedule]())
+    assert coord is not None and coord.schedule == schedule  # hybrid: the auto choice
     n_units = sum(1 for u in coord.units if u.params)
     if schedule == "release":
         assert coord.pool_size == 2 and coord.turn_keep == 0 and coord.pool_overflows == 0
         # forward: every unit; backward: every layer (the head is consumed at the turn)
         assert coord.gathers == 8 * (n_units + n_units - 2)
+    elif schedule == "hybrid":
+        # the last decoder layer resident (gathered once); embedding, layer 1 and the head go
+        # through a 2-buffer ring: 3 forward gathers + layer 1 again in the backward
+        assert [u.idx for u in coord.units if u.resident] == [2]
+        assert coord.pool_size == 2 and coord.pool_overflows == 0
+        assert coord.gathers == 8 * 4 + 1
     else:
         # keep: every unit gathered once, then resident (frozen weights never go stale)
         assert coord.gathers == n_units
@@ -125,12 +146,12 @@ def test_reference_zero3_config_with_cpu_offload(monkeypatch):
         assert (d > 3e-4 + 5e-3 * ref[k].abs()).float().mean().item() < 5e-3, k
 
 
-@pytest.mark.parametrize("schedule", ["keep", "release"])
+@pytest.mark.parametrize("schedule", ["keep", "release", "hybrid"])
 def test_zero3_schedules_race_free_under_nan_poison(schedule, monkeypatch):
     """Race detector: with LUMEN_ZERO3_POISON every buffer is NaN-filled right before each
     (re-)gather.  A read outside a buffer's live window would make the loss NaN; the run must
     match the unpoisoned one."""
-    ml = 1 if schedule == "release" else None   # release: a 2-buffer ring, re-used every unit
+    ml = _LIVE[schedule]()   # release: a 2-buffer ring, re-used every unit
     ref, ref_losses, _ = _train(monkeypatch, 3, schedule, ckpt=True, steps=3, max_live=ml)
     monkeypatch.setenv("LUMEN_ZERO3_POISON", "1")
     got, losses, coord = _train(monkeypatch, 3, schedule, ckpt=True, steps=3, max_live=ml)

@@ -134,6 +134,9 @@ def deep_reference(tmp_path_factory):
     dict(schedule="release", live_units=5, prefetch_units=1, reuse=0),
     # offloaded (host) shards: H2D + gather issued off the compute stream
     dict(schedule="keep", offload_param=True),
+    # hybrid (the auto choice for this budget): 2 of the 6 layers resident, the rest through a
+    # 2-buffer ring
+    dict(schedule="hybrid", live_units=4, gc=True),
 ])
 def test_zero3_world4_split_groups(case, deep_reference, tmp_path):
     """World 4 over gloo: every schedule, on a separate weight-gather process group, with
@@ -142,6 +145,8 @@ def test_zero3_world4_split_groups(case, deep_reference, tmp_path):
     # fuse=False: the two accumulation micro-steps run as two forward/backward passes (the
     # coordinator's per-micro-step hooks), not as one fused batch
     extra = {"schedule": case["schedule"], "gc": case.get("gc", False), "fuse": False}
+    if case["schedule"] == "hybrid":
+        extra.pop("schedule")  # picked by the auto rule from the budget
     if "live_units" in case:
         extra["max_live"] = int(case["live_units"] * L * 1.02)
     if "prefetch_units" in case:
@@ -157,11 +162,16 @@ def test_zero3_world4_split_groups(case, deep_reference, tmp_path):
     _close(r["sd"], deep_reference["sd"])
     z = r["zero3"]
     assert z["schedule"] == case["schedule"] and z["world"] == 4
-    # release re-gathers every use on its own communicator; keep gathers once, on the default
-    assert z["gather_group_separate"] == (case["schedule"] == "release")
+    # release / hybrid re-gather on their own communicator; keep gathers once, on the default
+    assert z["gather_group_separate"] == (case["schedule"] != "keep")
     assert z["pool_overflows"] == 0
     n_units = 8
-    if case["schedule"] == "release":
+    if case["schedule"] == "hybrid":
+        assert z["resident_units"] == 2 and z["pool_size"] == 2 and z["turn_keep"] == 0
+        # 2 steps x 2 micro-steps x (6 ring units forward + 4 ring layers backward) + the two
+        # resident layers, once
+        assert z["gathers"] == 2 * 2 * (6 + 4) + 2
+    elif case["schedule"] == "release":
         assert z["pool_size"] == case["live_units"]
         if case.get("reuse") == 0:
             assert z["turn_keep"] == 0
@@ -177,21 +187,42 @@ def test_zero3_world4_split_groups(case, deep_reference, tmp_path):
         assert z["gathers"] == n_units  # keep: once per unit, then resident
 
 
-@pytest.mark.parametrize("schedule", ["keep", "release"])
+@pytest.mark.parametrize("schedule", ["keep", "release", "hybrid"])
 def test_zero3_world8_split_groups(schedule, tmp_path):
     """World 8 over gloo (the rank count of the headline 8-GPU run): the schedule on its own
     weight-gather communicator next to the gradient group == single-process stage 0."""
     ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama-deep", micro=8, accum=1, steps=2)
     extra = {"schedule": schedule}
-    if schedule == "release":
+    if schedule != "keep":
         extra["max_live"] = int(3 * _layer_numel() * 1.02)
     r = _run(8, 3, str(tmp_path / "b"), model="tiny-llama-deep", micro=1, accum=1, steps=2,
              extra=extra)
     _close(r["sd"], ref["sd"])
     z = r["zero3"]
     assert z["schedule"] == schedule and z["world"] == 8
-    assert z["gather_group_separate"] == (schedule == "release")
+    assert z["gather_group_separate"] == (schedule != "keep")
+    if schedule == "hybrid":
+        assert z["resident_units"] == 1
     assert z["pool_overflows"] == 0
+
+
+def test_accumulation_fusion_agreed_across_ranks(tmp_path):
+    """Gradient-accumulation fusion (k equal-n_valid micro-batches as one forward / backward) is
+    decided for every rank at once: variable-length rows give groups that are fusable on one
+    rank and not on the other, and a rank-local decision would then issue a different number of
+    ZeRO-3 gathers / reduce-scatters than its peer (a hang).  Fused == unfused results."""
+    L = _layer_numel()
+    ex = {"min_len": 15, "max_live": int(3 * L * 1.02)}   # ring schedule: gathers per forward
+    got = _run(2, 3, str(tmp_path / "f"), model="tiny-llama-deep", micro=1, accum=2, steps=8,
+               extra=dict(ex, fuse=True))
+    ref = _run(2, 3, str(tmp_path / "u"), model="tiny-llama-deep", micro=1, accum=2, steps=8,
+               extra=dict(ex, fuse=False))
+    f = got["fusion"]
+    assert f["vetoed"] > 0 and f["fused"] + f["vetoed"] + f["unfused"] == 8, f
+    assert got["zero3"]["schedule"] in ("release", "hybrid")
+    _close(got["sd"], ref["sd"], tol=1e-5)
+    for a, b in zip(got["losses"], ref["losses"]):
+        assert abs(a - b) < 1e-5 * max(1.0, abs(b))
 
 
 def test_zero3_world1_identity(tmp_path):
@@ -254,3 +285,13 @@ def test_zero3_auto_schedule_rule():
     for w in (2, 3, 4, 8):
         s, why = PC.auto_schedule(100, 100, w)
         assert s == "keep" and "resident" in why
+    # hybrid between the two: embedding 5, 8 layers of 10, head 5 (model 90)
+    sizes = [5] + [10] * 8 + [5]
+    assert PC.auto_schedule(90, 89, 8, sizes)[0] == "hybrid"
+    assert PC.auto_schedule(90, 29, 8, sizes)[0] == "release"   # ring of 2 + not one layer
+    assert PC.auto_schedule(90, 30, 8, sizes)[0] == "hybrid"
+    # residents spread evenly over the decoder layers (indices 1..8)
+    assert PC.resident_plan(sizes, 30) == [5]
+    assert PC.resident_plan(sizes, 60) == [2, 4, 6, 8]
+    assert PC.resident_plan(sizes, 89) == [1, 3, 4, 5, 7, 8]
+    assert PC.resident_plan(sizes, 1000) == list(range(1, 9))
