@@ -229,6 +229,8 @@ def main():
                          "schedule (release = the reference live budget 1e9 [configs/"
                          "ds_config_zero3.json]; hybrid = half the model resident) -> "
                          "extra.zero3_<schedule>; '' = none")
+    ap.add_argument("--partitioned_steps", type=int, default=5,
+                    help="timed steps of each partitioned run (2 untimed warm-up steps first)")
     args = ap.parse_args()
 
     import torch
@@ -414,7 +416,9 @@ def main():
         # the partitioned ZeRO-3 paths, timed after (and outside) the headline region
         ml = 1e9 if sched == "release" else 0.5 * cfg.num_params()
         try:
-            parts[sched] = run_partitioned(args, env, ds, batches, sched, ml)
+            parts[sched] = run_partitioned(args, env, ds, batches, sched, ml,
+                                           steps=args.partitioned_steps,
+                                           warmup=min(2, args.partitioned_steps))
         except Exception as e:  # noqa: BLE001 - keep the headline result
             parts[sched] = {"error": repr(e)[:300]}
             if world > 1:

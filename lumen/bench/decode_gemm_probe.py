@@ -1,10 +1,14 @@
-"""Decode-batch projection GEMMs (serving, Llama-2-7B, TP=1): where hipBLASLt stands at M = 64..256.
+"""Decode-batch projection GEMMs (serving, Llama-2-7B, TP=1): hipBLASLt vs the decode MFMA GEMM.
 
-For every projection shape and decode batch M: y = x @ W^T with the shipped TunableOp table (what
-the serving engine runs), the same after fresh tuning, and the transposed orientation y^T = W @ x^T
-(fresh tuning).  Prints one JSON line per case: microseconds and the weight-streaming rate.
+For every projection shape and decode batch M (the serving graph buckets' block heights): the
+library GEMM y = x @ W^T with the shipped TunableOp table (what the serving engine ran so far),
+and every (BN, split-K) plan of ``kernels/decode_gemm.hip`` for the batch's block height.  The
+weights rotate over copies totalling > 512 MB, so each launch reads W from HBM as in a decode
+step (13 GB of weights per step; a repeated 100 MB matrix would be served by the 256 MB Infinity
+Cache).  Writes the plans that beat the library by > 3% to ``--plans`` (the serving engine's
+table, configs/decode_gemm_plans.json).
 
-    python -m lumen.bench.decode_gemm_probe [--ms 64,128,192,256]
+    python -m lumen.bench.decode_gemm_probe [--ms 64,128,192,256] [--plans out.json]
 """
 from __future__ import annotations
 
@@ -17,14 +21,14 @@ SHAPES = (("qkv", 12288, 4096), ("o", 4096, 4096), ("gate_up", 22016, 4096),
           ("down", 4096, 11008), ("lm_head", 32000, 4096))
 
 
-def _time(fn, iters=30):
-    for _ in range(5):
-        fn()
+def _time(fn, n_w, iters=40):
+    for i in range(6):
+        fn(i % n_w)
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        fn()
+    for i in range(iters):
+        fn(i % n_w)
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / iters * 1000.0
@@ -33,44 +37,68 @@ def _time(fn, iters=30):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="64,128,192,256")
+    ap.add_argument("--plans", default=None, help="write winning plans here (JSON)")
+    ap.add_argument("--win", type=float, default=0.97, help="plan kept if dgemm < win x library")
     a = ap.parse_args()
-    import torch.cuda.tunable as tn
-
+    from lumen.ops.gemm import DG_BNS, decode_gemm, dg_bucket
     from lumen.utils.gemm_tuning import load_tuned_gemms
 
+    load_tuned_gemms()
     dev = torch.device("cuda")
     ms = [int(x) for x in a.ms.split(",")]
-    # weights: distinct buffers per shape, 13 GB total is not needed -- one per shape
-    Ws = {n: torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for n, N, K in SHAPES}
-    xs = {(m, K): torch.randn(m, K, device=dev, dtype=torch.bfloat16)
-          for m in ms for K in {k for _, _, k in SHAPES}}
-    res = {}
-    for mode in ("table", "fresh"):
-        if mode == "table":
-            load_tuned_gemms()
-        else:
-            tn.enable(True)
-            tn.tuning_enable(True)
-            tn.set_max_tuning_duration(30)
-            tn.set_filename("/tmp/decode_probe_tunableop.csv", False)
-        for n, N, K in SHAPES:
-            W = Ws[n]
-            for m in ms:
-                x = xs[(m, K)]
-                us = _time(lambda: torch.matmul(x, W.t()))
-                res[(mode, "xWt", n, m)] = us
-                if mode == "fresh":
-                    res[(mode, "Wxt", n, m)] = _time(lambda: torch.matmul(W, x.t()))
-    for (mode, form, n, m), us in sorted(res.items()):
-        N, K = next((N, K) for nn, N, K in SHAPES if nn == n)
-        print(json.dumps({"mode": mode, "form": form, "shape": n, "M": m, "N": N, "K": K,
-                          "us": round(us, 2), "weight_TBps": round(N * K * 2 / us / 1e6, 2),
-                          "TFps": round(2 * m * N * K / us / 1e6, 1)}), flush=True)
-    # per-M totals of one decode step's projections (32 layers + lm_head)
-    for mode, form in (("table", "xWt"), ("fresh", "xWt"), ("fresh", "Wxt")):
+    plans, rows = [], []
+    tot = {}
+    for name, N, K in SHAPES:
+        n_w = max(2, -(-512 * 2**20 // (N * K * 2)))
+        Ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(n_w)]
         for m in ms:
-            tot = sum(res[(mode, form, n, m)] * (1 if n == "lm_head" else 32) for n, _, _ in SHAPES)
-            print(json.dumps({"mode": mode, "form": form, "M": m, "step_ms": round(tot / 1e3, 3)}))
+            x = torch.randn(m, K, device=dev, dtype=torch.bfloat16)
+            lib = _time(lambda i: torch.matmul(x, Ws[i].t()), n_w)
+            bm = dg_bucket(m)
+            best = None
+            for bn in DG_BNS[bm]:
+                for s in (1, 2, 3, 4, 6, 8):
+                    if s > K // 64:
+                        continue
+                    try:
+                        us = _time(lambda i: decode_gemm(x, Ws[i], bm, bn, s), n_w)
+                    except Exception as e:  # noqa: BLE001
+                        print(json.dumps({"shape": name, "M": m, "BN": bn, "S": s,
+                                          "error": repr(e)[:200]}), flush=True)
+                        continue
+                    rows.append({"shape": name, "M": m, "BM": bm, "BN": bn, "S": s,
+                                 "us": round(us, 2)})
+                    if best is None or us < best[0]:
+                        best = (us, bn, s)
+            ref = x.float() @ Ws[0].float().t()
+            err = ((decode_gemm(x, Ws[0], bm, best[1], best[2]).float() - ref).norm()
+                   / ref.norm()).item()
+            rec = {"shape": name, "M": m, "N": N, "K": K, "lib_us": round(lib, 2),
+                   "dgemm_us": round(best[0], 2), "BM": bm, "BN": best[1], "S": best[2],
+                   "speedup": round(lib / best[0], 3), "rel_err": round(err, 5),
+                   "lib_TBps": round(N * K * 2 / lib / 1e6, 2),
+                   "dgemm_TBps": round(N * K * 2 / best[0] / 1e6, 2)}
+            print(json.dumps(rec), flush=True)
+            layers = 1 if name == "lm_head" else 32
+            t = tot.setdefault(m, [0.0, 0.0])
+            t[0] += lib * layers
+            t[1] += min(lib, best[0]) * layers
+            if best[0] < a.win * lib:
+                plans.append({"N": N, "K": K, "BM": bm, "BN": best[1], "S": best[2],
+                              "M_measured": m, "us": round(best[0], 2), "lib_us": round(lib, 2)})
+        del Ws
+        torch.cuda.empty_cache()
+    for m, (l, d) in sorted(tot.items()):
+        print(json.dumps({"M": m, "step_projections_ms_library": round(l / 1e3, 3),
+                          "step_projections_ms_planned": round(d / 1e3, 3)}), flush=True)
+    for r in rows:
+        print(json.dumps(dict(r, sweep=True)))
+    if a.plans:
+        # one plan per (N, K, BM): the measured M of each bucket is its block height
+        with open(a.plans, "w") as f:
+            json.dump({"source": "lumen/bench/decode_gemm_probe.py (weights rotated over "
+                                 "> 512 MB: HBM-resident like a decode step)",
+                       "plans": plans}, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -64,6 +64,8 @@ hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, con
                             void*, const long long*, int, int, int, int, int, int, hipStream_t);
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
+hipError_t lumen_decode_gemm(int, const void*, const void*, void*, float*, int*, int, int, int,
+                             long long, long long, int, int, int, hipStream_t);
 void lumen_set_gemv_form(int);
 void lumen_set_rms_lds(int, int);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
@@ -208,6 +210,34 @@ void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
                           static_cast<int>(x.size(0)), static_cast<int>(w.size(0)),
                           static_cast<int>(w.size(1)), x.stride(0), y.stride(0), cur_stream()),
         "skinny_gemm");
+}
+
+// decode-batch MFMA GEMM (kernels/decode_gemm.hip): y = x @ w^T with block tile (bm, bn) and
+// split-K s (s > 1: ws f32 slabs + cnt zeroed tile counters)
+void decode_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
+                 const std::optional<at::Tensor>& ws, const std::optional<at::Tensor>& cnt,
+                 int64_t bm, int64_t bn, int64_t s) {
+  if (!x.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: decode_gemm needs GPU tensors");
+  need_cuda(w, "w");
+  if (x.dim() != 2 || w.dim() != 2 || y.dim() != 2 || x.stride(1) != 1 || y.stride(1) != 1 ||
+      !w.is_contiguous() || x.size(1) != w.size(1) || y.size(0) != x.size(0) ||
+      y.size(1) != w.size(0) || x.scalar_type() != w.scalar_type() ||
+      y.scalar_type() != w.scalar_type())
+    throw std::invalid_argument("lumen: decode_gemm shape/layout mismatch");
+  const long long tiles = (w.size(0) + bn - 1) / bn;
+  if (s > 1) {
+    if (!ws || !cnt || !ws->is_cuda() || !cnt->is_cuda() ||
+        ws->scalar_type() != at::kFloat || cnt->scalar_type() != at::kInt ||
+        ws->numel() < tiles * s * bm * bn || cnt->numel() < tiles)
+      throw std::invalid_argument("lumen: decode_gemm split-K workspace too small");
+  }
+  check(lumen_decode_gemm(dcode(w), x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                          s > 1 ? ws->data_ptr<float>() : nullptr,
+                          s > 1 ? cnt->data_ptr<int>() : nullptr, static_cast<int>(x.size(0)),
+                          static_cast<int>(w.size(0)), static_cast<int>(w.size(1)), x.stride(0),
+                          y.stride(0), static_cast<int>(bm), static_cast<int>(bn),
+                          static_cast<int>(s), cur_stream()),
+        "decode_gemm");
 }
 
 void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
@@ -839,6 +869,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora2", &lora2);
   m.def("transpose2d", &transpose2d);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("decode_gemm", &decode_gemm);
   m.def("lora3_w_tail_batch", &lora3_w_tail_batch);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
   m.def("set_rms_lds", [](int64_t f, int64_t b) {

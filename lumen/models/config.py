@@ -117,6 +117,11 @@ PRESETS = {
     "llama2-70b": dict(arch="llama", vocab_size=32000, hidden_size=8192, intermediate_size=28672,
                        num_hidden_layers=80, num_attention_heads=64, num_key_value_heads=8,
                        max_position_embeddings=4096, name="meta-llama/Llama-2-70b-hf"),
+    # Llama-2-7B layer shapes (H, F, heads, vocab) at reduced depth: multi-rank rehearsals with
+    # every rank on one shared GPU (8 full 7B ranks would not fit its HBM)
+    "llama2-7b-2l": dict(arch="llama", vocab_size=32000, hidden_size=4096, intermediate_size=11008,
+                         num_hidden_layers=2, num_attention_heads=32, num_key_value_heads=32,
+                         max_position_embeddings=4096, name="llama2-7b-2l"),
     # facebook/opt-125m
     "opt-125m": dict(arch="opt", vocab_size=50272, hidden_size=768, intermediate_size=3072,
                      ffn_dim=3072, num_hidden_layers=12, num_attention_heads=12,
@@ -138,6 +143,10 @@ PRESETS = {
     "tiny-llama-gqa": dict(arch="llama", vocab_size=512, hidden_size=256, intermediate_size=688,
                            num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
                            max_position_embeddings=512, name="tiny-llama-gqa"),
+    # 8 heads / 8 kv heads / FFN and vocab divisible by 8 x 8: tensor parallelism up to 8
+    "tiny-llama-tp8": dict(arch="llama", vocab_size=1024, hidden_size=512, intermediate_size=2048,
+                           num_hidden_layers=2, num_attention_heads=8, num_key_value_heads=8,
+                           max_position_embeddings=512, name="tiny-llama-tp8"),
     "tiny-opt": dict(arch="opt", vocab_size=512, hidden_size=64, intermediate_size=256,
                      ffn_dim=256, num_hidden_layers=2, num_attention_heads=4,
                      num_key_value_heads=4, max_position_embeddings=256, word_embed_proj_dim=64,

@@ -35,11 +35,75 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
                  if x.shape[0] <= 4 else w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0))
 
 
-# Decode batches 5..256: hipBLASLt with the tuned table.  Two hand-written decode-batch MFMA GEMMs
-# measured slower (scripts/probes/): decode_gemm.hip (32-row M tiles) lost 2x from M = 64, and
-# batch_gemm.hip (all M rows per workgroup, ~one workgroup per CU, W through LDS) reached only
-# 3.7-4.7 TB/s at M <= 64 and fell to 1.5 TB/s at M = 256 as every workgroup re-reads x
-# (profiles/r3_serve/batch_gemm_sweep.jsonl; serving 6.6k vs 7.6k tok/s with it).
+# Decode batches 5..256: the decode-batch MFMA GEMM (kernels/decode_gemm.hip) where the measured
+# plan table (configs/decode_gemm_plans.json, written by lumen/bench/decode_gemm_probe.py) has
+# a winning (BM, BN, split-K) for the shape, hipBLASLt with the tuned table otherwise.  (Two
+# earlier hand-written attempts lost, scripts/probes/: 32-row M tiles, and all-M-rows tiles over
+# all of K whose every workgroup pulled the whole x through its CU's load path.)
+DG_BMS = (64, 128, 192, 256)
+DG_BNS = {256: (64, 96, 128, 160), 192: (64, 96, 128), 128: (64, 96, 128, 192, 256),
+          64: (64, 128, 192, 256)}
+DGEMM = os.environ.get("LUMEN_DGEMM", "1") != "0"
+_dg_ws: dict = {}
+_dg_old: list = []
+_dg_plans: Optional[dict] = None
+
+
+def dg_bucket(M: int) -> int:
+    return next(b for b in DG_BMS if M <= b)
+
+
+def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w^T on the decode-batch MFMA kernel with block tile (bm, bn) and split-K s."""
+    y = out if out is not None else torch.empty(x.shape[0], w.shape[0], device=x.device,
+                                                dtype=x.dtype)
+    ws = cnt = None
+    if s > 1:
+        key = str(x.device)
+        got = _dg_ws.get(key)
+        need = -(-w.shape[0] // bn) * s * bm * bn
+        if got is None or got[0].numel() < need or got[1].numel() < -(-w.shape[0] // bn):
+            # generous size; a superseded pair stays alive (_dg_old): a captured decode graph
+            # keeps pointing at the buffers it was captured with
+            n = max(need, 1 << 24)
+            if got is not None:
+                _dg_old.append(got)
+            got = (torch.empty(n, dtype=torch.float32, device=x.device),
+                   torch.zeros(max(4096, -(-w.shape[0] // bn)), dtype=torch.int32,
+                               device=x.device))
+            _dg_ws[key] = got
+        ws, cnt = got
+    native().decode_gemm(x, w, y, ws, cnt, bm, bn, s)
+    return y
+
+
+def dg_plans() -> dict:
+    """{(N, K, BM): (BN, S)} from configs/decode_gemm_plans.json (measured wins only)."""
+    global _dg_plans
+    if _dg_plans is None:
+        import json
+
+        path = os.environ.get("LUMEN_DGEMM_PLANS", os.path.join(
+            os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+            "configs", "decode_gemm_plans.json"))
+        _dg_plans = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                for e in json.load(f).get("plans", []):
+                    _dg_plans[(e["N"], e["K"], e["BM"])] = (e["BN"], e["S"])
+    return _dg_plans
+
+
+def dg_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple]:
+    if not (DGEMM and use_native(x) and x.dim() == 2 and w.dim() == 2 and 4 < x.shape[0] <= 256
+            and x.dtype == w.dtype and x.dtype in (torch.bfloat16, torch.float16)
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()
+            and x.shape[1] == w.shape[1] and w.shape[1] % 64 == 0 and w.shape[0] % 4 == 0):
+        return None
+    bm = dg_bucket(x.shape[0])
+    p = dg_plans().get((w.shape[0], w.shape[1], bm))
+    return (bm,) + tuple(p) if p is not None else None
 
 
 # Training-shape GEMMs run 256 x 256 macro tiles, one per CU at a time, so a GEMM with 5.375 or
@@ -127,6 +191,9 @@ def linear_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
         native().skinny_gemm(x, w, y)
         return y
+    p = dg_plan(x, w)
+    if p is not None:
+        return decode_gemm(x, w, *p)
     return torch.matmul(x, w.t())
 
 

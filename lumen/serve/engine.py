@@ -129,6 +129,12 @@ class LLMEngine:
         model.eval()
         self.model_config = model.config
         tp_group = dist.group.WORLD if self.tp > 1 else None
+        if self.tp > 1:
+            # the host side of the step broadcast (lumen/serve/tp.py): created collectively here,
+            # where every rank constructs its engine
+            from ..parallel.dist import host_group
+
+            host_group()
         self.weights = ServeWeights(model, self.rank, self.tp)
         if cfg.kv_cache_dtype not in ("auto", "fp8"):
             raise ValueError(f"kv_cache_dtype must be 'auto' or 'fp8', got {cfg.kv_cache_dtype}")

@@ -1,13 +1,20 @@
 """Tensor-parallel serving plumbing: step broadcast from rank 0 and the worker loop.
 
-Rank 0 (scheduler + API) sends each step as ONE fixed-size int64 broadcast: a 12-int64 header
-followed by the payload (tokens | positions | slots | prefill cu / kv lens / block tables |
-decode block tables / context lens | sampled rows | LoRA slots) -- no pickled Python objects on
-the hot path.  A payload larger than the inline capacity (CAP, 16384 values: a
-256-sequence decode step with ~40 blocks per sequence fits) sends its remainder in a second
-broadcast.  Workers rebuild the StepInput and run the same model step; the row-parallel
-all-reduces inside the layers keep the ranks in lock-step.  With async scheduling (default)
-rank 0 broadcasts a step when it LAUNCHES it, decode tokens straight from the device.
+Each step travels in two parts (no pickled Python objects on the hot path):
+
+* a HOST header over the host (gloo) group -- kind, the shape integers every rank needs to pick
+  its graph bucket / kernel launch sizes, and the prefill chunks' ``cu_seqlens`` / ``kv_lens``
+  (launch parameters of the paged prefill kernel): a fixed-size CPU int64 message, host to host;
+* the DEVICE payload (tokens | positions | slots | prefill kv lens / block tables | decode
+  block tables / context lens | sampled rows | LoRA slots) as ONE int64 RCCL broadcast straight
+  into a device buffer, stream-ordered after the previous step.
+
+A worker never reads device memory on the host: it builds the StepInput as views of the
+payload and replays the decode graph (or runs the mixed step) as soon as the header arrives, so
+its host runs ahead of its GPU exactly like rank 0's with async scheduling.  (Until round 3 the
+header rode in the device message and the worker's ``msg[:10].tolist()`` synchronised its host
+with its GPU once per step.)  The row-parallel all-reduces inside the layers keep the ranks in
+lock-step on the devices.
 """
 from __future__ import annotations
 
@@ -16,27 +23,33 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..parallel.dist import host_group
 from .model_runner import StepInput
 
 KIND = {"mixed": 0, "decode": 1, "shutdown": 2}
 HDR = 12  # kind, T, P, maxb_p, N, maxb_d, max_context, R, lora, payload numel, -, -
-CAP = 16384  # payload values carried inline with the header
+HOST_CAP = 1024  # cu_seqlens + kv_lens values carried inline with the host header
+
+
+def _host_bcast(t: torch.Tensor) -> None:
+    dist.broadcast(t, src=0, group=host_group())
 
 
 def pack_step(inp: Optional[StepInput], device) -> None:
+    hdr = torch.zeros(HDR + HOST_CAP, dtype=torch.long)
     if inp is None:
-        msg = torch.zeros(HDR + CAP, dtype=torch.long, device=device)
-        msg[0] = KIND["shutdown"]
-        dist.broadcast(msg, src=0)
+        hdr[0] = KIND["shutdown"]
+        _host_bcast(hdr)
         return
     T = inp.tokens.numel()
     P = len(inp.cu_seqlens) - 1
     parts = [inp.tokens.long(), inp.positions.long(), inp.slots.long()]
     maxb_p = N = maxb_d = 0
+    host = []
     if P:
         maxb_p = inp.prefill_tables.shape[1]
-        parts += [torch.tensor(inp.cu_seqlens, dtype=torch.long, device=device),
-                  inp.kv_lens_t.long(), inp.prefill_tables.long().reshape(-1)]
+        host = list(inp.cu_seqlens) + list(inp.kv_lens)
+        parts += [inp.kv_lens_t.long(), inp.prefill_tables.long().reshape(-1)]
     if inp.block_tables is not None:
         N, maxb_d = inp.block_tables.shape
         parts += [inp.block_tables.long().reshape(-1), inp.context_lens.long()]
@@ -44,38 +57,42 @@ def pack_step(inp: Optional[StepInput], device) -> None:
     parts.append(inp.sample_rows.long())
     if inp.lora_ids is not None:  # multi-LoRA: per-token adapter slots ride at the end
         parts.append(inp.lora_ids.long())
-    payload = torch.cat(parts)
+    payload = torch.cat([p.to(device) for p in parts])
     n = payload.numel()
-    hdr = torch.tensor([KIND[inp.kind], T, P, maxb_p, N, maxb_d, inp.max_context, R,
-                        int(inp.lora_ids is not None), n, 0, 0], dtype=torch.long)
-    msg = torch.zeros(HDR + CAP, dtype=torch.long, device=device)
-    msg[:HDR].copy_(hdr, non_blocking=False)
-    msg[HDR:HDR + min(n, CAP)] = payload[:CAP]
-    dist.broadcast(msg, src=0)
-    if n > CAP:
-        dist.broadcast(payload[CAP:].contiguous(), src=0)
+    hdr[:10] = torch.tensor([KIND[inp.kind], T, P, maxb_p, N, maxb_d, inp.max_context, R,
+                             int(inp.lora_ids is not None), n])
+    k = min(len(host), HOST_CAP)
+    if k:
+        hdr[HDR:HDR + k] = torch.tensor(host[:k], dtype=torch.long)
+    _host_bcast(hdr)
+    if len(host) > HOST_CAP:
+        _host_bcast(torch.tensor(host[HOST_CAP:], dtype=torch.long))
+    dist.broadcast(payload, src=0)
 
 
 def recv_step(device) -> Optional[StepInput]:
-    msg = torch.empty(HDR + CAP, dtype=torch.long, device=device)
-    dist.broadcast(msg, src=0)
-    kind, T, P, maxb_p, N, maxb_d, maxc, R, has_lora, n = msg[:10].tolist()
+    hdr = torch.empty(HDR + HOST_CAP, dtype=torch.long)
+    _host_bcast(hdr)
+    kind, T, P, maxb_p, N, maxb_d, maxc, R, has_lora, n = hdr[:10].tolist()
     if kind == KIND["shutdown"]:
         return None
-    if n <= CAP:
-        payload = msg[HDR:HDR + n]
-    else:
-        rest = torch.empty(n - CAP, dtype=torch.long, device=device)
-        dist.broadcast(rest, src=0)
-        payload = torch.cat([msg[HDR:], rest])
+    host = []
+    if P:
+        nh = 2 * P + 1
+        host = hdr[HDR:HDR + min(nh, HOST_CAP)].tolist()
+        if nh > HOST_CAP:
+            rest = torch.empty(nh - HOST_CAP, dtype=torch.long)
+            _host_bcast(rest)
+            host += rest.tolist()
+    payload = torch.empty(n, dtype=torch.long, device=device)
+    dist.broadcast(payload, src=0)
     inp = StepInput("mixed" if kind == KIND["mixed"] else "decode", payload[:T],
                     payload[T:2 * T].int(), payload[2 * T:3 * T], [0])
     o = 3 * T
     if P:
-        inp.cu_seqlens = payload[o:o + P + 1].tolist()
-        o += P + 1
+        inp.cu_seqlens = host[:P + 1]
+        inp.kv_lens = host[P + 1:2 * P + 1]
         inp.kv_lens_t = payload[o:o + P].int()
-        inp.kv_lens = inp.kv_lens_t.tolist()
         o += P
         inp.prefill_tables = payload[o:o + P * maxb_p].view(P, maxb_p).int()
         o += P * maxb_p
@@ -93,10 +110,11 @@ def recv_step(device) -> Optional[StepInput]:
 
 
 def worker_loop(runner) -> None:
-    """Ranks 1..TP-1: execute broadcast steps until shutdown."""
+    """Ranks 1..TP-1: execute broadcast steps until shutdown.  The host blocks only on rank 0's
+    host header, never on this rank's GPU."""
     while True:
-        inp = recv_step(runner.device)   # host-syncs: the previous step has completed
-        runner.check_collectives()
+        inp = recv_step(runner.device)
+        runner.check_collectives()   # a pinned host word: no device sync
         if inp is None:
             return
         if inp.kind == "decode":

@@ -91,8 +91,8 @@ def serve_tp_worker(rank, world, port, outdir, loras=None, async_sched=True, cap
     import lumen.serve.tp as tp_mod
     from lumen.serve.tp import worker_loop
 
-    if cap is not None:  # small inline capacity: every step takes the two-broadcast path
-        tp_mod.CAP = cap
+    if cap is not None:  # small inline host capacity: prefill steps take the two-message path
+        tp_mod.HOST_CAP = cap
 
     init(device="cpu")
     model = _tp_test_model()
@@ -116,12 +116,12 @@ def serve_tp_worker(rank, world, port, outdir, loras=None, async_sched=True, cap
     shutdown()
 
 
-def _tp_test_model():
+def _tp_test_model(name="tiny-llama-gqa"):
     import torch
 
     from lumen.models import build_model
 
-    m = build_model("tiny-llama-gqa", dtype=torch.float32, device="cpu", init="random", seed=1)
+    m = build_model(name, dtype=torch.float32, device="cpu", init="random", seed=1)
     with torch.no_grad():
         for p in m.parameters():
             if p.dim() == 2:
@@ -242,14 +242,14 @@ def car_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def serve_tp_gpu_worker(rank, world, port, outdir, backend="gloo"):
-    """TP=2 serving with both ranks on the ONE GPU (``backend`` carries the step broadcast and
+def serve_tp_gpu_worker(rank, world, port, outdir, backend="gloo", model_name="tiny-llama-gqa"):
+    """TP=world serving with every rank on the ONE GPU (``backend`` carries the step payload and
     the vocab gather -- gloo, or RCCL under LUMEN_SHARED_GPU_REHEARSAL; the row-parallel sums
     take the custom IPC all-reduce, so decode buckets run as hipGraphs).  Rank 0 saves greedy
-    outputs + which paths were active."""
+    outputs + which paths were active.  world 1: the TP=1 reference run."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
-    if backend == "nccl":
+    if backend == "nccl" and world > 1:
         os.environ["LUMEN_SHARED_GPU_REHEARSAL"] = "1"
         os.environ.setdefault("LUMEN_DIST_TIMEOUT", "120")
     import torch
@@ -260,9 +260,9 @@ def serve_tp_gpu_worker(rank, world, port, outdir, backend="gloo"):
     from lumen.serve.tp import worker_loop
 
     init(backend=backend, device="cuda")
-    model = _tp_test_model().to("cuda")
+    model = _tp_test_model(model_name).to("cuda")
     model = model.to(torch.bfloat16)  # the paged-KV kernels are 16-bit
-    cfg = EngineConfig(model="tiny-llama-gqa", device="cuda:0", dtype="bf16", max_model_len=128,
+    cfg = EngineConfig(model=model_name, device="cuda:0", dtype="bf16", max_model_len=128,
                        block_size=16, use_graphs=True, num_blocks=64, tp_size=world,
                        max_num_seqs=8)
     eng = LLMEngine(cfg, model=model)
@@ -276,8 +276,10 @@ def serve_tp_gpu_worker(rank, world, port, outdir, backend="gloo"):
         eng.shutdown()
         info["captured"] = sorted(eng.runner._graphs)
         info["car_calls"] = eng.runner.car.calls if eng.runner.car is not None else 0
-        eng.runner.car.check()
-        info["backend"] = torch.distributed.get_backend()
+        if eng.runner.car is not None:
+            eng.runner.car.check()
+        info["backend"] = (torch.distributed.get_backend()
+                           if torch.distributed.is_initialized() else "none")
         torch.save({"out": [s.output_ids for s in seqs], "info": info},
                    os.path.join(outdir, "tp_gpu_out.pt"))
     else:

@@ -655,6 +655,56 @@ def test_skinny_gemm(M, N, K):
     assert rel(yv, xv.float() @ w.float().t()) < 1e-2
 
 
+@pytest.mark.parametrize("bm", [64, 128, 192, 256])
+def test_decode_gemm_variants(bm):
+    """Decode-batch MFMA GEMM (kernels/decode_gemm.hip) vs an f32 matmul: every compiled (BM, BN)
+    variant, split-K 1 / 2 / 3 (in-launch slab reduction, counters left zeroed for the next
+    launch), a ragged last column tile, M below the block height, strided x rows, fp16."""
+    from lumen.ops._native import native
+    from lumen.ops.gemm import DG_BNS, _dg_ws, decode_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(bm)
+    K = 640
+    for bn in DG_BNS[bm]:
+        for N in (3 * bn + 4 * 3, 2 * bn):        # ragged (N % BN != 0) and whole tiles
+            w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+            for M in sorted({bm, bm - 11, 5 if bm == 64 else bm // 2 + 3}):
+                xb = torch.randn(M, K + 64, generator=g).to(DEV, torch.bfloat16)
+                x = xb[:, :K]                      # row stride K + 64
+                ref = x.float() @ w.float().t()
+                for s in (1, 2, 3):
+                    y = decode_gemm(x, w, bm, bn, s)
+                    assert y.shape == (M, N)
+                    assert rel(y, ref) < 1e-2, (bm, bn, N, M, s, rel(y, ref))
+                    if s > 1:  # the tile counters are zero again after the launch
+                        assert int(_dg_ws[str(x.device)][1].abs().sum()) == 0
+    # fp16 operands
+    w = (torch.randn(256, K, generator=g) * 0.05).to(DEV, torch.float16)
+    x = torch.randn(bm - 3, K, generator=g).to(DEV, torch.float16)
+    y = decode_gemm(x, w, bm, DG_BNS[bm][0], 2)
+    assert rel(y, x.float() @ w.float().t()) < 1e-2
+    # argument checks fail loudly (M above the block height)
+    with pytest.raises(Exception):
+        native().decode_gemm(torch.randn(bm + 1, K, device=DEV).to(torch.bfloat16),
+                             w.to(torch.bfloat16), torch.empty(bm + 1, 256, device=DEV,
+                                                               dtype=torch.bfloat16),
+                             None, None, bm, DG_BNS[bm][0], 1)
+
+
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 4096), (22016, 4096), (4096, 11008),
+                                 (32000, 4096)])
+@pytest.mark.parametrize("M", [64, 100, 200, 256])
+def test_decode_gemm_planned_shapes(N, K, M):
+    """linear_nt on the serving shapes of Llama-2-7B: the planned decode GEMM (or hipBLASLt where
+    the plan table has no win) matches an f32 matmul."""
+    from lumen.ops.gemm import dg_plan, linear_nt
+
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    y = linear_nt(x, w)
+    assert rel(y, x.float() @ w.float().t()) < 1e-2, dg_plan(x, w)
+
+
 @pytest.mark.parametrize("N,F", [(4096, 11008), (1024, 2752)])
 def test_swiglu_down_projection(N, F):
     """Batch-1 MLP down projection of the serving path: SwiGLU kernel + weight-streaming GEMV ==

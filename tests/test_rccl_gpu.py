@@ -99,6 +99,64 @@ def test_async_offloaded_optimizer_world2_rccl(schedule, tmp_path):
     _close(asy["sd"], sync["sd"])
 
 
+@pytest.mark.parametrize("schedule", ["keep", "release", "hybrid"])
+def test_zero3_rccl_world8_matches_single_process(schedule, tmp_path):
+    """The headline rank count on RCCL: 8 ranks (sharing the box's GPU over RCCL's socket
+    transport) run ZeRO-3 with every gather schedule, each on its own weight-gather
+    communicator where it re-gathers, == the single-process run."""
+    from tests.test_zero_gloo import _layer_numel
+
+    ex = {"device": "cuda", "dtype": "bf16", "fuse": False}
+    ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama-deep", micro=8, accum=1, steps=2,
+               extra=dict(ex))
+    ex["schedule"] = schedule
+    if schedule != "keep":
+        ex["max_live"] = int(4 * _layer_numel() * 1.02)
+    r = _run(8, 3, str(tmp_path / "b"), model="tiny-llama-deep", micro=1, accum=1, steps=2,
+             extra=ex)
+    for x, y in zip(r["losses"], ref["losses"]):
+        assert abs(x - y) < 2e-2, (r["losses"], ref["losses"])
+    _close(r["sd"], ref["sd"])
+    z = r["zero3"]
+    assert z["schedule"] == schedule and z["world"] == 8 and z["gathers"] > 0
+    assert z["gather_group_separate"] == (schedule != "keep")
+    assert z["pool_overflows"] == 0
+
+
+def _tp_run(world, tmp_path, backend="nccl", model_name="tiny-llama-gqa"):
+    from tests._dist_worker import serve_tp_gpu_worker
+
+    d = tmp_path / f"{backend}{world}"
+    d.mkdir()
+    mp.start_processes(serve_tp_gpu_worker, args=(world, _port(), str(d), backend, model_name),
+                       nprocs=world, join=True, start_method="spawn")
+    return torch.load(d / "tp_gpu_out.pt", weights_only=True)
+
+
+def _agree(a, b, min_frac=0.9):
+    """Greedy token streams of two bf16 runs whose reductions run in different orders: the
+    same first tokens, and at most a late divergence (a near-tie flipped by rounding)."""
+    tot = same = 0
+    for x, y in zip(a, b):
+        assert x[:2] == y[:2], (a, b)
+        k = next((i for i, (p, q) in enumerate(zip(x, y)) if p != q), len(x))
+        same += k
+        tot += len(x)
+    assert same >= min_frac * tot, (a, b)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_tp_serving_rccl_matches_tp1(world, tmp_path):
+    """TP=2 and TP=8 serving on RCCL (custom IPC all-reduce for the row-parallel sums, decode
+    buckets as hipGraphs, the step's host header over gloo and its payload over RCCL) produce the
+    TP=1 greedy tokens."""
+    ref = _tp_run(1, tmp_path, "nccl", "tiny-llama-tp8")
+    got = _tp_run(world, tmp_path, "nccl", "tiny-llama-tp8")
+    assert got["info"]["backend"] == "nccl" and got["info"]["car"], got["info"]
+    assert got["info"]["captured"], got["info"]
+    _agree(got["out"], ref["out"])
+
+
 def test_tp2_serving_rccl_on_one_gpu(tmp_path):
     """TP=2 serving with the step broadcast and vocab gather on RCCL (custom IPC all-reduce for
     the row-parallel sums): same greedy tokens as the gloo-broadcast TP run."""

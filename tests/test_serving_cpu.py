@@ -128,12 +128,12 @@ def test_openai_api_surface(model):
     assert llama2_chat_prompt([{"role": "user", "content": "q"}]) == "[INST] q [/INST]"
 
 
-@pytest.mark.parametrize("async_sched,cap", [(True, None), (False, None), (True, 16)])
+@pytest.mark.parametrize("async_sched,cap", [(True, None), (False, None), (True, 4)])
 def test_tensor_parallel_serving_gloo(tmp_path, async_sched, cap):
     """TP=2 over gloo (head/FFN-sharded layers, row-parallel all-reduce, vocab-parallel LM head,
     step broadcast to the worker) reproduces single-process greedy decoding, with the async
-    scheduler (steps broadcast at launch, tokens gathered on the device) and without, and with a
-    payload larger than the inline capacity of the step message."""
+    scheduler (steps broadcast at launch, tokens gathered on the device) and without, and with
+    prefill launch parameters larger than the inline capacity of the host header."""
     import socket
 
     import torch.multiprocessing as mp
