@@ -79,7 +79,8 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--save_strategy", default=v["save"], choices=["steps", "epoch", "no"])
     ap.add_argument("--warmup_steps", type=int, default=0)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--gradient_checkpointing", default="auto", choices=["auto", "true", "false"],
+    ap.add_argument("--gradient_checkpointing", default="auto",
+                    choices=["auto", "true", "false", "selective", "full"],
                     help="per-layer recompute (the reference always enables it).  auto: on only "
                          "when the estimated activations do not fit in free HBM (logged)")
     ap.add_argument("--no_gradient_checkpointing", action="store_true",

@@ -21,7 +21,7 @@ import torch.utils.checkpoint as cp
 
 from ..ops.embedding import embedding
 from ..ops.lora import arena_reset
-from ..ops.activation import swiglu
+from ..ops.activation import recompute_mlp, swiglu
 from ..ops.attention import causal_attention, flash_attention_qkv, prepare_varlen
 from ..ops.loss import lm_head_cross_entropy
 from ..ops.rope import qkv_rope_split, rope_qkv_, rope_tables
@@ -98,9 +98,16 @@ class LlamaMLP(nn.Module):
         self.gate_up_proj = Linear(H, 2 * Fd, dtype=dtype, device=device, seg_sizes=[Fd, Fd],
                                    seg_names=["gate_proj", "up_proj"])
         self.down_proj = Linear(Fd, H, dtype=dtype, device=device, seg_names=["down_proj"])
+        self.recompute = False  # selective checkpointing: gate|up output recomputed in backward
 
     def forward(self, x2d):
-        return self.down_proj(swiglu(self.gate_up_proj(x2d)))
+        gu, dn = self.gate_up_proj, self.down_proj
+        if (self.recompute and self.training and torch.is_grad_enabled()
+                and not gu.has_active_lora
+                and not dn.has_active_lora and not gu.weight.requires_grad
+                and not dn.weight.requires_grad):
+            return recompute_mlp(x2d, gu, dn)
+        return dn(swiglu(gu(x2d)))
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -133,9 +140,36 @@ class LlamaForCausalLM(nn.Module):
                                      for _ in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(H, cfg.rms_norm_eps, dtype, device)
         self.lm_head = Linear(H, V, dtype=dtype, device=device, seg_names=["lm_head"])
-        self.gradient_checkpointing = False
+        self._ckpt = "none"
         self.unit_gate = None    # engine hook run before each unit (async optimizer offload)
         self.coordinator = None  # ZeRO-3 parameter coordinator (lumen.parallel.zero)
+
+    # --- activation checkpointing --------------------------------------------------------------
+    CKPT_POLICIES = ("none", "selective", "full")
+
+    @property
+    def gradient_checkpointing(self) -> str:
+        """Activation recompute policy: ``"none"``; ``"selective"`` -- every layer keeps its
+        activations except the [T, 2F] gate|up output, recomputed by one GEMM in the backward
+        (the layer's largest saved tensor: ~35% of its activation memory for ~one extra
+        projection GEMM per layer); ``"full"`` -- the reference's per-layer recompute (HF
+        ``gradient_checkpointing=True``: the layer input only, the whole forward re-run).
+        Assigning True picks ``LUMEN_CKPT_POLICY`` (default ``selective``), False ``none``."""
+        return self._ckpt
+
+    @gradient_checkpointing.setter
+    def gradient_checkpointing(self, v) -> None:
+        import os
+
+        if v is True or v == "true":
+            v = os.environ.get("LUMEN_CKPT_POLICY", "selective")
+        elif v is False or v is None or v == "false":
+            v = "none"
+        if v not in self.CKPT_POLICIES:
+            raise ValueError(f"gradient checkpointing policy must be one of {self.CKPT_POLICIES}")
+        self._ckpt = v
+        for layer in self.layers:
+            layer.mlp.recompute = v == "selective"
 
     # --- ZeRO-3 units, in execution order ------------------------------------------------------
     def zero_units(self) -> List[List[nn.Module]]:
@@ -183,7 +217,7 @@ class LlamaForCausalLM(nn.Module):
                            input_ids.reshape(-1))
         res = None
         for i, layer in enumerate(self.layers):
-            if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
+            if self._ckpt == "full" and self.training and torch.is_grad_enabled():
                 fn = lambda h_, r_, L=layer: cp.checkpoint(L, h_, r_, B, S, pos, cu, use_reentrant=False)  # noqa: E731
             else:
                 fn = lambda h_, r_, L=layer: L(h_, r_, B, S, pos, cu)  # noqa: E731

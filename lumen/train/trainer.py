@@ -99,7 +99,9 @@ class Trainer:
         gc = args.gradient_checkpointing
         gc = gc.lower() if isinstance(gc, str) else gc
         gc = {"true": True, "false": False}.get(gc, gc)
-        self.model.gradient_checkpointing = gc is True
+        # True -> the model's default recompute policy (Llama: selective, LUMEN_CKPT_POLICY);
+        # "selective" / "full" name one; "auto" is decided after the engine is up (below)
+        self.model.gradient_checkpointing = False if gc == "auto" else gc
         self.model.train()
         trainable, total = print_trainable_parameters(self.model, self.print)
         self.n_trainable, self.n_total = trainable, total
@@ -128,14 +130,16 @@ class Trainer:
         self.fusion_stats = {"fused": 0, "unfused": 0, "vetoed": 0}
 
     # ---------------------------------------------------------------------------------------
-    def _auto_checkpointing(self) -> bool:
+    def _auto_checkpointing(self):
         """Memory-aware activation checkpointing (``--gradient_checkpointing auto``).
 
         The reference always recomputes (training/train_baseline.py:181, zero3.py:230) because
-        a V100 has 32 GB; recompute costs ~35% of the step here.  Estimate the activations a
-        micro-step keeps for the backward -- ~16 H-wide 16-bit rows per token per layer
-        (measured: 14 GB for 8 x 512 Llama-2-7B tokens) -- and recompute only when twice that
-        does not fit in the HBM left after the model, its shards and optimizer state."""
+        a V100 has 32 GB; full recompute costs ~35% of the step here.  Estimate the activations
+        a micro-step keeps for the backward -- ~16 H-wide 16-bit rows per token per layer
+        (measured: 14 GB for 8 x 512 Llama-2-7B tokens) -- and pick the cheapest policy whose
+        activations fit twice in the HBM left after the model, its shards and optimizer state:
+        none, then selective (gate|up output recomputed: ~0.65x the activations, where the model
+        has that policy), then full per-layer recompute."""
         env, cfg, a = self.env, self.model_cfg, self.args
         if env.device.type != "cuda":
             return False
@@ -151,11 +155,17 @@ class Trainer:
         co = self.engine.coordinator
         if co is not None:
             free = max(0, free - co.pending_alloc_bytes())
-        on = 2 * est > free
-        self.print(f"[lumen] activation checkpointing {'ON' if on else 'off'} (auto): "
+        pols = getattr(type(self.model), "CKPT_POLICIES", None)
+        if 2 * est <= free:
+            pick = False
+        elif pols and "selective" in pols and 2 * 0.65 * est <= free:
+            pick = "selective"
+        else:
+            pick = "full" if pols and "full" in pols else True
+        self.print(f"[lumen] activation checkpointing {pick or 'off'} (auto): "
                    f"~{est / 1e9:.1f} GB of activations per micro-step vs {free / 1e9:.1f} GB "
-                   "free HBM (--gradient_checkpointing true|false to force)")
-        return on
+                   "free HBM (--gradient_checkpointing true|false|selective|full to force)")
+        return pick
 
     @property
     def token_budget(self) -> bool:

@@ -51,7 +51,7 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
                   save_steps=ex.get("save_steps", 100), resume_from_checkpoint=ex.get(
                       "resume", False), save_final=False,
                   output_dir=ex.get("ckdir") or os.path.join(outdir, "ck"),
-                  seed=7, gradient_checkpointing=bool((extra or {}).get("gc", False)),
+                  seed=7, gradient_checkpointing=(extra or {}).get("gc", False),
                   fuse_accumulation=ex.get("fuse", True), synthetic_min_len=ex.get("min_len"))
     try:
         t = Trainer(a, ds, env, printer=lambda *x, **k: None)

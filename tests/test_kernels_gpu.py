@@ -553,10 +553,11 @@ def test_transpose_2d(shape):
 
 
 @pytest.mark.parametrize("direct,arena,ckpt", [(False, False, False), (True, True, False),
-                                               (True, True, True)])
+                                               (True, True, "full"), (True, True, "selective")])
 def test_engine_lora_grad_paths_match(direct, arena, ckpt, monkeypatch):
     """Direct .grad accumulation + zero arena give the same training trajectory as the plain
-    path (adapter grads returned to autograd, torch.zeros scratch)."""
+    path (adapter grads returned to autograd, torch.zeros scratch); so do full per-layer
+    recompute and selective recompute (gate|up output recomputed in the backward)."""
     import lumen.ops.lora as lora_mod
     from lumen.lora import LoraConfig, adapter_state_dict, apply_lora
     from lumen.models import build_model
@@ -571,6 +572,7 @@ def test_engine_lora_grad_paths_match(direct, arena, ckpt, monkeypatch):
         m = build_model("small-llama", dtype=torch.bfloat16, device=torch.device("cuda"), seed=3)
         apply_lora(m, LoraConfig(r=16, lora_dropout=0.1))
         m.gradient_checkpointing = ckpt_
+        assert m.gradient_checkpointing == (ckpt_ or "none")
         m.train()
         env = init()
         ds = load_ds_config({"zero_optimization": {"stage": 1}}, 2, 2, 1, 1e-3)

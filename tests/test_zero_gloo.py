@@ -66,11 +66,13 @@ def test_zero3_release_mode_and_accumulation(tmp_path):
     _close(r["sd"], ref["sd"])
 
 
-@pytest.mark.parametrize("schedule,gc", [("keep", False), ("keep", True), ("release", True)])
+@pytest.mark.parametrize("schedule,gc", [("keep", False), ("keep", True), ("release", True),
+                                         ("release", "full"), ("keep", "selective")])
 def test_zero3_schedules_accumulation_checkpointing(schedule, gc, tmp_path):
     """Every ZeRO-3 gather schedule (keep: gathered once, resident; release: a ring of buffers,
     every unit re-gathered at each use) with gradient accumulation, with and without
-    activation checkpointing == single process."""
+    activation checkpointing (True = the default selective policy; full per-layer recompute)
+    == single process."""
     ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama", micro=2, accum=2, steps=2,
                extra={"fuse": False})
     r = _run(2, 3, str(tmp_path / "b"), model="tiny-llama", micro=1, accum=2, steps=2,
