@@ -37,7 +37,9 @@ def make_engine(a):
     cfg = EngineConfig(model=a.model, dtype="bf16", max_model_len=a.max_model_len,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_batched_tokens,
                        prefill_boost=a.prefill_boost, use_graphs=not a.no_graphs, init="random",
-                       async_scheduling=not a.sync_scheduling, kv_cache_dtype=a.kv_cache_dtype)
+                       async_scheduling=not a.sync_scheduling, kv_cache_dtype=a.kv_cache_dtype,
+                       tp_size=getattr(a, "tp", 1),
+                       num_blocks=getattr(a, "num_blocks", None))
     t0 = time.time()
     eng = LLMEngine(cfg)
     eng._bench_setup_s = time.time() - t0
@@ -200,7 +202,31 @@ def main():
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     ap.add_argument("--sync-scheduling", action="store_true",
                     help="engine mode: host waits for each step's tokens before the next step")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="engine mode, under torch.distributed.run: tensor-parallel degree; rank 0 "
+                         "runs the bench, the other ranks the worker loop")
+    ap.add_argument("--num-blocks", type=int, default=None, help="KV blocks (default: auto)")
     a = ap.parse_args()
+    if a.tp > 1:
+        from lumen.parallel.dist import init, shutdown
+
+        env = init()
+        if env.world_size != a.tp:
+            raise SystemExit(f"--tp {a.tp} but WORLD_SIZE={env.world_size}")
+        eng = make_engine(a)
+        if env.rank != 0:
+            from lumen.serve.tp import worker_loop
+
+            worker_loop(eng.runner)
+            shutdown()
+            return
+        res = bench_engine(a, eng)
+        eng.shutdown()
+        res.update(metric="serve tok/s + p50 TTFT", model=a.model, tp=a.tp, dtype="bf16",
+                   data="random token-id prompts; random-init weights")
+        print(json.dumps(res), flush=True)
+        shutdown()
+        return
     if a.mode == "both":
         eng = make_engine(a)
         res = bench_http(a, eng)

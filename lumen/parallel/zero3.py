@@ -131,6 +131,12 @@ class _Unit:
         # gathered once and kept (keep: every unit; hybrid: the units the live budget holds
         # beyond the ring); never released, W^T written once
         self.resident = False
+        # ring units: a second shard holding the unit's projections TRANSPOSED ([K, N] each):
+        # the backward gathers that instead of W, so its input-gradient GEMMs run in the TN form
+        # straight from the gathered buffer (no per-step transpose, no NN GEMMs)
+        self.shard_t: Optional[torch.Tensor] = None
+        self.padded_t = 0
+        self.layout = "w"                              # contents of buf: "w" | "wt"
 
 
 class ParamCoordinator:
@@ -184,6 +190,14 @@ class ParamCoordinator:
                         u.folds.append(fold_lin[id(p)])
             self.units.append(u)
         total = 0
+        # transposed backward shards: only where a ring schedule is already certain here (forced
+        # release / hybrid, or an explicit live budget below the model) -- an "auto" budget is
+        # sized from the HBM left after sharding, and building W^T shards first would shrink it
+        est_total = sum(_round_up(sum(_store_numel(p) for p in u.params), W * ALIGN)
+                        for u in self.units if u.params)
+        want_t = (os.environ.get("LUMEN_ZERO3_BWD_WT", "1") != "0" and not offload_param
+                  and env.device.type == "cuda" and schedule not in ("identity", "keep")
+                  and (schedule in ("release", "hybrid") or 0 <= max_live < est_total))
         for u in self.units:
             if not u.params:
                 continue
@@ -205,6 +219,14 @@ class ParamCoordinator:
                     shard = shard.pin_memory()
             u.shard = shard
             del flat
+            if want_t and 0 < u.idx < len(self.units) - 1 and _t_eligible(u):
+                ft = torch.cat([p.data.t().contiguous().reshape(-1) for p in u.params])
+                u.padded_t = _round_up(ft.numel(), W * ALIGN)
+                if ft.numel() < u.padded_t:
+                    ft = torch.cat([ft, ft.new_zeros(u.padded_t - ft.numel())])
+                st_ = u.padded_t // W
+                u.shard_t = ft[env.rank * st_:(env.rank + 1) * st_].clone() if W > 1 else ft
+                del ft
             if schedule == "identity":
                 self._bind_views(u, shard)       # the one-rank partition is the unit
             else:
@@ -251,6 +273,10 @@ class ParamCoordinator:
             for i in self.resident_plan(unit_sizes, self.max_live):
                 self.units[i].resident = True
         self.resident_numel = sum(u.padded for u in self.units if u.resident)
+        for u in self.units:
+            if u.resident or not self.ring:
+                u.shard_t, u.padded_t = None, 0
+        self._in_bwd = False
         if self.ring:
             ring_sizes = [u.padded for u in self.units if u.padded and not u.resident]
             n_units = len(ring_sizes)
@@ -275,6 +301,7 @@ class ParamCoordinator:
         self._in_step = False
         self.gathered_bytes = 0    # bytes materialised by gathers (all ranks' shards)
         self.gathers = 0
+        self.gathers_t = 0         # ... of them transposed backward gathers
         self.track_waits = False
         self._wait_events: List[tuple] = []
         self._wait_host_s = 0.0
@@ -348,6 +375,7 @@ class ParamCoordinator:
                     pool_size=self.pool_size, turn_keep=self.turn_keep,
                     resident_units=sum(1 for u in self.units if u.resident and u.params),
                     resident_numel=self.resident_numel,
+                    transposed_bwd_units=sum(1 for u in self.units if u.shard_t is not None),
                     pool_overflows=self.pool_overflows, separate_group=self.group is not None,
                     offload=self.offload)
 
@@ -423,14 +451,20 @@ class ParamCoordinator:
         buf = self._buffer(u)
         if self.poison:  # race detector: stale reads of this buffer now see NaN
             buf.fill_(float("nan"))
+        # the backward of a ring unit gathers its transposed shard (TN input-gradient GEMMs
+        # straight from the buffer) unless a recompute needs the forward layout
+        t = u.shard_t is not None and self._in_bwd and not self._bwd_needs_w()
+        u.layout = "wt" if t else "w"
+        shard, n = (u.shard_t, u.padded_t) if t else (u.shard, u.padded)
         if self.offload and buf.is_cuda:
             u.work = self._issue_offloaded(u, buf)
         elif self.local:
-            u.work = _LocalGather(buf, u.shard)
+            u.work = _LocalGather(buf, shard)
         else:
-            u.work = dist.all_gather_into_tensor(buf[:u.padded], u.shard, group=self.group,
+            u.work = dist.all_gather_into_tensor(buf[:n], shard, group=self.group,
                                                  async_op=True)
-        self.gathered_bytes += u.padded * buf.element_size()
+        self.gathered_bytes += n * buf.element_size()
+        self.gathers_t += int(t)
         self.gathers += 1
         u.state = "inflight"
         if u.tn:
@@ -481,6 +515,21 @@ class ParamCoordinator:
             ev = torch.cuda.Event()
             ev.record(side)
         u.wt_event = ev
+
+    def restrict_transposed_gathers(self, params: Sequence[nn.Parameter]) -> int:
+        """Keep the transposed backward shards only of units whose every weight belongs to a
+        linear that runs its input gradient in the TN form (``transpose_bwd``): any other would
+        need the forward layout in the backward.  Returns the units that keep them."""
+        ok = {id(p) for p in params}
+        n = 0
+        for u in self.units:
+            if u.shard_t is None:
+                continue
+            if all(id(p) in ok for p in u.params):
+                n += 1
+            else:
+                u.shard_t, u.padded_t = None, 0
+        return n
 
     def enable_transposes(self, params: Sequence[nn.Parameter]) -> int:
         """Keep W^T of these gathered weights next to the gathered buffer (resident units of
@@ -573,6 +622,16 @@ class ParamCoordinator:
             self._wait_work(u.work)
             u.work = None
             u.state = "ready"
+        if not u.bound and u.layout == "wt":
+            # backward-only binding: W^T views for the TN input-gradient GEMMs; the forward
+            # layout is absent (an accidental forward use fails on the empty weight)
+            o = 0
+            for p in u.params:
+                rows, cols = p._zero_shape
+                p.data = torch.empty(0, dtype=u.dtype, device=p.device)
+                p._lumen_wt = u.buf[o:o + rows * cols].view(cols, rows)
+                o += rows * cols
+            u.bound = True
         if not u.bound:
             self._bind_views(u, u.buf)
             for lin in u.folds:  # freshly gathered: the adapter tail is refilled from lora_B
@@ -636,9 +695,15 @@ class ParamCoordinator:
             j += step
 
     # ---- model hooks ------------------------------------------------------------------------
+    def _bwd_needs_w(self) -> bool:
+        """Activation recompute re-runs forward GEMMs inside the backward: W, not W^T."""
+        v = getattr(self.model, "gradient_checkpointing", False)
+        return v not in (False, None, "none")
+
     def begin_micro_step(self):
         self._bwd_seen.clear()
         self._in_step = True
+        self._in_bwd = False
         if self.identity:
             return
         for i in self._ahead(-1, 1):
@@ -684,6 +749,7 @@ class ParamCoordinator:
         self._bwd_seen.add(i)
         if self.identity:
             return
+        self._in_bwd = True
         if self.ring:
             self._release(i + 1)
         self._wait(i)
@@ -697,6 +763,7 @@ class ParamCoordinator:
         if not self._in_step:
             return
         self._in_step = False
+        self._in_bwd = False
         if self.identity or self.keep:
             return  # keep: the gathered frozen weights stay resident
         for i in range(self.last + 1):
@@ -705,7 +772,10 @@ class ParamCoordinator:
     def gather_all_full(self) -> None:
         """Materialise every unit (checkpoint save with gather_16bit_weights_on_model_save).
         The release ring grows for this (the save is outside the step loop)."""
+        self._in_bwd = False
         for i in range(self.last + 1):
+            if self.units[i].layout == "wt":
+                self._release(i)
             self._issue(i)
             self._wait(i)
 
@@ -725,6 +795,14 @@ class ParamCoordinator:
                 u.work.wait()
                 u.work = None
                 u.state = "ready"
+
+
+def _t_eligible(u: _Unit) -> bool:
+    """A unit whose backward can run on a transposed gather: every parameter a 16-bit 2-D
+    projection weight with 8-aligned dims (the TN input-gradient GEMM's operand)."""
+    return all(len(p._zero_shape) == 2 and p._zero_shape[0] % 8 == 0
+               and p._zero_shape[1] % 8 == 0 and p.dtype in (torch.bfloat16, torch.float16)
+               for p in u.params)
 
 
 def units_dtype_bytes(units: Sequence[_Unit]) -> int:

@@ -109,6 +109,14 @@ class ZeroEngine:
             from ..models.layers import configure_backward_layout
 
             configure_backward_layout(model)  # TN input-gradient GEMMs for persistent weights
+            if self.coordinator is not None:
+                # ring units' backward gathers their transposed shards: only for linears that
+                # take the TN input-gradient GEMM
+                from ..models.layers import Linear
+
+                self.coordinator.restrict_transposed_gathers(
+                    [m.weight for m in model.modules() if isinstance(m, Linear)
+                     and m.transpose_bwd])
             # ... and for resident (keep / hybrid) gathered ones: W^T written once, on a side
             # stream right after the unit's first gather, when HBM allows (ring units are
             # re-gathered every use and keep the on-the-fly q|k|v / down transposes,

@@ -21,3 +21,18 @@ print("w8", d["n_gpus"], d["value"], d["ms_per_step"], d["config"]["parallelism"
 for k in ("zero3", "zero3_release", "zero3_hybrid"):
     print(k, json.dumps(e.get(k)))
 EOF
+# TP serving: TP=1 vs TP=2 with both ranks on the one GPU (the host header over gloo, the payload
+# over RCCL, decode graphs with the custom all-reduce); reduced-depth Llama-2-7B, 64 x 256 / 64
+unset LUMEN_SHARED_GPU_REHEARSAL
+timeout -k 10 300 python -m lumen.bench.serve_bench --model llama2-7b-2l --num-requests 64 --prompt-len 256 \
+  --max-tokens 64 --max-model-len 512 --num-blocks 4096 > $O/serve_tp1.json 2> $O/serve_tp1.err || { tail -10 $O/serve_tp1.err; exit 1; }
+export LUMEN_SHARED_GPU_REHEARSAL=1
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29621 -m lumen.bench.serve_bench --tp 2 --model llama2-7b-2l --num-requests 64 --prompt-len 256 \
+  --max-tokens 64 --max-model-len 512 --num-blocks 4096 > $O/serve_tp2.json 2> $O/serve_tp2.err || { tail -20 $O/serve_tp2.err; exit 1; }
+python3 - <<EOF2
+import json
+for t in ("tp1", "tp2"):
+    d = json.loads([l for l in open("$O/serve_" + t + ".json") if l.startswith("{")][-1])
+    print(t, {k: d.get(k) for k in ("output_tok_s", "ttft_p50_ms", "itl_p50_ms", "itl_p99_ms", "graphs")})
+EOF2

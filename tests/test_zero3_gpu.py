@@ -110,6 +110,27 @@ def test_zero3_schedules_match_stage0_on_gpu(schedule, ckpt, monkeypatch):
         torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)
 
 
+@pytest.mark.parametrize("schedule", ["release", "hybrid"])
+def test_zero3_transposed_backward_gathers(schedule, monkeypatch):
+    """Ring units gather their TRANSPOSED shard for the backward (W^T [K, N] per projection),
+    so the input-gradient GEMMs run in the TN form straight from the gathered buffer: same
+    trajectory as stage 0 with persistent W^T copies (the same GEMM form)."""
+    ref, _, _ = _train(monkeypatch, 0, bwd_wt="all")
+    got, _, coord = _train(monkeypatch, 3, schedule, bwd_wt="all", max_live=_LIVE[schedule]())
+    assert coord.schedule == schedule
+    ring = [u for u in coord.units[1:-1] if not u.resident]
+    assert ring and all(u.shard_t is not None for u in ring)
+    assert all(u.shard_t is None for u in coord.units if u.resident)
+    # every ring decoder layer is gathered transposed once per backward (8 micro-steps)
+    assert coord.gathers_t == 8 * len(ring)
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)
+    # a recompute policy needs the forward layout in the backward: no transposed gathers
+    got2, _, coord2 = _train(monkeypatch, 3, schedule, bwd_wt="all", max_live=_LIVE[schedule](),
+                             ckpt="full")
+    assert coord2.gathers_t == 0
+
+
 def test_zero3_offpath_transposes_match_persistent_layout(monkeypatch):
     """keep: W^T of every gathered projection is written once, on a side stream right after its
     gather, so the backward runs the same TN GEMMs as with persistent weights."""
