@@ -110,7 +110,7 @@ def dg_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple]:
 # 2.69 waves of tiles on the 256-CU chip takes 6 or 3 waves (Llama-2-7B at T = 4096: gate|up
 # forward 16 x 86 tiles, down input-grad 16 x 43).  ``mm_nt`` splits the output columns at the
 # last whole wave and runs the remainder as its own (separately tuned) GEMM, both writing column
-# views of one buffer (ldc = full width, no copies).  lumen/bench/split_gemm_probe.py measures it.
+# views of one buffer (ldc = full width, no copies).  scripts/probes/split_gemm_probe.py measures it.
 GEMM_SPLIT = os.environ.get("LUMEN_GEMM_SPLIT", "1") != "0"
 SPLIT_TILE, SPLIT_CUS = 256, 256
 SPLIT_MAX_TAIL = float(os.environ.get("LUMEN_GEMM_SPLIT_MAX_TAIL", "0.5"))

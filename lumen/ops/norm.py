@@ -15,7 +15,7 @@ from ._native import native, use_native
 
 def _occupancy_cap(C) -> None:
     """(No-op.)  An occupancy cap through reserved dynamic LDS per workgroup measured no gain;
-    the knob stays reachable for lumen/bench/rmsnorm_probe.py via ``C.set_rms_lds``."""
+    the knob stays reachable for scripts/probes/rmsnorm_probe.py via ``C.set_rms_lds``."""
 
 
 def rms_norm_ref(x, w, eps, residual=None):

@@ -2,7 +2,7 @@
 duration (PYTORCH_TUNABLEOP_VERBOSE log), fastest first: the runner-ups are what
 ``scripts/gpu/insitu_gemm.sh`` then times inside the power-capped training step.
 
-    PYTORCH_TUNABLEOP_VERBOSE=3 python -m lumen.bench.gemm_candidates OUT.json"""
+    PYTORCH_TUNABLEOP_VERBOSE=3 PYTHONPATH=. python scripts/probes/gemm_candidates.py OUT.json"""
 from __future__ import annotations
 
 import json

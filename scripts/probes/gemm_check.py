@@ -1,7 +1,7 @@
 """Correctness + timing of one TN GEMM shape under a given TunableOp table (no tuning):
 max abs error vs an fp32 matmul, and us per call.
 
-    python -m lumen.bench.gemm_check TABLE M N K"""
+    PYTHONPATH=. python scripts/probes/gemm_check.py TABLE M N K"""
 from __future__ import annotations
 
 import sys

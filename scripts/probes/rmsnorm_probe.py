@@ -1,7 +1,7 @@
 """RMSNorm forward / backward at the training shape (4096 rows x 4096, bf16, fused residual)
 under different occupancy caps (``set_rms_lds``: dynamic LDS bytes per workgroup).  Prints us per
 call and effective TB/s (fwd: x + residual in, y + sum out; bwd: dy + s + residual grad in, dx
-out).    python -m lumen.bench.rmsnorm_probe"""
+out).    PYTHONPATH=. python scripts/probes/rmsnorm_probe.py"""
 from __future__ import annotations
 
 import json

@@ -11,7 +11,7 @@ two parts into column views of one buffer (ldc = full width, no copy) lets the t
 own, separately tuned GEMM.  This probe times one-piece vs split back to back (power-capped, as
 in a step) and prints the kernels a split call launches (no copy kernels expected).
 
-    python -m lumen.bench.split_gemm_probe --tune OUT.csv [--dtype fp16]
+    PYTHONPATH=. python scripts/probes/split_gemm_probe.py --tune OUT.csv [--dtype fp16]
 """
 from __future__ import annotations
 
