@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--plans", default=None, help="write winning plans here (JSON)")
     ap.add_argument("--win", type=float, default=0.97, help="plan kept if dgemm < win x library")
     a = ap.parse_args()
-    from lumen.ops.gemm import DG_BNS, decode_gemm, dg_bucket
+    from lumen.ops.gemm import DG_BNS, DG_BNS8, decode_gemm, dg_bucket
     from lumen.utils.gemm_tuning import load_tuned_gemms
 
     load_tuned_gemms()
@@ -56,25 +56,27 @@ def main():
             lib = _time(lambda i: torch.matmul(x, Ws[i].t()), n_w)
             bm = dg_bucket(m)
             best = None
-            for bn in DG_BNS[bm]:
+            cands = [(b, 4) for b in DG_BNS[bm]] + [(b, 8) for b in DG_BNS8.get(bm, ())]
+            for bn, nw in cands:
                 for s in (1, 2, 3, 4, 6, 8):
-                    if s > K // 64:
+                    if s > K // 64 or -(-N // bn) * s > 4 * 256:
                         continue
                     try:
-                        us = _time(lambda i: decode_gemm(x, Ws[i], bm, bn, s), n_w)
+                        us = _time(lambda i: decode_gemm(x, Ws[i], bm, bn, s, nw), n_w)
                     except Exception as e:  # noqa: BLE001
-                        print(json.dumps({"shape": name, "M": m, "BN": bn, "S": s,
+                        print(json.dumps({"shape": name, "M": m, "BN": bn, "S": s, "NW": nw,
                                           "error": repr(e)[:200]}), flush=True)
                         continue
-                    rows.append({"shape": name, "M": m, "BM": bm, "BN": bn, "S": s,
+                    rows.append({"shape": name, "M": m, "BM": bm, "BN": bn, "S": s, "NW": nw,
                                  "us": round(us, 2)})
                     if best is None or us < best[0]:
-                        best = (us, bn, s)
+                        best = (us, bn, s, nw)
             ref = x.float() @ Ws[0].float().t()
-            err = ((decode_gemm(x, Ws[0], bm, best[1], best[2]).float() - ref).norm()
+            err = ((decode_gemm(x, Ws[0], bm, best[1], best[2], best[3]).float() - ref).norm()
                    / ref.norm()).item()
             rec = {"shape": name, "M": m, "N": N, "K": K, "lib_us": round(lib, 2),
                    "dgemm_us": round(best[0], 2), "BM": bm, "BN": best[1], "S": best[2],
+                   "NW": best[3],
                    "speedup": round(lib / best[0], 3), "rel_err": round(err, 5),
                    "lib_TBps": round(N * K * 2 / lib / 1e6, 2),
                    "dgemm_TBps": round(N * K * 2 / best[0] / 1e6, 2)}
@@ -85,7 +87,7 @@ def main():
             t[1] += min(lib, best[0]) * layers
             if best[0] < a.win * lib:
                 plans.append({"N": N, "K": K, "BM": bm, "BN": best[1], "S": best[2],
-                              "M_measured": m, "us": round(best[0], 2), "lib_us": round(lib, 2)})
+                              "NW": best[3], "M_measured": m, "us": round(best[0], 2), "lib_us": round(lib, 2)})
         del Ws
         torch.cuda.empty_cache()
     for m, (l, d) in sorted(tot.items()):

@@ -65,7 +65,7 @@ hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, con
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
 hipError_t lumen_decode_gemm(int, const void*, const void*, void*, float*, int*, int, int, int,
-                             long long, long long, int, int, int, hipStream_t);
+                             long long, long long, int, int, int, int, hipStream_t);
 void lumen_set_gemv_form(int);
 void lumen_set_rms_lds(int, int);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
@@ -216,7 +216,7 @@ void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
 // split-K s (s > 1: ws f32 slabs + cnt zeroed tile counters)
 void decode_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
                  const std::optional<at::Tensor>& ws, const std::optional<at::Tensor>& cnt,
-                 int64_t bm, int64_t bn, int64_t s) {
+                 int64_t bm, int64_t bn, int64_t s, int64_t nw) {
   if (!x.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: decode_gemm needs GPU tensors");
   need_cuda(w, "w");
   if (x.dim() != 2 || w.dim() != 2 || y.dim() != 2 || x.stride(1) != 1 || y.stride(1) != 1 ||
@@ -236,7 +236,7 @@ void decode_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
                           s > 1 ? cnt->data_ptr<int>() : nullptr, static_cast<int>(x.size(0)),
                           static_cast<int>(w.size(0)), static_cast<int>(w.size(1)), x.stride(0),
                           y.stride(0), static_cast<int>(bm), static_cast<int>(bn),
-                          static_cast<int>(s), cur_stream()),
+                          static_cast<int>(nw), static_cast<int>(s), cur_stream()),
         "decode_gemm");
 }
 

@@ -47,7 +47,6 @@ template <> struct Mfma<fp16> {
   }
 };
 
-constexpr int NT = 256;     // 4 waves
 constexpr int BK = 64;      // k elements per stage = one 128-byte image row per matrix row
 constexpr int ROWB = 128;
 constexpr int NSTAGE = 3;
@@ -81,18 +80,18 @@ __device__ __forceinline__ void dma16(const void* base, unsigned off, const char
 }
 
 // One stage: image rows [0, BN) = W rows n0 .. n0+BN-1, rows [BN, BN+BM) = x rows 0 .. BM-1, k
-// range [k0, k0 + 64).  Piece p (8 rows) is issued by wave p % 4; rows past N / M re-read the
+// range [k0, k0 + 64).  Piece p (8 rows) is issued by wave p % NW; rows past N / M re-read the
 // last valid row (finite data; those outputs are never stored).
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, int NW>
 __device__ __forceinline__ void stage(char* img, const T* Wt, int K, int nvalid, const T* x,
                                       long long ldx, int M, int k0, int wid, int lane) {
   constexpr int PIECES = (BN + BM) / 8;
-  static_assert(PIECES % 4 == 0, "(BN + BM) must be a multiple of 32");
+  static_assert(PIECES % NW == 0, "(BN + BM) / 8 must be a multiple of the wave count");
   const int rr = lane >> 3;           // row within the piece
   const int c = lane & 7;             // LDS chunk (lane-linear)
 #pragma unroll
-  for (int q = 0; q < PIECES / 4; ++q) {
-    const int p = 4 * q + wid;
+  for (int q = 0; q < PIECES / NW; ++q) {
+    const int p = NW * q + wid;
     const int r = 8 * p + rr;         // image row
     const int ch = c ^ swz(r);        // source chunk that belongs at LDS chunk c
     if (8 * p < BN) {                 // piece-uniform: BN % 8 == 0
@@ -131,17 +130,20 @@ __device__ __forceinline__ void compute(const char* img, int nrow0, int mrow0,
   }
 }
 
-// WM x WN waves; each wave: BN / WN output columns (NI blocks of 16) x BM / WM rows (MJ blocks)
+// WM x WN waves (4 or 8); each wave: BN / WN output columns (NI blocks of 16) x BM / WM rows
+// (MJ blocks).  8 waves: half the accumulators per wave, two waves per SIMD to hide the LDS /
+// DMA latency.
 template <typename T, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(NT, 1)
+__global__ void __launch_bounds__(64 * WM * WN, 1)
 dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y,
              float* __restrict__ ws, int* __restrict__ cnt, int M, int N, int K, long long ldx,
              long long ldy, int tiles_n, int S, int kt_total) {
-  static_assert(WM * WN == 4, "4 waves");
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NI = BN / WN / 16, MJ = BM / WM / 16;
   static_assert(NI * WN * 16 == BN && MJ * WM * 16 == BM, "wave tiling");
   constexpr int STAGE_B = (BN + BM) * ROWB;
-  constexpr int G = (BN + BM) / 32;   // DMA instructions per wave per stage
+  constexpr int G = (BN + BM) / (8 * NW);  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE_B + 16];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -168,16 +170,17 @@ dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y
 #pragma unroll
     for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage<T, BM, BN>(lds, Wt, K, nvalid, x, ldx, M, kb * BK, wid, lane);
-  if (nk > 1) stage<T, BM, BN>(lds + STAGE_B, Wt, K, nvalid, x, ldx, M, (kb + 1) * BK, wid, lane);
+  stage<T, BM, BN, NW>(lds, Wt, K, nvalid, x, ldx, M, kb * BK, wid, lane);
+  if (nk > 1)
+    stage<T, BM, BN, NW>(lds + STAGE_B, Wt, K, nvalid, x, ldx, M, (kb + 1) * BK, wid, lane);
   int buf = 0;
   for (int t = 0; t < nk; ++t) {
     if (t + 1 < nk) wait_vm<G>(); else wait_vm<0>();
     lds_barrier();  // stage t landed for every wave; every wave is done with stage t - 1
     if (t + 2 < nk) {
       const int nbuf = buf >= 1 ? buf - 1 : 2;  // (t + 2) % 3 == (t - 1) % 3
-      stage<T, BM, BN>(lds + nbuf * STAGE_B, Wt, K, nvalid, x, ldx, M, (kb + t + 2) * BK, wid,
-                       lane);
+      stage<T, BM, BN, NW>(lds + nbuf * STAGE_B, Wt, K, nvalid, x, ldx, M, (kb + t + 2) * BK, wid,
+                           lane);
     }
     compute<T, NI, MJ>(lds + buf * STAGE_B, nrow0, mrow0, acc, lane);
     buf = buf == 2 ? 0 : buf + 1;
@@ -238,21 +241,23 @@ dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y
   }
 }
 
-// compiled (BM, BN) variants; WM x WN: BM 256 -> 4 x 1, 128 -> 2 x 2, 64 -> 1 x 4
+// compiled (BM, BN, waves) variants.  4 waves, WM x WN: BM 256 -> 4 x 1, 128 -> 2 x 2,
+// 64 -> 1 x 4; 8 waves: BM 256 -> 4 x 2, 128 -> 2 x 4
 #define LUMEN_DG_VARIANTS(X)                                                                   \
   X(256, 64, 4, 1) X(256, 96, 4, 1) X(256, 128, 4, 1) X(256, 160, 4, 1)                         \
   X(192, 64, 4, 1) X(192, 96, 4, 1) X(192, 128, 4, 1)                                           \
   X(128, 64, 2, 2) X(128, 96, 2, 2) X(128, 128, 2, 2) X(128, 192, 2, 2) X(128, 256, 2, 2)       \
-  X(64, 64, 1, 4) X(64, 128, 1, 4) X(64, 192, 1, 4) X(64, 256, 1, 4)
+  X(64, 64, 1, 4) X(64, 128, 1, 4) X(64, 192, 1, 4) X(64, 256, 1, 4)                            \
+  X(256, 64, 4, 2) X(256, 128, 4, 2) X(128, 128, 2, 4) X(128, 256, 2, 4)
 
 template <typename T>
 hipError_t launch(const void* x, const void* W, void* y, float* ws, int* cnt, int M, int N, int K,
-                  long long ldx, long long ldy, int BM, int BN, int S, hipStream_t st) {
+                  long long ldx, long long ldy, int BM, int BN, int NW, int S, hipStream_t st) {
   const int tiles_n = (N + BN - 1) / BN;
   const int kt = K / BK;
-  dim3 grid(tiles_n * S), block(NT);
+  dim3 grid(tiles_n * S), block(64 * NW);
 #define LUMEN_DG_CASE(bm, bn, wm, wn)                                                          \
-  if (BM == bm && BN == bn) {                                                                  \
+  if (BM == bm && BN == bn && NW == wm * wn) {                                                 \
     hipLaunchKernelGGL((dgemm_kernel<T, bm, bn, wm, wn>), grid, block, 0, st, (const T*)x,     \
                        (const T*)W, (T*)y, ws, cnt, M, N, K, ldx, ldy, tiles_n, S, kt);       \
     return hipGetLastError();                                                                  \
@@ -271,7 +276,8 @@ hipError_t launch(const void* x, const void* W, void* y, float* ws, int* cnt, in
 // slice of each tile re-zeroes its counter, so they stay zero between launches).
 extern "C" hipError_t lumen_decode_gemm(int dtype, const void* x, const void* W, void* y,
                                         float* ws, int* cnt, int M, int N, int K, long long ldx,
-                                        long long ldy, int BM, int BN, int S, hipStream_t st) {
+                                        long long ldy, int BM, int BN, int NW, int S,
+                                        hipStream_t st) {
   if (M < 1 || M > BM || N < 4 || N % 4 != 0 || K < 64 || K % 64 != 0 || ldx % 8 != 0 ||
       ldy % 4 != 0 || ldx < K || ldy < N || S < 1 || S > K / 64 ||
       ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W) |
@@ -282,8 +288,10 @@ extern "C" hipError_t lumen_decode_gemm(int dtype, const void* x, const void* W,
   if ((long long)BN * K * 2 >= (1LL << 32) || (long long)BM * ldx * 2 >= (1LL << 32))
     return hipErrorInvalidValue;
   if (dtype == lumen::kBF16)
-    return lumen::dg::launch<lumen::bf16>(x, W, y, ws, cnt, M, N, K, ldx, ldy, BM, BN, S, st);
+    return lumen::dg::launch<lumen::bf16>(x, W, y, ws, cnt, M, N, K, ldx, ldy, BM, BN, NW, S,
+                                          st);
   if (dtype == lumen::kF16)
-    return lumen::dg::launch<lumen::fp16>(x, W, y, ws, cnt, M, N, K, ldx, ldy, BM, BN, S, st);
+    return lumen::dg::launch<lumen::fp16>(x, W, y, ws, cnt, M, N, K, ldx, ldy, BM, BN, NW, S,
+                                          st);
   return hipErrorInvalidValue;
 }

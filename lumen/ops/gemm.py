@@ -43,6 +43,7 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 DG_BMS = (64, 128, 192, 256)
 DG_BNS = {256: (64, 96, 128, 160), 192: (64, 96, 128), 128: (64, 96, 128, 192, 256),
           64: (64, 128, 192, 256)}
+DG_BNS8 = {256: (64, 128), 128: (128, 256)}   # 8-wave variants
 DGEMM = os.environ.get("LUMEN_DGEMM", "1") != "0"
 _dg_ws: dict = {}
 _dg_old: list = []
@@ -53,9 +54,10 @@ def dg_bucket(M: int) -> int:
     return next(b for b in DG_BMS if M <= b)
 
 
-def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int,
+def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int, nw: int = 4,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x @ w^T on the decode-batch MFMA kernel with block tile (bm, bn) and split-K s."""
+    """y = x @ w^T on the decode-batch MFMA kernel with block tile (bm, bn), split-K s and nw
+    (4 or 8) waves per block."""
     y = out if out is not None else torch.empty(x.shape[0], w.shape[0], device=x.device,
                                                 dtype=x.dtype)
     ws = cnt = None
@@ -74,12 +76,12 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int,
                                device=x.device))
             _dg_ws[key] = got
         ws, cnt = got
-    native().decode_gemm(x, w, y, ws, cnt, bm, bn, s)
+    native().decode_gemm(x, w, y, ws, cnt, bm, bn, s, nw)
     return y
 
 
 def dg_plans() -> dict:
-    """{(N, K, BM): (BN, S)} from configs/decode_gemm_plans.json (measured wins only)."""
+    """{(N, K, BM): (BN, S, waves)} from configs/decode_gemm_plans.json (measured wins only)."""
     global _dg_plans
     if _dg_plans is None:
         import json
@@ -91,7 +93,7 @@ def dg_plans() -> dict:
         if os.path.exists(path):
             with open(path) as f:
                 for e in json.load(f).get("plans", []):
-                    _dg_plans[(e["N"], e["K"], e["BM"])] = (e["BN"], e["S"])
+                    _dg_plans[(e["N"], e["K"], e["BM"])] = (e["BN"], e["S"], e.get("NW", 4))
     return _dg_plans
 
 

@@ -663,11 +663,11 @@ def test_decode_gemm_variants(bm):
     variant, split-K 1 / 2 / 3 (in-launch slab reduction, counters left zeroed for the next
     launch), a ragged last column tile, M below the block height, strided x rows, fp16."""
     from lumen.ops._native import native
-    from lumen.ops.gemm import DG_BNS, _dg_ws, decode_gemm
+    from lumen.ops.gemm import DG_BNS, DG_BNS8, _dg_ws, decode_gemm
 
     g = torch.Generator(device="cpu").manual_seed(bm)
     K = 640
-    for bn in DG_BNS[bm]:
+    for bn, nw in [(b, 4) for b in DG_BNS[bm]] + [(b, 8) for b in DG_BNS8.get(bm, ())]:
         for N in (3 * bn + 4 * 3, 2 * bn):        # ragged (N % BN != 0) and whole tiles
             w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
             for M in sorted({bm, bm - 11, 5 if bm == 64 else bm // 2 + 3}):
@@ -675,9 +675,9 @@ def test_decode_gemm_variants(bm):
                 x = xb[:, :K]                      # row stride K + 64
                 ref = x.float() @ w.float().t()
                 for s in (1, 2, 3):
-                    y = decode_gemm(x, w, bm, bn, s)
+                    y = decode_gemm(x, w, bm, bn, s, nw)
                     assert y.shape == (M, N)
-                    assert rel(y, ref) < 1e-2, (bm, bn, N, M, s, rel(y, ref))
+                    assert rel(y, ref) < 1e-2, (bm, bn, nw, N, M, s, rel(y, ref))
                     if s > 1:  # the tile counters are zero again after the launch
                         assert int(_dg_ws[str(x.device)][1].abs().sum()) == 0
     # fp16 operands
@@ -690,7 +690,7 @@ def test_decode_gemm_variants(bm):
         native().decode_gemm(torch.randn(bm + 1, K, device=DEV).to(torch.bfloat16),
                              w.to(torch.bfloat16), torch.empty(bm + 1, 256, device=DEV,
                                                                dtype=torch.bfloat16),
-                             None, None, bm, DG_BNS[bm][0], 1)
+                             None, None, bm, DG_BNS[bm][0], 1, 4)
 
 
 @pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 4096), (22016, 4096), (4096, 11008),
