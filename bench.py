@@ -188,6 +188,15 @@ def run_partitioned(args, env, ds_base, batches, schedule: str, max_live: float,
     return out
 
 
+def _provenance():
+    try:
+        from lumen.ops._native import provenance
+
+        return provenance()
+    except Exception as e:  # noqa: BLE001
+        return {"error": repr(e)[:200]}
+
+
 def _claim_stdout():
     """The driver contract: stdout carries exactly one JSON line.  Keep a private handle on the
     real stdout for it and point fd 1 at stderr, so chatter from native libraries (gloo's
@@ -475,6 +484,7 @@ def main():
                 "zero3_exposed_wait_ms_per_step_max_rank": round(exposed_ms / args.steps, 2),
                 "baseline_tok_s": BASELINE_TOK_S,
                 "gemm_algos": gemm_table,
+                "native_build": _provenance(),
                 "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,
                 **{f"zero3_{k}": v for k, v in parts.items()},
                 "serve": serve,

@@ -53,6 +53,40 @@ def _torch_flags():
     return cflags, ldflags
 
 
+def sources() -> list:
+    """Every source the extension is built from (kernels, headers, host code, binding)."""
+    return sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip"))
+                  + glob.glob(os.path.join(HERE, "kernels", "*.h"))
+                  + [os.path.join(HERE, "cpu", "cpu_adam.cpp"), os.path.join(HERE, "binding.cpp")])
+
+
+def source_digest() -> dict:
+    """{relative path: sha256} of ``sources()`` and their combined digest."""
+    import hashlib
+
+    files = {}
+    for f in sources():
+        with open(f, "rb") as fh:
+            files[os.path.relpath(f, PKG)] = hashlib.sha256(fh.read()).hexdigest()
+    total = hashlib.sha256("".join(f"{k}:{v};" for k, v in sorted(files.items())).encode())
+    return {"sha256": total.hexdigest(), "files": files}
+
+
+def manifest_path(out: str = None) -> str:
+    out = out or ext_path()
+    return os.path.join(os.path.dirname(out), "_C.sources.json")
+
+
+def read_manifest(out: str = None):
+    import json
+
+    try:
+        with open(manifest_path(out)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
 def _newer(src_list, obj):
     if not os.path.exists(obj):
         return True
@@ -137,11 +171,25 @@ def _build_locked(jobs, force, asm, verbose, build_dir, out) -> str:
                 if verbose:
                     print(f"[lumen.build] {os.path.basename(cmd[-3] if cmd[-2] == '-o' else cmd[-1])}"
                           f" {dt:.1f}s", flush=True)
-    if jobs_list or not os.path.exists(out) or _newer(objs, out):
+    dig = source_digest()
+    man = read_manifest(out)
+    if (jobs_list or not os.path.exists(out) or _newer(objs, out) or man is None
+            or man.get("sha256") != dig["sha256"]):
         # atomic rename inside _run: a concurrent loader sees the old or the new file
         _run([HIPCC, "-shared", "-fPIC", "-fopenmp", *objs, "-o", out, *ldflags])
         if verbose:
             print(f"[lumen.build] linked {out}", flush=True)
+        # provenance: which sources this shared object was built from (checked at load time,
+        # lumen.ops._native: a stale extension on a GPU box fails loudly)
+        import json
+        import platform
+
+        tmp = manifest_path(out) + f".part{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(dict(dig, arch=ARCH, host=platform.node(),
+                           built_at=time.strftime("%Y-%m-%dT%H:%M:%S"),
+                           so_bytes=os.path.getsize(out)), f, indent=1)
+        os.replace(tmp, manifest_path(out))
     return out
 
 

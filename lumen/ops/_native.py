@@ -21,10 +21,43 @@ def _load():
     if _C is not None or _err is not None:
         return _C
     try:
+        stale = provenance_error()
+        if stale and os.environ.get("LUMEN_ALLOW_STALE_NATIVE", "0") != "1":
+            raise RuntimeError(stale)
         _C = importlib.import_module("lumen._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e
     return _C
+
+
+def provenance() -> dict:
+    """The build manifest of the loaded extension (source digest, arch, build host / time) and
+    whether the sources in the tree still match it."""
+    from ..csrc.build import read_manifest, source_digest
+
+    man = read_manifest() or {}
+    cur = source_digest()["sha256"]
+    return {"sources_sha256": man.get("sha256"), "tree_sha256": cur,
+            "matches_tree": man.get("sha256") == cur, "arch": man.get("arch"),
+            "built_at": man.get("built_at"), "build_host": man.get("host")}
+
+
+def provenance_error():
+    """A message when the in-tree extension was built from other sources than the tree holds
+    (a stale .so would silently run old kernels), else None."""
+    from ..csrc.build import ext_path, read_manifest, source_digest
+
+    if not os.path.exists(ext_path()):
+        return None  # the import error says it is missing
+    man = read_manifest()
+    if man is None:
+        return ("lumen native extension has no build manifest (lumen/_C.sources.json): rebuild "
+                "with `python -m lumen.csrc.build`")
+    if man.get("sha256") != source_digest()["sha256"]:
+        return ("lumen native extension is stale: built from sources "
+                f"{str(man.get('sha256'))[:12]}, the tree holds {source_digest()['sha256'][:12]}; "
+                "rebuild with `python -m lumen.csrc.build`")
+    return None
 
 
 def native():
