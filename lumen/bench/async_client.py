@@ -54,6 +54,8 @@ def summarize(results: List[ReqResult], wall: float) -> dict:
         "ttft_p99_ms": round(1000 * _pct(ttft, 0.99), 2),
         "itl_p50_ms": round(1000 * _pct(itl, 0.5), 3),
         "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
+        "itl_max_ms": round(1000 * max(itl), 2) if itl else 0.0,
+        "itl_mean_ms": round(1000 * sum(itl) / len(itl), 3) if itl else 0.0,
         "latency_p50_s": round(_pct(lat, 0.5), 3),
     }
 

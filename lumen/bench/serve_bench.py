@@ -39,6 +39,7 @@ def make_engine(a):
                        prefill_boost=a.prefill_boost, use_graphs=not a.no_graphs, init="random",
                        async_scheduling=not a.sync_scheduling, kv_cache_dtype=a.kv_cache_dtype,
                        tp_size=getattr(a, "tp", 1),
+                       scheduling_policy=getattr(a, "scheduling_policy", "chunked"),
                        num_blocks=getattr(a, "num_blocks", None))
     t0 = time.time()
     eng = LLMEngine(cfg)
@@ -104,6 +105,9 @@ def bench_engine(a, eng=None) -> dict:
             "ttft_p99_ms": round(1000 * _pct(ttft, 0.99), 2),
             "itl_p50_ms": round(1000 * _pct(itl, 0.5), 3),
             "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
+            "itl_max_ms": round(1000 * max(itl), 2) if itl else 0.0,
+            "itl_mean_ms": round(1000 * sum(itl) / len(itl), 3) if itl else 0.0,
+            "scheduling_policy": getattr(a, "scheduling_policy", "chunked"),
             "kv_blocks": eng.blocks.num_blocks, "preemptions": eng.scheduler.num_preemptions,
             "max_batched_tokens": a.max_batched_tokens, "steps": eng.stats["steps"],
             "async_scheduling": eng.async_sched, "kv_cache_dtype": a.kv_cache_dtype,
@@ -206,6 +210,7 @@ def main():
                     help="engine mode, under torch.distributed.run: tensor-parallel degree; rank 0 "
                          "runs the bench, the other ranks the worker loop")
     ap.add_argument("--num-blocks", type=int, default=None, help="KV blocks (default: auto)")
+    ap.add_argument("--scheduling-policy", default="chunked", choices=["chunked", "prefill_first"])
     a = ap.parse_args()
     if a.tp > 1:
         from lumen.parallel.dist import init, shutdown

@@ -31,6 +31,10 @@ def build_parser():
                     help="tokens per engine step (running decodes + prefill chunks)")
     ap.add_argument("--prefill-boost", type=int, default=1,
                     help="x token budget while at most max-num-seqs/4 sequences decode (1: off)")
+    ap.add_argument("--scheduling-policy", default="chunked", choices=["chunked", "prefill_first"],
+                    help="chunked: mixed prefill-chunk + decode steps (bounded inter-token "
+                         "latency); prefill_first: vLLM 0.6.0's default, prefill-only steps "
+                         "while prompts wait")
     ap.add_argument("--block-size", type=int, default=16)
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
     ap.add_argument("--no-graphs", action="store_true")
@@ -78,6 +82,7 @@ def main(argv=None):
                        gpu_memory_utilization=a.gpu_memory_utilization,
                        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_num_batched_tokens,
                        prefill_boost=a.prefill_boost, tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs,
+                       scheduling_policy=a.scheduling_policy,
                        kv_cache_dtype=a.kv_cache_dtype,
                        lora_modules=dict(m.split("=", 1) for m in a.lora_modules)
                        if a.lora_modules else None, max_loras=a.max_loras)

@@ -45,6 +45,11 @@ class EngineConfig:
     # Off by default: at x2 on the 256-request burst it moved TTFT p50 by -8% / +8% over two
     # runs and ITL p99 by +3-4 ms (profiles/r3d/serve_boost)
     prefill_boost: int = 1
+    # "chunked": every step decodes all running streams and fills the rest of the budget with
+    # prefill chunks (mixed steps: bounded inter-token latency); "prefill_first": vLLM 0.6.0's
+    # default (the version the reference pins) -- prefill-only steps while prompts wait, decode
+    # steps otherwise (scheduler.py)
+    scheduling_policy: str = "chunked"
     tp_size: int = 1
     seed: int = 0
     use_graphs: bool = True
@@ -174,7 +179,8 @@ class LLMEngine:
         self._inflight: Optional[dict] = None
         self.scheduler = Scheduler(SchedulerConfig(
             cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
-            prefill_boost=max(1, int(cfg.prefill_boost))), self.blocks)
+            prefill_boost=max(1, int(cfg.prefill_boost)), policy=cfg.scheduling_policy),
+            self.blocks)
         if tokenizer is None:
             from ..data.tokenizer import load_tokenizer
 

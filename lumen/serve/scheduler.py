@@ -16,6 +16,13 @@ The step is one forward over [prefill chunk tokens | decode tokens] (GEMMs see e
 once); a sequence gets a sampled token only when the chunk that completes its prompt runs.
 A step without prefill work is a pure decode step (hipGraph-captured in the runner).
 
+``policy="prefill_first"`` is vLLM 0.6.0's default scheduling instead (the version the
+reference pins; chunked prefill is opt-in there): while prompts wait and can be admitted, a step
+is PREFILL-ONLY (whole prompts, FCFS, up to the token budget; only a prompt longer than the
+budget is chunked); otherwise it is a decode step of every running sequence.  Prefills finish
+sooner (higher throughput, lower TTFT under a burst) at the cost of a long pause in the running
+streams while a burst is prefilled (its inter-token-latency maximum).
+
 KV blocks for a whole prompt are reserved when the request is admitted, so a chunked prefill
 never runs out of blocks halfway; decodes grow their tables a block at a time, and when none is
 left the youngest running sequence is preempted (blocks freed, requeued at the front, its prompt
@@ -42,6 +49,7 @@ class SchedulerConfig:
     # waiting prompts get their first token sooner (a burst of arrivals).  1 disables it.
     prefill_boost: int = 1
     boost_max_decodes: int = 0   # 0: max_num_seqs // 4
+    policy: str = "chunked"      # "chunked" (mixed steps) | "prefill_first" (vLLM 0.6 default)
 
 
 @dataclass
@@ -94,9 +102,39 @@ class Scheduler:
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
 
+    def _admit(self, batch: Batch, budget: int, skip=()) -> int:
+        """Prefill work into ``batch``: partially cached prompts first, then waiting requests in
+        arrival order, while the token budget, ``max_num_seqs`` and the free blocks allow."""
+        for s in self.running:
+            if budget <= 0:
+                break
+            if not s.prefilled and s.seq_id not in skip:
+                c = min(s.length - s.num_cached, budget)
+                batch.prefills.append((s, c))
+                budget -= c
+        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
+            s = self.waiting[0]
+            if not self.blocks.can_allocate(s.length + 1):
+                break
+            self.waiting.popleft()
+            self.blocks.allocate(s.seq_id, s.length + 1)
+            s.num_cached = 0
+            s.prefilled = False
+            s.status = Status.RUNNING
+            self.running.append(s)
+            c = min(s.length, budget)
+            batch.prefills.append((s, c))
+            budget -= c
+        return budget
+
     def schedule(self) -> Optional[Batch]:
         budget = self.cfg.max_num_batched_tokens
         batch = Batch("mixed")
+        if self.cfg.policy == "prefill_first":
+            # vLLM 0.6: a prefill-only step whenever prompt work can be scheduled
+            self._admit(batch, budget)
+            if batch.prefills:
+                return batch
         # 1) one token for every sequence past its prompt (grow block tables; preempt the
         #    youngest running sequence when the cache is exhausted)
         preempted = set()
@@ -120,27 +158,10 @@ class Scheduler:
                 self.cfg.boost_max_decodes or self.cfg.max_num_seqs // 4):
             budget *= self.cfg.prefill_boost
         budget -= len(batch.decodes)
-        # 2) continue partially cached prompts, then admit waiting requests (FCFS)
-        for s in self.running:
-            if budget <= 0:
-                break
-            if not s.prefilled and s.seq_id not in preempted:
-                c = min(s.length - s.num_cached, budget)
-                batch.prefills.append((s, c))
-                budget -= c
-        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
-            s = self.waiting[0]
-            if not self.blocks.can_allocate(s.length + 1):
-                break
-            self.waiting.popleft()
-            self.blocks.allocate(s.seq_id, s.length + 1)
-            s.num_cached = 0
-            s.prefilled = False
-            s.status = Status.RUNNING
-            self.running.append(s)
-            c = min(s.length, budget)
-            batch.prefills.append((s, c))
-            budget -= c
+        # 2) continue partially cached prompts, then admit waiting requests (FCFS); the
+        #    prefill-first policy reaches here only for decode steps
+        if self.cfg.policy != "prefill_first":
+            self._admit(batch, budget, skip=preempted)
         if not batch.prefills and not batch.decodes:
             return None
         if not batch.prefills:

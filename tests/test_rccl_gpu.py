@@ -103,10 +103,12 @@ def test_async_offloaded_optimizer_world2_rccl(schedule, tmp_path):
 def test_zero3_rccl_world8_matches_single_process(schedule, tmp_path):
     """The headline rank count on RCCL: 8 ranks (sharing the box's GPU over RCCL's socket
     transport) run ZeRO-3 with every gather schedule, each on its own weight-gather
-    communicator where it re-gathers, == the single-process run."""
+    communicator where it re-gathers, == the single-process run.  (fp32: eight bf16 partial
+    gradients summed in a different order than one 8-row batch differ by rounding that Adam
+    amplifies on near-zero elements -- the world-2 bf16 tests cover the 16-bit kernels.)"""
     from tests.test_zero_gloo import _layer_numel
 
-    ex = {"device": "cuda", "dtype": "bf16", "fuse": False}
+    ex = {"device": "cuda", "dtype": "fp32", "fuse": False}
     ref = _run(1, 0, str(tmp_path / "a"), model="tiny-llama-deep", micro=8, accum=1, steps=2,
                extra=dict(ex))
     ex["schedule"] = schedule
@@ -115,8 +117,8 @@ def test_zero3_rccl_world8_matches_single_process(schedule, tmp_path):
     r = _run(8, 3, str(tmp_path / "b"), model="tiny-llama-deep", micro=1, accum=1, steps=2,
              extra=ex)
     for x, y in zip(r["losses"], ref["losses"]):
-        assert abs(x - y) < 2e-2, (r["losses"], ref["losses"])
-    _close(r["sd"], ref["sd"])
+        assert abs(x - y) < 1e-4, (r["losses"], ref["losses"])
+    _close(r["sd"], ref["sd"], tol=1e-4, frac=0.002)
     z = r["zero3"]
     assert z["schedule"] == schedule and z["world"] == 8 and z["gathers"] > 0
     assert z["gather_group_separate"] == (schedule != "keep")
@@ -149,12 +151,15 @@ def _agree(a, b, min_frac=0.9):
 def test_tp_serving_rccl_matches_tp1(world, tmp_path):
     """TP=2 and TP=8 serving on RCCL (custom IPC all-reduce for the row-parallel sums, decode
     buckets as hipGraphs, the step's host header over gloo and its payload over RCCL) produce the
-    TP=1 greedy tokens."""
+    TP=1 greedy tokens (a model with decisive logits, so bf16 partial-sum rounding cannot flip a
+    greedy choice), and exactly the tokens of the same TP run with gloo carrying the steps."""
     ref = _tp_run(1, tmp_path, "nccl", "tiny-llama-tp8")
     got = _tp_run(world, tmp_path, "nccl", "tiny-llama-tp8")
     assert got["info"]["backend"] == "nccl" and got["info"]["car"], got["info"]
     assert got["info"]["captured"], got["info"]
     _agree(got["out"], ref["out"])
+    alt = _tp_run(world, tmp_path, "gloo", "tiny-llama-tp8")
+    assert alt["out"] == got["out"]
 
 
 def test_tp2_serving_rccl_on_one_gpu(tmp_path):

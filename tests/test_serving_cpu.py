@@ -333,6 +333,44 @@ def test_chunked_prefill_and_mixed_steps_match_naive(model):
     assert eng.blocks.num_free == eng.blocks.num_blocks
 
 
+@pytest.mark.parametrize("async_sched", [False, True])
+def test_prefill_first_policy_matches_naive(model, async_sched):
+    """vLLM 0.6.0's default scheduling (scheduling_policy="prefill_first"): while prompts wait,
+    steps are prefill-only (no decode rows ride along; a prompt longer than the budget is still
+    chunked); then decode-only steps.  Greedy outputs == full-recompute decoding, with requests
+    arriving mid-flight too."""
+    eng = _engine(model, num_blocks=256, max_num_batched_tokens=40,
+                  scheduling_policy="prefill_first", async_scheduling=async_sched)
+    prompts = [list(range(3, 40)), [5, 9, 33, 7], list(range(50, 80)), [42, 43]]
+    late = [list(range(90, 140))]                        # 50 tokens > budget: chunked
+    params = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    seqs = [eng.add_request(p, SamplingParams(**vars(params))) for p in prompts]
+    kinds = []
+    orig = eng.scheduler.schedule
+
+    def spy():
+        b = orig()
+        if b is not None:
+            kinds.append((len(b.prefills), len(b.decodes)))
+        return b
+
+    eng.scheduler.schedule = spy
+    steps = 0
+    while any(not s.finished for s in seqs):
+        eng.step()
+        steps += 1
+        if steps == 3:
+            seqs += [eng.add_request(p, SamplingParams(**vars(params))) for p in late]
+    while eng.has_work:
+        eng.step()
+    for p, s in zip(prompts + late, seqs):
+        assert s.output_ids == naive_greedy(model, p, 8), p
+    assert all(not (p and d) for p, d in kinds)          # never mixed
+    assert kinds[0] == (2, 0) and kinds[1][0] > 0        # prompts first (37 + 4 > 40: two steps)
+    assert sum(1 for p, d in kinds if p) >= 4            # the late 50-token prompt chunked
+    assert eng.blocks.num_free == eng.blocks.num_blocks
+
+
 def test_penalties_change_greedy_choice(model):
     """frequency / presence / repetition penalties act on the logits before sampling: a strong
     frequency penalty forbids repeating a generated token under greedy decoding."""
