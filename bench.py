@@ -35,13 +35,18 @@ METRIC = "train tok/s Llama-2-7B ZeRO-3+LoRA at 1/2/4/8 GPUs; serve tok/s + p50 
 def run_serve_bench(args) -> dict:
     """Serving half of the metric, after the timed training region (training model freed).
 
-    One LLMEngine (Llama-2-7B TP=1: continuous batching, chunked prefill with a 2048-token step
-    budget, hipGraph decode, async scheduling, bf16 KV, greedy), two measurements of the same
-    256-request burst (512 in / 128 out, all arriving at t=0):
+    One LLMEngine (Llama-2-7B TP=1: continuous batching, hipGraph decode, async scheduling, bf16
+    KV, greedy) with the scheduling of the vLLM version the reference pins (vllm==0.6.0,
+    requirements.txt:18): chunked prefill off, prefill-only steps while prompts wait, then decode
+    steps, max_num_batched_tokens = max(max_model_len, 2048) = 4096 for Llama-2's 4096 context.
+    Measurements of the same 256-request burst (512 in / 128 out, all arriving at t=0):
       * ``http`` -> ``extra.serve``: the reference's declared path -- the OpenAI HTTP server (a
         spawned process, the production layout of scripts/serve.py) streaming
         ``/v1/completions`` to the async load client (a third process; the Locust request shape);
-      * ``engine`` -> ``extra.serve_engine``: the same engine driven in-process (no HTTP).
+      * ``engine`` -> ``extra.serve_engine``: the same engine driven in-process (no HTTP);
+      * ``extra.serve_chunked``: in-process again with lumen's mixed-step policy (chunked
+        prefill, 2048 tokens per step: inter-token latency bounded by one mixed step instead of
+        the whole prefill backlog -- the itl_max_ms the prefill-first records show).
     A failure is reported in the record, never fatal to the training number already measured."""
     import gc
     import types
@@ -54,15 +59,17 @@ def run_serve_bench(args) -> dict:
 
     a = types.SimpleNamespace(
         model=args.serve_model or args.model, max_model_len=1024, max_num_seqs=256,
-        max_batched_tokens=2048, prefill_boost=int(os.environ.get("LUMEN_PREFILL_BOOST", "1")),
+        max_batched_tokens=4096, prefill_boost=int(os.environ.get("LUMEN_PREFILL_BOOST", "1")),
         no_graphs=False, sync_scheduling=False, kv_cache_dtype="auto",
+        scheduling_policy=os.environ.get("LUMEN_SERVE_POLICY", "prefill_first"),
         num_requests=256, concurrency=256, prompt_len=512, max_tokens=128, temperature=0.0,
         request_rate=None)
-    keep = ("output_tok_s", "ttft_p50_ms", "ttft_p99_ms", "itl_p50_ms", "itl_p99_ms", "wall_s",
-            "total_tok_s", "output_tokens", "preemptions", "steps", "setup_s", "ok", "errors",
-            "http_section_s")
+    keep = ("output_tok_s", "ttft_p50_ms", "ttft_p99_ms", "itl_p50_ms", "itl_p99_ms",
+            "itl_max_ms", "itl_mean_ms", "wall_s", "total_tok_s", "output_tokens", "preemptions",
+            "steps", "setup_s", "ok", "errors", "http_section_s")
     conf = {"model": a.model, "tp": 1, "requests": a.num_requests, "prompt_len": a.prompt_len,
             "max_tokens": a.max_tokens, "max_num_batched_tokens": a.max_batched_tokens,
+            "scheduling_policy": a.scheduling_policy,
             "prefill_boost": a.prefill_boost, "kv_cache_dtype": "bf16",
             "sampling": "greedy, ignore_eos", "arrival": "all at t=0"}
     t0 = time.time()
@@ -70,7 +77,7 @@ def run_serve_bench(args) -> dict:
         eng = make_engine(a)
         r = bench_engine(a, eng)
     except Exception as e:  # noqa: BLE001 - keep the training result
-        return {"error": repr(e)[:500]}, None
+        return {"error": repr(e)[:500]}, None, None
     e_out = {k: r[k] for k in keep if k in r}
     e_out["bench_s"] = round(time.time() - t0, 1)
     e_out["config"] = dict(conf, async_scheduling=r.get("async_scheduling"),
@@ -79,15 +86,30 @@ def run_serve_bench(args) -> dict:
     try:
         h = bench_http(a, eng)
     except Exception as e:  # noqa: BLE001 - the engine-mode number stands
-        return {"error": "http: " + repr(e)[:500], "engine_fallback": e_out}, e_out
-    finally:
         eng.shutdown()
+        return {"error": "http: " + repr(e)[:500], "engine_fallback": e_out}, e_out, None
     h_out = {k: h[k] for k in keep if k in h}
     h_out["bench_s"] = round(time.time() - t1, 1)
     h_out["vs_engine"] = round(h["output_tok_s"] / max(r["output_tok_s"], 1e-9), 3)
     h_out["config"] = dict(conf, concurrency=a.concurrency,
                            mode="OpenAI HTTP API (/v1/completions, SSE) + async load client")
-    return h_out, e_out
+    c_out = None
+    if a.scheduling_policy != "chunked":
+        t2 = time.time()
+        try:  # same engine (graphs captured): only the scheduler's policy and budget change
+            eng.scheduler.cfg.policy = "chunked"
+            eng.scheduler.cfg.max_num_batched_tokens = 2048
+            ac = types.SimpleNamespace(**dict(vars(a), scheduling_policy="chunked",
+                                              max_batched_tokens=2048))
+            c = bench_engine(ac, eng)
+            c_out = {k: c[k] for k in keep if k in c}
+            c_out["bench_s"] = round(time.time() - t2, 1)
+            c_out["config"] = dict(conf, scheduling_policy="chunked", max_num_batched_tokens=2048,
+                                   mode="in-process engine")
+        except Exception as e:  # noqa: BLE001
+            c_out = {"error": repr(e)[:500]}
+    eng.shutdown()
+    return h_out, e_out, c_out
 
 
 def run_partitioned(args, env, ds_base, batches, schedule: str, max_live: float,
@@ -409,7 +431,7 @@ def main():
     zstats = coord.stats() if coord else None
     if wd is not None:
         wd.close()
-    serve = serve_engine = None
+    serve = serve_engine = serve_chunked = None
     parts = {}
     want_parts = [x for x in args.partitioned.split(",") if x] if ds.stage == 3 else []
     if want_parts or (args.serve and world == 1 and on_gpu):
@@ -436,7 +458,7 @@ def main():
         # second half of the BASELINE metric ("serve tok/s + p50 TTFT"), after the timed
         # training region: the training model and engine are freed first
         del batches
-        serve, serve_engine = run_serve_bench(args)
+        serve, serve_engine, serve_chunked = run_serve_bench(args)
     if env.is_main:
         from lumen.train.trainer import model_flops_per_token
 
@@ -489,6 +511,7 @@ def main():
                 **{f"zero3_{k}": v for k, v in parts.items()},
                 "serve": serve,
                 "serve_engine": serve_engine,
+                "serve_chunked": serve_chunked,
             },
         }
         print(json.dumps(out), file=json_out, flush=True)

@@ -12,6 +12,19 @@ import os
 import sys
 
 
+def resolve_scheduling(policy, enable_chunked_prefill, budget, max_model_len):
+    """(policy, tokens per step) with vLLM 0.6.0's defaults (the version the reference pins,
+    requirements.txt:18): chunked prefill off -- prefill-only steps while prompts wait, at most
+    max(max_model_len, 2048) tokens per step; ``--enable-chunked-prefill`` = mixed steps."""
+    if policy is None:
+        policy = "chunked" if enable_chunked_prefill else "prefill_first"
+    elif enable_chunked_prefill and policy != "chunked":
+        raise SystemExit("--enable-chunked-prefill contradicts --scheduling-policy " + policy)
+    if budget is None:
+        budget = max(max_model_len, 2048) if policy == "prefill_first" else 2048
+    return policy, budget
+
+
 def build_parser():
     ap = argparse.ArgumentParser(description="lumen OpenAI-compatible server (MI355X)")
     ap.add_argument("--model", default="meta-llama/Llama-2-7b-hf",
@@ -27,14 +40,17 @@ def build_parser():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-num-seqs", type=int, default=256)
-    ap.add_argument("--max-num-batched-tokens", type=int, default=2048,
-                    help="tokens per engine step (running decodes + prefill chunks)")
+    ap.add_argument("--max-num-batched-tokens", type=int, default=None,
+                    help="tokens per engine step; default as vLLM 0.6.0: max(max-model-len, 2048) "
+                         "for prefill_first, 2048 for chunked")
     ap.add_argument("--prefill-boost", type=int, default=1,
                     help="x token budget while at most max-num-seqs/4 sequences decode (1: off)")
-    ap.add_argument("--scheduling-policy", default="chunked", choices=["chunked", "prefill_first"],
-                    help="chunked: mixed prefill-chunk + decode steps (bounded inter-token "
-                         "latency); prefill_first: vLLM 0.6.0's default, prefill-only steps "
-                         "while prompts wait")
+    ap.add_argument("--enable-chunked-prefill", action="store_true",
+                    help="vLLM's flag: same as --scheduling-policy chunked")
+    ap.add_argument("--scheduling-policy", default=None, choices=["chunked", "prefill_first"],
+                    help="prefill_first (default, vLLM 0.6.0's: prefill-only steps while prompts "
+                         "wait, then decode steps); chunked: mixed prefill-chunk + decode steps "
+                         "(bounded inter-token latency)")
     ap.add_argument("--block-size", type=int, default=16)
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
     ap.add_argument("--no-graphs", action="store_true")
@@ -77,12 +93,14 @@ def main(argv=None):
     env = init()
     if env.world_size != a.tp:
         raise SystemExit(f"--tp {a.tp} but WORLD_SIZE={env.world_size}")
+    policy, budget = resolve_scheduling(a.scheduling_policy, a.enable_chunked_prefill,
+                                        a.max_num_batched_tokens, a.max_model_len)
     cfg = EngineConfig(model=a.model, adapter=a.adapter, dtype=a.dtype,
                        max_model_len=a.max_model_len, block_size=a.block_size,
                        gpu_memory_utilization=a.gpu_memory_utilization,
-                       max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_num_batched_tokens,
+                       max_num_seqs=a.max_num_seqs, max_num_batched_tokens=budget,
                        prefill_boost=a.prefill_boost, tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs,
-                       scheduling_policy=a.scheduling_policy,
+                       scheduling_policy=policy,
                        kv_cache_dtype=a.kv_cache_dtype,
                        lora_modules=dict(m.split("=", 1) for m in a.lora_modules)
                        if a.lora_modules else None, max_loras=a.max_loras)

@@ -136,6 +136,9 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_row_kernel(
   }
 }
 
+// 8 elements of T kept packed in registers: 16 bytes for 16-bit T, 32 for f32
+template <typename T> struct alignas(16) Pack8 { T v[8]; };
+
 template <typename T, int VPL, int WPR>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ s, const T* __restrict__ w,
@@ -153,22 +156,24 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
   const bool rok = row < rows;  // no early return: the waves of a block meet at a barrier
   const size_t base = static_cast<size_t>(rok ? row : 0) * H;
   const float rs = rok ? rstd[row] : 0.f;
-  uint4 dyr[VPL], sr[VPL], rr[VPL];
+  using P = Pack8<T>;
+  P dyr[VPL], sr[VPL], rr[VPL];
+  const P zero{};
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = ((i * WPR + ws) * 64 + lane) * 8;
     const bool ok = rok && c < H;
-    dyr[i] = ok ? *reinterpret_cast<const uint4*>(dy + base + c) : make_uint4(0, 0, 0, 0);
-    sr[i] = ok ? *reinterpret_cast<const uint4*>(s + base + c) : make_uint4(0, 0, 0, 0);
-    rr[i] = (ok && ds_res) ? *reinterpret_cast<const uint4*>(ds_res + base + c) : make_uint4(0, 0, 0, 0);
+    dyr[i] = ok ? *reinterpret_cast<const P*>(dy + base + c) : zero;
+    sr[i] = ok ? *reinterpret_cast<const P*>(s + base + c) : zero;
+    rr[i] = (ok && ds_res) ? *reinterpret_cast<const P*>(ds_res + base + c) : zero;
   }
   float dot = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = ((i * WPR + ws) * 64 + lane) * 8;
     if (rok && c < H) {
-      const T* dyv = reinterpret_cast<const T*>(&dyr[i]);
-      const T* sv = reinterpret_cast<const T*>(&sr[i]);
+      const T* dyv = dyr[i].v;
+      const T* sv = sr[i].v;
       float wv[8];
       load8(w + c, wv);
 #pragma unroll
@@ -192,9 +197,9 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
   for (int i = 0; i < VPL; ++i) {
     const int c = ((i * WPR + ws) * 64 + lane) * 8;
     if (rok && c < H) {
-      const T* dyv = reinterpret_cast<const T*>(&dyr[i]);
-      const T* sv = reinterpret_cast<const T*>(&sr[i]);
-      const T* rv = reinterpret_cast<const T*>(&rr[i]);
+      const T* dyv = dyr[i].v;
+      const T* sv = sr[i].v;
+      const T* rv = rr[i].v;
       float wv[8], o[8];
       load8(w + c, wv);
 #pragma unroll

@@ -40,13 +40,14 @@ __global__ void __launch_bounds__(256) qkv_rope_kernel(
   else if (hs < nh + nkv) hm = k + ((static_cast<size_t>(b) * nkv + (hs - nh)) * S + s) * D;
   else hm = v + ((static_cast<size_t>(b) * nkv + (hs - nh - nkv)) * S + s) * D;
 
-  if (hs >= nh + nkv) {  // v: copy 16 elements
+  if (hs >= nh + nkv) {  // v: copy 16 elements (32 bytes for 16-bit T, 64 for f32)
     const T* src = BWD ? hm : tok;
     T* dst = BWD ? tok : hm;
+    constexpr int U = 16 * sizeof(T) / sizeof(uint4);
     const uint4* sp = reinterpret_cast<const uint4*>(src + c * 16);
     uint4* dp = reinterpret_cast<uint4*>(dst + c * 16);
-    dp[0] = sp[0];
-    dp[1] = sp[1];
+#pragma unroll
+    for (int u = 0; u < U; ++u) dp[u] = sp[u];
     return;
   }
   const int p = pos ? pos[t] : s;

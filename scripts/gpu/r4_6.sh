@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4_6}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_rccl_gpu.py -v --timeout 300 --timeout-method thread -k "world8 or matches_tp1" > $O/rccl_tests.txt 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_kernels_gpu.py tests/test_rccl_gpu.py -v --timeout 300 --timeout-method thread -k "rope or fp32 or world8 or matches_tp1" > $O/rccl_tests.txt 2>&1
 rc=$?; grep -E "PASSED|FAILED|ERROR" $O/rccl_tests.txt | tail -20; tail -1 $O/rccl_tests.txt; [ $rc -eq 0 ] || exit $rc
 sed -n '/^export LUMEN_SHARED_GPU_REHEARSAL/,$p' scripts/gpu/r4_2.sh > $O/rest.sh
 export LUMEN_SHARED_GPU_REHEARSAL=1 LUMEN_DIST_TIMEOUT=300

@@ -22,10 +22,14 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("H", [768, 4096, 8192])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("H", [128, 768, 4096, 8192])
 def test_rmsnorm_fwd_bwd(dtype, H):
+    """(fp32: the backward once held 8 elements per lane in a 16-byte register pack -- half of
+    every f32 row vector was lost; fp32 tolerances are 1e-5.)"""
     from lumen.ops.norm import rms_norm, rms_norm_ref
+
+    tf, tb = (1e-5, 1e-5) if dtype == torch.float32 else (1e-2, 2e-2)
 
     T = 300
     x = torch.randn(T, H, device=DEV, dtype=dtype, requires_grad=True)
@@ -35,30 +39,33 @@ def test_rmsnorm_fwd_bwd(dtype, H):
     x2 = x.detach().float().requires_grad_(True)
     r2 = r.detach().float().requires_grad_(True)
     y2, s2 = rms_norm_ref(x2, w.float(), 1e-5, r2)
-    assert rel(s, s2) < 1e-2 and rel(y, y2) < 1e-2
+    assert rel(s, s2) < tf and rel(y, y2) < tf
     dy = torch.randn_like(y)
     ds = torch.randn_like(s)
     torch.autograd.backward([y, s], [dy, ds])
     torch.autograd.backward([y2, s2], [dy.float(), ds.float()])
-    assert rel(x.grad, x2.grad) < 2e-2
-    assert rel(r.grad, r2.grad) < 2e-2
+    assert rel(x.grad, x2.grad) < tb
+    assert rel(r.grad, r2.grad) < tb
     # no-residual variant
     x3 = x.detach().clone().requires_grad_(True)
     y3, s3 = rms_norm(x3, w, 1e-5)
     x4 = x.detach().float().requires_grad_(True)
     y4, _ = rms_norm_ref(x4, w.float(), 1e-5)
-    assert rel(y3, y4) < 1e-2
+    assert rel(y3, y4) < tf
     y3.backward(dy)
     y4.backward(dy.float())
-    assert rel(x3.grad, x4.grad) < 2e-2
+    assert rel(x3.grad, x4.grad) < tb
 
 
-@pytest.mark.parametrize("nh,nkv", [(32, 32), (8, 2)])
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_qkv_rope_split(nh, nkv, dtype):
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (8, 2, 128), (4, 2, 32), (4, 4, 64)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_qkv_rope_split(nh, nkv, D, dtype):
+    """Split + rotate of the fused QKV buffer (the portable-attention path, head_dim != 128 and
+    --dtype fp32 models) vs the fp32 reference, v included (an fp32 v copy once moved only half
+    of each 16-element chunk)."""
     from lumen.ops.rope import qkv_rope_split, qkv_rope_split_ref, rope_tables
 
-    B, S, D = 2, 64, 128
+    B, S = 2, 64
     cos, sin = rope_tables(D, 4096, 10000.0, DEV)
     qkv = torch.randn(B * S, (nh + 2 * nkv) * D, device=DEV, dtype=dtype,
                       requires_grad=True)
@@ -66,7 +73,7 @@ def test_qkv_rope_split(nh, nkv, dtype):
     qkv2 = qkv.detach().float().requires_grad_(True)
     q2, k2, v2 = qkv_rope_split_ref(qkv2, B, S, nh, nkv, D, cos, sin)
     for a, b in ((q, q2), (k, k2), (v, v2)):
-        assert a.shape == b.shape and rel(a, b) < 1e-2
+        assert a.shape == b.shape and rel(a, b) < (1e-5 if dtype == torch.float32 else 1e-2)
     g = [torch.randn_like(t) for t in (q, k, v)]
     torch.autograd.backward([q, k, v], g)
     torch.autograd.backward([q2, k2, v2], [t.float() for t in g])
@@ -78,7 +85,7 @@ def test_qkv_rope_split(nh, nkv, dtype):
     assert rel(qp, qr) < 1e-2 and rel(kp, kr) < 1e-2
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 def test_rope_inplace(dtype):
     from lumen.ops.rope import rope_inplace, rope_tables, _rotate_ref
 
@@ -93,7 +100,7 @@ def test_rope_inplace(dtype):
     assert rel(x, ref) < 1e-2
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 def test_swiglu(dtype):
     from lumen.ops.activation import swiglu, swiglu_ref
 
@@ -109,7 +116,7 @@ def test_swiglu(dtype):
 
 
 @pytest.mark.parametrize("V", [32000, 50272])
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 def test_lm_head_cross_entropy(V, dtype):
     from lumen.ops.loss import lm_head_cross_entropy
 
@@ -1075,3 +1082,36 @@ def test_llama_delta_handoff_matches(monkeypatch):
     assert abs(l1 - l2) <= 1e-6 * abs(l2)
     for n in g1:
         assert rel(g1[n], g2[n]) < 1e-2, n
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama-deep"])
+def test_fp32_model_matches_cpu(name):
+    """--dtype fp32 on the GPU (portable attention with the HIP split/RoPE kernel, head_dim 64 /
+    32 with GQA; adapter products in torch) == the same weights on the CPU: loss and every
+    adapter gradient to fp32 accuracy."""
+    import copy
+
+    from lumen.lora import LoraConfig, apply_lora
+    from lumen.models import build_model
+
+    cpu = build_model(name, dtype=torch.float32, device="cpu", init="random", seed=7)
+    apply_lora(cpu, LoraConfig(r=4, lora_alpha=8, lora_dropout=0.0))
+    for n, p in cpu.named_parameters():
+        if "lora_B" in n:
+            p.data.normal_(0, 0.02, generator=torch.Generator().manual_seed(len(n)))
+    gpu = copy.deepcopy(cpu).to(DEV)
+    ids = torch.randint(0, 500, (8, 16), generator=torch.Generator().manual_seed(3))
+    lc = cpu(ids, labels=ids)
+    lg = gpu(ids.to(DEV), labels=ids.to(DEV))
+    lc, lg = (x[0] if isinstance(x, tuple) else x for x in (lc, lg))
+    assert abs(float(lc) - float(lg)) < 1e-4 * abs(float(lc)), (float(lc), float(lg))
+    lc.backward()
+    lg.backward()
+    gg = dict(gpu.named_parameters())
+    n_checked = 0
+    for n, p in cpu.named_parameters():
+        if p.grad is None:
+            continue
+        assert rel(gg[n].grad, p.grad.to(DEV)) < 1e-3, n
+        n_checked += 1
+    assert n_checked > 0

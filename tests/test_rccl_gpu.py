@@ -135,29 +135,46 @@ def _tp_run(world, tmp_path, backend="nccl", model_name="tiny-llama-gqa"):
     return torch.load(d / "tp_gpu_out.pt", weights_only=True)
 
 
-def _agree(a, b, min_frac=0.9):
-    """Greedy token streams of two bf16 runs whose reductions run in different orders: the
-    same first tokens, and at most a late divergence (a near-tie flipped by rounding)."""
-    tot = same = 0
-    for x, y in zip(a, b):
-        assert x[:2] == y[:2], (a, b)
-        k = next((i for i, (p, q) in enumerate(zip(x, y)) if p != q), len(x))
-        same += k
-        tot += len(x)
-    assert same >= min_frac * tot, (a, b)
+def _greedy_within_noise(outs, model_name, prompts, tol_sigma=0.15):
+    """Teacher-forced check of bf16 greedy streams against the un-sharded f32 model: at every
+    step the chosen token's f32 logit is within ``tol_sigma`` standard deviations (of that
+    step's logits) of the best one.  Greedy choices of a random toy model are often near-ties,
+    so a token-for-token comparison of runs whose bf16 sums are ordered differently (TP=1 GEMM
+    vs TP=W partial sums) flips on rounding; a wrong shard, head or reduction is off by many
+    sigma.  Returns the fraction of steps whose choice equals the f32 argmax."""
+    from tests._dist_worker import _tp_test_model
+
+    ref = _tp_test_model(model_name)
+    same = total = 0
+    for p, out in zip(prompts, outs):
+        with torch.no_grad():
+            lg = ref(torch.tensor(p + out)[None]).float().reshape(len(p) + len(out), -1)
+        lg = lg[len(p) - 1:len(p) - 1 + len(out)]
+        for i, t in enumerate(out):
+            row = lg[i]
+            gap = float(row.max() - row[t])
+            assert gap <= tol_sigma * float(row.std()), (p, out, i, gap, float(row.std()))
+            same += int(t == int(row.argmax()))
+            total += 1
+    return same / total
+
+
+TP_PROMPTS = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
 
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_tp_serving_rccl_matches_tp1(world, tmp_path):
     """TP=2 and TP=8 serving on RCCL (custom IPC all-reduce for the row-parallel sums, decode
-    buckets as hipGraphs, the step's host header over gloo and its payload over RCCL) produce the
-    TP=1 greedy tokens (a model with decisive logits, so bf16 partial-sum rounding cannot flip a
-    greedy choice), and exactly the tokens of the same TP run with gloo carrying the steps."""
+    buckets as hipGraphs, the step's host header over gloo and its payload over RCCL): every
+    greedy step of TP=1 and of TP=W is the f32 model's choice up to bf16 near-ties (teacher-
+    forced), and the TP=W tokens equal those of the same run with gloo carrying the steps."""
     ref = _tp_run(1, tmp_path, "nccl", "tiny-llama-tp8")
     got = _tp_run(world, tmp_path, "nccl", "tiny-llama-tp8")
     assert got["info"]["backend"] == "nccl" and got["info"]["car"], got["info"]
     assert got["info"]["captured"], got["info"]
-    _agree(got["out"], ref["out"])
+    f1 = _greedy_within_noise(ref["out"], "tiny-llama-tp8", TP_PROMPTS)
+    fw = _greedy_within_noise(got["out"], "tiny-llama-tp8", TP_PROMPTS)
+    assert f1 >= 0.75 and fw >= 0.75, (f1, fw)
     alt = _tp_run(world, tmp_path, "gloo", "tiny-llama-tp8")
     assert alt["out"] == got["out"]
 

@@ -603,3 +603,18 @@ def test_prefill_boost_budget():
     assert plan(2, 1).num_tokens == 64            # no boost: 2 decodes + 62 prefill tokens
     assert plan(2, 2).num_tokens == 128           # 2 <= 16 // 4 decoding: budget x 2
     assert plan(5, 2).num_tokens == 64            # 5 > 4 decoding: the plain budget
+
+
+def test_serve_cli_scheduling_defaults_follow_vllm_060():
+    """`lumen serve` without scheduling flags schedules like vLLM 0.6.0 (the reference's pin):
+    prefill-first with max(max_model_len, 2048) tokens per step; --enable-chunked-prefill or
+    --scheduling-policy chunked = mixed steps at 2048; an explicit budget always wins."""
+    from lumen.cli.serve import resolve_scheduling
+
+    assert resolve_scheduling(None, False, None, 4096) == ("prefill_first", 4096)
+    assert resolve_scheduling(None, False, None, 1024) == ("prefill_first", 2048)
+    assert resolve_scheduling(None, True, None, 4096) == ("chunked", 2048)
+    assert resolve_scheduling("chunked", False, 512, 4096) == ("chunked", 512)
+    assert resolve_scheduling("prefill_first", False, 8192, 4096) == ("prefill_first", 8192)
+    with pytest.raises(SystemExit):
+        resolve_scheduling("prefill_first", True, None, 4096)
