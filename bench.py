@@ -40,9 +40,10 @@ def run_serve_bench(args) -> dict:
     requirements.txt:18): chunked prefill off, prefill-only steps while prompts wait, then decode
     steps, max_num_batched_tokens = max(max_model_len, 2048) = 4096 for Llama-2's 4096 context.
     Measurements of the same 256-request burst (512 in / 128 out, all arriving at t=0):
-      * ``http`` -> ``extra.serve``: the reference's declared path -- the OpenAI HTTP server (a
-        spawned process, the production layout of scripts/serve.py) streaming
-        ``/v1/completions`` to the async load client (a third process; the Locust request shape);
+      * ``http`` -> ``extra.serve``: the reference's declared path -- the OpenAI HTTP server
+        (4 spawned API processes on one port, ``lumen serve --api-server-count 4``: one Python
+        front-end saturates at 256 streams) streaming ``/v1/completions`` to the async load
+        client (4 processes, Locust's distributed-worker layout; the Locust request shape);
       * ``engine`` -> ``extra.serve_engine``: the same engine driven in-process (no HTTP);
       * ``extra.serve_chunked``: in-process again with lumen's mixed-step policy (chunked
         prefill, 2048 tokens per step: inter-token latency bounded by one mixed step instead of
@@ -63,7 +64,8 @@ def run_serve_bench(args) -> dict:
         no_graphs=False, sync_scheduling=False, kv_cache_dtype="auto",
         scheduling_policy=os.environ.get("LUMEN_SERVE_POLICY", "prefill_first"),
         num_requests=256, concurrency=256, prompt_len=512, max_tokens=128, temperature=0.0,
-        request_rate=None)
+        request_rate=None, api_servers=int(os.environ.get("LUMEN_API_SERVERS", "4")),
+        client_procs=int(os.environ.get("LUMEN_CLIENT_PROCS", "4")))
     keep = ("output_tok_s", "ttft_p50_ms", "ttft_p99_ms", "itl_p50_ms", "itl_p99_ms",
             "itl_max_ms", "itl_mean_ms", "wall_s", "total_tok_s", "output_tokens", "preemptions",
             "steps", "setup_s", "ok", "errors", "http_section_s")
@@ -91,7 +93,8 @@ def run_serve_bench(args) -> dict:
     h_out = {k: h[k] for k in keep if k in h}
     h_out["bench_s"] = round(time.time() - t1, 1)
     h_out["vs_engine"] = round(h["output_tok_s"] / max(r["output_tok_s"], 1e-9), 3)
-    h_out["config"] = dict(conf, concurrency=a.concurrency,
+    h_out["config"] = dict(conf, concurrency=a.concurrency, api_servers=a.api_servers,
+                           client_procs=a.client_procs,
                            mode="OpenAI HTTP API (/v1/completions, SSE) + async load client")
     c_out = None
     if a.scheduling_policy != "chunked":

@@ -53,8 +53,10 @@ def summarize(results: List[ReqResult], wall: float) -> dict:
         "ttft_p90_ms": round(1000 * _pct(ttft, 0.9), 2),
         "ttft_p99_ms": round(1000 * _pct(ttft, 0.99), 2),
         "itl_p50_ms": round(1000 * _pct(itl, 0.5), 3),
+        "itl_p90_ms": round(1000 * _pct(itl, 0.9), 3),
+        "itl_p95_ms": round(1000 * _pct(itl, 0.95), 3),
         "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
-        "itl_max_ms": round(1000 * max(itl), 2) if itl else 0.0,
+        "itl_max_ms": round(1000 * max(itl), 3) if itl else 0.0,
         "itl_mean_ms": round(1000 * sum(itl) / len(itl), 3) if itl else 0.0,
         "latency_p50_s": round(_pct(lat, 0.5), 3),
     }
@@ -67,42 +69,54 @@ async def one_request(session, url: str, prompt, max_tokens: int, model: str) ->
     first = None
     last = t0
     itl = []
-    n = 0
+    buf = b""
+    done = False
     try:
         async with session.post(url + "/v1/completions", json=body) as resp:
             if resp.status != 200:
                 return ReqResult(False, error=f"HTTP {resp.status}")
-            async for raw in resp.content:
-                line = raw.decode().strip()
-                if not line.startswith("data: "):
-                    continue
-                data = line[6:]
-                if data == "[DONE]":
-                    break
-                j = json.loads(data)
-                if "error" in j:
-                    return ReqResult(False, error=j["error"]["message"])
+            # whole network chunks, split into SSE events here: one Python-level read per chunk
+            # instead of three readline() calls per event (at 256 streams x ~50 events/s the
+            # client's own per-event work would otherwise show up as inter-token latency); the
+            # events of one chunk arrived together and share its timestamp
+            async for chunk in resp.content.iter_any():
                 now = time.perf_counter()
-                if j.get("choices"):  # one event per generated-token step (text may be empty)
+                buf += chunk
+                while b"\n\n" in buf:
+                    ev, buf = buf.split(b"\n\n", 1)
+                    ev = ev.strip()
+                    if not ev.startswith(b"data: "):
+                        continue
+                    if ev.startswith(b"data: [DONE]"):
+                        done = True
+                        break
+                    if b'"choices"' not in ev:
+                        j = json.loads(ev[6:])
+                        return ReqResult(False, error=str(j.get("error", j)))
+                    # one event per generated-token step (text may be empty)
                     if first is None:
                         first = now
                     else:
                         itl.append(now - last)
                     last = now
-                    n += 1
+                if done:
+                    break
     except Exception as e:  # network error -> failed request
         return ReqResult(False, error=repr(e))
     plen = len(prompt) if isinstance(prompt, list) else 0
     return ReqResult(True, (first or last) - t0, last - t0, itl, max_tokens, plen)
 
 
-async def run_load(url: str, num_requests: int, concurrency: int, prompt_len: int,
-                   max_tokens: int, vocab: int = 32000, request_rate: Optional[float] = None,
-                   model: str = "lumen", seed: int = 0) -> dict:
+def _prompts(num_requests: int, prompt_len: int, vocab: int, seed: int):
+    rng = random.Random(seed)
+    return [[rng.randrange(3, vocab) for _ in range(prompt_len)] for _ in range(num_requests)]
+
+
+async def _drive(url, prompts, concurrency, max_tokens, request_rate, model, seed):
+    """Run ``prompts`` against the server; returns (results, wall seconds)."""
     import aiohttp
 
-    rng = random.Random(seed)
-    prompts = [[rng.randrange(3, vocab) for _ in range(prompt_len)] for _ in range(num_requests)]
+    rng = random.Random(seed + 1)
     results: List[ReqResult] = []
     timeout = aiohttp.ClientTimeout(total=3600)
     conn = aiohttp.TCPConnector(limit=max(concurrency, 1) + 8)
@@ -123,7 +137,64 @@ async def run_load(url: str, num_requests: int, concurrency: int, prompt_len: in
 
             await asyncio.gather(*[user() for _ in range(concurrency)])
         wall = time.perf_counter() - t0
+    return results, wall
+
+
+async def run_load(url: str, num_requests: int, concurrency: int, prompt_len: int,
+                   max_tokens: int, vocab: int = 32000, request_rate: Optional[float] = None,
+                   model: str = "lumen", seed: int = 0) -> dict:
+    prompts = _prompts(num_requests, prompt_len, vocab, seed)
+    results, wall = await _drive(url, prompts, concurrency, max_tokens, request_rate, model, seed)
     return summarize(results, wall)
+
+
+def _worker(i, url, prompts, concurrency, max_tokens, rate, model, seed, warmup, ready, go, out):
+    """One load-generator process (Locust's distributed worker): warm up, report ready, wait for
+    the common start, run its share, send back raw per-request results and its end time."""
+    if warmup:
+        asyncio.run(_drive(url, prompts[:warmup], warmup, 4, None, model, seed))
+    ready.put(i)
+    go.wait()
+    t0 = time.time()
+    results, _ = asyncio.run(_drive(url, prompts, concurrency, max_tokens, rate, model, seed + i))
+    out.put((i, t0, time.time(), [(r.ok, r.ttft, r.latency, r.itl, r.out_tokens, r.prompt_tokens,
+                                    r.error) for r in results]))
+
+
+def run_load_procs(url: str, num_requests: int, concurrency: int, prompt_len: int,
+                   max_tokens: int, vocab: int = 32000, request_rate: Optional[float] = None,
+                   model: str = "lumen", seed: int = 0, procs: int = 1, warmup: int = 0) -> dict:
+    """``run_load`` spread over ``procs`` client processes (requests and concurrency split
+    round-robin, one common start): at hundreds of streams a single asyncio client saturates
+    its core and its own lag reads as server latency.  Wall = first start to last end."""
+    import multiprocessing as mp
+
+    prompts = _prompts(num_requests, prompt_len, vocab, seed)
+    ctx = mp.get_context("spawn")
+    ready, out, go = ctx.Queue(), ctx.Queue(), ctx.Event()
+    ps = []
+    for i in range(procs):
+        share = prompts[i::procs]
+        conc = len(range(i, concurrency, procs))
+        rate = request_rate / procs if request_rate else None
+        wu = len(range(i, warmup, procs))
+        p = ctx.Process(target=_worker, args=(i, url, share, max(conc, 1), max_tokens, rate, model,
+                                              seed, wu, ready, go, out), daemon=True)
+        p.start()
+        ps.append(p)
+    for _ in range(procs):
+        ready.get(timeout=600)
+    go.set()
+    parts = [out.get(timeout=3600) for _ in range(procs)]
+    for p in ps:
+        p.join(30)
+    t0 = min(x[1] for x in parts)
+    t1 = max(x[2] for x in parts)
+    results = [ReqResult(ok, ttft, lat, itl, n, pt, err)
+               for _, _, _, rs in parts for ok, ttft, lat, itl, n, pt, err in rs]
+    res = summarize(results, t1 - t0)
+    res["client_procs"] = procs
+    return res
 
 
 def main():
@@ -138,7 +209,14 @@ def main():
     ap.add_argument("--model", default="lumen")
     ap.add_argument("--warmup", type=int, default=0,
                     help="first run this many short (4-token) requests, untimed")
+    ap.add_argument("--procs", type=int, default=1,
+                    help="client processes (Locust-style distributed workers)")
     a = ap.parse_args()
+    if a.procs > 1:
+        res = run_load_procs(a.url, a.num_requests, a.concurrency, a.prompt_len, a.max_tokens,
+                             a.vocab, a.request_rate, a.model, procs=a.procs, warmup=a.warmup)
+        print(json.dumps(res))
+        return
     if a.warmup:
         asyncio.run(run_load(a.url, a.warmup, a.warmup, a.prompt_len, 4, a.vocab,
                              model=a.model, seed=1))

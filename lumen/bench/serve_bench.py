@@ -90,14 +90,18 @@ def bench_engine(a, eng=None) -> dict:
                 time.sleep(max(0.0, next_t - time.perf_counter()))
     else:
         seqs = [eng.add_request(p, SamplingParams(**params)) for p in prompts]
-        while eng.has_work:
-            eng.step()
+        if getattr(a, "trace_steps", False):
+            trace = _trace_steps(eng)
+        else:
+            while eng.has_work:
+                eng.step()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
     out_toks = sum(len(s.output_ids) for s in seqs)
     ttft = [s.first_token_time - s.arrival for s in seqs]
     itl = [b - a_ for s in seqs for a_, b in zip(s.token_times, s.token_times[1:])]
-    return {"mode": "engine", "requests": len(seqs), "prompt_len": a.prompt_len,
+    extra = {"step_trace": trace} if getattr(a, "trace_steps", False) else {}
+    return {**extra, "mode": "engine", "requests": len(seqs), "prompt_len": a.prompt_len,
             "max_tokens": a.max_tokens, "wall_s": round(wall, 3), "output_tokens": out_toks,
             "output_tok_s": round(out_toks / wall, 1),
             "total_tok_s": round((out_toks + a.prompt_len * len(seqs)) / wall, 1),
@@ -105,7 +109,7 @@ def bench_engine(a, eng=None) -> dict:
             "ttft_p99_ms": round(1000 * _pct(ttft, 0.99), 2),
             "itl_p50_ms": round(1000 * _pct(itl, 0.5), 3),
             "itl_p99_ms": round(1000 * _pct(itl, 0.99), 3),
-            "itl_max_ms": round(1000 * max(itl), 2) if itl else 0.0,
+            "itl_max_ms": round(1000 * max(itl), 3) if itl else 0.0,
             "itl_mean_ms": round(1000 * sum(itl) / len(itl), 3) if itl else 0.0,
             "scheduling_policy": getattr(a, "scheduling_policy", "chunked"),
             "kv_blocks": eng.blocks.num_blocks, "preemptions": eng.scheduler.num_preemptions,
@@ -115,32 +119,71 @@ def bench_engine(a, eng=None) -> dict:
             "graphs": sorted(eng.runner._graphs)}
 
 
+def _trace_steps(eng) -> dict:
+    """Drive the engine to completion timing every step on the device clock (synchronous: each
+    step is waited for), grouped by composition: decode-only, prefill-only and mixed steps with
+    their mean prefill tokens / decode rows -- where a scheduling policy's time goes."""
+    import torch
+
+    kinds = {}
+    orig = eng.scheduler.schedule
+    last = {}
+
+    def spy():
+        b = orig()
+        if b is not None:
+            last["p"] = sum(c for _, c in b.prefills)
+            last["d"] = len(b.decodes)
+        return b
+
+    eng.scheduler.schedule = spy
+    try:
+        while eng.has_work:
+            last.clear()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.step()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if not last:
+                continue
+            k = "mixed" if last["p"] and last["d"] else ("prefill" if last["p"] else "decode")
+            g = kinds.setdefault(k, [0, 0.0, 0, 0])
+            g[0] += 1
+            g[1] += dt
+            g[2] += last["p"]
+            g[3] += last["d"]
+    finally:
+        eng.scheduler.schedule = orig
+    return {k: {"steps": n, "ms_total": round(1000 * t, 1), "ms_mean": round(1000 * t / n, 2),
+                "prefill_tokens_mean": round(p / n, 1), "decode_rows_mean": round(d / n, 1)}
+            for k, (n, t, p, d) in kinds.items()}
+
+
 def bench_http(a, eng=None) -> dict:
     """The production serving path (``scripts/serve.py``): the engine core loop in THIS (GPU)
-    process, the OpenAI HTTP server in a spawned process talking to it over two queues, and the
-    async client (the Locust request shape: streamed ``/v1/completions`` with ``ignore_eos``) in
-    a third process -- the client's SSE parsing never competes with the engine for a GIL.  With
-    ``eng`` (already warm, e.g. after ``bench_engine``) no model load or graph capture is paid
-    again."""
-    import multiprocessing as mp
+    process, the OpenAI HTTP server in ``a.api_servers`` spawned processes talking to it over
+    queues (one port, SO_REUSEPORT), and the async client (the Locust request shape: streamed
+    ``/v1/completions`` with ``ignore_eos``) in ``a.client_procs`` more processes (Locust's
+    distributed workers) -- neither the front-end's nor the client's per-event Python work
+    competes with the engine for a GIL or saturates a core.  With ``eng`` (already warm, e.g.
+    after ``bench_engine``) no model load or graph capture is paid again."""
     import threading
     import urllib.request
 
-    from lumen.serve.frontend import api_process_main, run_engine_core
+    from lumen.serve.frontend import run_engine_core, start_api_servers
 
     t0 = time.time()
     eng = eng if eng is not None else make_engine(a)
+    n_api = int(getattr(a, "api_servers", 1))
+    n_cli = int(getattr(a, "client_procs", 1))
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     url = f"http://127.0.0.1:{port}"
-    ctx = mp.get_context("spawn")
-    req_q, out_q = ctx.Queue(), ctx.Queue()
-    api = ctx.Process(target=api_process_main, name="lumen-api",
-                      args=(req_q, out_q, a.model, a.max_model_len, "127.0.0.1", port, "lumen",
-                            eng.model_config.vocab_size), daemon=True)
-    api.start()
+    req_q, out_qs, apis = start_api_servers(n_api, a.model, a.max_model_len, "127.0.0.1", port,
+                                            "lumen", eng.model_config.vocab_size)
     client = None
     try:
         while True:
@@ -148,14 +191,14 @@ def bench_http(a, eng=None) -> dict:
                 urllib.request.urlopen(url + "/health", timeout=2)
                 break
             except Exception:
-                if not api.is_alive() or time.time() - t0 > 300:
+                if not all(p.is_alive() for p in apis) or time.time() - t0 > 300:
                     raise RuntimeError("API server did not come up")
                 time.sleep(0.2)
         cmd = [sys.executable, "-m", "lumen.bench.async_client", "--url", url,
                "--num-requests", str(a.num_requests), "--concurrency", str(a.concurrency),
                "--prompt-len", str(a.prompt_len), "--max-tokens", str(a.max_tokens),
                "--vocab", str(eng.model_config.vocab_size),
-               "--warmup", str(min(a.concurrency, a.num_requests))]
+               "--warmup", str(min(a.concurrency, a.num_requests)), "--procs", str(n_cli)]
         if a.request_rate:
             cmd += ["--request-rate", str(a.request_rate)]
         client = subprocess.Popen(cmd, stdout=subprocess.PIPE, cwd=ROOT,
@@ -168,19 +211,23 @@ def bench_http(a, eng=None) -> dict:
 
         w = threading.Thread(target=watch, daemon=True)
         w.start()
-        run_engine_core(eng, req_q, out_q)
+        run_engine_core(eng, req_q, out_qs)
         w.join()
         if client.returncode != 0:
             raise RuntimeError(f"load client exited with {client.returncode}")
         lines = [x for x in out["stdout"].decode().splitlines() if x.startswith("{")]
         res = json.loads(lines[-1])
     finally:
-        out_q.put(None)
+        for q in out_qs:
+            q.put(None)
         if client is not None and client.poll() is None:
             client.kill()
-        api.terminate()
-        api.join(10)
+        for p in apis:
+            p.terminate()
+        for p in apis:
+            p.join(10)
     res["mode"] = "http"
+    res["api_servers"], res["client_procs"] = n_api, n_cli
     res["prompt_len"], res["max_tokens"] = a.prompt_len, a.max_tokens
     res["http_section_s"] = round(time.time() - t0, 1)
     return res
@@ -211,6 +258,12 @@ def main():
                          "runs the bench, the other ranks the worker loop")
     ap.add_argument("--num-blocks", type=int, default=None, help="KV blocks (default: auto)")
     ap.add_argument("--scheduling-policy", default="chunked", choices=["chunked", "prefill_first"])
+    ap.add_argument("--api-servers", type=int, default=1,
+                    help="http mode: OpenAI API processes sharing the port (SO_REUSEPORT)")
+    ap.add_argument("--client-procs", type=int, default=1,
+                    help="http mode: load-client processes (Locust-style workers)")
+    ap.add_argument("--trace-steps", action="store_true",
+                    help="engine mode: time every step synchronously, grouped by composition")
     a = ap.parse_args()
     if a.tp > 1:
         from lumen.parallel.dist import init, shutdown

@@ -57,6 +57,9 @@ def build_parser():
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
                     help="KV-cache element type (fp8 = e4m3: 2x capacity, half the decode K/V reads)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--api-server-count", type=int, default=1,
+                    help="OpenAI API processes sharing --port (SO_REUSEPORT), each streaming its "
+                         "own requests' tokens from the one engine core")
     ap.add_argument("--in-process", action="store_true",
                     help="run the HTTP server on a thread of the GPU process (default: the API "
                          "runs in its own process and talks to the engine core over queues)")
@@ -70,22 +73,17 @@ def main(argv=None):
     from lumen.models import get_config
 
     rank = int(os.environ.get("RANK", "0"))
-    api = req_q = out_q = None
+    apis, req_q, out_qs = [], None, []
     if rank == 0 and not a.in_process:
-        # OpenAI HTTP front-end in a spawned process (no GPU, its own GIL), started before this
-        # process initialises the GPU; it talks to the engine core below over two queues
-        import multiprocessing as mp
-
-        from lumen.serve.frontend import api_process_main
+        # OpenAI HTTP front-end(s) in spawned processes (no GPU, their own GILs), started before
+        # this process initialises the GPU; they talk to the engine core below over queues
+        from lumen.serve.frontend import start_api_servers
 
         mcfg = get_config(a.model)
         lora_names = [m.split("=", 1)[0] for m in (a.lora_modules or [])]
-        ctx = mp.get_context("spawn")
-        req_q, out_q = ctx.Queue(), ctx.Queue()
-        api = ctx.Process(target=api_process_main, name="lumen-api",
-                          args=(req_q, out_q, a.model, a.max_model_len, a.host, a.port,
-                                a.served_model_name, mcfg.vocab_size, lora_names), daemon=True)
-        api.start()
+        req_q, out_qs, apis = start_api_servers(a.api_server_count, a.model, a.max_model_len,
+                                                a.host, a.port, a.served_model_name,
+                                                mcfg.vocab_size, lora_names)
 
     from lumen.parallel.dist import init
     from lumen.serve.engine import AsyncEngine, EngineConfig, LLMEngine
@@ -132,13 +130,16 @@ def main(argv=None):
 
     signal.signal(signal.SIGTERM, _term)
     try:
-        run_engine_core(eng, req_q, out_q)
+        run_engine_core(eng, req_q, out_qs)
     except KeyboardInterrupt:
         pass
     finally:
-        out_q.put(None)
-        api.terminate()
-        api.join(10)
+        for q in out_qs:
+            q.put(None)
+        for p in apis:
+            p.terminate()
+        for p in apis:
+            p.join(10)
         eng.shutdown()
 
 

@@ -152,13 +152,25 @@ class IncrementalDetokenizer:
         self.read = 0
         self._prefix_text = ""   # decode(ids[prefix:read]), kept across steps (one decode/token)
 
+    # tokens that decode to no text at all (specials, ids outside a byte-level vocabulary) would
+    # otherwise keep the window growing: after this many, the window restarts past them
+    MAX_SILENT = 4
+    # a U+FFFD still open after this many tokens is an invalid sequence, not an incomplete one
+    # (UTF-8 needs at most 4 bytes): it is emitted as is
+    MAX_HELD = 16
+
     def step(self, ids: List[int]) -> str:
         prefix_text = self._prefix_text
         new_text = self.tok.decode(ids[self.prefix:])
-        if len(new_text) > len(prefix_text) and not new_text.endswith("\ufffd"):
+        if len(new_text) > len(prefix_text) and (not new_text.endswith("\ufffd")
+                                                 or len(ids) - self.read >= self.MAX_HELD):
             self.prefix, self.read = self.read, len(ids)
             self._prefix_text = self.tok.decode(ids[self.prefix:self.read])
             return new_text[len(prefix_text):]
+        if (new_text == prefix_text and len(ids) - self.read >= self.MAX_SILENT
+                and not new_text.endswith("\ufffd")):
+            self.prefix = self.read = len(ids)
+            self._prefix_text = ""
         return ""
 
     def flush(self, ids: List[int]) -> str:

@@ -8,9 +8,16 @@ bookkeeping for the GIL; at 256 concurrent streams that serialisation, not the G
 client-side inter-token latency (1.2 s vs 22 ms engine-side).  The split keeps the engine step
 loop free of HTTP work, as vLLM's engine-core process does.
 
+Several API processes (``--api-server-count``, as in later vLLM releases) may share one
+engine core: each listens on the same port (SO_REUSEPORT: the kernel spreads the connections),
+all of them put requests on the one request queue, and each has its own output queue -- the core
+routes every request's tokens to the front-end that submitted it.  At 256 concurrent streams one
+Python front-end is CPU-bound (request intake + ~13k SSE events/s), and its lag reads as
+inter-token latency at the client.
+
 Protocol (all plain tuples/lists, pickled by multiprocessing):
-  front -> core: ("add", rid, prompt_ids, params_dict, arrival, lora_name|None) | ("abort", rid)
-                 | ("stop",)
+  front -> core: ("add", rid, prompt_ids, params_dict, arrival, lora_name|None, front_index)
+                 | ("abort", rid) | ("stop",)
   core -> front: ("step", [(rid, new_ids, new_logprobs, finish_reason|None), ...], stats)
                  ("error", rid, message)
 """
@@ -32,9 +39,13 @@ from .sequence import SamplingParams
 # ------------------------------------------------------------------------------------------
 
 def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
-    """Serve requests from ``req_q`` until a ("stop",) message; one out message per step."""
+    """Serve requests from ``req_q`` until a ("stop",) message; one out message per step and
+    front-end.  ``out_q``: one queue, or a list (one per API process, indexed by the "add"
+    message's front index)."""
+    outs = list(out_q) if isinstance(out_q, (list, tuple)) else [out_q]
     live: Dict[str, object] = {}
     sent: Dict[str, int] = {}
+    origin: Dict[str, int] = {}
     stop = False
     while not stop:
         block = not engine.has_work
@@ -46,18 +57,21 @@ def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
             block = False
             kind = op[0]
             if kind == "add":
-                _, rid, ids, pdict, arrival, lora = op
+                _, rid, ids, pdict, arrival, lora = op[:6]
+                o = op[6] if len(op) > 6 else 0
                 try:
                     seq = engine.add_request(ids, SamplingParams(**pdict), rid, lora)
                     seq.arrival = arrival
                     live[rid] = seq
                     sent[rid] = 0
+                    origin[rid] = o
                 except Exception as e:  # noqa: BLE001 - report to the request's stream
-                    out_q.put(("error", rid, str(e)))
+                    outs[o].put(("error", rid, str(e)))
             elif kind == "abort":
                 engine.abort(op[1])
                 live.pop(op[1], None)
                 sent.pop(op[1], None)
+                origin.pop(op[1], None)
             elif kind == "stop":
                 stop = True
         if stop or not engine.has_work:
@@ -68,9 +82,9 @@ def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
             seqs = engine.step()
         except Exception as e:  # noqa: BLE001 - surface to every open stream, then fail
             for rid in list(live):
-                out_q.put(("error", rid, repr(e)))
+                outs[origin.get(rid, 0)].put(("error", rid, repr(e)))
             raise
-        updates = []
+        updates: Dict[int, list] = {}
         for s in seqs:
             rid = s.request_id
             if rid not in live:
@@ -80,15 +94,17 @@ def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
             lps = s.output_logprobs[k:] if s.output_logprobs else []
             sent[rid] = len(s.output_ids)
             fin = s.finish_reason if s.finished else None
-            updates.append((rid, new, lps, fin))
+            updates.setdefault(origin[rid], []).append((rid, new, lps, fin))
             if fin is not None:
                 live.pop(rid, None)
                 sent.pop(rid, None)
+                origin.pop(rid, None)
         if updates:
             sch = engine.scheduler
-            out_q.put(("step", updates, {"kv_usage": engine.blocks.usage(),
-                                         "running": len(sch.running), "waiting": len(sch.waiting),
-                                         "preemptions": sch.num_preemptions}))
+            stats = {"kv_usage": engine.blocks.usage(), "running": len(sch.running),
+                     "waiting": len(sch.waiting), "preemptions": sch.num_preemptions}
+            for o, ups in updates.items():
+                outs[o].put(("step", ups, stats))
 
 
 # ------------------------------------------------------------------------------------------
@@ -121,8 +137,9 @@ class EngineCoreClient:
     engine core in another process."""
 
     def __init__(self, req_q, out_q, tokenizer, model_name: str, max_model_len: int,
-                 eos_id: Optional[int], lora_names: Optional[List[str]] = None):
+                 eos_id: Optional[int], lora_names: Optional[List[str]] = None, index: int = 0):
         self.req_q, self.out_q = req_q, out_q
+        self.index = index  # which of the core's output queues carries this front-end's tokens
         self.lora_names = list(lora_names or [])
         self.tokenizer = tokenizer
         self.model_name = model_name
@@ -170,7 +187,8 @@ class EngineCoreClient:
         q: asyncio.Queue = asyncio.Queue()
         self._streams[rid] = (asyncio.get_running_loop(), q)
         view = SeqView(ids, rid, time.perf_counter())
-        self.req_q.put(("add", rid, ids, dataclasses.asdict(params), view.arrival, lora))
+        self.req_q.put(("add", rid, ids, dataclasses.asdict(params), view.arrival, lora,
+                        self.index))
         try:
             while True:
                 kind, payload = await q.get()
@@ -202,8 +220,10 @@ def _deliver(items):
 
 def api_process_main(req_q, out_q, model: str, max_model_len: int, host: str, port: int,
                      served_model_name: Optional[str], vocab_size: int,
-                     lora_names: Optional[List[str]] = None) -> None:
-    """Entry point of the spawned HTTP process (no GPU)."""
+                     lora_names: Optional[List[str]] = None, index: int = 0,
+                     reuse_port: bool = False) -> None:
+    """Entry point of a spawned HTTP process (no GPU).  ``reuse_port``: one of several API
+    processes listening on the same port (SO_REUSEPORT)."""
     import os
 
     import uvicorn
@@ -223,6 +243,37 @@ def api_process_main(req_q, out_q, model: str, max_model_len: int, host: str, po
     tok = load_tokenizer(model, vocab_size)
     eos = getattr(tok, "eos_token_id", None)
     client = EngineCoreClient(req_q, out_q, tok, served_model_name or model, max_model_len, eos,
-                              lora_names)
+                              lora_names, index)
     app = create_app(client, served_model_name)
-    uvicorn.run(app, host=host, port=port, log_level="warning")
+    if not reuse_port:
+        uvicorn.run(app, host=host, port=port, log_level="warning")
+        return
+    import socket
+
+    sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    sock.bind((host, port))
+    sock.listen(2048)
+    uvicorn.Server(uvicorn.Config(app, log_level="warning")).run(sockets=[sock])
+
+
+def start_api_servers(count: int, model: str, max_model_len: int, host: str, port: int,
+                      served_model_name: Optional[str], vocab_size: int,
+                      lora_names: Optional[List[str]] = None):
+    """Spawn ``count`` API processes on ``host:port`` sharing one request queue; returns
+    (request queue, [output queue per process], [processes]) for ``run_engine_core``."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    req_q = ctx.Queue()
+    out_qs, procs = [], []
+    for i in range(max(1, count)):
+        out_q = ctx.Queue()
+        p = ctx.Process(target=api_process_main, name=f"lumen-api{i}",
+                        args=(req_q, out_q, model, max_model_len, host, port, served_model_name,
+                              vocab_size, lora_names, i, count > 1), daemon=True)
+        p.start()
+        out_qs.append(out_q)
+        procs.append(p)
+    return req_q, out_qs, procs

@@ -618,3 +618,89 @@ def test_serve_cli_scheduling_defaults_follow_vllm_060():
     assert resolve_scheduling("prefill_first", False, 8192, 4096) == ("prefill_first", 8192)
     with pytest.raises(SystemExit):
         resolve_scheduling("prefill_first", True, None, 4096)
+
+
+def test_async_load_client_against_live_server(model):
+    """The load client (lumen/bench/async_client.py, the Locust request shape: streamed
+    /v1/completions with ignore_eos) against a live uvicorn server on a CPU engine: every
+    request completes with max_tokens output tokens, TTFT / ITL are measured per SSE event."""
+    import asyncio
+    import socket
+    import threading
+    import time
+
+    import uvicorn
+
+    from lumen.bench.async_client import run_load
+    from lumen.serve.api_server import create_app
+    from lumen.serve.engine import AsyncEngine
+
+    ae = AsyncEngine(_engine(model, num_blocks=256))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    server = uvicorn.Server(uvicorn.Config(create_app(ae, "tiny"), host="127.0.0.1", port=port,
+                                           log_level="warning"))
+    th = threading.Thread(target=server.run, daemon=True)
+    th.start()
+    try:
+        t0 = time.time()
+        while not server.started:
+            assert time.time() - t0 < 30, "server did not start"
+            time.sleep(0.05)
+        res = asyncio.run(run_load(f"http://127.0.0.1:{port}", 6, 3, 8, 5, vocab=500,
+                                   model="tiny"))
+        assert res["ok"] == 6 and res["errors"] == 0 and res["output_tokens"] == 30, res
+        assert res["ttft_p50_ms"] > 0 and res["itl_p50_ms"] > 0 and res["itl_max_ms"] >= res["itl_p99_ms"]
+    finally:
+        server.should_exit = True
+        th.join(10)
+        ae.shutdown()
+
+
+def test_multiple_api_processes_share_one_engine_core(model):
+    """`lumen serve --api-server-count 2`: two spawned OpenAI API processes on one port
+    (SO_REUSEPORT), one engine core; every request's tokens are routed back to the front-end
+    that submitted it, and a 4-process load client (Locust-style workers) gets every stream
+    complete."""
+    import asyncio  # noqa: F401
+    import socket
+    import threading
+    import time
+    import urllib.request
+
+    from lumen.bench.async_client import run_load_procs
+    from lumen.serve.frontend import run_engine_core, start_api_servers
+
+    eng = _engine(model, num_blocks=256, async_scheduling=False)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    req_q, out_qs, apis = start_api_servers(2, "tiny-llama-gqa", 256, "127.0.0.1", port, "tiny",
+                                            512)
+    core = threading.Thread(target=run_engine_core, args=(eng, req_q, out_qs), daemon=True)
+    core.start()
+    try:
+        url = f"http://127.0.0.1:{port}"
+        t0 = time.time()
+        while True:
+            try:
+                urllib.request.urlopen(url + "/health", timeout=2)
+                break
+            except Exception:
+                assert time.time() - t0 < 120 and all(p.is_alive() for p in apis)
+                time.sleep(0.2)
+        time.sleep(1.0)  # both listeners up
+        res = run_load_procs(url, 8, 4, 6, 4, vocab=500, model="tiny", procs=4)
+        assert res["ok"] == 8 and res["errors"] == 0 and res["output_tokens"] == 32, res
+        assert res["client_procs"] == 4
+    finally:
+        req_q.put(("stop",))
+        core.join(30)
+        for q in out_qs:
+            q.put(None)
+        for p in apis:
+            p.terminate()
+            p.join(10)
