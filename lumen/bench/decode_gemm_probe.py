@@ -6,7 +6,7 @@ and every (BN, split-K) plan of ``kernels/decode_gemm.hip`` for the batch's bloc
 weights rotate over copies totalling > 512 MB, so each launch reads W from HBM as in a decode
 step (13 GB of weights per step; a repeated 100 MB matrix would be served by the 256 MB Infinity
 Cache).  Writes the plans that beat the library by > 3% to ``--plans`` (the serving engine's
-table, configs/decode_gemm_plans.json).
+table, configs/kernels/decode_gemm_plans.json).
 
     python -m lumen.bench.decode_gemm_probe [--ms 64,128,192,256] [--plans out.json]
 """

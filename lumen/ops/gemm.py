@@ -36,7 +36,7 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 # Decode batches 5..256: the decode-batch MFMA GEMM (kernels/decode_gemm.hip) where the measured
-# plan table (configs/decode_gemm_plans.json, written by lumen/bench/decode_gemm_probe.py) has
+# plan table (configs/kernels/decode_gemm_plans.json, written by lumen/bench/decode_gemm_probe.py) has
 # a winning (BM, BN, split-K) for the shape, hipBLASLt with the tuned table otherwise.  (Two
 # earlier hand-written attempts lost, scripts/probes/: 32-row M tiles, and all-M-rows tiles over
 # all of K whose every workgroup pulled the whole x through its CU's load path.)
@@ -81,14 +81,14 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int, nw: 
 
 
 def dg_plans() -> dict:
-    """{(N, K, BM): (BN, S, waves)} from configs/decode_gemm_plans.json (measured wins only)."""
+    """{(N, K, BM): (BN, S, waves)} from configs/kernels/decode_gemm_plans.json (measured wins only)."""
     global _dg_plans
     if _dg_plans is None:
         import json
 
         path = os.environ.get("LUMEN_DGEMM_PLANS", os.path.join(
             os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-            "configs", "decode_gemm_plans.json"))
+            "configs", "kernels", "decode_gemm_plans.json"))
         _dg_plans = {}
         if os.path.exists(path):
             with open(path) as f:

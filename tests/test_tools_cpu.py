@@ -367,3 +367,15 @@ def test_gemm_wave_split_plan():
         assert split_cols(M, N) == 0, (M, N)     # whole waves, >half-full tail, or ragged M
     x, w = torch.randn(8, 16), torch.randn(24, 16)
     assert torch.allclose(mm_nt(x, w), x @ w.t())  # CPU: plain matmul
+
+
+def test_decode_gemm_plan_table_loads():
+    """The shipped decode-GEMM plan table (configs/kernels/, outside the DeepSpeed config glob)
+    parses into (N, K, BM) -> (BN, split-K, waves) entries the serving projections look up."""
+    from lumen.ops import gemm
+
+    gemm._dg_plans = None
+    plans = gemm.dg_plans()
+    assert plans, "configs/kernels/decode_gemm_plans.json missing or empty"
+    for (n, k, bm), (bn, s, nw) in plans.items():
+        assert k % 64 == 0 and bm in gemm.DG_BMS and nw in (4, 8) and 1 <= s <= k // 64
