@@ -182,10 +182,22 @@ def run_load_procs(url: str, num_requests: int, concurrency: int, prompt_len: in
                                               seed, wu, ready, go, out), daemon=True)
         p.start()
         ps.append(p)
-    for _ in range(procs):
-        ready.get(timeout=600)
+    def collect(q, n, limit):
+        got, t0 = [], time.time()
+        while len(got) < n:
+            try:
+                got.append(q.get(timeout=1.0))
+            except Exception:  # queue.Empty: fail fast if a worker died instead of waiting
+                dead = [p.exitcode for p in ps if p.exitcode not in (None, 0)]
+                if dead or time.time() - t0 > limit:
+                    for p in ps:
+                        p.kill()
+                    raise RuntimeError(f"load-client worker failed (exit codes {dead})")
+        return got
+
+    collect(ready, procs, 600)
     go.set()
-    parts = [out.get(timeout=3600) for _ in range(procs)]
+    parts = collect(out, procs, 3600)
     for p in ps:
         p.join(30)
     t0 = min(x[1] for x in parts)

@@ -95,6 +95,10 @@ def init(backend: Optional[str] = None, device: Optional[str] = None,
         if backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
+        if backend == "nccl":
+            # the host-side gloo group, created here where every rank is at the same point
+            # (new_group is collective): later first uses cannot be reached in different orders
+            host_group()
     _ENV = DistEnv(rank, world, local, local_world, backend if world > 1 else "none", dev)
     return _ENV
 
@@ -128,8 +132,8 @@ _HOST_GROUP = None
 def host_group():
     """A gloo group over every rank for host-side agreements (values the host already holds,
     e.g. a per-step scheduling decision): no device work, no stream sync.  On a gloo world this
-    is the default group (None).  Created on first use -- every rank must reach the first call
-    at the same point of its program (``new_group`` is collective)."""
+    is the default group (None).  ``init`` creates it right after the process group (every rank
+    at the same point: ``new_group`` is collective)."""
     global _HOST_GROUP
     if not dist.is_initialized() or dist.get_backend() == "gloo":
         return None
