@@ -704,3 +704,26 @@ def test_multiple_api_processes_share_one_engine_core(model):
         for p in apis:
             p.terminate()
             p.join(10)
+
+
+def test_step_trace_groups_steps_by_composition(model, monkeypatch):
+    """serve_bench --trace-steps: every step timed and grouped as prefill-only / decode-only /
+    mixed with its token counts; prefill_first never produces mixed steps."""
+    from lumen.bench.serve_bench import _trace_steps
+
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    out = {}
+    for pol in ("chunked", "prefill_first"):
+        eng = _engine(model, num_blocks=256, max_num_batched_tokens=48, scheduling_policy=pol,
+                      async_scheduling=False)
+        for i in range(6):
+            eng.add_request(list(range(3, 30 + i)), SamplingParams(max_tokens=5, temperature=0.0,
+                                                                   ignore_eos=True))
+        out[pol] = _trace_steps(eng)
+        assert eng.blocks.num_free == eng.blocks.num_blocks
+    for tr in out.values():
+        # 6 prompts of 27..32 tokens = 177 prefill tokens; 6 x 4 decode rows after the first token
+        # (the trace rounds its means to 0.1)
+        assert abs(sum(g["prefill_tokens_mean"] * g["steps"] for g in tr.values()) - 177) < 0.5
+        assert abs(sum(g["decode_rows_mean"] * g["steps"] for g in tr.values()) - 24) < 0.5
+    assert "mixed" in out["chunked"] and "mixed" not in out["prefill_first"]
