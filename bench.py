@@ -115,6 +115,50 @@ def run_serve_bench(args) -> dict:
     return h_out, e_out, c_out
 
 
+def run_serve_tp(args, env) -> dict:
+    """TP = world serving after the training sections (N > 1): Llama-2-7B sharded over the N
+    GPUs -- heads / FFN columns / vocab split, row-parallel sums on the custom IPC all-reduce
+    (kernels/custom_ar.hip) over xGMI, decode buckets as hipGraphs, each step's host header over
+    a gloo group and its payload as one RCCL broadcast (lumen/serve/tp.py).  Rank 0 drives the
+    engine through the same 256-request burst as the TP = 1 section (engine mode, vLLM 0.6.0
+    scheduling); the other ranks run the worker loop.  Returns rank 0's record (None elsewhere)."""
+    import gc
+    import types
+
+    import torch
+
+    gc.collect()
+    torch.cuda.empty_cache()
+    from lumen.bench.serve_bench import bench_engine, make_engine
+    from lumen.serve.tp import worker_loop
+
+    a = types.SimpleNamespace(
+        model=args.serve_model or args.model, max_model_len=1024, max_num_seqs=256,
+        max_batched_tokens=4096, prefill_boost=1, no_graphs=False, sync_scheduling=False,
+        kv_cache_dtype="auto", scheduling_policy="prefill_first", tp=env.world_size,
+        num_requests=256, concurrency=256, prompt_len=512, max_tokens=128, temperature=0.0,
+        request_rate=None)
+    t0 = time.time()
+    eng = make_engine(a)
+    if env.rank != 0:
+        worker_loop(eng.runner)
+        return None
+    try:
+        r = bench_engine(a, eng)
+    finally:
+        eng.shutdown()  # releases the workers' loops
+    keep = ("output_tok_s", "ttft_p50_ms", "ttft_p99_ms", "itl_p50_ms", "itl_p99_ms",
+            "itl_max_ms", "wall_s", "total_tok_s", "output_tokens", "steps", "graphs")
+    out = {k: r[k] for k in keep if k in r}
+    out["bench_s"] = round(time.time() - t0, 1)
+    out["config"] = {"model": a.model, "tp": env.world_size, "requests": a.num_requests,
+                     "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
+                     "scheduling_policy": a.scheduling_policy,
+                     "max_num_batched_tokens": a.max_batched_tokens, "kv_cache_dtype": "bf16",
+                     "custom_allreduce": eng.runner.car is not None, "mode": "in-process engine"}
+    return out
+
+
 def run_partitioned(args, env, ds_base, batches, schedule: str, max_live: float,
                     steps: int = 5, warmup: int = 2) -> dict:
     """Extra timed steps of a PARTITIONED ZeRO-3 schedule on a fresh model + engine (after the
@@ -263,6 +307,13 @@ def main():
                          "schedule (release = the reference live budget 1e9 [configs/"
                          "ds_config_zero3.json]; hybrid = half the model resident) -> "
                          "extra.zero3_<schedule>; '' = none")
+    ap.add_argument("--serve_tp", type=int, default=1,
+                    help="at N > 1 on GPUs (1 = default): after the training sections, Llama-2-7B "
+                         "served with TP = N (custom all-reduce over xGMI, 256 x 512 / 128, "
+                         "engine mode) -> extra.serve_tp; 0 = skip")
+    ap.add_argument("--serve_tp_deadline", type=float, default=420.0,
+                    help="seconds the TP serving section may take: past it rank 0 prints the "
+                         "JSON line with extra.serve_tp = an error, and every rank exits")
     ap.add_argument("--partitioned_steps", type=int, default=5,
                     help="timed steps of each partitioned run (2 untimed warm-up steps first)")
     args = ap.parse_args()
@@ -462,6 +513,7 @@ def main():
         # training region: the training model and engine are freed first
         del batches
         serve, serve_engine, serve_chunked = run_serve_bench(args)
+    out = None
     if env.is_main:
         from lumen.train.trainer import model_flops_per_token
 
@@ -517,7 +569,38 @@ def main():
                 "serve_chunked": serve_chunked,
             },
         }
+    if args.serve_tp and world > 1 and on_gpu:
+        # TP = N serving over the N GPUs.  A hung collective must not cost the training record:
+        # past the deadline rank 0 prints the JSON line with the error and every rank exits
+        import threading
+
+        if engine is not None:
+            engine.close()
+            engine = None
+
+        def _deadline():
+            if out is not None:
+                out["extra"]["serve_tp"] = {"error": f"timed out after {args.serve_tp_deadline} s"}
+                print(json.dumps(out), file=json_out, flush=True)
+            os._exit(0)
+
+        timer = threading.Timer(args.serve_tp_deadline + (0 if env.is_main else 15), _deadline)
+        timer.daemon = True
+        timer.start()
+        try:
+            stp = run_serve_tp(args, env)
+        except Exception as e:  # noqa: BLE001 - keep the training record
+            stp = {"error": repr(e)[:500]}
+        timer.cancel()
+        if out is not None:
+            out["extra"]["serve_tp"] = stp
+    if out is not None:
         print(json.dumps(out), file=json_out, flush=True)
+        stp = out["extra"].get("serve_tp")
+        if isinstance(stp, dict) and "error" in stp and world > 1:
+            # the TP section failed on this rank: peers may sit in one of its collectives, so do
+            # not wait for them at the closing barrier (the record is already out)
+            os._exit(0)
     if engine is not None:
         engine.close()  # drain in-flight (next-step) gathers before teardown
     if dist.is_initialized():
