@@ -145,6 +145,14 @@ class LLMEngine:
             raise ValueError(f"kv_cache_dtype must be 'auto' or 'fp8', got {cfg.kv_cache_dtype}")
         self.kv_dtype = torch.float8_e4m3fn if cfg.kv_cache_dtype == "fp8" else dt
         nb = cfg.num_blocks or self._auto_blocks(self.kv_dtype)
+        if self.tp > 1 and dist.is_initialized():
+            # one block count for the whole TP group: rank 0 schedules block ids that every
+            # worker's cache must hold (free memory, hence the auto count, can differ per rank)
+            from ..parallel.dist import host_group
+
+            t = torch.tensor([nb], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group())
+            nb = int(t.item())
         self.blocks = BlockManager(nb, cfg.block_size)
         car = None
         if self.tp > 1 and dev.type == "cuda":
