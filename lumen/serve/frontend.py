@@ -11,7 +11,8 @@ loop free of HTTP work, as vLLM's engine-core process does.
 Several API processes (``--api-server-count``, as in later vLLM releases) may share one
 engine core: each listens on the same port (SO_REUSEPORT: the kernel spreads the connections),
 all of them put requests on the one request queue, and each has its own output queue -- the core
-routes every request's tokens to the front-end that submitted it.  At 256 concurrent streams one
+routes every request's tokens to the front-end that submitted it (each process's ``/metrics``
+counts the requests it served; the engine-state gauges are the core's).  At 256 concurrent streams one
 Python front-end is CPU-bound (request intake + ~13k SSE events/s), and its lag reads as
 inter-token latency at the client.
 
@@ -58,7 +59,7 @@ def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
             kind = op[0]
             if kind == "add":
                 _, rid, ids, pdict, arrival, lora = op[:6]
-                o = op[6] if len(op) > 6 else 0
+                o = op[6] if len(op) > 6 and 0 <= op[6] < len(outs) else 0
                 try:
                     seq = engine.add_request(ids, SamplingParams(**pdict), rid, lora)
                     seq.arrival = arrival
