@@ -727,3 +727,18 @@ def test_step_trace_groups_steps_by_composition(model, monkeypatch):
         assert abs(sum(g["prefill_tokens_mean"] * g["steps"] for g in tr.values()) - 177) < 0.5
         assert abs(sum(g["decode_rows_mean"] * g["steps"] for g in tr.values()) - 24) < 0.5
     assert "mixed" in out["chunked"] and "mixed" not in out["prefill_first"]
+
+
+def test_prefill_first_preemption_is_transparent(model):
+    """prefill_first with too few KV blocks for every running stream: decodes preempt
+    (recompute) and the greedy outputs still equal full-recompute decoding."""
+    eng = _engine(model, num_blocks=14, scheduling_policy="prefill_first",
+                  max_num_batched_tokens=64)
+    eng.blocks.watermark_blocks = 0
+    params = SamplingParams(max_tokens=20, temperature=0.0, ignore_eos=True)
+    prompts = [[3, 4, 5, 6], [9, 10, 11, 12], [20, 21, 22, 23]]
+    seqs = eng.generate(prompts, params)
+    assert eng.scheduler.num_preemptions > 0
+    for p, s in zip(prompts, seqs):
+        assert s.output_ids == naive_greedy(model, p, 20)
+    assert eng.blocks.num_free == eng.blocks.num_blocks
