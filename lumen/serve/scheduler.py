@@ -77,7 +77,11 @@ class Batch:
 
 
 class Scheduler:
+    POLICIES = ("chunked", "prefill_first")
+
     def __init__(self, cfg: SchedulerConfig, blocks: BlockManager):
+        if cfg.policy not in self.POLICIES:
+            raise ValueError(f"scheduling policy must be one of {self.POLICIES}, got {cfg.policy!r}")
         self.cfg = cfg
         self.blocks = blocks
         self.waiting: Deque[Sequence] = deque()

@@ -742,3 +742,8 @@ def test_prefill_first_preemption_is_transparent(model):
     for p, s in zip(prompts, seqs):
         assert s.output_ids == naive_greedy(model, p, 20)
     assert eng.blocks.num_free == eng.blocks.num_blocks
+
+
+def test_unknown_scheduling_policy_rejected(model):
+    with pytest.raises(ValueError):
+        _engine(model, num_blocks=64, scheduling_policy="fifo")
