@@ -569,19 +569,30 @@ def main():
                 "serve_chunked": serve_chunked,
             },
         }
+    import threading
+
+    timer = None
+    printed = [False]
+    print_lock = threading.Lock()
+
+    def _print_once():
+        with print_lock:
+            if out is not None and not printed[0]:
+                print(json.dumps(out), file=json_out, flush=True)
+                printed[0] = True
+
     if args.serve_tp and world > 1 and on_gpu:
         # TP = N serving over the N GPUs.  A hung collective must not cost the training record:
-        # past the deadline rank 0 prints the JSON line with the error and every rank exits
-        import threading
-
+        # past the deadline (TP section + closing barrier) rank 0 prints the JSON line with the
+        # error (unless it already did) and every rank exits
         if engine is not None:
             engine.close()
             engine = None
 
         def _deadline():
-            if out is not None:
+            if out is not None and not printed[0]:
                 out["extra"]["serve_tp"] = {"error": f"timed out after {args.serve_tp_deadline} s"}
-                print(json.dumps(out), file=json_out, flush=True)
+            _print_once()
             os._exit(0)
 
         timer = threading.Timer(args.serve_tp_deadline + (0 if env.is_main else 15), _deadline)
@@ -591,16 +602,9 @@ def main():
             stp = run_serve_tp(args, env)
         except Exception as e:  # noqa: BLE001 - keep the training record
             stp = {"error": repr(e)[:500]}
-        timer.cancel()
         if out is not None:
             out["extra"]["serve_tp"] = stp
-    if out is not None:
-        print(json.dumps(out), file=json_out, flush=True)
-        stp = out["extra"].get("serve_tp")
-        if isinstance(stp, dict) and "error" in stp and world > 1:
-            # the TP section failed on this rank: peers may sit in one of its collectives, so do
-            # not wait for them at the closing barrier (the record is already out)
-            os._exit(0)
+    _print_once()
     if engine is not None:
         engine.close()  # drain in-flight (next-step) gathers before teardown
     if dist.is_initialized():
@@ -608,6 +612,8 @@ def main():
 
         barrier()
         dist.destroy_process_group()
+    if timer is not None:
+        timer.cancel()
 
 
 if __name__ == "__main__":
