@@ -128,15 +128,17 @@ def run_serve_tp(args, env) -> dict:
     import torch
 
     gc.collect()
-    torch.cuda.empty_cache()
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
     from lumen.bench.serve_bench import bench_engine, make_engine
     from lumen.serve.tp import worker_loop
 
+    nreq, plen, mtok = (int(x) for x in args.serve_tp_shape.split(","))
     a = types.SimpleNamespace(
         model=args.serve_model or args.model, max_model_len=1024, max_num_seqs=256,
         max_batched_tokens=4096, prefill_boost=1, no_graphs=False, sync_scheduling=False,
         kv_cache_dtype="auto", scheduling_policy="prefill_first", tp=env.world_size,
-        num_requests=256, concurrency=256, prompt_len=512, max_tokens=128, temperature=0.0,
+        num_requests=nreq, concurrency=nreq, prompt_len=plen, max_tokens=mtok, temperature=0.0,
         request_rate=None)
     t0 = time.time()
     eng = make_engine(a)
@@ -310,7 +312,10 @@ def main():
     ap.add_argument("--serve_tp", type=int, default=1,
                     help="at N > 1 on GPUs (1 = default): after the training sections, Llama-2-7B "
                          "served with TP = N (custom all-reduce over xGMI, 256 x 512 / 128, "
-                         "engine mode) -> extra.serve_tp; 0 = skip")
+                         "engine mode) -> extra.serve_tp; 0 = skip; 2 = also on CPU / gloo "
+                         "(tests)")
+    ap.add_argument("--serve_tp_shape", default="256,512,128",
+                    help="TP serving burst: requests,prompt_len,max_tokens")
     ap.add_argument("--serve_tp_deadline", type=float, default=420.0,
                     help="seconds the TP serving section may take: past it rank 0 prints the "
                          "JSON line with extra.serve_tp = an error, and every rank exits")
@@ -581,7 +586,7 @@ def main():
                 print(json.dumps(out), file=json_out, flush=True)
                 printed[0] = True
 
-    if args.serve_tp and world > 1 and on_gpu:
+    if args.serve_tp and world > 1 and (on_gpu or args.serve_tp == 2):
         # TP = N serving over the N GPUs.  A hung collective must not cost the training record:
         # past the deadline (TP section + closing barrier) rank 0 prints the JSON line with the
         # error (unless it already did) and every rank exits
@@ -610,8 +615,14 @@ def main():
     if dist.is_initialized():
         from lumen.parallel.dist import barrier
 
-        barrier()
-        dist.destroy_process_group()
+        try:
+            barrier()
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            if timer is not None:
+                # a peer gave up on the TP section (its deadline); rank 0's record is out
+                os._exit(0)
+            raise
     if timer is not None:
         timer.cancel()
 

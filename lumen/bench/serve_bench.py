@@ -59,7 +59,8 @@ def _warm(eng, a, rng):
             for _ in range(min(a.num_requests, a.max_num_seqs))]
     while any(not s.finished for s in warm):
         eng.step()
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
 
 
 def bench_engine(a, eng=None) -> dict:
@@ -95,7 +96,8 @@ def bench_engine(a, eng=None) -> dict:
         else:
             while eng.has_work:
                 eng.step()
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
     out_toks = sum(len(s.output_ids) for s in seqs)
     ttft = [s.first_token_time - s.arrival for s in seqs]

@@ -379,3 +379,35 @@ def test_decode_gemm_plan_table_loads():
     assert plans, "configs/kernels/decode_gemm_plans.json missing or empty"
     for (n, k, bm), (bn, s, nw) in plans.items():
         assert k % 64 == 0 and bm in gemm.DG_BMS and nw in (4, 8) and 1 <= s <= k // 64
+
+
+@pytest.mark.parametrize("deadline", [300.0, 0.01])
+def test_bench_tp_serving_section_and_deadline(deadline):
+    """bench.py's TP = N serving section (forced on gloo with --serve_tp 2, tiny model, 8
+    requests): with time to finish, rank 0's single JSON line carries extra.serve_tp from the
+    TP = 2 engine; with a deadline the section cannot meet, the line still comes out, once,
+    with extra.serve_tp = the timeout, and every rank exits 0."""
+    import json
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                          str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--steps", "1", "--warmup", "1", "--model", "tiny-llama-gqa",
+                          "--seq_len", "32", "--micro_batch", "2", "--partitioned", "",
+                          "--serve_tp", "2", "--serve_tp_shape", "8,24,6",
+                          "--serve_tp_deadline", str(deadline)],
+                         capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    stp = json.loads(lines[0])["extra"]["serve_tp"]
+    if deadline > 100:
+        assert stp["output_tokens"] == 8 * 6 and stp["config"]["tp"] == 2, stp
+    else:
+        assert "timed out" in stp["error"], stp
