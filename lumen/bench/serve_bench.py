@@ -40,7 +40,8 @@ def make_engine(a):
                        async_scheduling=not a.sync_scheduling, kv_cache_dtype=a.kv_cache_dtype,
                        tp_size=getattr(a, "tp", 1),
                        scheduling_policy=getattr(a, "scheduling_policy", "chunked"),
-                       num_blocks=getattr(a, "num_blocks", None))
+                       num_blocks=getattr(a, "num_blocks", None),
+                       enable_prefix_caching=getattr(a, "enable_prefix_caching", False))
     t0 = time.time()
     eng = LLMEngine(cfg)
     eng._bench_setup_s = time.time() - t0
@@ -74,7 +75,10 @@ def bench_engine(a, eng=None) -> dict:
     mk = lambda n: [rng.randrange(3, V) for _ in range(n)]  # noqa: E731
     _warm(eng, a, rng)
     params = dict(max_tokens=a.max_tokens, temperature=a.temperature, ignore_eos=True)
-    prompts = [mk(a.prompt_len) for _ in range(a.num_requests)]
+    # --shared-prefix N: every prompt starts with the same N tokens (a shared system prompt)
+    shared = mk(min(getattr(a, "shared_prefix", 0), a.prompt_len))
+    prompts = [shared + mk(a.prompt_len - len(shared)) for _ in range(a.num_requests)]
+    hit0, q0, pf0 = eng.blocks.hit_tokens, eng.blocks.query_tokens, eng.stats["prefill_tokens"]
     seqs = []
     t_start = time.perf_counter()
     if a.request_rate:
@@ -118,7 +122,11 @@ def bench_engine(a, eng=None) -> dict:
             "max_batched_tokens": a.max_batched_tokens, "steps": eng.stats["steps"],
             "async_scheduling": eng.async_sched, "kv_cache_dtype": a.kv_cache_dtype,
             "setup_s": round(getattr(eng, "_bench_setup_s", 0.0), 1),
-            "graphs": sorted(eng.runner._graphs)}
+            "graphs": sorted(eng.runner._graphs),
+            "shared_prefix": len(shared), "prefix_caching": eng.blocks.prefix_caching,
+            "prefix_hit_rate": round((eng.blocks.hit_tokens - hit0)
+                                     / max(1, eng.blocks.query_tokens - q0), 4),
+            "prefill_tokens_computed": eng.stats["prefill_tokens"] - pf0}
 
 
 def _trace_steps(eng) -> dict:
@@ -260,6 +268,9 @@ def main():
                          "runs the bench, the other ranks the worker loop")
     ap.add_argument("--num-blocks", type=int, default=None, help="KV blocks (default: auto)")
     ap.add_argument("--scheduling-policy", default="chunked", choices=["chunked", "prefill_first"])
+    ap.add_argument("--enable-prefix-caching", action="store_true")
+    ap.add_argument("--shared-prefix", type=int, default=0,
+                    help="engine mode: the first N prompt tokens are the same in every request")
     ap.add_argument("--api-servers", type=int, default=1,
                     help="http mode: OpenAI API processes sharing the port (SO_REUSEPORT)")
     ap.add_argument("--client-procs", type=int, default=1,

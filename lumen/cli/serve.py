@@ -56,6 +56,9 @@ def build_parser():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
                     help="KV-cache element type (fp8 = e4m3: 2x capacity, half the decode K/V reads)")
+    ap.add_argument("--enable-prefix-caching", action="store_true",
+                    help="share the cached K/V of equal leading prompt blocks across requests "
+                         "(vLLM's flag; finished requests' blocks stay cached until evicted)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--api-server-count", type=int, default=1,
                     help="OpenAI API processes sharing --port (SO_REUSEPORT), each streaming its "
@@ -100,6 +103,7 @@ def main(argv=None):
                        prefill_boost=a.prefill_boost, tp_size=a.tp, seed=a.seed, use_graphs=not a.no_graphs,
                        scheduling_policy=policy,
                        kv_cache_dtype=a.kv_cache_dtype,
+                       enable_prefix_caching=a.enable_prefix_caching,
                        lora_modules=dict(m.split("=", 1) for m in a.lora_modules)
                        if a.lora_modules else None, max_loras=a.max_loras)
     eng = LLMEngine(cfg)

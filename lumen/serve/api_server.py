@@ -256,6 +256,8 @@ def create_app(aengine, served_model_name: Optional[str] = None):
             "# TYPE lumen_waiting_requests gauge", f"lumen_waiting_requests {live['waiting']}",
             "# TYPE lumen_preemptions_total counter",
             f"lumen_preemptions_total {live['preemptions']}",
+            "# TYPE lumen_prefix_cache_hit_ratio gauge",
+            f"lumen_prefix_cache_hit_ratio {live.get('prefix_hit_rate', 0.0):.4f}",
         ]
         return PlainTextResponse("\n".join(lines) + "\n")
 

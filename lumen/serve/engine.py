@@ -65,6 +65,9 @@ class EngineConfig:
     # KV-cache element type: "auto" = model dtype; "fp8" = e4m3 (vLLM --kv-cache-dtype fp8):
     # twice the cache capacity and half the K/V bytes per decode step, at fp8 K/V precision
     kv_cache_dtype: str = "auto"
+    # automatic prefix caching (vLLM --enable-prefix-caching): prompts share the cached K/V of
+    # equal leading full blocks; finished sequences' blocks stay cached until evicted
+    enable_prefix_caching: bool = False
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -153,7 +156,7 @@ class LLMEngine:
             t = torch.tensor([nb], dtype=torch.int64)
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group())
             nb = int(t.item())
-        self.blocks = BlockManager(nb, cfg.block_size)
+        self.blocks = BlockManager(nb, cfg.block_size, prefix_caching=cfg.enable_prefix_caching)
         car = None
         if self.tp > 1 and dev.type == "cuda":
             # TP decode: row-parallel sums on the custom IPC all-reduce, which also lets the
@@ -463,6 +466,7 @@ class LLMEngine:
             if ev is not None:
                 ev.record()
             rec.update(toks=t, th=th, lh=lh, ev=ev, sampled=sampled)
+        self.scheduler.launched(batch)
         for s, c in batch.prefills:
             s.num_cached += c
         for s in batch.decodes:
@@ -527,6 +531,7 @@ class LLMEngine:
             toks = t.tolist()
             lps = lp.tolist() if lp is not None else [None] * len(toks)
         self.runner.check_collectives()  # a timed-out TP reduction never returns its tokens
+        self.scheduler.launched(batch)
         for s, c in batch.prefills:
             s.num_cached += c
         for s in batch.decodes:
@@ -613,7 +618,8 @@ class AsyncEngine:
     def live_stats(self) -> dict:
         sch = self.engine.scheduler
         return {"kv_usage": self.engine.blocks.usage(), "running": len(sch.running),
-                "waiting": len(sch.waiting), "preemptions": sch.num_preemptions}
+                "waiting": len(sch.waiting), "preemptions": sch.num_preemptions,
+                "prefix_hit_rate": self.engine.blocks.hit_rate}
 
     def _push(self, rid, item):
         st = self._streams.get(rid)

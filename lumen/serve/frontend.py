@@ -103,7 +103,8 @@ def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
         if updates:
             sch = engine.scheduler
             stats = {"kv_usage": engine.blocks.usage(), "running": len(sch.running),
-                     "waiting": len(sch.waiting), "preemptions": sch.num_preemptions}
+                     "waiting": len(sch.waiting), "preemptions": sch.num_preemptions,
+                     "prefix_hit_rate": engine.blocks.hit_rate}
             for o, ups in updates.items():
                 outs[o].put(("step", ups, stats))
 

@@ -23,6 +23,9 @@ budget is chunked); otherwise it is a decode step of every running sequence.  Pr
 sooner (higher throughput, lower TTFT under a burst) at the cost of a long pause in the running
 streams while a burst is prefilled (its inter-token-latency maximum).
 
+With prefix caching on (block_manager.py), admission shares the prompt's leading full blocks
+that are already cached and only the rest of the prompt is prefilled.
+
 KV blocks for a whole prompt are reserved when the request is admitted, so a chunked prefill
 never runs out of blocks halfway; decodes grow their tables a block at a time, and when none is
 left the youngest running sequence is preempted (blocks freed, requeued at the front, its prompt
@@ -121,12 +124,13 @@ class Scheduler:
             if not self.blocks.can_allocate(s.length + 1):
                 break
             self.waiting.popleft()
-            self.blocks.allocate(s.seq_id, s.length + 1)
-            s.num_cached = 0
+            # prefix caching: the leading full blocks already in the cache are shared and only
+            # the rest of the prompt is computed (0 without it)
+            s.num_cached = self.blocks.allocate(s.seq_id, s.length + 1, s.all_ids, s.lora_slot)
             s.prefilled = False
             s.status = Status.RUNNING
             self.running.append(s)
-            c = min(s.length, budget)
+            c = min(s.length - s.num_cached, budget)
             batch.prefills.append((s, c))
             budget -= c
         return budget
@@ -172,9 +176,22 @@ class Scheduler:
             batch.kind = "decode"
         return batch
 
+    def launched(self, batch: Batch) -> None:
+        """The engine launched ``batch`` (before it advances ``num_cached``): with prefix
+        caching, the full prompt blocks its prefill chunks write become shareable."""
+        if self.blocks.prefix_caching:
+            for s, c in batch.prefills:
+                self.blocks.publish(s.seq_id, s.all_ids, s.num_cached + c, s.lora_slot)
+
+    def _release(self, s: Sequence) -> None:
+        """Free a retired / preempted sequence's blocks; with prefix caching its full blocks
+        whose K/V launched steps wrote stay cached (a recomputed or follow-up prompt hits them)."""
+        self.blocks.free_seq(s.seq_id, s.all_ids, min(s.num_cached, len(s.all_ids)),
+                             s.lora_slot)
+
     def _preempt(self, s: Sequence) -> None:
         self.running.remove(s)
-        self.blocks.free_seq(s.seq_id)
+        self._release(s)
         s.status = Status.WAITING
         s.num_cached = 0
         s.prefilled = False
@@ -195,5 +212,5 @@ class Scheduler:
             ids = {s.seq_id for s in done}
             self.running = [s for s in self.running if s.seq_id not in ids]
             for s in done:
-                self.blocks.free_seq(s.seq_id)
+                self._release(s)
         return done

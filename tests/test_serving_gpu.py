@@ -111,3 +111,34 @@ def test_multi_lora_graph_decode_matches_merged(tmp_path):
         ref = full[len(p) - 1:].argmax(-1).tolist()
         agree = sum(int(a == b) for a, b in zip(ref, s.output_ids)) / len(ref)
         assert agree >= 0.85, (i, agree)
+
+
+def test_prefix_caching_matches_full_forward():
+    """Prompts sharing a 48-token prefix (3 blocks) on the HIP paged-prefill path: the later
+    ones read the first one's cached K/V (published at its launch) and still agree with the
+    full forward, teacher-forced."""
+    from lumen.models import build_model
+    from lumen.serve.engine import EngineConfig, LLMEngine
+    from lumen.serve.sequence import SamplingParams
+
+    dev = torch.device("cuda", 0)
+    m = build_model("tiny-llama-gqa", dtype=torch.bfloat16, device=dev, init="random", seed=3)
+    m.eval()
+    eng = LLMEngine(EngineConfig(model="tiny-llama-gqa", device="cuda", max_model_len=512,
+                                 block_size=16, num_blocks=128, use_graphs=True,
+                                 scheduling_policy="prefill_first", max_num_batched_tokens=52,
+                                 enable_prefix_caching=True), model=m)  # one prompt per step
+    shared = [(7 * i + 3) % 500 for i in range(48)]
+    prompts = [shared + [60 + i, 61, 62, 63 + i] for i in range(4)]
+    seqs = [eng.add_request(p, SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True))
+            for p in prompts]
+    while eng.has_work:
+        eng.step()
+    assert eng.blocks.hit_tokens == 3 * 48
+    for p, s in zip(prompts, seqs):
+        ids = torch.tensor([p + s.output_ids[:-1]], device=dev)
+        with torch.no_grad():
+            full = m(ids).float().view(ids.shape[1], -1)
+        ref = full[len(p) - 1:].argmax(-1).tolist()
+        agree = sum(int(a == b) for a, b in zip(ref, s.output_ids)) / len(ref)
+        assert agree >= 0.9, agree
