@@ -119,10 +119,13 @@ class Scheduler:
                 c = min(s.length - s.num_cached, budget)
                 batch.prefills.append((s, c))
                 budget -= c
+        whole = self.cfg.policy == "prefill_first"
         while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
             s = self.waiting[0]
             if not self.blocks.can_allocate(s.length + 1):
                 break
+            if whole and batch.prefills and not self._fits(s, budget):
+                break   # vLLM 0.6 (no chunked prefill): whole prompts only, FCFS
             self.waiting.popleft()
             # prefix caching: the leading full blocks already in the cache are shared and only
             # the rest of the prompt is computed (0 without it)
@@ -134,6 +137,22 @@ class Scheduler:
             batch.prefills.append((s, c))
             budget -= c
         return budget
+
+    def _fits(self, s: Sequence, budget: int) -> bool:
+        """Would ``s``'s whole uncached prompt fit ``budget``?  (Prefix-cache hits are counted
+        only by looking the blocks up; the allocation itself happens at admission.)"""
+        if s.length <= budget:
+            return True
+        bm = self.blocks
+        if not bm.prefix_caching:
+            return False
+        ids = s.all_ids
+        hit = 0
+        for d in bm._digests(ids, (len(ids) - 1) // bm.block_size, s.lora_slot):
+            if d not in bm.cached:
+                break
+            hit += bm.block_size
+        return s.length - hit <= budget
 
     def schedule(self) -> Optional[Batch]:
         budget = self.cfg.max_num_batched_tokens

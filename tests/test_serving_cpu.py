@@ -336,8 +336,8 @@ def test_chunked_prefill_and_mixed_steps_match_naive(model):
 @pytest.mark.parametrize("async_sched", [False, True])
 def test_prefill_first_policy_matches_naive(model, async_sched):
     """vLLM 0.6.0's default scheduling (scheduling_policy="prefill_first"): while prompts wait,
-    steps are prefill-only (no decode rows ride along; a prompt longer than the budget is still
-    chunked); then decode-only steps.  Greedy outputs == full-recompute decoding, with requests
+    steps are prefill-only (whole prompts, FCFS; no decode rows ride along; only a prompt longer
+    than the budget is chunked); then decode-only steps.  Greedy outputs == full-recompute decoding, with requests
     arriving mid-flight too."""
     eng = _engine(model, num_blocks=256, max_num_batched_tokens=40,
                   scheduling_policy="prefill_first", async_scheduling=async_sched)
@@ -366,7 +366,8 @@ def test_prefill_first_policy_matches_naive(model, async_sched):
     for p, s in zip(prompts + late, seqs):
         assert s.output_ids == naive_greedy(model, p, 8), p
     assert all(not (p and d) for p, d in kinds)          # never mixed
-    assert kinds[0] == (2, 0) and kinds[1][0] > 0        # prompts first (37 + 4 > 40: two steps)
+    # whole prompts, FCFS (37 + 4 > 40: the 4-token prompt waits for the next step, 4 + 30 + 2)
+    assert kinds[0] == (1, 0) and kinds[1] == (3, 0)
     assert sum(1 for p, d in kinds if p) >= 4            # the late 50-token prompt chunked
     assert eng.blocks.num_free == eng.blocks.num_blocks
 
