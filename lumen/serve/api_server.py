@@ -80,10 +80,64 @@ def _params(body: Dict[str, Any], eos: Optional[int]) -> SamplingParams:
                           temperature=float(body.get("temperature", 1.0)),
                           top_p=float(body.get("top_p", 1.0)), top_k=int(body.get("top_k", 0) or 0),
                           stop_token_ids=list(stop_ids), ignore_eos=bool(body.get("ignore_eos", False)),
-                          seed=body.get("seed"), logprobs=bool(body.get("logprobs", False)),
+                          seed=body.get("seed"),
                           presence_penalty=float(body.get("presence_penalty") or 0.0),
                           frequency_penalty=float(body.get("frequency_penalty") or 0.0),
                           repetition_penalty=float(body.get("repetition_penalty") or 1.0))
+
+
+def _logprob_request(body: Dict[str, Any], chat: bool, params: SamplingParams) -> bool:
+    """OpenAI logprobs fields onto ``params``; returns whether the response carries logprobs.
+    Completions: ``logprobs: k`` (the chosen token + the k most likely, 0 <= k <= 20) and
+    ``echo`` (the prompt is scored too).  Chat: ``logprobs: true`` + ``top_logprobs: k``."""
+    if chat:
+        if not body.get("logprobs"):
+            return False
+        k = int(body.get("top_logprobs") or 0)
+    else:
+        lp = body.get("logprobs")
+        if lp is None or lp is False:
+            return False
+        k = int(lp)
+        if body.get("echo"):
+            params.prompt_logprobs = k
+    if not 0 <= k <= 20:
+        raise ValueError("top logprobs must be in [0, 20]")
+    params.logprobs = True
+    params.top_logprobs = k
+    return True
+
+
+def completion_logprobs(decode, ids: List[int], lps: List[Optional[float]],
+                        tops: List[Optional[list]], offset: int = 0) -> Dict[str, Any]:
+    """OpenAI completions ``logprobs`` object: tokens, token_logprobs, top_logprobs (the
+    alternatives plus the chosen token, None where a token has no score: the first prompt
+    token) and text_offset (character offsets from ``offset``)."""
+    toks = [decode([t]) for t in ids]
+    top_out, offs = [], []
+    for i, (t, lp, alt) in enumerate(zip(toks, lps, tops)):
+        if lp is None:
+            top_out.append(None)
+        else:
+            # token strings can collide (byte-fallback pieces): a key keeps its best score
+            d: Dict[str, float] = {}
+            for a, v in list(alt or []) + [(None, lp)]:
+                key = t if a is None else decode([a])
+                d[key] = max(d.get(key, v), v)
+            top_out.append(d)
+        offs.append(offset)
+        offset += len(t)
+    return {"tokens": toks, "token_logprobs": list(lps), "top_logprobs": top_out,
+            "text_offset": offs}
+
+
+def chat_logprobs(decode, ids: List[int], lps: List[float], tops: List[Optional[list]]):
+    """OpenAI chat ``logprobs`` object: {"content": [{token, logprob, bytes, top_logprobs}]}."""
+    def ent(t, lp):
+        s = decode([t])
+        return {"token": s, "logprob": lp, "bytes": list(s.encode("utf-8"))}
+    return {"content": [dict(ent(t, lp), top_logprobs=[ent(a, v) for a, v in (alt or [])])
+                        for t, lp, alt in zip(ids, lps, tops)]}
 
 
 def _stops(body: Dict[str, Any]) -> List[str]:
@@ -178,14 +232,16 @@ class IncrementalDetokenizer:
 
 
 def stream_chunk(rid: str, chat: bool, created: int, model: str, delta_text: str,
-                 finish: Optional[str], index: int = 0) -> Dict[str, Any]:
+                 finish: Optional[str], index: int = 0, logprobs=None) -> Dict[str, Any]:
     """One OpenAI streaming chunk (``chat.completion.chunk`` / ``text_completion``)."""
     if chat:
         d = {"content": delta_text} if delta_text else {}
         ch = {"index": index, "delta": d, "finish_reason": finish}
+        if logprobs is not None:
+            ch["logprobs"] = logprobs
         o = "chat.completion.chunk"
     else:
-        ch = {"index": index, "text": delta_text, "logprobs": None, "finish_reason": finish}
+        ch = {"index": index, "text": delta_text, "logprobs": logprobs, "finish_reason": finish}
         o = "text_completion"
     return {"id": rid, "object": o, "created": created, "model": model, "choices": [ch]}
 
@@ -300,12 +356,39 @@ def create_app(aengine, served_model_name: Optional[str] = None):
         created = int(time.time())
         stats.requests += 1
         obj = "chat.completion" if chat else "text_completion"
+        echo = not chat and bool(body.get("echo", False))
+        score_only = echo and body.get("max_tokens") == 0   # score the prompt, generate nothing
         try:
             stops = _stops(body)
             n, best_of = _n_best_of(body, stream)
+            want_lp = _logprob_request(body, chat, params)
+            if score_only and stream:
+                raise ValueError("echo with max_tokens 0 is not streamed")
         except ValueError as e:
             raise HTTPException(status_code=400, detail=str(e))
+        if score_only:
+            params.max_tokens = 1   # one token is sampled (and dropped): the prompt forward
         include_stop = bool(body.get("include_stop_str_in_output", False))
+        prompt_text = (prompt if isinstance(prompt, str) else decode(list(prompt))) if echo else ""
+
+        def tops_of(seq, a=0):
+            t = getattr(seq, "output_top_logprobs", None) or []
+            n_out = len(seq.output_ids)
+            return t[a:n_out] if len(t) >= n_out else [None] * (n_out - a)
+
+        def lp_object(seq, a, with_prompt, end=None):
+            """logprobs of output tokens a..end (and, for echo, of the prompt first)."""
+            ids, lps, tops = (seq.output_ids[a:end], seq.output_logprobs[a:end],
+                              tops_of(seq, a)[:None if end is None else end - a])
+            if chat:
+                return chat_logprobs(decode, ids, lps, tops)
+            if with_prompt:
+                ps = list(getattr(seq, "prompt_scores", None) or [])
+                ps += [None] * (len(seq.prompt_ids) - len(ps))
+                ids = list(seq.prompt_ids) + list(ids)
+                lps = [None if x is None else x[0] for x in ps] + list(lps)
+                tops = [None if x is None else x[1] for x in ps] + list(tops)
+            return completion_logprobs(decode, ids, lps, tops)
 
         def sub_params(i):
             p = SamplingParams(**vars(params))
@@ -315,8 +398,23 @@ def create_app(aengine, served_model_name: Optional[str] = None):
 
         head = sse_head(rid, chat, created, model)
 
-        def sse(delta_text, finish, index=0):
-            return sse_event(head, chat, delta_text, finish, index)
+        def sse(delta_text, finish, index=0, lpo=None):
+            if lpo is None:
+                return sse_event(head, chat, delta_text, finish, index)
+            return "data: %s\n\n" % json.dumps(stream_chunk(rid, chat, created, model, delta_text,
+                                                            finish, index, lpo))
+
+        def streamed(out, fin, seq, index, st):
+            """One event; ``st`` = [tokens already reported, first event pending]."""
+            lpo = None
+            first = st[1]
+            st[1] = False
+            if first and echo:
+                out = prompt_text + out
+            if want_lp:
+                lpo = lp_object(seq, st[0], first and echo)
+                st[0] = len(seq.output_ids)
+            return sse(out, fin, index, lpo)
 
         if stream and n == 1:
             async def gen1():
@@ -329,9 +427,11 @@ def create_app(aengine, served_model_name: Optional[str] = None):
                                                           "finish_reason": None}]}
                     yield f"data: {json.dumps(first)}\n\n"
                 stop = StopChecker(stops, include_stop)
+                st = [0, True]
                 try:
-                    async for out, fin, _seq in _deltas(prompt, sub_params(0), rid, lora, stop):
-                        yield sse(out, fin)
+                    async for out, fin, seq in _deltas(prompt, sub_params(0), rid, lora, stop):
+                        yield (streamed(out, fin, seq, 0, st) if want_lp or echo
+                               else sse(out, fin))
                 except ValueError as e:
                     stats.errors += 1
                     yield f"data: {json.dumps({'error': {'message': str(e)}})}\n\n"
@@ -343,11 +443,13 @@ def create_app(aengine, served_model_name: Optional[str] = None):
                 q: asyncio.Queue = asyncio.Queue()
 
                 async def run_choice(i):
+                    st = [0, True]
+
                     async def on_delta(text, fin, seq):
                         # one event per engine step that produced tokens, even when the text
                         # delta is still empty (incomplete UTF-8 / held-back stop prefix):
                         # clients see token timing (TTFT, inter-token latency)
-                        await q.put(sse(text, fin, i))
+                        await q.put(streamed(text, fin, seq, i, st))
                     try:
                         await _one(prompt, sub_params(i), f"{rid}-{i}" if n > 1 else rid, lora,
                                    stops, include_stop, on_delta)
@@ -392,16 +494,17 @@ def create_app(aengine, served_model_name: Optional[str] = None):
         choices = []
         n_out = 0
         for i, (text, seq, fin) in enumerate(res):
-            n_out += len(seq.output_ids)
+            n_gen = len(seq.output_ids)
+            if score_only:   # the sampled token is not part of the answer
+                text, fin, n_gen = "", "length", 0
+            n_out += n_gen
+            lp = lp_object(seq, 0, echo, n_gen) if want_lp else None
             if chat:
                 choices.append({"index": i, "message": {"role": "assistant", "content": text},
-                                "finish_reason": fin})
+                                "logprobs": lp, "finish_reason": fin})
             else:
-                lp = None
-                if params.logprobs:
-                    lp = {"tokens": [decode([t]) for t in seq.output_ids],
-                          "token_logprobs": list(seq.output_logprobs)}
-                choices.append({"index": i, "text": text, "logprobs": lp, "finish_reason": fin})
+                choices.append({"index": i, "text": prompt_text + text, "logprobs": lp,
+                                "finish_reason": fin})
         p_tok = len(res[0][1].prompt_ids)
         usage = {"prompt_tokens": p_tok, "completion_tokens": n_out,
                  "total_tokens": p_tok + n_out}

@@ -235,6 +235,8 @@ class LLMEngine:
                              f"{self.cfg.max_model_len}")
         if params.max_tokens > budget:
             params.max_tokens = budget
+        if params.prompt_logprobs is not None and self.tp > 1:
+            raise ValueError("prompt_logprobs is served at tensor-parallel size 1 only")
         seq = Sequence(ids, params, request_id or uuid.uuid4().hex)
         if lora:
             if self.runner.lora is None or lora not in self.lora_names:
@@ -274,6 +276,17 @@ class LLMEngine:
             ptables.append(tbl)
             if use_lora:
                 lora.append(np.full(c, s.lora_slot, dtype=np.int64))
+        # prompt_logprobs: the row at position p scores prompt token p + 1
+        prows: List[int] = []
+        pmeta = []
+        for i, (s, c) in enumerate(batch.prefills):
+            if s.params.prompt_logprobs is None:
+                continue
+            a = s.num_cached
+            hi = min(a + c, len(s.prompt_ids) - 1)
+            if hi > a:
+                pmeta.append((s, a + 1, hi - a, len(prows)))
+                prows.extend(range(cu[i], cu[i] + hi - a))
         Tp = cu[-1]
         N = len(batch.decodes)
         parts = toks + pos + slots
@@ -331,6 +344,8 @@ class LLMEngine:
             extra += [np.fromiter((p.temperature for p in ps), np.float64, R).view(np.int64),
                       np.fromiter((p.top_p for p in ps), np.float64, R).view(np.int64),
                       np.fromiter((p.top_k for p in ps), np.int64, R)]
+        if prows:
+            extra.append(np.asarray(prows, dtype=np.int64))
         if use_lora:
             extra.append(np.concatenate(lora))
         host = np.concatenate([np.concatenate(parts)] + extra)
@@ -363,6 +378,10 @@ class LLMEngine:
             inp.top_ps = dev[o + R:o + 2 * R].view(torch.float64).float()
             inp.top_ks = dev[o + 2 * R:o + 3 * R].int()
             o += 3 * R
+        if prows:
+            inp.extra_rows = dev[o:o + len(prows)]
+            inp.prompt_meta = pmeta
+            o += len(prows)
         if use_lora:
             inp.lora_ids = dev[o:o + T].int()
         return inp
@@ -403,6 +422,11 @@ class LLMEngine:
         batch = self.scheduler.schedule()
         if batch is None:
             return self._resolve()
+        if any(s.params.wants_extras for s in batch.seqs):
+            # logprob alternatives / prompt scores: this step runs resolved (synchronously)
+            done = self._resolve() if self._inflight is not None else []
+            batch = self._drop_finished(batch)
+            return done + (self._run_batch(batch) if batch is not None else [])
         if self._inflight is not None and self._needs_host_tokens(batch):
             done = self._resolve()     # this step reads real token values on the host
             # the resolved tokens may have finished (EOS / stop id / max_tokens) sequences of
@@ -530,20 +554,56 @@ class LLMEngine:
                                        self.step_count, want_logprobs=True)
             toks = t.tolist()
             lps = lp.tolist() if lp is not None else [None] * len(toks)
+        tops = self._extras(inp, logits, sampled)
         self.runner.check_collectives()  # a timed-out TP reduction never returns its tokens
         self.scheduler.launched(batch)
         for s, c in batch.prefills:
             s.num_cached += c
         for s in batch.decodes:
             s.num_cached = s.length
-        for s, t, lp in zip(sampled, toks, lps):
+        for s, t, lp, top in zip(sampled, toks, lps, tops):
             s.prefilled = True
-            s.append(int(t), lp, self.eos_id)
+            s.append(int(t), lp, self.eos_id, top)
         done = self.scheduler.finish(batch)
         self.stats["finished"] += len(done)
         self.stats["steps"] += 1
         self.step_count += 1
         return sampled
+
+    def _extras(self, inp: StepInput, logits: torch.Tensor, sampled: List[Sequence]) -> list:
+        """Host lists of the ``top_logprobs`` alternatives of each sampled row (None where not
+        asked; from the distribution the row was sampled from: logits / temperature, raw when
+        greedy), and the prompt scores of this step's prefill rows (stored on the sequences)."""
+        tops: list = [None] * len(sampled)
+        ks = [s.params.top_logprobs for s in sampled]
+        if any(ks):
+            z = logits.float()
+            t = inp.temps.float()[:, None]
+            z = torch.where(t > 0, z / t.clamp(min=1e-6), z)
+            v, ix = torch.log_softmax(z, -1).topk(max(ks), -1)
+            v, ix = v.tolist(), ix.tolist()
+            tops = [list(zip(ix[i][:k], v[i][:k])) if k else None for i, k in enumerate(ks)]
+        meta = inp.prompt_meta
+        if meta:
+            lp = torch.log_softmax(self.runner.extra_logits.float(), -1)
+            tgt = torch.tensor([t for s, j0, n, _ in meta for t in s.prompt_ids[j0:j0 + n]],
+                               dtype=torch.long, device=lp.device)
+            tl = lp.gather(1, tgt[:, None])[:, 0].tolist()
+            kp = max(s.params.prompt_logprobs for s, *_ in meta)
+            pv = pi = None
+            if kp:
+                pv, pi = lp.topk(kp, -1)
+                pv, pi = pv.tolist(), pi.tolist()
+            for s, j0, n, r0 in meta:
+                if not s.prompt_scores:
+                    s.prompt_scores.append(None)   # the first token has no prefix to score it
+                k = s.params.prompt_logprobs
+                for q in range(n):
+                    if j0 + q != len(s.prompt_scores):
+                        continue                   # scored before (recompute after preemption)
+                    alts = list(zip(pi[r0 + q][:k], pv[r0 + q][:k])) if k else []
+                    s.prompt_scores.append((tl[r0 + q], alts))
+        return tops
 
     def generate(self, prompts: Iterable[Union[str, List[int]]],
                  params: Optional[SamplingParams] = None) -> List[Sequence]:

@@ -19,7 +19,9 @@ inter-token latency at the client.
 Protocol (all plain tuples/lists, pickled by multiprocessing):
   front -> core: ("add", rid, prompt_ids, params_dict, arrival, lora_name|None, front_index)
                  | ("abort", rid) | ("stop",)
-  core -> front: ("step", [(rid, new_ids, new_logprobs, finish_reason|None), ...], stats)
+  core -> front: ("step", [(rid, new_ids, new_logprobs, finish_reason|None[, extras]), ...],
+                  stats)   extras (only for requests asking logprob alternatives / prompt
+                  scores): {"top": new tokens' alternatives, "prompt": prompt scores (once)}
                  ("error", rid, message)
 """
 from __future__ import annotations
@@ -95,7 +97,13 @@ def run_engine_core(engine, req_q, out_q, idle_sleep: float = 0.0005) -> None:
             lps = s.output_logprobs[k:] if s.output_logprobs else []
             sent[rid] = len(s.output_ids)
             fin = s.finish_reason if s.finished else None
-            updates.setdefault(origin[rid], []).append((rid, new, lps, fin))
+            if s.params.wants_extras:
+                ex = {"top": s.output_top_logprobs[k:]}
+                if k == 0 and s.prompt_scores:
+                    ex["prompt"] = s.prompt_scores
+                updates.setdefault(origin[rid], []).append((rid, new, lps, fin, ex))
+            else:
+                updates.setdefault(origin[rid], []).append((rid, new, lps, fin))
             if fin is not None:
                 live.pop(rid, None)
                 sent.pop(rid, None)
@@ -124,6 +132,8 @@ class SeqView:
     token_times: List[float] = dataclasses.field(default_factory=list)
     first_token_time: Optional[float] = None
     finish_reason: Optional[str] = None
+    output_top_logprobs: List[list] = dataclasses.field(default_factory=list)
+    prompt_scores: List[object] = dataclasses.field(default_factory=list)
 
     @property
     def finished(self) -> bool:
@@ -165,11 +175,12 @@ class EngineCoreClient:
                 self._stats = stats
                 now = time.perf_counter()
                 by_loop: Dict[object, list] = {}
-                for rid, new, lps, fin in updates:
-                    st = self._streams.get(rid)
+                for u in updates:
+                    st = self._streams.get(u[0])
                     if st is None:
                         continue
-                    by_loop.setdefault(st[0], []).append((st[1], ("token", (new, lps, fin, now))))
+                    by_loop.setdefault(st[0], []).append(
+                        (st[1], ("token", (u[1], u[2], u[3], now, u[4] if len(u) > 4 else None))))
                 for loop, items in by_loop.items():
                     loop.call_soon_threadsafe(_deliver, items)
             elif msg[0] == "error":
@@ -196,11 +207,15 @@ class EngineCoreClient:
                 kind, payload = await q.get()
                 if kind == "error":
                     raise ValueError(payload)
-                new, lps, fin, now = payload
+                new, lps, fin, now, ex = payload
                 if new and view.first_token_time is None:
                     view.first_token_time = now
                 view.output_ids.extend(new)
                 view.output_logprobs.extend(lps)
+                if ex is not None:
+                    view.output_top_logprobs.extend(ex.get("top", []))
+                    if "prompt" in ex:
+                        view.prompt_scores = list(ex["prompt"])
                 view.token_times.extend([now] * len(new))
                 view.finish_reason = fin
                 yield view

@@ -107,6 +107,8 @@ class StepInput:
     temps: Optional[torch.Tensor] = None         # [R] f32 sampling temperature per sampled row
     top_ps: Optional[torch.Tensor] = None        # [R] f32
     top_ks: Optional[torch.Tensor] = None        # [R] int32
+    extra_rows: Optional[torch.Tensor] = None    # prompt-logprob rows (TP = 1), int64 [E]
+    prompt_meta: Optional[list] = None           # host: (seq, first scored token, count, row)
 
     @property
     def num_prefill_rows(self) -> int:
@@ -236,7 +238,11 @@ class ModelRunner:
             dist.all_gather(parts, logits.contiguous(), group=self.tp_group)
         return torch.cat(parts, 1)
 
-    def _logits(self, h, res, rows):
+    def _logits(self, h, res, rows, extra=None):
+        if extra is not None and extra.numel():
+            # prompt scoring rows (TP = 1): their logits are left in ``extra_logits``
+            y, _ = rms_norm(h[extra], self.w.norm, self.cfg.rms_norm_eps, res[extra])
+            self.extra_logits = torch.matmul(y, self.w.lm_head.t())
         if rows.numel() == 0:  # a chunk that completes no prompt samples nothing
             return torch.empty(0, self.cfg.vocab_size, device=h.device, dtype=h.dtype)
         y, _ = rms_norm(h[rows], self.w.norm, self.cfg.rms_norm_eps, res[rows])
@@ -276,7 +282,7 @@ class ModelRunner:
             return o
 
         h, res = self._layers(h, inp.positions, inp.slots, attn, inp.lora_ids)
-        return self._logits(h, res, inp.sample_rows)
+        return self._logits(h, res, inp.sample_rows, inp.extra_rows)
 
     prefill = execute  # a whole-prompt step is a mixed step without decode rows
 

@@ -129,7 +129,10 @@ class Scheduler:
             self.waiting.popleft()
             # prefix caching: the leading full blocks already in the cache are shared and only
             # the rest of the prompt is computed (0 without it)
-            s.num_cached = self.blocks.allocate(s.seq_id, s.length + 1, s.all_ids, s.lora_slot)
+            # (a prompt to be scored is computed whole: no shared blocks)
+            s.num_cached = self.blocks.allocate(
+                s.seq_id, s.length + 1,
+                s.all_ids if s.params.prompt_logprobs is None else None, s.lora_slot)
             s.prefilled = False
             s.status = Status.RUNNING
             self.running.append(s)
@@ -144,7 +147,7 @@ class Scheduler:
         if s.length <= budget:
             return True
         bm = self.blocks
-        if not bm.prefix_caching:
+        if not bm.prefix_caching or s.params.prompt_logprobs is not None:
             return False
         ids = s.all_ids
         hit = 0

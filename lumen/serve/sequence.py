@@ -5,7 +5,7 @@ import enum
 import itertools
 import time
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 
 @dataclass
@@ -18,6 +18,12 @@ class SamplingParams:
     ignore_eos: bool = False
     seed: Optional[int] = None
     logprobs: bool = False
+    # OpenAI / vLLM logprobs: alternatives per generated token (the most likely ``top_logprobs``
+    # tokens of the distribution the token was sampled from), and prompt_logprobs (None: off):
+    # the log probability of every prompt token given its prefix plus that many alternatives
+    # (``echo`` scoring; TP = 1)
+    top_logprobs: int = 0
+    prompt_logprobs: Optional[int] = None
     # OpenAI penalties (logit -= frequency * count + presence * [count > 0], over the generated
     # tokens) and vLLM's repetition penalty (prompt + generated tokens: positive logits divided,
     # negative multiplied)
@@ -41,6 +47,15 @@ class SamplingParams:
             raise ValueError("temperature must be >= 0")
         if not 0.0 < self.top_p <= 1.0:
             raise ValueError("top_p must be in (0, 1]")
+        if not 0 <= self.top_logprobs <= 20:
+            raise ValueError("top_logprobs must be in [0, 20]")
+        if self.prompt_logprobs is not None and not 0 <= self.prompt_logprobs <= 20:
+            raise ValueError("prompt_logprobs must be in [0, 20]")
+
+    @property
+    def wants_extras(self) -> bool:
+        """Alternatives or prompt scores: the step is resolved on the host before the next."""
+        return self.top_logprobs > 0 or self.prompt_logprobs is not None
 
 
 class Status(enum.Enum):
@@ -63,6 +78,11 @@ class Sequence:
     seq_id: int = field(default_factory=lambda: next(_ids))
     output_ids: List[int] = field(default_factory=list)
     output_logprobs: List[float] = field(default_factory=list)
+    # per generated token: [(token id, logprob)] of the top_logprobs alternatives
+    output_top_logprobs: List[List[Tuple[int, float]]] = field(default_factory=list)
+    # prompt_logprobs: per prompt token (None for the first), (logprob, alternatives)
+    prompt_scores: List[Optional[Tuple[float, List[Tuple[int, float]]]]] = field(
+        default_factory=list)
     status: Status = Status.WAITING
     finish_reason: Optional[str] = None
     arrival: float = field(default_factory=time.perf_counter)
@@ -124,7 +144,10 @@ class Sequence:
     def has_pending(self) -> bool:
         return self.n_pending > 0
 
-    def append(self, tok: int, logprob: Optional[float], eos_id: Optional[int]) -> None:
+    def append(self, tok: int, logprob: Optional[float], eos_id: Optional[int],
+               top: Optional[List[Tuple[int, float]]] = None) -> None:
+        if top is not None:
+            self.output_top_logprobs.append(top)
         now = time.perf_counter()
         if self.first_token_time is None:
             self.first_token_time = now
