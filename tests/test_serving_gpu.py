@@ -142,3 +142,35 @@ def test_prefix_caching_matches_full_forward():
         ref = full[len(p) - 1:].argmax(-1).tolist()
         agree = sum(int(a == b) for a, b in zip(ref, s.output_ids)) / len(ref)
         assert agree >= 0.9, agree
+
+
+def test_prompt_scores_and_alternatives_match_full_forward():
+    """prompt_logprobs (echo scoring) and top_logprobs on the GPU path: the paged prefill's
+    extra rows and the sampled rows against the full forward's log-softmax (bf16 tolerance)."""
+    from lumen.models import build_model
+    from lumen.serve.engine import EngineConfig, LLMEngine
+    from lumen.serve.sequence import SamplingParams
+
+    dev = torch.device("cuda", 0)
+    m = build_model("tiny-llama-gqa", dtype=torch.bfloat16, device=dev, init="random", seed=3)
+    m.eval()
+    eng = LLMEngine(EngineConfig(model="tiny-llama-gqa", device="cuda", max_model_len=512,
+                                 block_size=16, num_blocks=128, use_graphs=True,
+                                 max_num_batched_tokens=32), model=m)   # chunked prompt
+    prompt = [(11 * i + 5) % 500 for i in range(70)]
+    s = eng.add_request(prompt, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True,
+                                               top_logprobs=4, prompt_logprobs=3))
+    while eng.has_work:
+        eng.step()
+    ids = torch.tensor([prompt + s.output_ids], device=dev)
+    with torch.no_grad():
+        lp = torch.log_softmax(m(ids).float().view(ids.shape[1], -1), -1)
+    assert len(s.prompt_scores) == len(prompt) and s.prompt_scores[0] is None
+    got = torch.tensor([x[0] for x in s.prompt_scores[1:]])
+    ref = lp[torch.arange(len(prompt) - 1), torch.tensor(prompt[1:], device=dev)].cpu()
+    assert (got - ref).abs().max().item() < 0.1, (got - ref).abs().max().item()
+    assert len(s.output_top_logprobs) == 6
+    for i, alts in enumerate(s.output_top_logprobs):
+        row = lp[len(prompt) - 1 + i]
+        assert abs(alts[0][1] - row.max().item()) < 0.1
+        assert all(a[1] >= b[1] for a, b in zip(alts, alts[1:]))
