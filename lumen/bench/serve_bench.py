@@ -41,7 +41,8 @@ def make_engine(a):
                        tp_size=getattr(a, "tp", 1),
                        scheduling_policy=getattr(a, "scheduling_policy", "chunked"),
                        num_blocks=getattr(a, "num_blocks", None),
-                       enable_prefix_caching=getattr(a, "enable_prefix_caching", False))
+                       enable_prefix_caching=getattr(a, "enable_prefix_caching", False),
+                       num_speculative_tokens=getattr(a, "num_speculative_tokens", 0))
     t0 = time.time()
     eng = LLMEngine(cfg)
     eng._bench_setup_s = time.time() - t0
@@ -126,7 +127,8 @@ def bench_engine(a, eng=None) -> dict:
             "shared_prefix": len(shared), "prefix_caching": eng.blocks.prefix_caching,
             "prefix_hit_rate": round((eng.blocks.hit_tokens - hit0)
                                      / max(1, eng.blocks.query_tokens - q0), 4),
-            "prefill_tokens_computed": eng.stats["prefill_tokens"] - pf0}
+            "prefill_tokens_computed": eng.stats["prefill_tokens"] - pf0,
+            "spec": {k: eng.stats[k] for k in ("spec_steps", "spec_proposed", "spec_accepted")}}
 
 
 def _trace_steps(eng) -> dict:
@@ -269,6 +271,8 @@ def main():
     ap.add_argument("--num-blocks", type=int, default=None, help="KV blocks (default: auto)")
     ap.add_argument("--scheduling-policy", default="chunked", choices=["chunked", "prefill_first"])
     ap.add_argument("--enable-prefix-caching", action="store_true")
+    ap.add_argument("--num-speculative-tokens", type=int, default=0,
+                    help="prompt-lookup speculative decoding (greedy requests)")
     ap.add_argument("--shared-prefix", type=int, default=0,
                     help="engine mode: the first N prompt tokens are the same in every request")
     ap.add_argument("--api-servers", type=int, default=1,

@@ -59,6 +59,12 @@ def build_parser():
     ap.add_argument("--enable-prefix-caching", action="store_true",
                     help="share the cached K/V of equal leading prompt blocks across requests "
                          "(vLLM's flag; finished requests' blocks stay cached until evicted)")
+    ap.add_argument("--speculative-model", default=None,
+                    help='"[ngram]": speculative decoding by prompt lookup (the only drafter)')
+    ap.add_argument("--num-speculative-tokens", type=int, default=0,
+                    help="draft tokens per step with --speculative-model [ngram]")
+    ap.add_argument("--ngram-prompt-lookup-max", type=int, default=4)
+    ap.add_argument("--ngram-prompt-lookup-min", type=int, default=1)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--api-server-count", type=int, default=1,
                     help="OpenAI API processes sharing --port (SO_REUSEPORT), each streaming its "
@@ -94,6 +100,9 @@ def main(argv=None):
     env = init()
     if env.world_size != a.tp:
         raise SystemExit(f"--tp {a.tp} but WORLD_SIZE={env.world_size}")
+    if a.speculative_model not in (None, "[ngram]"):
+        raise SystemExit('--speculative-model: only "[ngram]" (prompt lookup) is served')
+    spec_k = a.num_speculative_tokens if a.speculative_model == "[ngram]" else 0
     policy, budget = resolve_scheduling(a.scheduling_policy, a.enable_chunked_prefill,
                                         a.max_num_batched_tokens, a.max_model_len)
     cfg = EngineConfig(model=a.model, adapter=a.adapter, dtype=a.dtype,
@@ -104,6 +113,8 @@ def main(argv=None):
                        scheduling_policy=policy,
                        kv_cache_dtype=a.kv_cache_dtype,
                        enable_prefix_caching=a.enable_prefix_caching,
+                       num_speculative_tokens=spec_k,
+                       ngram_max=a.ngram_prompt_lookup_max, ngram_min=a.ngram_prompt_lookup_min,
                        lora_modules=dict(m.split("=", 1) for m in a.lora_modules)
                        if a.lora_modules else None, max_loras=a.max_loras)
     eng = LLMEngine(cfg)

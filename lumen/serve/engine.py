@@ -68,6 +68,13 @@ class EngineConfig:
     # automatic prefix caching (vLLM --enable-prefix-caching): prompts share the cached K/V of
     # equal leading full blocks; finished sequences' blocks stay cached until evicted
     enable_prefix_caching: bool = False
+    # speculative decoding by prompt lookup (vLLM --speculative-model "[ngram]"): up to this many
+    # draft tokens per greedy sequence, copied from where the sequence's last n tokens (n from
+    # ngram_max down to ngram_min) occurred before; a decode step then verifies every draft in
+    # one forward (0 = off).  Scheduling is synchronous while it is on.
+    num_speculative_tokens: int = 0
+    ngram_max: int = 4
+    ngram_min: int = 1
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -186,7 +193,9 @@ class LLMEngine:
         # TP > 1 too: a step is broadcast when it is launched, its decode tokens straight from
         # the device (gathered from the previous step's samples), so workers never wait for
         # rank 0's host to see the tokens
-        self.async_sched = bool(cfg.async_scheduling)
+        self.spec_k = max(0, int(cfg.num_speculative_tokens))
+        # drafting reads every sequence's latest token on the host: no step in flight
+        self.async_sched = bool(cfg.async_scheduling) and self.spec_k == 0
         self._inflight: Optional[dict] = None
         self.scheduler = Scheduler(SchedulerConfig(
             cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
@@ -200,7 +209,8 @@ class LLMEngine:
         self.eos_id = getattr(tokenizer, "eos_token_id", self.model_config.eos_token_id)
         self.step_count = 0
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "requests": 0,
-                      "finished": 0, "overlapped_steps": 0}
+                      "finished": 0, "overlapped_steps": 0, "spec_proposed": 0,
+                      "spec_accepted": 0, "spec_steps": 0}
 
     # --------------------------------------------------------------------------------------
     def _auto_blocks(self, dt) -> int:
@@ -265,7 +275,7 @@ class LLMEngine:
         cu, kv_lens, ptables = [0], [], []
         for s, c in batch.prefills:
             a = s.num_cached
-            ids = s.all_ids
+            ids = s.all_ids + s.draft if s.draft else s.all_ids
             toks.append(np.asarray(ids[a:a + c], dtype=np.int64))
             p = np.arange(a, a + c, dtype=np.int64)
             pos.append(p)
@@ -328,10 +338,17 @@ class LLMEngine:
                 src = None
             else:
                 extra.append(src)
-        n_done = len(batch.completing())
-        done_rows = [cu[i + 1] - 1 for i, (s, c) in enumerate(batch.prefills)
-                     if s.num_cached + c == s.length]
-        assert len(done_rows) == n_done
+        if batch.kind == "verify":
+            # speculative verification: every row of a drafted chunk is scored
+            done_rows = list(range(Tp))
+            ps = [s.params for s, c in batch.prefills for _ in range(c)]
+            ps += [s.params for s in batch.decodes]
+        else:
+            n_done = len(batch.completing())
+            done_rows = [cu[i + 1] - 1 for i, (s, c) in enumerate(batch.prefills)
+                         if s.num_cached + c == s.length]
+            assert len(done_rows) == n_done
+            ps = [s.params for s in batch.sampled]
         rows = np.concatenate([np.asarray(done_rows, dtype=np.int64),
                                np.arange(Tp, T, dtype=np.int64)])
         extra.append(rows)
@@ -340,7 +357,6 @@ class LLMEngine:
             # sampling parameters of the sampled rows ride in the same async copy: building them
             # with torch.tensor(list, device=...) is a blocking copy -- a stream synchronise per
             # step that would serialise the host with the GPU and undo async scheduling
-            ps = [s.params for s in batch.sampled]
             extra += [np.fromiter((p.temperature for p in ps), np.float64, R).view(np.int64),
                       np.fromiter((p.top_p for p in ps), np.float64, R).view(np.int64),
                       np.fromiter((p.top_k for p in ps), np.int64, R)]
@@ -351,7 +367,8 @@ class LLMEngine:
         host = np.concatenate([np.concatenate(parts)] + extra)
         dev = self._to_device(host)
         o = 3 * T
-        inp = StepInput(batch.kind, dev[:T], dev[T:2 * T].int(), dev[2 * T:3 * T], cu)
+        inp = StepInput("mixed" if batch.kind == "verify" else batch.kind, dev[:T],
+                        dev[T:2 * T].int(), dev[2 * T:3 * T], cu)
         if P:
             inp.prefill_tables = dev[o:o + P * maxb_p].view(P, maxb_p).int()
             o += P * maxb_p
@@ -418,6 +435,8 @@ class LLMEngine:
             batch = self.scheduler.schedule()
             if batch is None:
                 return []
+            if self.spec_k and batch.kind == "decode" and self._propose(batch):
+                return self._run_verify(batch)
             return self._run_batch(batch)
         batch = self.scheduler.schedule()
         if batch is None:
@@ -569,6 +588,96 @@ class LLMEngine:
         self.stats["steps"] += 1
         self.step_count += 1
         return sampled
+
+    # ---- speculative decoding (prompt lookup) ----------------------------------------------
+    def _lookup(self, ids: List[int], k: int) -> List[int]:
+        """Up to k tokens that followed the most recent earlier occurrence of the sequence's
+        last n tokens (n = ngram_max .. ngram_min; the last 2048 tokens are searched)."""
+        arr = np.asarray(ids[-2048:], dtype=np.int64)
+        L = arr.shape[0]
+        for n in range(min(self.cfg.ngram_max, L - 1), max(1, self.cfg.ngram_min) - 1, -1):
+            win = np.lib.stride_tricks.sliding_window_view(arr[:L - 1], n)
+            hit = np.nonzero((win == arr[L - n:]).all(axis=1))[0]
+            if hit.size:
+                j = int(hit[-1]) + n          # first token after the earlier occurrence
+                return arr[j:j + k].tolist()
+        return []
+
+    def _propose(self, batch: Batch) -> bool:
+        """Drafts for the greedy decode rows of ``batch`` (``Sequence.draft``), their KV slots
+        reserved; False when nothing was drafted."""
+        if any(s.params.wants_extras for s in batch.decodes):
+            return False                      # alternatives are computed on the plain path
+        any_draft = False
+        for s in batch.decodes:
+            p = s.params
+            if p.temperature > 0 or p.has_penalties or p.wants_extras:
+                continue
+            room = min(self.spec_k, p.max_tokens - len(s.output_ids) - 1,
+                       self.cfg.max_model_len - s.length - 1)
+            if room <= 0:
+                continue
+            d = self._lookup(s.all_ids, room)
+            if not d:
+                continue
+            try:
+                self.blocks.ensure(s.seq_id, s.length + len(d) + 1)
+            except RuntimeError:
+                continue                      # no blocks for the draft: plain decode row
+            s.draft = d
+            any_draft = True
+        return any_draft
+
+    def _run_verify(self, batch: Batch) -> List[Sequence]:
+        """One forward over [last token + draft] chunks of the drafted sequences and the other
+        decode rows: the longest draft prefix the model's argmax agrees with is accepted, plus
+        the model's own next token -- greedy outputs identical to one-token decoding."""
+        drafted = [s for s in batch.decodes if s.draft]
+        vb = Batch("verify", [(s, 1 + len(s.draft)) for s in drafted],
+                   [s for s in batch.decodes if not s.draft])
+        inp = self._build_input(vb)
+        if self.tp > 1:
+            self._broadcast(inp)
+        logits = self.runner.execute(inp)
+        # drafted rows are greedy (argmax); the undrafted decode rows keep their own sampling
+        if any(s.params.has_penalties for s in vb.decodes):
+            logits = apply_penalties(logits, [s for s, c in vb.prefills for _ in range(c)]
+                                     + vb.decodes)
+        p0 = vb.seqs[0].params
+        t, lp = self.runner.sample(logits, inp.temps, inp.top_ps, inp.top_ks,
+                                   self.cfg.seed if p0.seed is None else p0.seed,
+                                   self.step_count, want_logprobs=True)
+        amv = t.tolist()
+        lpv = lp.tolist() if lp is not None else [None] * len(amv)
+        self.runner.check_collectives()
+        self.stats["prefill_tokens"] += inp.num_prefill_rows
+        self.stats["decode_tokens"] += len(vb.decodes)
+        self.stats["spec_steps"] += 1
+        r = 0
+        out = []
+        for s, c in vb.prefills:
+            d, s.draft = s.draft, []
+            acc = 0
+            while acc < len(d) and amv[r + acc] == d[acc]:
+                acc += 1
+            self.stats["spec_proposed"] += len(d)
+            self.stats["spec_accepted"] += acc
+            for t, lp in zip(d[:acc] + [amv[r + acc]], lpv[r:r + acc + 1]):
+                s.append(int(t), lp, self.eos_id)
+                if s.finished:
+                    break
+            s.num_cached = s.length - 1       # K/V valid up to the last accepted input
+            r += c
+            out.append(s)
+        for s in vb.decodes:
+            s.num_cached = s.length
+            s.append(int(amv[r]), lpv[r], self.eos_id)
+            r += 1
+            out.append(s)
+        self.stats["finished"] += len(self.scheduler.finish(vb))
+        self.stats["steps"] += 1
+        self.step_count += 1
+        return out
 
     def _extras(self, inp: StepInput, logits: torch.Tensor, sampled: List[Sequence]) -> list:
         """Host lists of the ``top_logprobs`` alternatives of each sampled row (None where not

@@ -95,6 +95,7 @@ class Sequence:
     lora_slot: int = 0           # multi-LoRA serving: adapter slot (0 = base model)
     n_pending: int = 0           # async scheduling: sampled tokens still on the device
     capped: bool = False         # max_tokens reached counting in-flight tokens
+    draft: List[int] = field(default_factory=list)   # speculative tokens under verification
 
     @property
     def all_ids(self) -> List[int]:

@@ -174,3 +174,32 @@ def test_prompt_scores_and_alternatives_match_full_forward():
         row = lp[len(prompt) - 1 + i]
         assert abs(alts[0][1] - row.max().item()) < 0.1
         assert all(a[1] >= b[1] for a, b in zip(alts, alts[1:]))
+
+
+def test_prompt_lookup_speculative_decoding_matches_full_forward():
+    """Speculative verification on the GPU path (paged prefill over [last token | draft]
+    chunks next to graph-free decode rows): teacher-forced agreement with the full forward."""
+    from lumen.models import build_model
+    from lumen.serve.engine import EngineConfig, LLMEngine
+    from lumen.serve.sequence import SamplingParams
+
+    dev = torch.device("cuda", 0)
+    m = build_model("tiny-llama-gqa", dtype=torch.bfloat16, device=dev, init="random", seed=3)
+    m.eval()
+    eng = LLMEngine(EngineConfig(model="tiny-llama-gqa", device="cuda", max_model_len=512,
+                                 block_size=16, num_blocks=128, use_graphs=True,
+                                 num_speculative_tokens=4), model=m)
+    prompts = [[5, 9, 33, 7] * 10, list(range(3, 60)) * 2, [42, 43]]
+    seqs = [eng.add_request(p, SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True))
+            for p in prompts]
+    while eng.has_work:
+        eng.step()
+    assert eng.stats["spec_steps"] > 0
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 40
+        ids = torch.tensor([p + s.output_ids[:-1]], device=dev)
+        with torch.no_grad():
+            full = m(ids).float().view(ids.shape[1], -1)
+        ref = full[len(p) - 1:].argmax(-1).tolist()
+        agree = sum(int(a == b) for a, b in zip(ref, s.output_ids)) / len(ref)
+        assert agree >= 0.9, agree
