@@ -75,6 +75,10 @@ class EngineConfig:
     num_speculative_tokens: int = 0
     ngram_max: int = 4
     ngram_min: int = 1
+    # a verify step is a mixed forward (slower than a graph-replayed decode step): it runs only
+    # when at least this fraction of the decode rows has a draft; a sequence whose drafts were
+    # all rejected backs off (1, 3, 7 .. 63 steps) before it drafts again
+    spec_min_fraction: float = 0.5
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -608,10 +612,13 @@ class LLMEngine:
         reserved; False when nothing was drafted."""
         if any(s.params.wants_extras for s in batch.decodes):
             return False                      # alternatives are computed on the plain path
-        any_draft = False
+        drafted = []
         for s in batch.decodes:
             p = s.params
             if p.temperature > 0 or p.has_penalties or p.wants_extras:
+                continue
+            if s.spec_wait > 0:
+                s.spec_wait -= 1
                 continue
             room = min(self.spec_k, p.max_tokens - len(s.output_ids) - 1,
                        self.cfg.max_model_len - s.length - 1)
@@ -625,8 +632,12 @@ class LLMEngine:
             except RuntimeError:
                 continue                      # no blocks for the draft: plain decode row
             s.draft = d
-            any_draft = True
-        return any_draft
+            drafted.append(s)
+        if drafted and len(drafted) < self.cfg.spec_min_fraction * len(batch.decodes):
+            for s in drafted:             # too few drafts to pay for a verify step
+                s.draft = []
+            return False
+        return bool(drafted)
 
     def _run_verify(self, batch: Batch) -> List[Sequence]:
         """One forward over [last token + draft] chunks of the drafted sequences and the other
@@ -662,6 +673,11 @@ class LLMEngine:
                 acc += 1
             self.stats["spec_proposed"] += len(d)
             self.stats["spec_accepted"] += acc
+            if acc:
+                s.spec_misses = 0
+            else:
+                s.spec_misses += 1
+                s.spec_wait = min(2 ** s.spec_misses - 1, 63)
             for t, lp in zip(d[:acc] + [amv[r + acc]], lpv[r:r + acc + 1]):
                 s.append(int(t), lp, self.eos_id)
                 if s.finished:

@@ -96,6 +96,8 @@ class Sequence:
     n_pending: int = 0           # async scheduling: sampled tokens still on the device
     capped: bool = False         # max_tokens reached counting in-flight tokens
     draft: List[int] = field(default_factory=list)   # speculative tokens under verification
+    spec_wait: int = 0           # decode steps before this sequence drafts again (back-off)
+    spec_misses: int = 0         # consecutive verifications that accepted nothing
 
     @property
     def all_ids(self) -> List[int]:
