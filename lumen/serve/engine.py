@@ -594,17 +594,24 @@ class LLMEngine:
         return sampled
 
     # ---- speculative decoding (prompt lookup) ----------------------------------------------
-    def _lookup(self, ids: List[int], k: int) -> List[int]:
+    def _lookup(self, ids: List[int], k: int, s: Optional[Sequence] = None) -> List[int]:
         """Up to k tokens that followed the most recent earlier occurrence of the sequence's
-        last n tokens (n = ngram_max .. ngram_min; the last 2048 tokens are searched)."""
-        arr = np.asarray(ids[-2048:], dtype=np.int64)
-        L = arr.shape[0]
-        for n in range(min(self.cfg.ngram_max, L - 1), max(1, self.cfg.ngram_min) - 1, -1):
-            win = np.lib.stride_tricks.sliding_window_view(arr[:L - 1], n)
-            hit = np.nonzero((win == arr[L - n:]).all(axis=1))[0]
-            if hit.size:
-                j = int(hit[-1]) + n          # first token after the earlier occurrence
-                return arr[j:j + k].tolist()
+        last n tokens (n = ngram_max .. ngram_min).  The n-gram index of ``s`` is extended
+        incrementally (a few dict updates per new token: O(1) per sequence and step, where a
+        scan of the history cost ~60 us per sequence, 15 ms per 256-row step)."""
+        lo, hi = max(1, self.cfg.ngram_min), self.cfg.ngram_max
+        idx = s.ngram_idx if s is not None else {}
+        upto = s.ngram_upto if s is not None else 0
+        L = len(ids)
+        for p in range(upto, L - 1):          # n-grams ending before the current suffix
+            for n in range(lo, min(hi, p + 1) + 1):
+                idx[tuple(ids[p - n + 1:p + 1])] = p + 1
+        if s is not None:
+            s.ngram_upto = max(upto, L - 1)
+        for n in range(min(hi, L - 1), lo - 1, -1):
+            j = idx.get(tuple(ids[L - n:]))
+            if j is not None:
+                return ids[j:j + k]
         return []
 
     def _propose(self, batch: Batch) -> bool:
@@ -624,7 +631,7 @@ class LLMEngine:
                        self.cfg.max_model_len - s.length - 1)
             if room <= 0:
                 continue
-            d = self._lookup(s.all_ids, room)
+            d = self._lookup(s.all_ids, room, s)
             if not d:
                 continue
             try:

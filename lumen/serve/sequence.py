@@ -98,6 +98,9 @@ class Sequence:
     draft: List[int] = field(default_factory=list)   # speculative tokens under verification
     spec_wait: int = 0           # decode steps before this sequence drafts again (back-off)
     spec_misses: int = 0         # consecutive verifications that accepted nothing
+    # prompt lookup: n-gram -> position after its latest occurrence, over all_ids[:ngram_upto]
+    ngram_idx: dict = field(default_factory=dict, repr=False)
+    ngram_upto: int = 0
 
     @property
     def all_ids(self) -> List[int]:

@@ -48,6 +48,13 @@ def test_lookup_finds_latest_longest_match(model):
     assert eng._lookup(ids, 3) == [4, 5, 6]      # latest occurrence of [1, 2, 3]
     assert eng._lookup([8, 1, 2, 7, 5, 2], 2) == [7, 5]   # falls back to a 1-gram
     assert eng._lookup([1, 2, 3], 4) == []
+    # the incremental index of a growing sequence gives the same answers as a fresh one
+    from lumen.serve.sequence import Sequence
+    seq = Sequence([1, 2, 3], SamplingParams())
+    grow = [1, 2, 3]
+    for t in [9, 9, 1, 2, 3, 4, 5, 6, 7, 1, 2, 3]:
+        grow.append(t)
+        assert eng._lookup(grow, 3, seq) == eng._lookup(grow, 3)
 
 
 def test_oracle_drafts_all_part_none_accepted(model):
@@ -64,7 +71,7 @@ def test_oracle_drafts_all_part_none_accepted(model):
                 return [] if p is PROMPTS[2] else d
         raise AssertionError("unexpected sequence")
 
-    eng._lookup = oracle
+    eng._lookup = lambda ids, k, s=None: oracle(ids, k)
     seqs = eng.generate(PROMPTS, SamplingParams(max_tokens=24, **GREEDY))
     for s, r in zip(seqs, refs):
         assert s.output_ids == r
@@ -74,7 +81,7 @@ def test_oracle_drafts_all_part_none_accepted(model):
     assert eng.blocks.num_free == eng.blocks.num_blocks
     # alone, the always-right drafts give k + 1 tokens per step: 1 prefill + 4 verify steps
     solo = _engine(model, k=5)
-    solo._lookup = oracle
+    solo._lookup = lambda ids, k, s=None: oracle(ids, k)
     s = solo.generate([PROMPTS[0]], SamplingParams(max_tokens=24, **GREEDY))[0]
     assert s.output_ids == refs[0] and solo.stats["steps"] == 5
 
@@ -104,7 +111,7 @@ def test_stop_token_inside_accepted_draft(model):
     p = PROMPTS[0]
     ref = naive_greedy(model, p, 16)
     eng = _engine(model, k=6)
-    eng._lookup = lambda ids, k: (p + ref)[len(ids):len(ids) + k]
+    eng._lookup = lambda ids, k, s=None: (p + ref)[len(ids):len(ids) + k]
     s = eng.generate([p], SamplingParams(max_tokens=16, temperature=0.0,
                                           stop_token_ids=[ref[5]], ignore_eos=True))[0]
     stop_at = ref.index(ref[5])
