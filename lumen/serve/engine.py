@@ -643,6 +643,7 @@ class LLMEngine:
         if drafted and len(drafted) < self.cfg.spec_min_fraction * len(batch.decodes):
             for s in drafted:             # too few drafts to pay for a verify step
                 s.draft = []
+                s.spec_wait = 3           # (and look again in a few steps, not every step)
             return False
         return bool(drafted)
 
