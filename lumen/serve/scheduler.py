@@ -57,7 +57,7 @@ class SchedulerConfig:
 
 @dataclass
 class Batch:
-    kind: str                                                    # "mixed" | "decode"
+    kind: str          # "mixed" | "decode" | "verify" (speculative drafts, engine-built)
     prefills: List[Tuple[Sequence, int]] = field(default_factory=list)  # (seq, chunk length)
     decodes: List[Sequence] = field(default_factory=list)
 
