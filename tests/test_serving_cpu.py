@@ -748,3 +748,16 @@ def test_prefill_first_preemption_is_transparent(model):
 def test_unknown_scheduling_policy_rejected(model):
     with pytest.raises(ValueError):
         _engine(model, num_blocks=64, scheduling_policy="fifo")
+
+
+def test_serve_cli_feature_flags_parse():
+    """vLLM-named flags of the features added in round 4 reach the parser."""
+    from lumen.cli.serve import build_parser
+
+    a = build_parser().parse_args(["--enable-prefix-caching", "--speculative-model", "[ngram]",
+                                   "--num-speculative-tokens", "3", "--ngram-prompt-lookup-max",
+                                   "5"])
+    assert a.enable_prefix_caching and a.speculative_model == "[ngram]"
+    assert a.num_speculative_tokens == 3 and a.ngram_prompt_lookup_max == 5
+    d = build_parser().parse_args([])
+    assert not d.enable_prefix_caching and d.num_speculative_tokens == 0
