@@ -282,6 +282,32 @@ def create_app(aengine, served_model_name: Optional[str] = None):
     async def health():
         return {"status": "ok"}
 
+    @app.get("/version")
+    async def version():
+        import lumen
+        return {"version": getattr(lumen, "__version__", "0")}
+
+    @app.post("/tokenize")
+    async def tokenize(req: Request):
+        """vLLM's /tokenize: {"prompt"} or chat {"messages"} -> token ids and count."""
+        body = await req.json()
+        if body.get("messages"):
+            text = llama2_chat_prompt(body["messages"])
+        else:
+            text = body.get("prompt", "")
+        if not isinstance(text, str):
+            raise HTTPException(status_code=400, detail="prompt must be a string")
+        ids = tok.encode(text)
+        return {"tokens": ids, "count": len(ids), "max_model_len": aengine.max_model_len}
+
+    @app.post("/detokenize")
+    async def detokenize(req: Request):
+        body = await req.json()
+        ids = body.get("tokens")
+        if not isinstance(ids, list) or not all(isinstance(t, int) for t in ids):
+            raise HTTPException(status_code=400, detail="tokens must be a list of ints")
+        return {"prompt": decode(ids)}
+
     loras = list(getattr(aengine, "lora_names", []) or [])
 
     @app.get("/v1/models")

@@ -137,3 +137,23 @@ def test_openai_logprobs_through_engine_core(model):
         req_q.put(("stop",))
         core.join(timeout=30)
         out_q.put(None)
+
+
+def test_tokenize_detokenize_version_endpoints(model):
+    from starlette.testclient import TestClient
+
+    from lumen.serve.api_server import create_app
+
+    eng = _engine(model)
+    ae = AsyncEngine(eng)
+    try:
+        c = TestClient(create_app(ae, "tiny"))
+        t = c.post("/tokenize", json={"prompt": "hello world"}).json()
+        assert t["count"] == len(t["tokens"]) > 0 and t["max_model_len"] == 256
+        assert c.post("/detokenize", json={"tokens": t["tokens"]}).json()["prompt"] == "hello world"
+        m = c.post("/tokenize", json={"messages": [{"role": "user", "content": "hi"}]}).json()
+        assert m["count"] > t["count"] - 5
+        assert c.post("/detokenize", json={"tokens": "x"}).status_code == 400
+        assert "version" in c.get("/version").json()
+    finally:
+        ae.shutdown()
