@@ -273,8 +273,9 @@ void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                                 "(lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, "
                                 "window, hysteresis, min_scale)");
   if (p.scalar_type() != at::kFloat) throw std::invalid_argument("lumen: adamw master must be f32");
-  std::vector<double> sched10 = sched;  // optional 10th value (decay_total) defaults to 0
-  if (!sched10.empty() && sched10.size() < 10) sched10.resize(10, 0.0);
+  // optional values 10-12 (decay_total, decay_kind, cos_min_ratio) default to 0
+  std::vector<double> sched10 = sched;
+  if (!sched10.empty() && sched10.size() < 12) sched10.resize(12, 0.0);
   const int od = out_copy.has_value() ? dcode(*out_copy) : 0;
   check(lumen_adamw(p.data_ptr<float>(), dcode(g), g.data_ptr(), m.data_ptr<float>(),
                     v.data_ptr<float>(), od, ptr(out_copy), p.numel(), static_cast<float>(lr),

@@ -33,10 +33,29 @@ struct OptSched {
   float scale_window;
   int hysteresis;
   float min_scale;
-  float decay_total;  // > 0: HF get_linear_schedule_with_warmup over this many steps
+  float decay_total;  // > 0: a decaying schedule over this many steps (kind below)
+  int decay_kind;     // 0: HF get_linear_schedule_with_warmup; 1: DeepSpeed WarmupDecayLR;
+                      // 2: DeepSpeed WarmupCosineLR (lr_min = warmup_min_ratio * lr_max)
+  float cos_min;      // WarmupCosineLR cos_min_ratio
 };
 
 __device__ __forceinline__ float sched_lr(const OptSched& s, float it) {
+  if (s.decay_total > 0.f && s.decay_kind > 0) {
+    // DeepSpeed WarmupDecayLR / WarmupCosineLR: the WarmupLR warm-up (length clamped to >= 2,
+    // log or linear from lr_min), then a linear (to lr_min) or cosine (to cos_min * lr_max)
+    // decay reaching its floor at decay_total
+    const float n = (float)(s.warm_n > 2 ? s.warm_n : 2);
+    if (it < n) {
+      const float gamma = s.warm_linear ? it / n : logf(it + 1.f) / logf(n);
+      return s.lr_min + (s.lr_max - s.lr_min) * gamma;
+    }
+    if (s.decay_kind == 1)
+      return s.lr_min + (s.lr_max - s.lr_min) *
+                            fmaxf(0.f, (s.decay_total - it) / fmaxf(1.f, s.decay_total - n));
+    const float c = 0.5f * (1.f + cosf(3.14159265358979f * (it - n + 1.f) /
+                                       fmaxf(1.f, s.decay_total - n)));
+    return s.lr_max * fmaxf(0.f, s.cos_min + (1.f - s.cos_min) * c);
+  }
   if (s.decay_total > 0.f) {
     // HF Trainer's default (no DeepSpeed scheduler): linear warm-up from 0, then linear decay
     // to 0 at decay_total (transformers get_linear_schedule_with_warmup)
@@ -193,7 +212,7 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
   sc.state = step_state;
   if (step_state) {
     // sched: lr_min, lr_max, warm_n, warm_linear, inv_world, dynamic, window, hysteresis, min,
-    // decay_total (the binding pads the list to 10 values)
+    // decay_total, decay_kind, cos_min (the binding pads the list to 12 values)
     sc.lr_min = (float)sched[0];
     sc.lr_max = (float)sched[1];
     sc.warm_n = (int)sched[2];
@@ -204,6 +223,8 @@ extern "C" hipError_t lumen_adamw(float* p, int gdtype, const void* g, float* m,
     sc.hysteresis = (int)sched[7];
     sc.min_scale = (float)sched[8];
     sc.decay_total = (float)sched[9];
+    sc.decay_kind = (int)sched[10];
+    sc.cos_min = (float)sched[11];
   }
   if (n == 0) return hipSuccess;
   dim3 grid(lumen::grid_for(n)), block(256);

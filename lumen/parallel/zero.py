@@ -203,7 +203,8 @@ class ShardAdamW:
             self.state[2] = 1.0
 
     def configure_schedule(self, lr_min: float, lr_max: float, warm_n: int, warm_linear: bool,
-                           world: int, scaler=None, decay_total: int = 0) -> bool:
+                           world: int, scaler=None, decay_total: int = 0, decay_kind: int = 0,
+                           cos_min: float = 0.0) -> bool:
         """Move the LR schedule (DeepSpeed WarmupLR, or HF's linear warm-up + decay when
         ``decay_total`` > 0) and (fp16) the dynamic loss scaler onto the device.
         Returns True when the device path is active (GPU, fused kernel available)."""
@@ -213,7 +214,8 @@ class ShardAdamW:
         self.sched = [lr_min, lr_max, float(warm_n), 1.0 if warm_linear else 0.0, 1.0 / world,
                       1.0 if dyn else 0.0, float(scaler.window if scaler else 1000),
                       float(scaler.hysteresis if scaler else 2),
-                      float(scaler.min_scale if scaler else 1.0), float(decay_total)]
+                      float(scaler.min_scale if scaler else 1.0), float(decay_total),
+                      float(decay_kind), float(cos_min)]
         st = [0.0, 0.0, float(scaler.scale) if scaler else 1.0,
               float(scaler.cur_hysteresis if scaler else 2), 0.0, -1.0, 0.0, 0.0]
         self.state.copy_(torch.tensor(st, dtype=torch.float32))

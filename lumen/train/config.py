@@ -51,6 +51,9 @@ class DSConfig:
     # once the run length is known)
     lr_schedule: str = "warmup"
     decay_total_steps: int = 0
+    # DeepSpeed WarmupDecayLR ("warmup_decay") / WarmupCosineLR ("warmup_cosine"): the decay
+    # horizon is the scheduler's total_num_steps ("auto": the run length, set by the trainer)
+    cos_min_ratio: float = 0.0
     gradient_clipping: float = 1.0
     # batch
     train_batch_size: int = 1
@@ -120,6 +123,16 @@ def load_ds_config(src, micro_batch: int, grad_accum: int, world_size: int,
     c.warmup_max_lr = float(_auto(sp.get("warmup_max_lr"), c.lr))
     c.warmup_num_steps = int(_auto(sp.get("warmup_num_steps"), warmup_steps))
     c.warmup_type = sp.get("warmup_type", "log")
+    kind = sch.get("type", "WarmupLR")
+    if kind not in ("WarmupLR", "WarmupDecayLR", "WarmupCosineLR"):
+        raise ValueError(f"scheduler type {kind!r}: WarmupLR, WarmupDecayLR or WarmupCosineLR")
+    if kind in ("WarmupDecayLR", "WarmupCosineLR"):
+        c.lr_schedule = "warmup_decay" if kind == "WarmupDecayLR" else "warmup_cosine"
+        c.decay_total_steps = int(_auto(sp.get("total_num_steps"), 0))
+        if kind == "WarmupCosineLR":   # ratios of the optimizer's lr
+            c.warmup_max_lr = c.lr
+            c.warmup_min_lr = float(sp.get("warmup_min_ratio", 0.0)) * c.lr
+            c.cos_min_ratio = float(sp.get("cos_min_ratio", 1e-4))
     if not raw:
         c.lr_schedule = "hf_linear"
         c.warmup_min_lr, c.warmup_max_lr = 0.0, c.lr
@@ -182,6 +195,14 @@ def warmup_lr(step: int, c: DSConfig) -> float:
             return c.warmup_max_lr * step / w
         return c.warmup_max_lr * max(0.0, (T - step) / max(1, T - w))
     n = max(2, c.warmup_num_steps)
+    if c.lr_schedule in ("warmup_decay", "warmup_cosine") and c.decay_total_steps > 0 and step >= n:
+        import math
+        T = c.decay_total_steps
+        if c.lr_schedule == "warmup_decay":
+            return c.warmup_min_lr + (c.warmup_max_lr - c.warmup_min_lr) * max(
+                0.0, (T - step) / max(1, T - n))
+        r = 0.5 * (1 + math.cos(math.pi * (step - n + 1) / max(1, T - n)))
+        return c.warmup_max_lr * max(0.0, c.cos_min_ratio + (1 - c.cos_min_ratio) * r)
     if step >= n:
         return c.warmup_max_lr
     if c.warmup_type == "linear":

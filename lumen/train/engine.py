@@ -154,7 +154,9 @@ class ZeroEngine:
         self.device_sched = self.opt.configure_schedule(
             cfg.warmup_min_lr, cfg.warmup_max_lr, cfg.warmup_num_steps,
             cfg.warmup_type == "linear", W, self.scaler,
-            cfg.decay_total_steps if cfg.lr_schedule == "hf_linear" else 0)
+            cfg.decay_total_steps if cfg.lr_schedule in self._DECAYING else 0,
+            self._DECAYING.index(cfg.lr_schedule) if cfg.lr_schedule in self._DECAYING else 0,
+            cfg.cos_min_ratio)
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._k = 1  # accumulation micro-steps fused into the current forward / backward
         # ZeRO-Offload optimizer: the CPU step overlaps the next forward (exact semantics)
@@ -192,9 +194,14 @@ class ZeroEngine:
         applied = self.opt.step_count
         return warmup_lr(max(applied - 1, 0), self.cfg) if applied else warmup_lr(0, self.cfg)
 
+    # decaying schedules, by the device kernel's decay_kind
+    _DECAYING = ("hf_linear", "warmup_decay", "warmup_cosine")
+
     def set_total_steps(self, n: int) -> None:
-        """Run length for a decaying schedule (HF linear: no DeepSpeed config)."""
-        if self.cfg.lr_schedule != "hf_linear":
+        """Run length for a decaying schedule (HF linear: no DeepSpeed config; DeepSpeed
+        WarmupDecayLR / WarmupCosineLR with total_num_steps "auto")."""
+        if self.cfg.lr_schedule not in self._DECAYING or (
+                self.cfg.lr_schedule != "hf_linear" and self.cfg.decay_total_steps > 0):
             return
         self.cfg.decay_total_steps = int(n)
         if self.device_sched:

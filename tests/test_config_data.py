@@ -219,3 +219,30 @@ def test_no_scheduler_section_means_constant_lr():
                                                                      "warmup_num_steps": "auto"}}},
                        2, 1, 1, 3e-4)
     assert warmup_lr(0, w) == 0.0 and warmup_lr(1, w) == 3e-4
+
+
+def test_deepspeed_warmup_decay_and_cosine_schedules():
+    """DeepSpeed WarmupDecayLR (linear decay to warmup_min_lr at total_num_steps) and
+    WarmupCosineLR (ratios of the optimizer lr; cosine to cos_min_ratio), both after the
+    WarmupLR warm-up; "auto" total steps come from the trainer's run length."""
+    d = load_ds_config({"scheduler": {"type": "WarmupDecayLR", "params": {
+        "warmup_min_lr": 1e-5, "warmup_max_lr": 1e-3, "warmup_num_steps": 10,
+        "warmup_type": "linear", "total_num_steps": 110}}}, 1, 1, 1, 1e-3)
+    assert d.lr_schedule == "warmup_decay" and d.decay_total_steps == 110
+    assert warmup_lr(0, d) == pytest.approx(1e-5) and warmup_lr(5, d) == pytest.approx(5.05e-4)
+    assert warmup_lr(10, d) == pytest.approx(1e-3)
+    assert warmup_lr(60, d) == pytest.approx(1e-5 + (1e-3 - 1e-5) * 0.5)
+    assert warmup_lr(110, d) == pytest.approx(1e-5) and warmup_lr(500, d) == pytest.approx(1e-5)
+    c = load_ds_config({"optimizer": {"type": "AdamW", "params": {"lr": 2e-4}},
+                        "scheduler": {"type": "WarmupCosineLR", "params": {
+                            "total_num_steps": "auto", "warmup_min_ratio": 0.1,
+                            "warmup_num_steps": 4, "cos_min_ratio": 0.05,
+                            "warmup_type": "linear"}}}, 1, 1, 1, 2e-4)
+    assert c.lr_schedule == "warmup_cosine" and c.decay_total_steps == 0
+    assert warmup_lr(0, c) == pytest.approx(2e-5)
+    c.decay_total_steps = 104
+    assert warmup_lr(4, c) == pytest.approx(2e-4 * (0.05 + 0.95 * 0.5 * (1 + math.cos(math.pi / 100))))
+    assert warmup_lr(53, c) == pytest.approx(2e-4 * (0.05 + 0.95 * 0.5), rel=1e-3)
+    assert warmup_lr(103, c) == pytest.approx(2e-4 * 0.05)
+    with pytest.raises(ValueError):
+        load_ds_config({"scheduler": {"type": "OneCycle"}}, 1, 1, 1, 1e-3)
