@@ -188,7 +188,8 @@ def test_prompt_lookup_speculative_decoding_matches_full_forward():
     m.eval()
     eng = LLMEngine(EngineConfig(model="tiny-llama-gqa", device="cuda", max_model_len=512,
                                  block_size=16, num_blocks=128, use_graphs=True,
-                                 num_speculative_tokens=4), model=m)
+                                 num_speculative_tokens=4, spec_min_fraction=0.0),
+                    model=m)   # verify every draft: exercise the GPU verify path
     prompts = [[5, 9, 33, 7] * 10, list(range(3, 60)) * 2, [42, 43]]
     seqs = [eng.add_request(p, SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True))
             for p in prompts]
