@@ -166,3 +166,22 @@ def test_burst_shares_prompt_blocks_published_at_launch(model, async_sched):
         assert s.output_ids == naive_greedy(model, p, 5), p
     assert eng.blocks.hit_tokens == 4 * 12
     assert eng.blocks.num_free == eng.blocks.num_blocks
+
+
+def test_abort_releases_shared_blocks(model):
+    """Aborting requests that share cached blocks (waiting and running) drops only their
+    references: the cache stays valid for the others and every block comes back."""
+    eng = _engine(model, num_blocks=128, scheduling_policy="prefill_first")
+    eng.generate([SYSTEM + [1, 2]], SamplingParams(max_tokens=2, **GREEDY))
+    a = eng.add_request(SYSTEM + [3, 4], SamplingParams(max_tokens=30, **GREEDY), "a")
+    b = eng.add_request(SYSTEM + [5, 6], SamplingParams(max_tokens=8, **GREEDY), "b")
+    for _ in range(3):
+        eng.step()
+    eng.abort("a")
+    c = eng.add_request(SYSTEM + [7], SamplingParams(max_tokens=4, **GREEDY), "c")
+    eng.abort("c")                                   # aborted while waiting
+    while eng.has_work:
+        eng.step()
+    assert b.output_ids == naive_greedy(model, SYSTEM + [5, 6], 8)
+    assert a.finish_reason == "abort" and c.finish_reason == "abort"
+    assert eng.blocks.num_free == eng.blocks.num_blocks and not eng.blocks.ref
