@@ -239,6 +239,10 @@ def bench_http(a, eng=None) -> dict:
         for p in apis:
             p.join(10)
     res["mode"] = "http"
+    # leak check: every request finished, every KV block back (prefix-cached ones parked)
+    res["kv_blocks"], res["kv_blocks_free_at_end"] = eng.blocks.num_blocks, eng.blocks.num_free
+    res["engine_requests_left"] = len(eng.scheduler.running) + len(eng.scheduler.waiting)
+    res["prefix_hit_rate"] = round(eng.blocks.hit_rate, 4)
     res["api_servers"], res["client_procs"] = n_api, n_cli
     res["prompt_len"], res["max_tokens"] = a.prompt_len, a.max_tokens
     res["http_section_s"] = round(time.time() - t0, 1)
