@@ -120,12 +120,19 @@ class Scheduler:
                 batch.prefills.append((s, c))
                 budget -= c
         whole = self.cfg.policy == "prefill_first"
+        share = self.blocks.prefix_caching
+        pending = set()   # first blocks this batch computes (named when it is launched)
         while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
             s = self.waiting[0]
             if not self.blocks.can_allocate(s.length + 1):
                 break
             if whole and batch.prefills and not self._fits(s, budget):
                 break   # vLLM 0.6 (no chunked prefill): whole prompts only, FCFS
+            d0 = self._first_block(s) if share else None
+            if d0 is not None and d0 in pending and s.params.prompt_logprobs is None:
+                # the same prompt start is being computed by this step (n > 1 choices, a
+                # shared system prompt): wait one step and share its blocks instead
+                break
             self.waiting.popleft()
             # prefix caching: the leading full blocks already in the cache are shared and only
             # the rest of the prompt is computed (0 without it)
@@ -139,7 +146,17 @@ class Scheduler:
             c = min(s.length - s.num_cached, budget)
             batch.prefills.append((s, c))
             budget -= c
+            if d0 is not None and s.num_cached == 0:
+                pending.add(d0)
         return budget
+
+    def _first_block(self, s: Sequence):
+        """Name of the sequence's first full block (None if its prompt has none to share)."""
+        bs = self.blocks.block_size
+        if s.length - 1 < bs:
+            return None
+        from .block_manager import block_digest
+        return block_digest(b"", s.lora_slot, s.all_ids[:bs])
 
     def _fits(self, s: Sequence, budget: int) -> bool:
         """Would ``s``'s whole uncached prompt fit ``budget``?  (Prefix-cache hits are counted

@@ -185,3 +185,17 @@ def test_abort_releases_shared_blocks(model):
     assert b.output_ids == naive_greedy(model, SYSTEM + [5, 6], 8)
     assert a.finish_reason == "abort" and c.finish_reason == "abort"
     assert eng.blocks.num_free == eng.blocks.num_blocks and not eng.blocks.ref
+
+
+@pytest.mark.parametrize("policy", ["prefill_first", "chunked"])
+def test_same_step_duplicates_wait_and_share(model, policy):
+    """A burst whose prompts start alike, all fitting one step: the first computes the shared
+    blocks, the rest wait one step and share them (n > 1 choices, a common system prompt)."""
+    eng = _engine(model, num_blocks=256, scheduling_policy=policy,
+                  max_num_batched_tokens=256)
+    prompts = [SYSTEM + [80 + i] for i in range(4)] + [SYSTEM + [80]] * 2   # 14 tokens each
+    seqs = eng.generate(prompts, SamplingParams(max_tokens=5, **GREEDY))
+    for p, s in zip(prompts, seqs):
+        assert s.output_ids == naive_greedy(model, p, 5), p
+    assert eng.blocks.hit_tokens == 5 * 12        # 3 full blocks, shared by the 5 later ones
+    assert eng.blocks.num_free == eng.blocks.num_blocks
