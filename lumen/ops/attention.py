@@ -463,6 +463,23 @@ def flash_attention_qkv(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int
     return flash_attention_ref(qkv, cu, nh, nkv, D, causal)
 
 
+def flash_attention_fresh(qkv: torch.Tensor, cu, nh: int, nkv: int, D: int, scale: float,
+                          out: torch.Tensor) -> torch.Tensor:
+    """Inference causal attention of whole fresh prompts straight from the rotated fused qkv rows
+    [T, (nh + 2 nkv) D] (the training forward kernel, no autograd), into ``out`` [T, nh D]
+    (row-strided views allowed)."""
+    cu = tuple(int(c) for c in cu)
+    T = qkv.shape[0]
+    q = qkv[:, :nh * D]
+    k = qkv[:, nh * D:(nh + nkv) * D]
+    v = qkv[:, (nh + nkv) * D:(nh + 2 * nkv) * D]
+    lse = torch.empty(nh, T, device=qkv.device, dtype=torch.float32)
+    native().flash_attn(0, True, FA_FWD_MT, q, k, v, out, lse, _cu_tensor(cu, qkv.device),
+                        _tiles(cu, FA_FWD_ROWS, qkv.device), nh, nkv, scale, None, None, None,
+                        None, None, None, None, None)
+    return out
+
+
 def flash_attention_ref(qkv, cu, nh, nkv, D, causal=True):
     outs = []
     for s in range(len(cu) - 1):

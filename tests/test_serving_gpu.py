@@ -204,3 +204,42 @@ def test_prompt_lookup_speculative_decoding_matches_full_forward():
         ref = full[len(p) - 1:].argmax(-1).tolist()
         agree = sum(int(a == b) for a, b in zip(ref, s.output_ids)) / len(ref)
         assert agree >= 0.9, agree
+
+
+@pytest.mark.parametrize("kv", ["auto", "fp8"])
+def test_fresh_prompt_prefill_matches_paged(kv, monkeypatch):
+    """Whole fresh prompts take flash attention straight from the q|k|v rows; the first-token
+    logits equal the paged-cache prefill's (GQA tiny model, several prompts in one step)."""
+    import lumen.serve.model_runner as mr
+    from lumen.models import build_model
+    from lumen.serve.engine import EngineConfig, LLMEngine
+    from lumen.serve.sequence import SamplingParams
+
+    dev = torch.device("cuda", 0)
+    m = build_model("tiny-llama-gqa", dtype=torch.bfloat16, device=dev, init="random", seed=3)
+    m.eval()
+    prompts = [list(range(3, 200)), [5, 9, 33, 7] * 20, list(range(100, 140))]
+
+    def first_logits(fresh):
+        monkeypatch.setattr(mr, "FRESH_PREFILL", fresh)
+        eng = LLMEngine(EngineConfig(model="tiny-llama-gqa", device="cuda", max_model_len=512,
+                                     block_size=16, num_blocks=128, use_graphs=False,
+                                     max_num_batched_tokens=1024, kv_cache_dtype=kv), model=m)
+        got = []
+        orig = eng.runner.execute
+
+        def spy(inp):
+            out = orig(inp)
+            got.append(out.float().clone())
+            return out
+        eng.runner.execute = spy
+        for p in prompts:
+            eng.add_request(p, SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
+        while eng.has_work:
+            eng.step()
+        return got[0]
+
+    a, b = first_logits(True), first_logits(False)
+    assert a.shape == b.shape == (3, m.config.vocab_size)
+    rel = ((a - b).norm() / b.norm()).item()
+    assert rel < 2e-2, rel
