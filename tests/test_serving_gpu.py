@@ -242,4 +242,5 @@ def test_fresh_prompt_prefill_matches_paged(kv, monkeypatch):
     a, b = first_logits(True), first_logits(False)
     assert a.shape == b.shape == (3, m.config.vocab_size)
     rel = ((a - b).norm() / b.norm()).item()
-    assert rel < 2e-2, rel
+    # fp8: the paged path reads e4m3-rounded K/V, the fresh path the 16-bit rows
+    assert rel < (2e-2 if kv == "auto" else 6e-2), rel
