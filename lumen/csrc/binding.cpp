@@ -71,7 +71,7 @@ void lumen_set_rms_lds(int, int);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
                                         const int*, const int*, int, int, int, int, int, int, int,
                                         float, float*, float*, void*, int, unsigned*, int, int,
-                                        hipStream_t);
+                                        int, hipStream_t);
 hipError_t lumen_kv_dequant(int, const void*, const void*, void*, void*, const int*, int,
                             const int*, int, int, int, int, int, hipStream_t);
 hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, const long long*,
@@ -553,6 +553,12 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
   const int num_seqs = static_cast<int>(q.size(0));
   const int nh = static_cast<int>(q.size(1));
   const int D = static_cast<int>(q.size(2));
+  // q may be a view into the fused qkv rows: heads contiguous, rows at any multiple of D
+  if (q.dim() != 3 || q.stride(2) != 1 || q.stride(1) != D || q.stride(0) % D != 0 ||
+      q.stride(0) < static_cast<int64_t>(nh) * D)
+    throw std::invalid_argument("lumen: paged_attention_decode q must be [nseq, nh, D] with "
+                                "contiguous heads");
+  const int qldh = static_cast<int>(q.stride(0) / D);
   unsigned* cnt = nullptr;
   if (counters.has_value()) {
     const at::Tensor& c = *counters;
@@ -569,7 +575,8 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                                      static_cast<int>(tmp_m.size(-1)), static_cast<float>(scale),
                                      tmp_m.data_ptr<float>(), tmp_l.data_ptr<float>(),
                                      tmp_o.data_ptr(), static_cast<int>(partition_size), cnt,
-                                     one_pass ? 1 : 0, is_fp8(k_cache) ? 1 : 0, cur_stream()),
+                                     one_pass ? 1 : 0, is_fp8(k_cache) ? 1 : 0, qldh,
+                                     cur_stream()),
         "paged_attention_decode");
 }
 

@@ -104,7 +104,7 @@ template <typename T, int D, int G>
 __global__ void __launch_bounds__(256) pa_decode_kernel(
     T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
     const T* __restrict__ vc, const int* __restrict__ block_tables,
-    const int* __restrict__ context_lens, int nh, int nkv, int BS, int max_blocks, int max_parts,
+    const int* __restrict__ context_lens, int nh, int qldh, int nkv, int BS, int max_blocks, int max_parts,
     float scale, float* __restrict__ tmp_m, float* __restrict__ tmp_l, float* __restrict__ tmp_o,
     int PART, unsigned* __restrict__ counters) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(256) pa_decode_kernel(
   float qv[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    load8(q + (static_cast<size_t>(seq) * nh + kvh * G + h) * D + d0, qv[h]);
+    load8(q + (static_cast<size_t>(seq) * qldh + kvh * G + h) * D + d0, qv[h]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) qv[h][j] *= scale;
   }
@@ -291,7 +291,7 @@ template <typename T, int D, int G, typename KT = T>
 __global__ void __launch_bounds__(256) pa_decode1_kernel(
     T* __restrict__ out, const T* __restrict__ q, const KT* __restrict__ kc,
     const KT* __restrict__ vc, const int* __restrict__ block_tables,
-    const int* __restrict__ context_lens, int nh, int nkv, int BS, int max_blocks, int max_parts,
+    const int* __restrict__ context_lens, int nh, int qldh, int nkv, int BS, int max_blocks, int max_parts,
     float scale, float* __restrict__ tmp_m, float* __restrict__ tmp_l, float* __restrict__ tmp_o,
     int PART) {
   constexpr int LPT = D / 8;        // lanes per cache row (8 elements each)
@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(256) pa_decode1_kernel(
   float qv[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    load8(q + (static_cast<size_t>(seq) * nh + kvh * G + h) * D + d0, qv[h]);
+    load8(q + (static_cast<size_t>(seq) * qldh + kvh * G + h) * D + d0, qv[h]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) qv[h][j] *= scale;
   }
@@ -543,20 +543,21 @@ __global__ void __launch_bounds__(256) kv_dequant_kernel(
 template <typename T, int D>
 static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out, const void* q,
                         const void* kc, const void* vc, const int* bt, const int* cl, int nh,
-                        int nkv, int BS, int max_blocks, int max_parts, float scale, float* tm,
+                        int qldh, int nkv, int BS, int max_blocks, int max_parts, float scale,
+                        float* tm,
                         float* tl, void* to, int PART, unsigned* cnt, bool one_pass, bool fp8kv) {
 #define LUMEN_PA_G(GG)                                                                         \
   if (fp8kv)                                                                                    \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8>), grid, dim3(256), 0, st, (T*)out,     \
-                       (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, nkv, BS,        \
+                       (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh, nkv, BS,        \
                        max_blocks, max_parts, scale, tm, tl, (float*)to, PART);                 \
   else if (one_pass)                                                                            \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG>), grid, dim3(256), 0, st, (T*)out,          \
-                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, \
+                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, qldh, nkv, BS, max_blocks, \
                        max_parts, scale, tm, tl, (float*)to, PART);                             \
   else                                                                                          \
     hipLaunchKernelGGL((pa_decode_kernel<T, D, GG>), grid, dim3(256), smem, st, (T*)out,       \
-                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, nkv, BS, max_blocks, \
+                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, qldh, nkv, BS, max_blocks, \
                        max_parts, scale, tm, tl, (float*)to, PART, cnt)
   if (G == 1) LUMEN_PA_G(1);
   else if (G == 2) LUMEN_PA_G(2);
@@ -570,16 +571,16 @@ static hipError_t launch_pa(void* out, const void* q, const void* kc, const void
                             const int* bt, const int* cl, int nseq, int nh, int nkv, int D, int BS,
                             int max_blocks, int max_parts, float scale, float* tm, float* tl,
                             void* to, int PART, unsigned* cnt, int one_pass, int fp8kv,
-                            hipStream_t st) {
+                            int qldh, hipStream_t st) {
   const int G = nh / nkv;
   if (fp8kv) one_pass = 1;  // the fp8 cache is read by the single-pass kernel only
   if (G != 1 && G != 2 && G != 4 && G != 8) return hipErrorInvalidValue;
   dim3 grid(nseq, nkv, max_parts);
   const size_t smem = (static_cast<size_t>(G) * PART + 4 * G * D + 2 * G + 8) * sizeof(float);
-  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
-  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
-  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
-  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
   else return hipErrorInvalidValue;
   if (max_parts > 1 && (cnt == nullptr || one_pass)) {  // unfused merge: second kernel
     dim3 g2(nseq, nh), b2(128);
@@ -599,19 +600,22 @@ extern "C" hipError_t lumen_paged_attention_decode(int dtype, void* out, const v
                                                    int max_parts, float scale, float* tmp_m,
                                                    float* tmp_l, void* tmp_o, int PART,
                                                    unsigned* counters, int one_pass,
-                                                   int fp8kv, hipStream_t st) {
+                                                   int fp8kv, int qldh, hipStream_t st) {
   // counters: nullptr = merge split contexts in a second kernel; else >= nseq * nkv zeroed
   // arrival counters (left zeroed again) and the last partition to finish merges in place.
   if (nseq == 0) return hipSuccess;
-  if (nh % nkv != 0 || nh / nkv > lumen::kMaxGroup || PART <= 0) return hipErrorInvalidValue;
+  // qldh: q row stride in heads (nh for a contiguous [nseq, nh, D] q; the fused qkv row's
+  // head count when q is read in place from it)
+  if (nh % nkv != 0 || nh / nkv > lumen::kMaxGroup || PART <= 0 || qldh < nh)
+    return hipErrorInvalidValue;
   if (dtype == lumen::kBF16)
     return lumen::launch_pa<lumen::bf16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, counters, one_pass, fp8kv, st);
+                                         tmp_o, PART, counters, one_pass, fp8kv, qldh, st);
   if (dtype == lumen::kF16)
     return lumen::launch_pa<lumen::fp16>(out, q, kc, vc, block_tables, context_lens, nseq, nh,
                                          nkv, D, BS, max_blocks, max_parts, scale, tmp_m, tmp_l,
-                                         tmp_o, PART, counters, one_pass, fp8kv, st);
+                                         tmp_o, PART, counters, one_pass, fp8kv, qldh, st);
   return hipErrorInvalidValue;
 }
 

@@ -73,7 +73,7 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     nb, nkv, bs, _ = k_cache.shape
     if use_native(q):
         max_parts = max(1, math.ceil(max_context / partition_size))
-        out = torch.empty_like(q)
+        out = torch.empty(num_seqs, nh, D, device=q.device, dtype=q.dtype)
         if max_parts > 1:
             tm = torch.empty(num_seqs, nh, max_parts, device=q.device, dtype=torch.float32)
             tl = torch.empty_like(tm)
@@ -85,7 +85,11 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         fused = bool(fused_merge) and not one
         cnt = (_pa_counters(q.device, num_seqs * nkv) if fused and max_parts > 1
                else None)
-        native().paged_attention_decode(out, q.contiguous(), k_cache, v_cache, block_tables,
+        # q read in place when its heads are contiguous (a view into the fused qkv rows):
+        # no per-layer copy of the decode rows' q
+        qk = q if (q.stride(2) == 1 and q.stride(1) == D and q.stride(0) % D == 0
+                   and q.data_ptr() % 16 == 0) else q.contiguous()
+        native().paged_attention_decode(out, qk, k_cache, v_cache, block_tables,
                                         context_lens, nkv, bs, block_tables.shape[1], scale, tm,
                                         tl, to, partition_size, cnt, one)
         return out
