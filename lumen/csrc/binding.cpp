@@ -549,7 +549,8 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                             int64_t max_blocks_per_seq, double scale, at::Tensor& tmp_m,
                             at::Tensor& tmp_l, at::Tensor& tmp_o, int64_t partition_size,
                             const std::optional<at::Tensor>& counters, bool one_pass) {
-  need_cuda(q, "q"); need_cuda(out, "out");
+  if (!q.is_cuda()) throw std::invalid_argument("lumen: q must be a GPU tensor");
+  need_cuda(out, "out");
   const int num_seqs = static_cast<int>(q.size(0));
   const int nh = static_cast<int>(q.size(1));
   const int D = static_cast<int>(q.size(2));
