@@ -77,7 +77,8 @@ def train_worker(rank, world, port, stage, outdir, model="tiny-llama", micro=2, 
     shutdown()
 
 
-def serve_tp_worker(rank, world, port, outdir, loras=None, async_sched=True, cap=None):
+def serve_tp_worker(rank, world, port, outdir, loras=None, async_sched=True, cap=None,
+                    extra=None):
     """TP serving on gloo: rank 0 runs the engine, rank 1 the worker loop; greedy outputs of
     rank 0 are saved for comparison with a single-process engine."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -98,10 +99,16 @@ def serve_tp_worker(rank, world, port, outdir, loras=None, async_sched=True, cap
     model = _tp_test_model()
     cfg = EngineConfig(model="tiny-llama-gqa", device="cpu", max_model_len=128, block_size=4,
                        use_graphs=False, num_blocks=128, tp_size=world, lora_modules=loras,
-                       async_scheduling=async_sched)
+                       async_scheduling=async_sched, **(extra or {}))
     eng = LLMEngine(cfg, model=model)
     if rank == 0:
         prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
+        if (extra or {}).get("enable_prefix_caching"):
+            # a finished request's blocks: the later prompts share its first 24 tokens
+            warm = eng.add_request(list(range(3, 30)) + [1], SamplingParams(
+                max_tokens=2, temperature=0.0, ignore_eos=True))
+            while not warm.finished:
+                eng.step()
         sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
         names = list(loras or {}) + [None] * 3
         seqs = [eng.add_request(p, SamplingParams(**vars(sp)), lora=names[i])
@@ -109,7 +116,9 @@ def serve_tp_worker(rank, world, port, outdir, loras=None, async_sched=True, cap
         while any(not s.finished for s in seqs):
             eng.step()
         eng.shutdown()
-        assert eng.async_sched == async_sched
+        assert eng.async_sched == (async_sched and not (extra or {}).get("num_speculative_tokens"))
+        if (extra or {}).get("enable_prefix_caching"):
+            assert eng.blocks.hit_tokens > 0
         torch.save([s.output_ids for s in seqs], os.path.join(outdir, "tp_out.pt"))
     else:
         worker_loop(eng.runner)

@@ -153,6 +153,31 @@ def test_tensor_parallel_serving_gloo(tmp_path, async_sched, cap):
         assert out == naive_greedy(ref_model, p, 8), p
 
 
+@pytest.mark.parametrize("extra", [{"enable_prefix_caching": True},
+                                   {"num_speculative_tokens": 3, "spec_min_fraction": 0.0}])
+def test_tensor_parallel_serving_features_gloo(tmp_path, extra):
+    """TP=2 over gloo with prefix caching (shared blocks in rank 0's tables, broadcast to the
+    worker) and with prompt-lookup speculative decoding (verify steps broadcast as mixed steps):
+    greedy outputs equal single-process full-recompute decoding."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from tests._dist_worker import _tp_test_model, serve_tp_worker
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(serve_tp_worker, args=(2, port, str(tmp_path), None, True, None, extra),
+                       nprocs=2, join=True, start_method="spawn")
+    got = torch.load(tmp_path / "tp_out.pt", weights_only=True)
+    ref_model = _tp_test_model()
+    prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
+    for p, out in zip(prompts, got):
+        assert out == naive_greedy(ref_model, p, 8), p
+
+
 def test_serve_cli_engine_core_split(tmp_path):
     """scripts/serve.py on CPU: API in a spawned process, engine core in the main one."""
     import os
