@@ -81,7 +81,10 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--gradient_checkpointing", default="auto",
                     choices=["auto", "true", "false", "selective", "full"],
-                    help="per-layer recompute (the reference always enables it).  auto: on only "
+                    help="activation recompute (the reference always enables it).  true = the "
+                         "model's default policy (Llama: 'selective', the gate|up output "
+                         "recomputed; layers whose MLP is trainable or adapted are recomputed "
+                         "whole, as 'full'); full = per-layer recompute like HF; auto: on only "
                          "when the estimated activations do not fit in free HBM (logged)")
     ap.add_argument("--no_gradient_checkpointing", action="store_true",
                     help="same as --gradient_checkpointing false")

@@ -122,6 +122,12 @@ PRESETS = {
     "llama2-7b-2l": dict(arch="llama", vocab_size=32000, hidden_size=4096, intermediate_size=11008,
                          num_hidden_layers=2, num_attention_heads=32, num_key_value_heads=32,
                          max_position_embeddings=4096, name="llama2-7b-2l"),
+    # Llama-2-70B layer shapes (H 8192, GQA 64 / 8 heads, F 28672, vocab 32000) at depth 2:
+    # world-8 rehearsals of BASELINE config 5's per-layer shapes on one shared GPU
+    "llama2-70b-2l": dict(arch="llama", vocab_size=32000, hidden_size=8192,
+                          intermediate_size=28672, num_hidden_layers=2, num_attention_heads=64,
+                          num_key_value_heads=8, max_position_embeddings=4096,
+                          name="llama2-70b-2l"),
     # facebook/opt-125m
     "opt-125m": dict(arch="opt", vocab_size=50272, hidden_size=768, intermediate_size=3072,
                      ffn_dim=3072, num_hidden_layers=12, num_attention_heads=12,

@@ -100,12 +100,17 @@ class LlamaMLP(nn.Module):
         self.down_proj = Linear(Fd, H, dtype=dtype, device=device, seg_names=["down_proj"])
         self.recompute = False  # selective checkpointing: gate|up output recomputed in backward
 
+    @property
+    def recompute_eligible(self) -> bool:
+        """Selective recompute needs frozen gate|up / down weights without active adapters
+        (``recompute_mlp`` re-runs only the frozen gate|up GEMM in the backward)."""
+        gu, dn = self.gate_up_proj, self.down_proj
+        return not (gu.has_active_lora or dn.has_active_lora or gu.weight.requires_grad
+                    or dn.weight.requires_grad)
+
     def forward(self, x2d):
         gu, dn = self.gate_up_proj, self.down_proj
-        if (self.recompute and self.training and torch.is_grad_enabled()
-                and not gu.has_active_lora
-                and not dn.has_active_lora and not gu.weight.requires_grad
-                and not dn.weight.requires_grad):
+        if self.recompute and self.training and torch.is_grad_enabled() and self.recompute_eligible:
             return recompute_mlp(x2d, gu, dn)
         return dn(swiglu(gu(x2d)))
 
@@ -154,7 +159,25 @@ class LlamaForCausalLM(nn.Module):
         (the layer's largest saved tensor: ~35% of its activation memory for ~one extra
         projection GEMM per layer); ``"full"`` -- the reference's per-layer recompute (HF
         ``gradient_checkpointing=True``: the layer input only, the whole forward re-run).
-        Assigning True picks ``LUMEN_CKPT_POLICY`` (default ``selective``), False ``none``."""
+        Assigning True picks ``LUMEN_CKPT_POLICY`` (default ``selective``), False ``none``.
+
+        A layer whose MLP cannot use the selective recompute (trainable gate|up / down weights,
+        or adapters on them) is checkpointed whole instead (``full`` for that layer), so asking
+        for checkpointing never silently keeps every activation."""
+        return self._ckpt
+
+    def selective_eligible(self) -> bool:
+        """True when every layer can run the ``selective`` policy as such."""
+        return all(l.mlp.recompute_eligible for l in self.layers)
+
+    def _layer_policy(self, layer) -> str:
+        if self._ckpt == "selective" and not layer.mlp.recompute_eligible:
+            if not getattr(self, "_warned_selective", False):
+                self._warned_selective = True
+                import sys
+                print("[lumen] selective checkpointing: MLP weights are trainable or adapted, "
+                      "those layers fall back to full per-layer recompute", file=sys.stderr)
+            return "full"
         return self._ckpt
 
     @gradient_checkpointing.setter
@@ -217,7 +240,8 @@ class LlamaForCausalLM(nn.Module):
                            input_ids.reshape(-1))
         res = None
         for i, layer in enumerate(self.layers):
-            if self._ckpt == "full" and self.training and torch.is_grad_enabled():
+            if (self._ckpt != "none" and self.training and torch.is_grad_enabled()
+                    and self._layer_policy(layer) == "full"):
                 fn = lambda h_, r_, L=layer: cp.checkpoint(L, h_, r_, B, S, pos, cu, use_reentrant=False)  # noqa: E731
             else:
                 fn = lambda h_, r_, L=layer: L(h_, r_, B, S, pos, cu)  # noqa: E731

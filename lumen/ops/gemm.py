@@ -62,7 +62,9 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int, nw: 
                                                 dtype=x.dtype)
     ws = cnt = None
     if s > 1:
-        key = str(x.device)
+        # one slab workspace + ticket counters per (device, stream): split-K slabs and tickets
+        # of GEMMs on different streams never interleave (a side-stream GEMM gets its own)
+        key = _dg_key(x.device)
         got = _dg_ws.get(key)
         need = -(-w.shape[0] // bn) * s * bm * bn
         if got is None or got[0].numel() < need or got[1].numel() < -(-w.shape[0] // bn):
@@ -78,6 +80,16 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int, nw: 
         ws, cnt = got
     native().decode_gemm(x, w, y, ws, cnt, bm, bn, s, nw)
     return y
+
+
+def _dg_key(device) -> tuple:
+    return (str(device), torch.cuda.current_stream(device).cuda_stream)
+
+
+def dg_workspace(device) -> Optional[tuple]:
+    """(slab workspace, ticket counters) of the current stream on ``device`` (None before the
+    first split-K call there)."""
+    return _dg_ws.get(_dg_key(device))
 
 
 def dg_plans() -> dict:

@@ -61,6 +61,7 @@ class BlockManager:
         self.name: Dict[int, bytes] = {}                 # block -> digest
         self.parked: "OrderedDict[int, None]" = OrderedDict()  # named, unreferenced (LRU first)
         self.chains: Dict[Optional[int], List[bytes]] = {}   # seq -> names of its full blocks
+        self.stale: set = set()  # running sequences whose K/V predate a reset: never published
         self.hit_tokens = 0
         self.query_tokens = 0
 
@@ -104,7 +105,7 @@ class BlockManager:
         written by steps already launched, so any later step may read them).  A block whose
         content is already cached under another id stays unnamed."""
         tbl = self.tables.get(seq_id)
-        if not self.prefix_caching or not tbl:
+        if not self.prefix_caching or not tbl or seq_id in self.stale:
             return
         nfull = min(n_computed, len(token_ids), len(tbl) * self.block_size) // self.block_size
         for b, d in zip(tbl[:nfull], self._digests(token_ids, nfull, lora, seq_id)):
@@ -169,6 +170,7 @@ class BlockManager:
             return
         if token_ids is not None:
             self.publish(seq_id, token_ids, n_computed, lora)
+        self.stale.discard(seq_id)
         self.chains.pop(seq_id, None)
         tbl = self.tables.pop(seq_id, None)
         if not tbl:
@@ -186,11 +188,14 @@ class BlockManager:
 
     def reset_prefix_cache(self) -> None:
         """Forget every block's name (the cache's content is no longer trusted, e.g. after the
-        weights changed): parked blocks become free, blocks in use are freed unnamed."""
+        weights changed): parked blocks become free; blocks in use are freed unnamed, and the
+        sequences holding them never publish (their K/V were computed before the reset)."""
         self.free.extend(reversed(list(self.parked)))
         self.parked.clear()
         self.cached.clear()
         self.name.clear()
+        self.chains.clear()
+        self.stale.update(self.tables)
 
     def usage(self) -> float:
         return 1.0 - self.num_free / max(self.num_blocks, 1)

@@ -79,6 +79,10 @@ class EngineConfig:
     # when at least this fraction of the decode rows has a draft; a sequence whose drafts were
     # all rejected backs off (1, 3, 7 .. 63 steps) before it drafts again
     spec_min_fraction: float = 0.5
+    # the prompt-lookup index covers the n-grams of the last ngram_window tokens of a sequence
+    # (int keys, pruned as the window slides): at most ngram_window * (ngram_max - ngram_min + 1)
+    # dict entries per sequence -- 4 * 1024 with the defaults, ~0.4 MB; 256 sequences ~100 MB
+    ngram_window: int = 1024
 
 
 _DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -594,32 +598,51 @@ class LLMEngine:
         return sampled
 
     # ---- speculative decoding (prompt lookup) ----------------------------------------------
+    @staticmethod
+    def _ngram_key(ids: List[int], a: int, b: int) -> int:
+        return hash(tuple(ids[a:b]))
+
     def _lookup(self, ids: List[int], k: int, s: Optional[Sequence] = None) -> List[int]:
         """Up to k tokens that followed the most recent earlier occurrence of the sequence's
-        last n tokens (n = ngram_max .. ngram_min).  The n-gram index of ``s`` is extended
-        incrementally (a few dict updates per new token: O(1) per sequence and step, where a
-        scan of the history cost ~60 us per sequence, 15 ms per 256-row step)."""
+        last n tokens (n = ngram_max .. ngram_min) within its last ``ngram_window`` tokens.
+        The n-gram index of ``s`` (int hash of the n-gram -> position after it) is extended
+        incrementally -- a few dict updates per new token, where a scan of the history cost
+        ~60 us per sequence, 15 ms per 256-row step -- and pruned as the window slides, so its
+        size is bounded.  A hash collision can only propose a wrong draft, which the verify
+        step rejects (outputs stay identical to plain decoding)."""
         lo, hi = max(1, self.cfg.ngram_min), self.cfg.ngram_max
+        W = max(1, int(self.cfg.ngram_window))
         idx = s.ngram_idx if s is not None else {}
         upto = s.ngram_upto if s is not None else 0
         L = len(ids)
-        for p in range(upto, L - 1):          # n-grams ending before the current suffix
+        start = max(upto, L - 1 - W)
+        key = self._ngram_key
+        for p in range(start, L - 1):          # n-grams ending before the current suffix
             for n in range(lo, min(hi, p + 1) + 1):
-                idx[tuple(ids[p - n + 1:p + 1])] = p + 1
+                idx[key(ids, p - n + 1, p + 1)] = p + 1
         if s is not None:
+            # n-grams ending before the window start leave the index (unless a later
+            # occurrence has taken the key over)
+            for p in range(max(0, upto - W - 1), max(0, L - 1 - W)):
+                for n in range(lo, min(hi, p + 1) + 1):
+                    kk = key(ids, p - n + 1, p + 1)
+                    if idx.get(kk) == p + 1:
+                        del idx[kk]
             s.ngram_upto = max(upto, L - 1)
         for n in range(min(hi, L - 1), lo - 1, -1):
-            j = idx.get(tuple(ids[L - n:]))
-            if j is not None:
+            j = idx.get(key(ids, L - n, L))
+            if j is not None and j < L:
                 return ids[j:j + k]
         return []
 
     def _propose(self, batch: Batch) -> bool:
         """Drafts for the greedy decode rows of ``batch`` (``Sequence.draft``), their KV slots
-        reserved; False when nothing was drafted."""
+        reserved; False when nothing was drafted.  The spec_min_fraction check and the token
+        budget (verify rows + plain decode rows <= max_num_batched_tokens) are applied BEFORE
+        any block is reserved, so dropped drafts never grow a table or evict cached blocks."""
         if any(s.params.wants_extras for s in batch.decodes):
             return False                      # alternatives are computed on the plain path
-        drafted = []
+        cand = []
         for s in batch.decodes:
             p = s.params
             if p.temperature > 0 or p.has_penalties or p.wants_extras:
@@ -632,19 +655,30 @@ class LLMEngine:
             if room <= 0:
                 continue
             d = self._lookup(s.all_ids, room, s)
+            if d:
+                cand.append((s, d))
+        # budget: every decode row costs 1, a draft adds len(d) verify rows
+        spare = self.cfg.max_num_batched_tokens - len(batch.decodes)
+        kept = []
+        for s, d in cand:
+            d = d[:max(0, spare)]
             if not d:
-                continue
-            try:
-                self.blocks.ensure(s.seq_id, s.length + len(d) + 1)
-            except RuntimeError:
-                continue                      # no blocks for the draft: plain decode row
-            s.draft = d
-            drafted.append(s)
-        if drafted and len(drafted) < self.cfg.spec_min_fraction * len(batch.decodes):
-            for s in drafted:             # too few drafts to pay for a verify step
-                s.draft = []
+                break
+            spare -= len(d)
+            kept.append((s, d))
+        if not kept or len(kept) < self.cfg.spec_min_fraction * len(batch.decodes):
+            for s, _ in cand:             # too few drafts to pay for a verify step
                 s.spec_wait = 3           # (and look again in a few steps, not every step)
             return False
+        drafted = []
+        for s, d in kept:
+            need = s.length + len(d) + 1
+            extra = self.blocks.blocks_needed(need) - len(self.blocks.tables.get(s.seq_id, []))
+            if extra > self.blocks.num_free:
+                continue                      # no blocks for the draft: plain decode row
+            self.blocks.ensure(s.seq_id, need)
+            s.draft = d
+            drafted.append(s)
         return bool(drafted)
 
     def _run_verify(self, batch: Batch) -> List[Sequence]:

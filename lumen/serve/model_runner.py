@@ -370,7 +370,10 @@ class ModelRunner:
             st["lora_ids"] = torch.zeros(bucket, dtype=torch.int32, device=dev)
         args = (st["tokens"], st["positions"], st["slots"], st["block_tables"],
                 st["context_lens"], self.max_model_len, st.get("lora_ids"), self._graph_gathers)
-        s = torch.cuda.Stream()
+        # one warm-up stream for every bucket (per-stream decode-GEMM workspaces stay few)
+        s = getattr(self, "_warm_stream", None)
+        if s is None:
+            s = self._warm_stream = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up (allocator, hipBLASLt heuristics) outside capture

@@ -156,9 +156,12 @@ class Trainer:
         if co is not None:
             free = max(0, free - co.pending_alloc_bytes())
         pols = getattr(type(self.model), "CKPT_POLICIES", None)
+        # selective only where every layer's MLP can recompute (frozen, unadapted gate|up/down)
+        sel_ok = bool(pols and "selective" in pols
+                      and getattr(self.model, "selective_eligible", lambda: False)())
         if 2 * est <= free:
             pick = False
-        elif pols and "selective" in pols and 2 * 0.65 * est <= free:
+        elif sel_ok and 2 * 0.65 * est <= free:
             pick = "selective"
         else:
             pick = "full" if pols and "full" in pols else True

@@ -670,7 +670,7 @@ def test_decode_gemm_variants(bm):
     variant, split-K 1 / 2 / 3 (in-launch slab reduction, counters left zeroed for the next
     launch), a ragged last column tile, M below the block height, strided x rows, fp16."""
     from lumen.ops._native import native
-    from lumen.ops.gemm import DG_BNS, DG_BNS8, _dg_ws, decode_gemm
+    from lumen.ops.gemm import DG_BNS, DG_BNS8, decode_gemm, dg_workspace
 
     g = torch.Generator(device="cpu").manual_seed(bm)
     K = 640
@@ -686,12 +686,21 @@ def test_decode_gemm_variants(bm):
                     assert y.shape == (M, N)
                     assert rel(y, ref) < 1e-2, (bm, bn, nw, N, M, s, rel(y, ref))
                     if s > 1:  # the tile counters are zero again after the launch
-                        assert int(_dg_ws[str(x.device)][1].abs().sum()) == 0
+                        assert int(dg_workspace(x.device)[1].abs().sum()) == 0
     # fp16 operands
     w = (torch.randn(256, K, generator=g) * 0.05).to(DEV, torch.float16)
     x = torch.randn(bm - 3, K, generator=g).to(DEV, torch.float16)
     y = decode_gemm(x, w, bm, DG_BNS[bm][0], 2)
     assert rel(y, x.float() @ w.float().t()) < 1e-2
+    # a split-K GEMM on a side stream gets a workspace of its own
+    main_ws = dg_workspace(x.device)[0].data_ptr()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        y2 = decode_gemm(x, w, bm, DG_BNS[bm][0], 2)
+        assert dg_workspace(x.device)[0].data_ptr() != main_ws
+    torch.cuda.current_stream().wait_stream(side)
+    assert torch.equal(y2, y)
     # argument checks fail loudly (M above the block height)
     with pytest.raises(Exception):
         native().decode_gemm(torch.randn(bm + 1, K, device=DEV).to(torch.bfloat16),

@@ -100,3 +100,35 @@ def test_sparse_segments_q_v_only():
     ref[:, q_off:q_off + q_len] += lin.lora.scale * (x @ qA.t()) @ qB.t()
     ref[:, v_off:v_off + v_len] += lin.lora.scale * (x @ vA.t()) @ vB.t()
     assert torch.allclose(y, ref, atol=1e-5)
+
+
+def test_checkpointing_true_never_silently_off(monkeypatch):
+    """``gradient_checkpointing=True`` picks ``selective``, which can only
+    recompute frozen, unadapted MLPs.  With adapters on gate/up/down every layer must fall back
+    to a whole-layer recompute instead of keeping every activation."""
+    import lumen.models.llama as L
+
+    calls = []
+    real = L.cp.checkpoint
+
+    def counting(fn, *a, **k):
+        calls.append(fn)
+        return real(fn, *a, **k)
+
+    monkeypatch.setattr(L.cp, "checkpoint", counting)
+    torch.manual_seed(0)
+    ids = torch.randint(0, 100, (2, 16))
+    labels = ids.clone()
+    for targets, eligible in ((["q_proj", "v_proj"], True),
+                              (["q_proj", "gate_proj", "down_proj"], False)):
+        m = build_model("tiny-llama", dtype=torch.float32, init="random")
+        apply_lora(m, LoraConfig(r=4, target_modules=targets))
+        m.gradient_checkpointing = True
+        m.train()
+        assert m.gradient_checkpointing == "selective"
+        assert m.selective_eligible() is eligible
+        calls.clear()
+        m(ids, labels).backward()
+        # eligible: the MLP recomputes its gate|up itself, no whole-layer checkpoint;
+        # not eligible: one whole-layer checkpoint per layer
+        assert len(calls) == (0 if eligible else m.config.num_hidden_layers)

@@ -51,6 +51,20 @@ def test_only_computed_blocks_are_published_and_duplicates_released():
     assert not bm.cached and not bm.parked and bm.num_free == 16
 
 
+def test_reset_never_publishes_blocks_computed_before_it():
+    """A sequence running across ``reset_prefix_cache`` holds K/V of the old weights: freeing it
+    afterwards must not name its blocks."""
+    bm = BlockManager(16, 4, watermark=0.0, prefix_caching=True)
+    ids = list(range(10))
+    bm.allocate(1, 11, ids)
+    bm.reset_prefix_cache()
+    bm.free_seq(1, ids, n_computed=10)
+    assert not bm.cached and not bm.parked and bm.num_free == 16
+    assert bm.allocate(2, 11, ids) == 0              # no hit on pre-reset content
+    bm.free_seq(2, ids, n_computed=10)               # a post-reset sequence publishes again
+    assert len(bm.cached) == 2 and not bm.stale
+
+
 def test_eviction_is_lru_and_tail_first():
     bm = BlockManager(5, 2, watermark=0.0, prefix_caching=True)
     a, b = [1, 2, 3, 4, 5], [6, 7, 8, 9, 10, 11, 12]

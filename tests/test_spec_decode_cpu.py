@@ -119,3 +119,26 @@ def test_stop_token_inside_accepted_draft(model):
     s2 = eng.generate([p], SamplingParams(max_tokens=7, **GREEDY))[0]
     assert s2.output_ids == ref[:7] and s2.finish_reason == "length"
     assert eng.blocks.num_free == eng.blocks.num_blocks
+
+
+def test_lookup_index_is_windowed_and_bounded():
+    """the per-sequence n-gram index is bounded by ngram_window (pruned as it
+    slides) and still finds a repeat inside the window."""
+    from types import SimpleNamespace
+
+    from lumen.serve.engine import EngineConfig, LLMEngine
+
+    eng = SimpleNamespace(cfg=EngineConfig(ngram_window=64, ngram_max=4, ngram_min=1),
+                          _ngram_key=LLMEngine._ngram_key)
+    s = SimpleNamespace(ngram_idx={}, ngram_upto=0)
+    ids = list(range(1000, 1600))                       # 600 distinct tokens
+    for L in range(2, len(ids) + 1, 7):
+        LLMEngine._lookup(eng, ids[:L], 3, s)
+    LLMEngine._lookup(eng, ids, 3, s)
+    assert len(s.ngram_idx) <= 64 * 4 + 8
+    # a repeat of a recent n-gram is proposed, one from before the window is not
+    rec = ids + ids[-10:-8]
+    assert LLMEngine._lookup(eng, rec, 3, s) == ids[-8:-5]
+    s2 = SimpleNamespace(ngram_idx={}, ngram_upto=0)
+    old = ids + ids[5:7]
+    assert LLMEngine._lookup(eng, old, 3, s2) == []
