@@ -158,6 +158,10 @@ def run_serve_tp(args, env) -> dict:
                      "scheduling_policy": a.scheduling_policy,
                      "max_num_batched_tokens": a.max_batched_tokens, "kv_cache_dtype": "bf16",
                      "custom_allreduce": eng.runner.car is not None, "mode": "in-process engine"}
+    car = eng.runner.car
+    if car is not None and car.calibration is not None:
+        # the crossovers measured on this TP group at engine start (replaces guessed limits)
+        out["car_plan"] = car.calibration
     return out
 
 
@@ -259,6 +263,96 @@ def run_partitioned(args, env, ds_base, batches, schedule: str, max_live: float,
     return out
 
 
+def run_comm_probe(env, gather_group=None, unit_mb: float = 386.0, bucket_numel: int = 2_000_000,
+                   car_sizes=(8 << 10, 256 << 10, 2 << 20), iters: int = 5) -> dict:
+    """N > 1: what the transport itself delivers, so a sub-linear scaling record says whether
+    the links or the schedule are at fault (Next #4).  Collective on every rank.
+
+    * ``all_gather``: one Llama-2-7B decoder unit (386 MiB of bf16) gathered with
+      ``all_gather_into_tensor`` on the weight-gather communicator (the default group when the
+      schedule has none) -- time, algorithm GB/s (bytes / time) and bus GB/s (x (W-1)/W, the
+      nccl-tests convention: the per-rank link load a ring or mesh must carry);
+    * ``reduce_scatter``: one LoRA gradient bucket (2e6 fp32 elements, SURVEY X5);
+    * ``allreduce``: custom one-shot / two-shot vs RCCL all-reduce latency at the TP decode
+      message sizes (GPU only: the IPC kernel needs the native extension).
+    Times are the max over ranks of the mean over ``iters`` calls after one warm-up call."""
+    import torch
+    import torch.distributed as dist
+
+    W = env.world_size
+    on_gpu = env.device.type == "cuda"
+    dev = env.device
+    res = {"world": W}
+
+    def timed(fn):
+        fn()
+        if on_gpu:
+            torch.cuda.synchronize()
+        dist.barrier()
+        t = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        if on_gpu:
+            torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / iters
+        x = torch.tensor([dt], dtype=torch.float64, device=dev if on_gpu else "cpu")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        return float(x.item())
+
+    dt_bf = torch.bfloat16 if on_gpu else torch.float32
+    esz = torch.empty((), dtype=dt_bf).element_size()
+    n = int(unit_mb * 2**20 / esz) // W * W
+    shard = torch.ones(n // W, dtype=dt_bf, device=dev)
+    full = torch.empty(n, dtype=dt_bf, device=dev)
+    t = timed(lambda: dist.all_gather_into_tensor(full, shard, group=gather_group))
+    nbytes = n * esz
+    res["all_gather"] = {"mib": round(nbytes / 2**20, 1), "ms": round(t * 1e3, 3),
+                         "algbw_gbps": round(nbytes / t / 1e9, 1),
+                         "busbw_gbps": round(nbytes / t / 1e9 * (W - 1) / W, 1),
+                         "group": "weight-gather" if gather_group is not None else "default"}
+    del shard, full
+    m = bucket_numel // W * W
+    g = torch.ones(m, dtype=torch.float32, device=dev)
+    o = torch.empty(m // W, dtype=torch.float32, device=dev)
+    t = timed(lambda: dist.reduce_scatter_tensor(o, g))
+    res["reduce_scatter"] = {"numel": m, "ms": round(t * 1e3, 3),
+                             "busbw_gbps": round(m * 4 / t / 1e9 * (W - 1) / W, 1)}
+    del g, o
+    if on_gpu:
+        try:
+            from lumen.parallel.custom_ar import CustomAllReduce
+
+            car = CustomAllReduce(None, dev, max_bytes=max(car_sizes))
+            try:
+                cal = car.calibrate(rccl_group=dist.group.WORLD, sizes=car_sizes, apply=False)
+            finally:
+                car.close()
+            res["allreduce_us"] = cal["table"]
+            res["allreduce_plan"] = cal["plan"]
+        except Exception as e:  # noqa: BLE001 - the RCCL numbers stand
+            res["allreduce_us"] = {"error": repr(e)[:300]}
+    return res
+
+
+def _with_link_time(parts: dict, comm, world: int) -> dict:
+    """Per partitioned schedule: the link time its per-step gather volume implies at the
+    probe's measured all-gather bus bandwidth (each rank receives (W-1)/W of every gathered
+    unit), next to the measured step and exposed wait -- comm-bound vs schedule-bound."""
+    try:
+        bus = comm["all_gather"]["busbw_gbps"] if comm else None
+    except (KeyError, TypeError):
+        bus = None
+    out = {}
+    for k, v in parts.items():
+        v = dict(v)
+        if bus and "gathered_mb_per_step" in v and world > 1:
+            v["probe_busbw_gbps"] = bus
+            v["implied_link_ms_per_step"] = round(
+                v["gathered_mb_per_step"] * 1e6 * (world - 1) / world / (bus * 1e9) * 1e3, 2)
+        out[k] = v
+    return out
+
+
 def _provenance():
     try:
         from lumen.ops._native import provenance
@@ -319,6 +413,13 @@ def main():
     ap.add_argument("--serve_tp_deadline", type=float, default=420.0,
                     help="seconds the TP serving section may take: past it rank 0 prints the "
                          "JSON line with extra.serve_tp = an error, and every rank exits")
+    ap.add_argument("--comm_probe", dest="comm_probe", action="store_true", default=True,
+                    help="(default) at N > 1, after the timed steps: RCCL all-gather / "
+                         "reduce-scatter bandwidth and custom vs RCCL all-reduce latency -> "
+                         "extra.comm")
+    ap.add_argument("--no_comm_probe", dest="comm_probe", action="store_false")
+    ap.add_argument("--comm_probe_cpu_mb", type=float, default=8.0,
+                    help="all-gather size of the probe on CPU / gloo runs (GPU: 386 MiB)")
     ap.add_argument("--partitioned_steps", type=int, default=5,
                     help="timed steps of each partitioned run (2 untimed warm-up steps first)")
     args = ap.parse_args()
@@ -490,6 +591,15 @@ def main():
     zstats = coord.stats() if coord else None
     if wd is not None:
         wd.close()
+    comm = None
+    if world > 1 and args.comm_probe:
+        # after (and outside) the timed region: the transport's own numbers
+        try:
+            comm = run_comm_probe(env, engine.gather_group,
+                                  unit_mb=386.0 if on_gpu else args.comm_probe_cpu_mb)
+        except Exception as e:  # noqa: BLE001 - keep the headline result
+            comm = {"error": repr(e)[:300]}
+            raise  # ranks may disagree on where they failed: do not continue collectives
     serve = serve_engine = serve_chunked = None
     parts = {}
     want_parts = [x for x in args.partitioned.split(",") if x] if ds.stage == 3 else []
@@ -568,7 +678,8 @@ def main():
                 "gemm_algos": gemm_table,
                 "native_build": _provenance(),
                 "gemm_table_entries": tuned_entries() if gemm_table != "heuristic" else 0,
-                **{f"zero3_{k}": v for k, v in parts.items()},
+                "comm": comm,
+                **{f"zero3_{k}": v for k, v in _with_link_time(parts, comm, world).items()},
                 "serve": serve,
                 "serve_engine": serve_engine,
                 "serve_chunked": serve_chunked,

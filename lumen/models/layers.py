@@ -309,8 +309,9 @@ def _transpose_budget(model: nn.Module) -> float:
     # blocks the caching allocator holds but no tensor uses (e.g. init temporaries) are free
     # for the W^T copies too (mem_get_info counts them as used)
     free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-    reserve = float(os.environ.get("LUMEN_BWD_WT_RESERVE_GB", "0")) * 2**30 or max(48 * 2**30, 0.25 * total)
-    return max(0.0, free - reserve)
+    from ..parallel.memory_plan import activation_reserve
+
+    return max(0.0, free - activation_reserve(total, "LUMEN_BWD_WT_RESERVE_GB"))
 
 
 def invalidate_weight_caches(model: nn.Module) -> None:

@@ -24,6 +24,13 @@ Use ``eligible(t)`` to decide whether a tensor goes here or to RCCL. The tensor 
 
 Messages up to ``one_shot_max`` bytes use one-shot (every rank reads all peers); larger ones
 use two-shot (reduce-scatter then all-gather through the same buffers).
+
+``calibrate()`` replaces the guessed crossovers with measured ones: on the real group it times
+one-shot, two-shot and RCCL at a ladder of message sizes (max over ranks), then ``pick_plan``
+sets ``one_shot_max`` (one- vs two-shot) and ``rccl_from`` (the smallest size from which RCCL
+won: eager calls of that size and up go to RCCL; captured decode graphs keep the custom
+kernel, since RCCL is not captured).  The serving engine calibrates at TP start-up and the
+bench reports the table (``extra.serve_tp.car_plan``).
 """
 from __future__ import annotations
 
@@ -46,6 +53,34 @@ def _default_one_shot_max(world: int) -> int:
     # one-shot reads (W-1)·n over the links vs 2(W-1)/W·n for two-shot plus one more barrier;
     # the crossover moves down as W grows
     return {2: 1 << 20, 4: 512 << 10}.get(world, 256 << 10)
+
+
+CAL_SIZES = (8 << 10, 32 << 10, 128 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20,
+             8 << 20)
+
+
+def pick_plan(table: List[dict], margin: float = 0.03) -> dict:
+    """Crossovers from a calibration table (rows ``{"bytes", "one", "two"[, "rccl"]}``, times in
+    us, sorted by size).  ``one_shot_max``: the largest size below the first one at which
+    two-shot beats one-shot by more than ``margin`` (every size when it never does);
+    ``rccl_from``: the smallest size from which RCCL beats the better custom variant by more than
+    ``margin`` at that size and every larger one (None: the custom kernel wins throughout)."""
+    rows = sorted(table, key=lambda r: r["bytes"])
+    if not rows:
+        raise ValueError("empty calibration table")
+    one_max = rows[-1]["bytes"]
+    for i, r in enumerate(rows):
+        if r["two"] < r["one"] * (1.0 - margin):
+            one_max = rows[i - 1]["bytes"] if i else 0
+            break
+    best = [min(r["one"] if r["bytes"] <= one_max else r["two"], r["two"]) for r in rows]
+    rccl_from = None
+    for i in range(len(rows) - 1, -1, -1):
+        rc = rows[i].get("rccl")
+        if rc is None or not rc < best[i] * (1.0 - margin):
+            break
+        rccl_from = rows[i]["bytes"]
+    return {"one_shot_max": int(one_max), "rccl_from": rccl_from}
 
 
 class CustomAllReduce:
@@ -116,6 +151,71 @@ class CustomAllReduce:
         # with a plain host load after each step (no device sync)
         self._flag_host, self._flag_dev = C.car_host_flag_alloc()
         self.calls = 0
+        self.rccl_from: Optional[int] = None   # eager calls of this size and up prefer RCCL
+        self.calibration: Optional[dict] = None
+
+    # ------------------------------------------------------------------------------------------
+    def _time_us(self, fn, iters: int, warmup: int) -> float:
+        for _ in range(warmup):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1000.0 / iters
+
+    def calibrate(self, rccl_group=None, sizes=CAL_SIZES, iters: int = 20, warmup: int = 3,
+                  apply: bool = True) -> dict:
+        """Time one-shot / two-shot (and RCCL on ``rccl_group``) all-reduces of bf16 messages
+        of each size on this group; per size the max over ranks.  Collective over the group
+        (and ``rccl_group``): every rank calls it with the same arguments.  ``apply`` installs
+        ``pick_plan``'s crossovers.  Returns {"table": [...], "plan": {...}}."""
+        table = []
+        with torch.cuda.device(self.device):
+            for nb in sizes:
+                if nb > self.max_bytes or nb % 16:
+                    continue
+                t = torch.ones(nb // 2, dtype=torch.bfloat16, device=self.device)
+                row = {"bytes": int(nb)}
+                for name, two in (("one", False), ("two", True)):
+                    _, blocks = self.plan(nb, t.numel())
+                    row[name] = self._time_us(
+                        lambda: self.C.car_allreduce(self.data, self.sig, self.rank, t, t, two,
+                                                     blocks, self.timeout_s, self._flag_dev),
+                        iters, warmup)
+                if rccl_group is not None:
+                    row["rccl"] = self._time_us(lambda: dist.all_reduce(t, group=rccl_group),
+                                                iters, warmup)
+                table.append(row)
+            self.poll()
+            keys = ["one", "two"] + (["rccl"] if rccl_group is not None else [])
+            vals = torch.tensor([[r[k] for k in keys] for r in table], dtype=torch.float64)
+            if dist.get_backend(self.group) == "nccl":
+                dv = vals.to(self.device)
+                dist.all_reduce(dv, op=dist.ReduceOp.MAX, group=self.group)
+                vals = dv.cpu()
+            else:
+                dist.all_reduce(vals, op=dist.ReduceOp.MAX, group=self.group)
+        for r, v in zip(table, vals.tolist()):
+            for k, x in zip(keys, v):
+                r[k] = round(float(x), 2)
+        plan = pick_plan(table)
+        if apply:
+            self.one_shot_max = plan["one_shot_max"]
+            self.rccl_from = plan["rccl_from"]
+        self.calibration = {"world": self.world, "table": table, "plan": plan}
+        return self.calibration
+
+    def prefer(self, t: torch.Tensor) -> bool:
+        """Eager call: custom kernel (True) or RCCL (False) for this message, per calibration.
+        Inside a graph capture the custom kernel is the only capturable choice."""
+        if not self.eligible(t):
+            return False
+        if self.rccl_from is None or torch.cuda.is_current_stream_capturing():
+            return True
+        return t.numel() * t.element_size() < self.rccl_from
 
     # ------------------------------------------------------------------------------------------
     def eligible(self, t: torch.Tensor) -> bool:
@@ -206,8 +306,18 @@ def maybe_custom_allreduce(group, device, max_bytes: int) -> Optional[CustomAllR
             or os.environ.get("LUMEN_CUSTOM_AR", "1") == "0"):
         return None
     try:
-        return CustomAllReduce(group, device, max_bytes=max_bytes)
+        car = CustomAllReduce(group, device, max_bytes=max_bytes)
     except Exception as e:  # noqa: BLE001 - fall back to RCCL, but say so
         if dist.get_rank(group) == 0:
             print(f"[lumen] custom all-reduce unavailable ({e}); TP uses RCCL", flush=True)
         return None
+    if os.environ.get("LUMEN_CAR_CALIBRATE", "1") != "0":
+        # measured crossovers on THIS group (xGMI on a node; shared-device rehearsals measure
+        # nonsense but run the same code): replaces the guessed one-shot limit
+        cal = car.calibrate(rccl_group=group if dist.get_backend(group) == "nccl" else None)
+        if dist.get_rank(group) == 0:
+            import sys
+
+            print(f"[lumen] custom all-reduce calibrated (world {car.world}): "
+                  f"{cal['plan']}", file=sys.stderr, flush=True)
+    return car

@@ -360,13 +360,13 @@ class ParamCoordinator:
         any world size and of Llama-2-70B from 8 ranks.  Unlimited off-GPU."""
         if self.env.device.type != "cuda":
             return 1 << 62
+        from .memory_plan import live_budget_elems
+
         free, total = torch.cuda.mem_get_info(self.env.device)
         # blocks the caching allocator holds but no tensor uses (the full weights just sharded)
         free += torch.cuda.memory_reserved(self.env.device) - torch.cuda.memory_allocated(
             self.env.device)
-        reserve = float(os.environ.get("LUMEN_ZERO3_RESERVE_GB", "0")) * 2**30 or max(
-            48 * 2**30, 0.25 * total)
-        return max(0, int((free - reserve) // max(elem_bytes, 1)))
+        return live_budget_elems(free, total, elem_bytes)
 
     def stats(self) -> Dict:
         return dict(schedule=self.schedule, world=self.world, units=len(self.units),
@@ -561,7 +561,9 @@ class ParamCoordinator:
         gathered = sum(u.padded * u.dtype.itemsize for u in self.units
                        if u.params and u.buf is None and u.resident)
         gathered += self.pool_size * self.max_unit * units_dtype_bytes(self.units)
-        if need + gathered > free - max(48 * 2**30, 0.25 * total):
+        from .memory_plan import transposes_fit
+
+        if not transposes_fit(need, gathered, free, total):
             return 0
         n = 0
         for u, tn, wo in plan:

@@ -192,7 +192,7 @@ class ModelRunner:
 
     def _allreduce(self, x):
         if self.tp > 1:
-            if self.car is not None and self.car.eligible(x):
+            if self.car is not None and self.car.prefer(x):
                 self.car.all_reduce(x)
             else:
                 dist.all_reduce(x, group=self.tp_group)

@@ -146,7 +146,9 @@ class Trainer:
         tokens = max(a.pack_tokens, self.ds.micro_batch * a.max_length)
         if a.fuse_accumulation:
             tokens *= self.ds.grad_accum
-        est = tokens * cfg.num_hidden_layers * 16 * cfg.hidden_size * 2
+        from ..parallel.memory_plan import activation_bytes, pick_checkpointing
+
+        est = activation_bytes(cfg, tokens, "none")
         free, _ = torch.cuda.mem_get_info(env.device)
         # blocks the caching allocator holds but no tensor uses are free for activations
         free += torch.cuda.memory_reserved(env.device) - torch.cuda.memory_allocated(env.device)
@@ -159,12 +161,9 @@ class Trainer:
         # selective only where every layer's MLP can recompute (frozen, unadapted gate|up/down)
         sel_ok = bool(pols and "selective" in pols
                       and getattr(self.model, "selective_eligible", lambda: False)())
-        if 2 * est <= free:
-            pick = False
-        elif sel_ok and 2 * 0.65 * est <= free:
-            pick = "selective"
-        else:
-            pick = "full" if pols and "full" in pols else True
+        pick = pick_checkpointing(est, free, sel_ok)
+        if pick == "full" and not (pols and "full" in pols):
+            pick = True
         self.print(f"[lumen] activation checkpointing {pick or 'off'} (auto): "
                    f"~{est / 1e9:.1f} GB of activations per micro-step vs {free / 1e9:.1f} GB "
                    "free HBM (--gradient_checkpointing true|false|selective|full to force)")

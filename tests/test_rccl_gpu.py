@@ -210,3 +210,32 @@ def test_fp32_model_trains_on_gpu(tmp_path):
              extra={"device": "cuda", "dtype": "fp32"})
     assert len(r["losses"]) == 2 and all(x == x and abs(x) < 1e3 for x in r["losses"])
     assert any(v.abs().sum() > 0 for k, v in r["sd"].items() if "lora_B" in k)
+
+
+@pytest.mark.parametrize("schedule", ["keep", "hybrid", "release"])
+def test_zero3_rccl_world8_llama70b_layers(schedule, tmp_path):
+    """BASELINE config 5's per-layer shapes at its own rank count: Llama-2-70B layers (H 8192,
+    GQA 64 / 8 heads, F 28672, vocab 32000) at depth 2 ('llama2-70b-2l', 2.2 B parameters),
+    ZeRO-3 over 8 RCCL ranks sharing the box's GPU, every gather schedule, == the single-
+    process run (fp32 for the same reason as the world-8 test above).  hybrid: the live budget
+    holds the two-buffer ring plus one decoder layer (one resident, one re-gathered);
+    release: the ring only."""
+    from lumen.models import get_config
+    from lumen.parallel.memory_plan import llama_units
+
+    layer = llama_units(get_config("llama2-70b-2l"), lora_r=4)[1]["stored"]
+    ex = {"device": "cuda", "dtype": "fp32", "fuse": False}
+    ref = _run(1, 0, str(tmp_path / "a"), model="llama2-70b-2l", micro=8, accum=1, steps=2,
+               extra=dict(ex))
+    ex["schedule"] = schedule
+    if schedule != "keep":
+        ex["max_live"] = int(layer * (3.1 if schedule == "hybrid" else 2.5))
+    r = _run(8, 3, str(tmp_path / "b"), model="llama2-70b-2l", micro=1, accum=1, steps=2,
+             extra=ex)
+    for x, y in zip(r["losses"], ref["losses"]):
+        assert abs(x - y) < 1e-4 * max(1.0, abs(y)), (r["losses"], ref["losses"])
+    _close(r["sd"], ref["sd"], tol=1e-4, frac=0.002)
+    z = r["zero3"]
+    assert z["schedule"] == schedule and z["world"] == 8 and z["gathers"] > 0
+    assert z["resident_units"] == {"keep": 4, "hybrid": 1, "release": 0}[schedule], z
+    assert z["pool_overflows"] == 0

@@ -353,6 +353,17 @@ def test_bench_contract_torchrun(world):
     assert "peak_hbm_gb_max_rank" in x and x["setup_s"] > 0
     tokens = 2 * world * 32 * 2
     assert abs(j["value"] - tokens / (j["ms_per_step"] * 2 / 1000)) / j["value"] < 0.02
+    # transport self-diagnosis (VERDICT r4 Next #4): probe numbers and the link time each
+    # partitioned schedule's gather volume implies at the probe's bus bandwidth
+    c = x["comm"]
+    assert c["world"] == world and c["all_gather"]["busbw_gbps"] > 0, c
+    assert c["all_gather"]["busbw_gbps"] == pytest.approx(
+        c["all_gather"]["algbw_gbps"] * (world - 1) / world, rel=0.05, abs=0.11)
+    assert c["reduce_scatter"]["ms"] > 0 and c["reduce_scatter"]["numel"] > 0
+    for sched in ("release", "hybrid"):
+        p = x[f"zero3_{sched}"]
+        assert p["probe_busbw_gbps"] == c["all_gather"]["busbw_gbps"]
+        assert p["implied_link_ms_per_step"] > 0
 
 
 def test_gemm_wave_split_plan():
@@ -411,3 +422,27 @@ def test_bench_tp_serving_section_and_deadline(deadline):
         assert stp["output_tokens"] == 8 * 6 and stp["config"]["tp"] == 2, stp
     else:
         assert "timed out" in stp["error"], stp
+
+
+def test_custom_allreduce_crossover_selection():
+    """pick_plan (lumen/parallel/custom_ar.py): the measured one-/two-shot crossover and the
+    size from which RCCL takes eager calls (VERDICT r4 Next #4: replaces guessed constants)."""
+    from lumen.parallel.custom_ar import pick_plan
+
+    KB, MB = 1 << 10, 1 << 20
+    t = [dict(bytes=8 * KB, one=9, two=14, rccl=30), dict(bytes=256 * KB, one=20, two=21, rccl=40),
+         dict(bytes=512 * KB, one=35, two=26, rccl=41), dict(bytes=2 * MB, one=90, two=60, rccl=70),
+         dict(bytes=8 * MB, one=300, two=200, rccl=120)]
+    p = pick_plan(t)
+    # two-shot first wins (by > 3 %) at 512 KiB -> one-shot up to 256 KiB; RCCL only at 8 MiB
+    assert p == {"one_shot_max": 256 * KB, "rccl_from": 8 * MB}
+    # within the noise margin one-shot keeps the size; RCCL must win at every larger size too
+    t2 = [dict(bytes=8 * KB, one=10, two=9.8, rccl=9), dict(bytes=1 * MB, one=40, two=30, rccl=50),
+          dict(bytes=4 * MB, one=100, two=80, rccl=70)]
+    p2 = pick_plan(t2)
+    assert p2["one_shot_max"] == 8 * KB and p2["rccl_from"] == 4 * MB
+    # one-shot never loses, RCCL never wins; no RCCL column at all
+    t3 = [dict(bytes=8 * KB, one=5, two=9), dict(bytes=64 * KB, one=8, two=12)]
+    assert pick_plan(t3) == {"one_shot_max": 64 * KB, "rccl_from": None}
+    # two-shot wins from the smallest size
+    assert pick_plan([dict(bytes=8 * KB, one=20, two=10)])["one_shot_max"] == 0
