@@ -101,6 +101,7 @@ int lumen_car_handle_bytes();
 hipError_t lumen_car_open_handle(const void*, void**);
 hipError_t lumen_car_close_handle(void*);
 hipError_t lumen_car_read_err(void*, unsigned int*);
+hipError_t lumen_car_read_diag(void*, unsigned int*);
 hipError_t lumen_car_allreduce(int, const long long*, const long long*, int, int, const void*,
                                void*, long long, int, int, double, void*, hipStream_t);
 hipError_t lumen_car_allgather(int, const long long*, const long long*, int, int, const void*,
@@ -831,6 +832,13 @@ int64_t car_err(int64_t sig) {
   return e;
 }
 
+// (err, err_info, long_wait_us, long_waits) of a signal block: synchronous, diagnostics only
+std::vector<int64_t> car_diag(int64_t sig) {
+  unsigned int v[4] = {0, 0, 0, 0};
+  check(lumen_car_read_diag(reinterpret_cast<void*>(sig), v), "car_diag");
+  return {v[0], v[1], v[2], v[3]};
+}
+
 void car_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>& sig, int rank,
                    const at::Tensor& in, at::Tensor& out, bool two_shot, int blocks,
                    double timeout_s, int64_t host_err) {
@@ -897,6 +905,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("car_open", &car_open);
   m.def("car_close", &car_close);
   m.def("car_err", &car_err);
+  m.def("car_diag", &car_diag);
   m.def("car_host_flag_alloc", &car_host_flag_alloc);
   m.def("car_host_flag_free", &car_host_flag_free);
   m.def("car_host_flag_read", &car_host_flag_read);

@@ -50,7 +50,16 @@ struct Signal {
   uint32_t bar[kBarriers][kMaxBlocks][kMaxRanks];
   uint32_t epoch[kMaxBlocks];
   uint32_t err;
+  // diagnostics (read by the host after a timeout or at the end of a run, never per step):
+  // err_info = the FIRST timed-out wait: 1<<31 | barrier << 24 | block << 16 | missing peer << 8
+  // | low 8 bits of the epoch (= call count of that block); long_wait_us = the longest barrier
+  // wait above kLongWaitTicks (1 ms), so a shared-device rehearsal shows how far ranks drift
+  uint32_t err_info;
+  uint32_t long_wait_us;
+  uint32_t long_waits;
 };
+
+constexpr uint64_t kLongWaitTicks = 100000;  // 1 ms of the 100 MHz s_memrealtime clock
 
 struct Peers {
   void* data[kMaxRanks];
@@ -72,14 +81,27 @@ __device__ __forceinline__ void block_barrier(const Peers& P, Signal* self, int 
                        __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = &self->bar[slot][b][t];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t waited = 0;
     while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > deadline_ticks) {
+      waited = __builtin_amdgcn_s_memrealtime() - t0;
+      if (waited > deadline_ticks) {
         __hip_atomic_fetch_or(&self->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t expect = 0u;
+        const uint32_t info = (1u << 31) | ((uint32_t)slot << 24) | ((uint32_t)b << 16) |
+                              ((uint32_t)t << 8) | (epoch & 0xffu);
+        __hip_atomic_compare_exchange_strong(&self->err_info, &expect, info, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (P.host_err)
           __hip_atomic_store(P.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
+    }
+    if (waited > kLongWaitTicks) {  // rare path: no extra atomic on a prompt barrier
+      const uint64_t us = waited / 100;
+      __hip_atomic_fetch_max(&self->long_wait_us, us > 0xffffffffull ? 0xffffffffu : (uint32_t)us,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_fetch_add(&self->long_waits, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -274,6 +296,12 @@ hipError_t lumen_car_host_flag_free(void* host) { return hipHostFree(host); }
 
 hipError_t lumen_car_read_err(void* sig, unsigned int* err) {
   return hipMemcpy(err, &reinterpret_cast<Signal*>(sig)->err, sizeof(unsigned int),
+                   hipMemcpyDeviceToHost);
+}
+
+// out[4] = err, err_info, long_wait_us, long_waits (synchronous: diagnostics only)
+hipError_t lumen_car_read_diag(void* sig, unsigned int* out) {
+  return hipMemcpy(out, &reinterpret_cast<Signal*>(sig)->err, 4 * sizeof(unsigned int),
                    hipMemcpyDeviceToHost);
 }
 

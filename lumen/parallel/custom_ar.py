@@ -120,16 +120,19 @@ class CustomAllReduce:
             try:
                 self._buf = C.car_alloc(self.max_bytes, self.cached)
                 self._sig = C.car_alloc(C.car_signal_bytes(), False)
-                mine = (C.car_handle(self._buf), C.car_handle(self._sig))
+                mine = (C.car_handle(self._buf), C.car_handle(self._sig), _device_id(self.device))
             except Exception as e:  # noqa: BLE001
                 err = e
             allh: List = [None] * self.world
             dist.all_gather_object(allh, mine, group=group)
             if err is None and any(h is None for h in allh):
                 err = RuntimeError("a peer could not allocate its staging buffer")
+            # every rank on one physical device: a shared-GPU rehearsal (processes time-share
+            # the chip, so barrier timings mean nothing and calibration is skipped)
+            self.shared_device = (err is None and len({h[2] for h in allh}) == 1)
             if err is None:
                 try:
-                    for r, (hb, hs) in enumerate(allh):
+                    for r, (hb, hs, _) in enumerate(allh):
                         if r == self.rank:
                             self.data.append(self._buf)
                             self.sig.append(self._sig)
@@ -267,15 +270,36 @@ class CustomAllReduce:
         self.calls += 1
         return out
 
+    def diagnostics(self) -> dict:
+        """This rank's barrier record (synchronous device read: call after a timeout or at the
+        end of a run, never per step): the first timed-out wait -- which barrier, block and
+        MISSING PEER, and the low 8 bits of that block's call count -- and the longest barrier
+        wait above 1 ms with the number of such waits (how far the ranks drifted apart)."""
+        err, info, long_us, n_long = self.C.car_diag(self._sig)
+        d = {"rank": self.rank, "timed_out": bool(err), "long_wait_ms": long_us / 1000.0,
+             "long_waits": int(n_long), "calls": self.calls}
+        if info >> 31:
+            d.update(barrier=(info >> 24) & 0x7F, block=(info >> 16) & 0xFF,
+                     missing_peer=(info >> 8) & 0xFF, epoch_lo8=info & 0xFF)
+        return d
+
     def poll(self) -> None:
         """Raise if a kernel launched so far and already finished hit a barrier timeout.  A plain
         read of the pinned host word: call it after each step's host sync (the serving engine
         does, right after reading the sampled tokens) so a step whose reduction went wrong never
         returns its tokens."""
         if self._flag_host and self.C.car_host_flag_read(self._flag_host):
+            try:
+                d = self.diagnostics()
+                where = (f" (barrier {d['barrier']} of block {d['block']} waited for rank "
+                         f"{d['missing_peer']}; call {d['epoch_lo8']} mod 256; "
+                         f"{self.calls} calls issued on this rank)") if "missing_peer" in d else ""
+            except Exception:  # noqa: BLE001 - the timeout itself is the error to report
+                where = ""
             raise CollectiveTimeout(
                 f"custom all-reduce rank {self.rank}: a barrier timed out (a peer did not "
-                f"arrive within {self.timeout_s:.0f} s); this step's TP reduction is invalid")
+                f"arrive within {self.timeout_s:.0f} s){where}; this step's TP reduction is "
+                "invalid")
 
     def check(self) -> None:
         """Raise if any barrier of this rank timed out (a peer never arrived).  Syncs."""
@@ -299,6 +323,19 @@ class CustomAllReduce:
             self._flag_host = self._flag_dev = 0
 
 
+def _device_id(device) -> str:
+    """Identity of the PHYSICAL device (UUID where torch reports it, else PCI location)."""
+    try:
+        p = torch.cuda.get_device_properties(device)
+        u = getattr(p, "uuid", None)
+        if u is not None:
+            return str(u)
+        return f"{getattr(p, 'pci_domain_id', 0)}:{getattr(p, 'pci_bus_id', 0)}:" \
+               f"{getattr(p, 'pci_device_id', 0)}"
+    except Exception:  # noqa: BLE001
+        return str(device)
+
+
 def maybe_custom_allreduce(group, device, max_bytes: int) -> Optional[CustomAllReduce]:
     """The custom all-reduce for a TP group on GPUs, or None (CPU, world 1, disabled with
     ``LUMEN_CUSTOM_AR=0``, or peer mapping unavailable: then RCCL serves every call)."""
@@ -311,7 +348,8 @@ def maybe_custom_allreduce(group, device, max_bytes: int) -> Optional[CustomAllR
         if dist.get_rank(group) == 0:
             print(f"[lumen] custom all-reduce unavailable ({e}); TP uses RCCL", flush=True)
         return None
-    if os.environ.get("LUMEN_CAR_CALIBRATE", "1") != "0":
+    mode = os.environ.get("LUMEN_CAR_CALIBRATE", "1")
+    if mode == "force" or (mode != "0" and not car.shared_device):
         # measured crossovers on THIS group (xGMI on a node; shared-device rehearsals measure
         # nonsense but run the same code): replaces the guessed one-shot limit
         cal = car.calibrate(rccl_group=group if dist.get_backend(group) == "nccl" else None)

@@ -18,6 +18,9 @@ lock-step on the devices.
 """
 from __future__ import annotations
 
+import os
+import random
+import time
 from typing import Optional
 
 import torch
@@ -33,6 +36,18 @@ HOST_CAP = 1024  # cu_seqlens + kv_lens values carried inline with the host head
 
 def _host_bcast(t: torch.Tensor) -> None:
     dist.broadcast(t, src=0, group=host_group())
+
+
+# fault injection (tests): LUMEN_TP_INJECT_DELAY_MS=N makes every rank sleep a pseudo-random
+# 0..N ms at each protocol point (between header and payload on both sides, before a worker
+# launches its step), so ranks drift apart on the host the way a loaded box makes them
+_DELAY_MS = float(os.environ.get("LUMEN_TP_INJECT_DELAY_MS", "0") or 0)
+_rng = random.Random(int(os.environ.get("RANK", "0")) * 7919 + 1)
+
+
+def _inject_delay() -> None:
+    if _DELAY_MS > 0:
+        time.sleep(_rng.random() * _DELAY_MS / 1000.0)
 
 
 def pack_step(inp: Optional[StepInput], device) -> None:
@@ -67,6 +82,7 @@ def pack_step(inp: Optional[StepInput], device) -> None:
     _host_bcast(hdr)
     if len(host) > HOST_CAP:
         _host_bcast(torch.tensor(host[HOST_CAP:], dtype=torch.long))
+    _inject_delay()
     dist.broadcast(payload, src=0)
 
 
@@ -85,6 +101,7 @@ def recv_step(device) -> Optional[StepInput]:
             _host_bcast(rest)
             host += rest.tolist()
     payload = torch.empty(n, dtype=torch.long, device=device)
+    _inject_delay()
     dist.broadcast(payload, src=0)
     inp = StepInput("mixed" if kind == KIND["mixed"] else "decode", payload[:T],
                     payload[T:2 * T].int(), payload[2 * T:3 * T], [0])
@@ -117,6 +134,7 @@ def worker_loop(runner) -> None:
         runner.check_collectives()   # a pinned host word: no device sync
         if inp is None:
             return
+        _inject_delay()
         if inp.kind == "decode":
             runner.decode(inp)
         else:

