@@ -549,7 +549,7 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                             const at::Tensor& context_lens, int64_t num_kv_heads, int64_t block_size,
                             int64_t max_blocks_per_seq, double scale, at::Tensor& tmp_m,
                             at::Tensor& tmp_l, at::Tensor& tmp_o, int64_t partition_size,
-                            const std::optional<at::Tensor>& counters, bool one_pass) {
+                            const std::optional<at::Tensor>& counters, int64_t one_pass) {
   if (!q.is_cuda()) throw std::invalid_argument("lumen: q must be a GPU tensor");
   need_cuda(out, "out");
   const int num_seqs = static_cast<int>(q.size(0));
@@ -577,7 +577,7 @@ void paged_attention_decode(at::Tensor& out, const at::Tensor& q, const at::Tens
                                      static_cast<int>(tmp_m.size(-1)), static_cast<float>(scale),
                                      tmp_m.data_ptr<float>(), tmp_l.data_ptr<float>(),
                                      tmp_o.data_ptr(), static_cast<int>(partition_size), cnt,
-                                     one_pass ? 1 : 0, is_fp8(k_cache) ? 1 : 0, qldh,
+                                     static_cast<int>(one_pass), is_fp8(k_cache) ? 1 : 0, qldh,
                                      cur_stream()),
         "paged_attention_decode");
 }

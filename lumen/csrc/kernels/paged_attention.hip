@@ -287,7 +287,29 @@ __device__ __forceinline__ void pa_merge(float& m, float& l, float (&acc)[8], fl
   m = M;
 }
 
-template <typename T, int D, int G, typename KT = T>
+typedef unsigned int pa_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int pa_u32x2 __attribute__((ext_vector_type(2)));
+
+// a K/V row piece read once per decode step: non-temporal (streamed past L2 / MALL retention)
+template <typename R>
+__device__ __forceinline__ R pa_ld_nt(const void* p) {
+  R r;
+  if constexpr (sizeof(R) == 16) {
+    const pa_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const pa_u32x4*>(p));
+    __builtin_memcpy(&r, &v, 16);
+  } else {
+    const pa_u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const pa_u32x2*>(p));
+    __builtin_memcpy(&r, &v, 8);
+  }
+  return r;
+}
+
+// UNI (block_size == rows per workgroup step, the launcher checks): row t = base + u * NGR + grp
+// of an iteration lies in block (base / BS + u) at offset grp, so the block ids are
+// workgroup-uniform -- scalar loads issued one iteration ahead -- instead of a per-lane block
+// table load feeding every K / V address (a dependent L2 round trip per iteration); the K / V
+// pieces are non-temporal loads.
+template <typename T, int D, int G, typename KT = T, bool UNI = false>
 __global__ void __launch_bounds__(256) pa_decode1_kernel(
     T* __restrict__ out, const T* __restrict__ q, const KT* __restrict__ kc,
     const KT* __restrict__ vc, const int* __restrict__ block_tables,
@@ -329,15 +351,40 @@ __global__ void __launch_bounds__(256) pa_decode1_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
   }
-  for (int t0 = start + grp; t0 < end; t0 += NGR * U) {
-    Raw kraw[U], vraw[U];
+  int nbid[U];
+  if constexpr (UNI) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int t = t0 + u * NGR;
-      if (t < end) {
-        const size_t off = bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
-        kraw[u] = *reinterpret_cast<const Raw*>(kc + off);
-        vraw[u] = *reinterpret_cast<const Raw*>(vc + off);
+    for (int u = 0; u < U; ++u) nbid[u] = start + u * NGR < end ? bt[start / NGR + u] : 0;
+  }
+  for (int base = start; base < end; base += NGR * U) {
+    const int t0 = base + grp;
+    Raw kraw[U], vraw[U];
+    if constexpr (UNI) {
+      int bid[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) bid[u] = nbid[u];
+      const int nb = base + NGR * U;
+#pragma unroll
+      for (int u = 0; u < U; ++u) nbid[u] = nb + u * NGR < end ? bt[nb / NGR + u] : 0;
+      const KT* kr0 = kc + head_off + static_cast<size_t>(grp) * D + d0;
+      const KT* vr0 = vc + head_off + static_cast<size_t>(grp) * D + d0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (t0 + u * NGR < end) {
+          const size_t off = static_cast<size_t>(bid[u]) * blk_stride;
+          kraw[u] = pa_ld_nt<Raw>(kr0 + off);
+          vraw[u] = pa_ld_nt<Raw>(vr0 + off);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int t = t0 + u * NGR;
+        if (t < end) {
+          const size_t off = bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
+          kraw[u] = *reinterpret_cast<const Raw*>(kc + off);
+          vraw[u] = *reinterpret_cast<const Raw*>(vc + off);
+        }
       }
     }
 #pragma unroll
@@ -545,11 +592,21 @@ static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out
                         const void* kc, const void* vc, const int* bt, const int* cl, int nh,
                         int qldh, int nkv, int BS, int max_blocks, int max_parts, float scale,
                         float* tm,
-                        float* tl, void* to, int PART, unsigned* cnt, bool one_pass, bool fp8kv) {
+                        float* tl, void* to, int PART, unsigned* cnt, int one_pass, bool fp8kv) {
+  // one_pass 2: the uniform-block-id variant where the block size equals the rows per step
+  const bool uni = one_pass == 2 && BS == 256 / (D / 8) && PART % BS == 0;
 #define LUMEN_PA_G(GG)                                                                         \
-  if (fp8kv)                                                                                    \
+  if (fp8kv && uni)                                                                             \
+    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8, true>), grid, dim3(256), 0, st,        \
+                       (T*)out, (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh,    \
+                       nkv, BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);         \
+  else if (fp8kv)                                                                               \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8>), grid, dim3(256), 0, st, (T*)out,     \
                        (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh, nkv, BS,        \
+                       max_blocks, max_parts, scale, tm, tl, (float*)to, PART);                 \
+  else if (uni)                                                                                 \
+    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, T, true>), grid, dim3(256), 0, st, (T*)out, \
+                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, qldh, nkv, BS,          \
                        max_blocks, max_parts, scale, tm, tl, (float*)to, PART);                 \
   else if (one_pass)                                                                            \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG>), grid, dim3(256), 0, st, (T*)out,          \
@@ -573,14 +630,14 @@ static hipError_t launch_pa(void* out, const void* q, const void* kc, const void
                             void* to, int PART, unsigned* cnt, int one_pass, int fp8kv,
                             int qldh, hipStream_t st) {
   const int G = nh / nkv;
-  if (fp8kv) one_pass = 1;  // the fp8 cache is read by the single-pass kernel only
+  if (fp8kv && one_pass == 0) one_pass = 1;  // the fp8 cache: single-pass kernels only
   if (G != 1 && G != 2 && G != 4 && G != 8) return hipErrorInvalidValue;
   dim3 grid(nseq, nkv, max_parts);
   const size_t smem = (static_cast<size_t>(G) * PART + 4 * G * D + 2 * G + 8) * sizeof(float);
-  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
-  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
-  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
-  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass != 0, fp8kv != 0);
+  if (D == 128) launch_pa_g<T, 128>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass, fp8kv != 0);
+  else if (D == 64) launch_pa_g<T, 64>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass, fp8kv != 0);
+  else if (D == 256) launch_pa_g<T, 256>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass, fp8kv != 0);
+  else if (D == 32) launch_pa_g<T, 32>(G, grid, smem, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS, max_blocks, max_parts, scale, tm, tl, to, PART, cnt, one_pass, fp8kv != 0);
   else return hipErrorInvalidValue;
   if (max_parts > 1 && (cnt == nullptr || one_pass)) {  // unfused merge: second kernel
     dim3 g2(nseq, nh), b2(128);

@@ -42,8 +42,10 @@ def causal_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
 _merge_counters: dict = {}
 # Fused split-context merge (two-pass kernel only): measured neutral in decode steps (batch 1:
 # 3.857 vs 3.865 ms ITL, profiles/r02_serve); callers may still ask for it (``fused_merge``).
-# single-pass decode kernel (K and V streamed together, online softmax per row group)
-PA_ONE_PASS = os.environ.get("LUMEN_PA_1PASS", "1") == "1"
+# decode kernel: 0 = two-pass; 1 = single-pass (K and V streamed together, online softmax per
+# row group); 2 = single-pass with workgroup-uniform block ids and non-temporal K / V loads
+# (used where the block size equals the kernel's rows per step, else 1)
+PA_ONE_PASS = int(os.environ.get("LUMEN_PA_1PASS", "2"))
 
 
 def _pa_counters(device: torch.device, n: int) -> torch.Tensor:
@@ -81,7 +83,7 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         else:
             tm = torch.empty(1, 1, 1, device=q.device, dtype=torch.float32)
             tl, to = tm, tm
-        one = PA_ONE_PASS if one_pass is None else one_pass
+        one = PA_ONE_PASS if one_pass is None else int(one_pass)
         fused = bool(fused_merge) and not one
         cnt = (_pa_counters(q.device, num_seqs * nkv) if fused and max_parts > 1
                else None)
