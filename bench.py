@@ -301,23 +301,34 @@ def run_comm_probe(env, gather_group=None, unit_mb: float = 386.0, bucket_numel:
 
     dt_bf = torch.bfloat16 if on_gpu else torch.float32
     esz = torch.empty((), dtype=dt_bf).element_size()
-    n = int(unit_mb * 2**20 / esz) // W * W
-    shard = torch.ones(n // W, dtype=dt_bf, device=dev)
-    full = torch.empty(n, dtype=dt_bf, device=dev)
-    t = timed(lambda: dist.all_gather_into_tensor(full, shard, group=gather_group))
-    nbytes = n * esz
-    res["all_gather"] = {"mib": round(nbytes / 2**20, 1), "ms": round(t * 1e3, 3),
-                         "algbw_gbps": round(nbytes / t / 1e9, 1),
-                         "busbw_gbps": round(nbytes / t / 1e9 * (W - 1) / W, 1),
-                         "group": "weight-gather" if gather_group is not None else "default"}
-    del shard, full
-    m = bucket_numel // W * W
-    g = torch.ones(m, dtype=torch.float32, device=dev)
-    o = torch.empty(m // W, dtype=torch.float32, device=dev)
-    t = timed(lambda: dist.reduce_scatter_tensor(o, g))
-    res["reduce_scatter"] = {"numel": m, "ms": round(t * 1e3, 3),
-                             "busbw_gbps": round(m * 4 / t / 1e9 * (W - 1) / W, 1)}
-    del g, o
+
+    def gather(mib):
+        n = int(mib * 2**20 / esz) // W * W
+        shard = torch.ones(n // W, dtype=dt_bf, device=dev)
+        full = torch.empty(n, dtype=dt_bf, device=dev)
+        t = timed(lambda: dist.all_gather_into_tensor(full, shard, group=gather_group))
+        nbytes = n * esz
+        return {"mib": round(nbytes / 2**20, 1), "ms": round(t * 1e3, 3),
+                "algbw_gbps": round(nbytes / t / 1e9, 1),
+                "busbw_gbps": round(nbytes / t / 1e9 * (W - 1) / W, 1)}
+
+    def rscatter(numel):
+        m = max(W, numel // W * W)
+        g = torch.ones(m, dtype=torch.float32, device=dev)
+        o = torch.empty(m // W, dtype=torch.float32, device=dev)
+        t = timed(lambda: dist.reduce_scatter_tensor(o, g))
+        return {"numel": m, "ms": round(t * 1e3, 3),
+                "busbw_gbps": round(m * 4 / t / 1e9 * (W - 1) / W, 1)}
+
+    res["all_gather"] = dict(gather(unit_mb),
+                             group="weight-gather" if gather_group is not None else "default")
+    res["reduce_scatter"] = rscatter(bucket_numel)
+    # size sweeps (bucket tuning data for the 7 xGMI links): the all-gather from a DeepSpeed
+    # 5e7-element bucket (95 MiB bf16) down, the gradient reduce-scatter around the LoRA bucket
+    scale = unit_mb / 386.0
+    res["all_gather_sweep"] = [gather(mib * scale) for mib in (8, 32, 95)]
+    res["reduce_scatter_sweep"] = [rscatter(int(n * scale)) for n in
+                                   (500_000, 8_000_000, 16_777_216)]
     if on_gpu:
         try:
             from lumen.parallel.custom_ar import CustomAllReduce
@@ -332,6 +343,15 @@ def run_comm_probe(env, gather_group=None, unit_mb: float = 386.0, bucket_numel:
         except Exception as e:  # noqa: BLE001 - the RCCL numbers stand
             res["allreduce_us"] = {"error": repr(e)[:300]}
     return res
+
+
+def _max_unit(cfg) -> int:
+    try:
+        from lumen.parallel.memory_plan import llama_units
+
+        return max(u["stored"] for u in llama_units(cfg))
+    except Exception:  # noqa: BLE001 - non-Llama configs
+        return 0
 
 
 def _with_link_time(parts: dict, comm, world: int) -> dict:
@@ -614,7 +634,11 @@ def main():
             torch.cuda.empty_cache()
     for sched in want_parts:
         # the partitioned ZeRO-3 paths, timed after (and outside) the headline region
-        ml = 1e9 if sched == "release" else 0.5 * cfg.num_params()
+        # hybrid = release's ring budget PLUS resident units: at least the reference live budget
+        # and one decoder unit beyond it (half the model on Llama-2-7B), so a shallow model
+        # never runs a hybrid whose ring is smaller than release's (r4 world-8 rehearsal:
+        # 2,147 vs 1,338 MB gathered per step at half of a 2-layer model)
+        ml = 1e9 if sched == "release" else max(0.5 * cfg.num_params(), 1e9 + _max_unit(cfg))
         try:
             parts[sched] = run_partitioned(args, env, ds, batches, sched, ml,
                                            steps=args.partitioned_steps,
