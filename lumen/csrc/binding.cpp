@@ -65,7 +65,7 @@ hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, con
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
 hipError_t lumen_decode_gemm(int, const void*, const void*, void*, float*, int*, int, int, int,
-                             long long, long long, int, int, int, int, hipStream_t);
+                             long long, long long, int, int, int, int, int, hipStream_t);
 void lumen_set_gemv_form(int);
 void lumen_set_rms_lds(int, int);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
@@ -217,11 +217,16 @@ void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
 // split-K s (s > 1: ws f32 slabs + cnt zeroed tile counters)
 void decode_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
                  const std::optional<at::Tensor>& ws, const std::optional<at::Tensor>& cnt,
-                 int64_t bm, int64_t bn, int64_t s, int64_t nw) {
+                 int64_t bm, int64_t bn, int64_t s, int64_t nw, int64_t flags) {
   if (!x.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: decode_gemm needs GPU tensors");
   need_cuda(w, "w");
-  if (x.dim() != 2 || w.dim() != 2 || y.dim() != 2 || x.stride(1) != 1 || y.stride(1) != 1 ||
-      !w.is_contiguous() || x.size(1) != w.size(1) || y.size(0) != x.size(0) ||
+  // flags bit 1: x in the k-tiled layout, a contiguous [K / 64, bm, 64] tensor (M = y rows)
+  const bool xt = (flags & 2) != 0;
+  if (xt ? (!x.is_contiguous() || x.numel() != w.size(1) / 64 * bm * 64 || bm != 256)
+         : (x.dim() != 2 || x.stride(1) != 1 || x.size(1) != w.size(1) ||
+            y.size(0) != x.size(0)))
+    throw std::invalid_argument("lumen: decode_gemm x shape/layout mismatch");
+  if (w.dim() != 2 || y.dim() != 2 || y.stride(1) != 1 || !w.is_contiguous() ||
       y.size(1) != w.size(0) || x.scalar_type() != w.scalar_type() ||
       y.scalar_type() != w.scalar_type())
     throw std::invalid_argument("lumen: decode_gemm shape/layout mismatch");
@@ -234,10 +239,11 @@ void decode_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
   }
   check(lumen_decode_gemm(dcode(w), x.data_ptr(), w.data_ptr(), y.data_ptr(),
                           s > 1 ? ws->data_ptr<float>() : nullptr,
-                          s > 1 ? cnt->data_ptr<int>() : nullptr, static_cast<int>(x.size(0)),
-                          static_cast<int>(w.size(0)), static_cast<int>(w.size(1)), x.stride(0),
-                          y.stride(0), static_cast<int>(bm), static_cast<int>(bn),
-                          static_cast<int>(nw), static_cast<int>(s), cur_stream()),
+                          s > 1 ? cnt->data_ptr<int>() : nullptr, static_cast<int>(y.size(0)),
+                          static_cast<int>(w.size(0)), static_cast<int>(w.size(1)),
+                          xt ? w.size(1) : x.stride(0), y.stride(0), static_cast<int>(bm),
+                          static_cast<int>(bn), static_cast<int>(nw), static_cast<int>(s),
+                          static_cast<int>(flags), cur_stream()),
         "decode_gemm");
 }
 

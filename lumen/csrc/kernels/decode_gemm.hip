@@ -82,7 +82,7 @@ __device__ __forceinline__ void dma16(const void* base, unsigned off, const char
 // One stage: image rows [0, BN) = W rows n0 .. n0+BN-1, rows [BN, BN+BM) = x rows 0 .. BM-1, k
 // range [k0, k0 + 64).  Piece p (8 rows) is issued by wave p % NW; rows past N / M re-read the
 // last valid row (finite data; those outputs are never stored).
-template <typename T, int BM, int BN, int NW>
+template <typename T, int BM, int BN, int NW, bool XT = false>
 __device__ __forceinline__ void stage(char* img, const T* Wt, int K, int nvalid, const T* x,
                                       long long ldx, int M, int k0, int wid, int lane) {
   constexpr int PIECES = (BN + BM) / 8;
@@ -98,6 +98,12 @@ __device__ __forceinline__ void stage(char* img, const T* Wt, int K, int nvalid,
       const int n = min(r, nvalid - 1);
       const unsigned off = (unsigned)(((long long)n * K + k0 + 8 * ch) * (long long)sizeof(T));
       dma16(Wt, off, img + 8 * p * ROWB);
+    } else if constexpr (XT) {
+      // k-tiled x ([K / 64][BM][64]): the stage's x rows are one contiguous BM x 128-byte run
+      const int m = r - BN;
+      const unsigned off = (unsigned)(((long long)(k0 >> 6) * BM * 64 + m * 64 + 8 * ch) *
+                                      (long long)sizeof(T));
+      dma16(x, off, img + 8 * p * ROWB);
     } else {
       const int m = min(r - BN, M - 1);
       const unsigned off = (unsigned)(((long long)m * ldx + k0 + 8 * ch) * (long long)sizeof(T));
@@ -133,11 +139,14 @@ __device__ __forceinline__ void compute(const char* img, int nrow0, int mrow0,
 // WM x WN waves (4 or 8); each wave: BN / WN output columns (NI blocks of 16) x BM / WM rows
 // (MJ blocks).  8 waves: half the accumulators per wave, two waves per SIMD to hide the LDS /
 // DMA latency.
-template <typename T, int BM, int BN, int WM, int WN>
+// ROT (runtime, rot != 0): each block starts its k loop at a different stage (tile-dependent
+// rotation), so the blocks running at once read different x / W k-ranges instead of all
+// sweeping the same x lines together; XT: x in the k-tiled layout (see stage)
+template <typename T, int BM, int BN, int WM, int WN, bool XT = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
 dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y,
              float* __restrict__ ws, int* __restrict__ cnt, int M, int N, int K, long long ldx,
-             long long ldy, int tiles_n, int S, int kt_total) {
+             long long ldy, int tiles_n, int S, int kt_total, int rot) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NI = BN / WN / 16, MJ = BM / WM / 16;
@@ -170,17 +179,22 @@ dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y
 #pragma unroll
     for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage<T, BM, BN, NW>(lds, Wt, K, nvalid, x, ldx, M, kb * BK, wid, lane);
+  const int r0 = rot ? (tile * rot) % nk : 0;
+  const auto kat = [&](int t) {  // k offset of loop step t
+    const int u = t + r0;
+    return (kb + (u >= nk ? u - nk : u)) * BK;
+  };
+  stage<T, BM, BN, NW, XT>(lds, Wt, K, nvalid, x, ldx, M, kat(0), wid, lane);
   if (nk > 1)
-    stage<T, BM, BN, NW>(lds + STAGE_B, Wt, K, nvalid, x, ldx, M, (kb + 1) * BK, wid, lane);
+    stage<T, BM, BN, NW, XT>(lds + STAGE_B, Wt, K, nvalid, x, ldx, M, kat(1), wid, lane);
   int buf = 0;
   for (int t = 0; t < nk; ++t) {
     if (t + 1 < nk) wait_vm<G>(); else wait_vm<0>();
     lds_barrier();  // stage t landed for every wave; every wave is done with stage t - 1
     if (t + 2 < nk) {
       const int nbuf = buf >= 1 ? buf - 1 : 2;  // (t + 2) % 3 == (t - 1) % 3
-      stage<T, BM, BN, NW>(lds + nbuf * STAGE_B, Wt, K, nvalid, x, ldx, M, (kb + t + 2) * BK, wid,
-                           lane);
+      stage<T, BM, BN, NW, XT>(lds + nbuf * STAGE_B, Wt, K, nvalid, x, ldx, M, kat(t + 2), wid,
+                               lane);
     }
     compute<T, NI, MJ>(lds + buf * STAGE_B, nrow0, mrow0, acc, lane);
     buf = buf == 2 ? 0 : buf + 1;
@@ -250,20 +264,34 @@ dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y
   X(64, 64, 1, 4) X(64, 128, 1, 4) X(64, 192, 1, 4) X(64, 256, 1, 4)                            \
   X(256, 64, 4, 2) X(256, 128, 4, 2) X(128, 128, 2, 4) X(128, 256, 2, 4)
 
+// k-tiled x variants (flags bit 1): the BM = 256 tiles
+#define LUMEN_DG_XT_VARIANTS(X) X(256, 64, 4, 1) X(256, 128, 4, 1) X(256, 64, 4, 2) X(256, 128, 4, 2)
+
 template <typename T>
 hipError_t launch(const void* x, const void* W, void* y, float* ws, int* cnt, int M, int N, int K,
-                  long long ldx, long long ldy, int BM, int BN, int NW, int S, hipStream_t st) {
+                  long long ldx, long long ldy, int BM, int BN, int NW, int S, int flags,
+                  hipStream_t st) {
   const int tiles_n = (N + BN - 1) / BN;
   const int kt = K / BK;
+  const int rot = (flags & 1) ? 1 : 0;
   dim3 grid(tiles_n * S), block(64 * NW);
 #define LUMEN_DG_CASE(bm, bn, wm, wn)                                                          \
-  if (BM == bm && BN == bn && NW == wm * wn) {                                                 \
+  if (BM == bm && BN == bn && NW == wm * wn && !(flags & 2)) {                                 \
     hipLaunchKernelGGL((dgemm_kernel<T, bm, bn, wm, wn>), grid, block, 0, st, (const T*)x,     \
-                       (const T*)W, (T*)y, ws, cnt, M, N, K, ldx, ldy, tiles_n, S, kt);       \
+                       (const T*)W, (T*)y, ws, cnt, M, N, K, ldx, ldy, tiles_n, S, kt, rot);  \
     return hipGetLastError();                                                                  \
   }
   LUMEN_DG_VARIANTS(LUMEN_DG_CASE)
 #undef LUMEN_DG_CASE
+#define LUMEN_DG_XT_CASE(bm, bn, wm, wn)                                                       \
+  if (BM == bm && BN == bn && NW == wm * wn && (flags & 2)) {                                  \
+    hipLaunchKernelGGL((dgemm_kernel<T, bm, bn, wm, wn, true>), grid, block, 0, st,            \
+                       (const T*)x, (const T*)W, (T*)y, ws, cnt, M, N, K, ldx, ldy, tiles_n, S, \
+                       kt, rot);                                                               \
+    return hipGetLastError();                                                                  \
+  }
+  LUMEN_DG_XT_VARIANTS(LUMEN_DG_XT_CASE)
+#undef LUMEN_DG_XT_CASE
   return hipErrorInvalidValue;
 }
 
@@ -274,9 +302,11 @@ hipError_t launch(const void* x, const void* W, void* y, float* ws, int* cnt, in
 // at stride ldx (% 8), y rows at stride ldy (% 4), 16-byte aligned bases.  S > 1: ``ws`` holds
 // ceil(N / BN) * S * 256 * (BM * BN / 256) floats and ``cnt`` ceil(N / BN) zeroed ints (the last
 // slice of each tile re-zeroes its counter, so they stay zero between launches).
+// flags: bit 0 = per-tile k rotation; bit 1 = x in the k-tiled layout [K / 64][BM][64]
+// (ldx ignored; BM = 256 variants only)
 extern "C" hipError_t lumen_decode_gemm(int dtype, const void* x, const void* W, void* y,
                                         float* ws, int* cnt, int M, int N, int K, long long ldx,
-                                        long long ldy, int BM, int BN, int NW, int S,
+                                        long long ldy, int BM, int BN, int NW, int S, int flags,
                                         hipStream_t st) {
   if (M < 1 || M > BM || N < 4 || N % 4 != 0 || K < 64 || K % 64 != 0 || ldx % 8 != 0 ||
       ldy % 4 != 0 || ldx < K || ldy < N || S < 1 || S > K / 64 ||
@@ -289,9 +319,9 @@ extern "C" hipError_t lumen_decode_gemm(int dtype, const void* x, const void* W,
     return hipErrorInvalidValue;
   if (dtype == lumen::kBF16)
     return lumen::dg::launch<lumen::bf16>(x, W, y, ws, cnt, M, N, K, ldx, ldy, BM, BN, NW, S,
-                                          st);
+                                          flags, st);
   if (dtype == lumen::kF16)
     return lumen::dg::launch<lumen::fp16>(x, W, y, ws, cnt, M, N, K, ldx, ldy, BM, BN, NW, S,
-                                          st);
+                                          flags, st);
   return hipErrorInvalidValue;
 }

@@ -55,11 +55,13 @@ def dg_bucket(M: int) -> int:
 
 
 def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int, nw: int = 4,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, flags: int = 0,
+                m: Optional[int] = None) -> torch.Tensor:
     """y = x @ w^T on the decode-batch MFMA kernel with block tile (bm, bn), split-K s and nw
-    (4 or 8) waves per block."""
-    y = out if out is not None else torch.empty(x.shape[0], w.shape[0], device=x.device,
-                                                dtype=x.dtype)
+    (4 or 8) waves per block.  ``flags``: bit 0 rotates each tile's k loop start; bit 1 takes
+    x in the k-tiled layout [K / 64, bm, 64] (``x_ktiled``) with ``m`` valid rows."""
+    rows = x.shape[0] if not flags & 2 else int(m)
+    y = out if out is not None else torch.empty(rows, w.shape[0], device=x.device, dtype=x.dtype)
     ws = cnt = None
     if s > 1:
         # one slab workspace + ticket counters per (device, stream): split-K slabs and tickets
@@ -78,8 +80,16 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, bm: int, bn: int, s: int, nw: 
                                device=x.device))
             _dg_ws[key] = got
         ws, cnt = got
-    native().decode_gemm(x, w, y, ws, cnt, bm, bn, s, nw)
+    native().decode_gemm(x, w, y, ws, cnt, bm, bn, s, nw, flags)
     return y
+
+
+def x_ktiled(x: torch.Tensor, bm: int = 256) -> torch.Tensor:
+    """[M, K] -> [K / 64, bm, 64] (rows past M zero): the decode GEMM's k-tiled x layout."""
+    M, K = x.shape
+    t = torch.zeros(K // 64, bm, 64, device=x.device, dtype=x.dtype)
+    t[:, :M].copy_(x.reshape(M, K // 64, 64).transpose(0, 1))
+    return t
 
 
 def _dg_key(device) -> tuple:

@@ -706,7 +706,23 @@ def test_decode_gemm_variants(bm):
         native().decode_gemm(torch.randn(bm + 1, K, device=DEV).to(torch.bfloat16),
                              w.to(torch.bfloat16), torch.empty(bm + 1, 256, device=DEV,
                                                                dtype=torch.bfloat16),
-                             None, None, bm, DG_BNS[bm][0], 1, 4)
+                             None, None, bm, DG_BNS[bm][0], 1, 4, 0)
+    # k-rotated loop (flags 1) and the k-tiled x layout (flags 2, BM 256): same products
+    from lumen.ops.gemm import x_ktiled
+
+    w = (torch.randn(3 * 64 + 8, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    for M in sorted({bm, bm - 11}):
+        x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        ref = x.float() @ w.float().t()
+        for s in (1, 3):
+            assert rel(decode_gemm(x, w, bm, DG_BNS[bm][0], s, 4, flags=1), ref) < 1e-2
+            if bm == 256:
+                xt = x_ktiled(x)
+                for fl in (2, 3):
+                    for bn, nw in ((64, 4), (128, 4), (64, 8), (128, 8)):
+                        y = decode_gemm(xt, w, bm, bn, s, nw, flags=fl, m=M)
+                        assert y.shape == (M, w.shape[0])
+                        assert rel(y, ref) < 1e-2, (fl, bn, nw, s, M, rel(y, ref))
 
 
 @pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 4096), (22016, 4096), (4096, 11008),
