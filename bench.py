@@ -282,7 +282,16 @@ def run_comm_probe(env, gather_group=None, unit_mb: float = 386.0, bucket_numel:
     W = env.world_size
     on_gpu = env.device.type == "cuda"
     dev = env.device
-    res = {"world": W}
+    res = {"world": W,
+           # what the transport was configured with (defaults unless set): the first record
+           # from a real node says which RCCL and which knobs produced its numbers
+           "env": {k: v for k, v in sorted(os.environ.items())
+                   if k.startswith(("NCCL_", "RCCL_", "HSA_", "GPU_MAX_HW_QUEUES"))}}
+    try:
+        res["rccl_version"] = ".".join(str(x) for x in torch.cuda.nccl.version()) if on_gpu \
+            else None
+    except Exception:  # noqa: BLE001
+        res["rccl_version"] = None
 
     def timed(fn):
         fn()
