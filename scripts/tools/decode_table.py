@@ -14,9 +14,16 @@ def main(d, layers=32):
     f = next(os.path.join(r, n) for r, _, fs in os.walk(d) for n in fs
              if n.endswith("kernel_trace.csv"))
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-    st = [int(r["Start_Timestamp"]) for r in rows]
-    gap = max(range(1, len(st)), key=lambda i: st[i] - st[i - 1])
-    seg = rows[gap:]
+    # decode steps = everything after the last prefill kernel (flash-attention prefill or a
+    # 256 x 256 macro-tile prefill GEMM), from the first paged-decode launch on
+    last_pf = max((i for i, r in enumerate(rows)
+                   if "fwd32_kernel" in r["Kernel_Name"] or "MT256x256" in r["Kernel_Name"]),
+                  default=-1)
+    first = next(i for i in range(last_pf + 1, len(rows)) if "pa_decode" in rows[i]["Kernel_Name"])
+    # start at the first kernel of that step: back up to the step's first RMSNorm / embedding
+    while first > last_pf + 1 and "embedding" not in rows[first - 1]["Kernel_Name"]:
+        first -= 1
+    seg = rows[first:]
     t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
     c = collections.defaultdict(lambda: [0, 0])
     for r in seg:
