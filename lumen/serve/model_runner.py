@@ -42,6 +42,9 @@ from ..ops.rope import rope_tables
 # prefill of whole fresh prompts from the q|k|v rows instead of the paged cache (model_runner
 # _execute); LUMEN_FRESH_PREFILL=0 always reads the cache
 FRESH_PREFILL = os.environ.get("LUMEN_FRESH_PREFILL", "1") != "0"
+# decode batches of at least this many rows run as two half-batches on two streams (TP = 1;
+# 0 = off): ModelRunner._decode_split
+DECODE_SPLIT_MIN = int(os.environ.get("LUMEN_DECODE_SPLIT", "0"))
 
 
 @dataclass
@@ -198,7 +201,7 @@ class ModelRunner:
                 dist.all_reduce(x, group=self.tp_group)
         return x
 
-    def _layers(self, h, positions, slots, attn_fn, lora_ids=None):
+    def _layers(self, h, positions, slots, attn_fn, lora_ids=None, mark=None):
         cfg = self.cfg
         res = None
         T = h.shape[0]
@@ -208,6 +211,8 @@ class ModelRunner:
         for i, L in enumerate(self.w.layers):
             y, res = rms_norm(h, L.ln1, cfg.rms_norm_eps, res)
             qkv = linear_nt(y, L.qkv)
+            if mark is not None and i == 0:
+                mark.record()   # split decode: the second half starts here
             if ml is not None:
                 ml.apply(i, "qkv", y, qkv, masks)
             rope_write_kv(qkv, positions, self.w.nh, self.w.nkv, D, self.cos, self.sin,
@@ -303,8 +308,48 @@ class ModelRunner:
     prefill = execute  # a whole-prompt step is a mixed step without decode rows
 
     # ---- decode: one token per sequence ----------------------------------------------------
+    def _split_ok(self, N: int, lora_ids) -> bool:
+        return (DECODE_SPLIT_MIN > 0 and N >= DECODE_SPLIT_MIN and N % 32 == 0 and self.tp == 1
+                and lora_ids is None and self.device.type == "cuda")
+
     def _decode_eager(self, tokens, positions, slots, block_tables, context_lens, max_context,
                       lora_ids=None, gather: bool = True):
+        N = tokens.shape[0]
+        if self._split_ok(N, lora_ids):
+            return self._decode_split(tokens, positions, slots, block_tables, context_lens,
+                                      max_context)
+        return self._decode_rows(tokens, positions, slots, block_tables, context_lens,
+                                 max_context, lora_ids, gather)
+
+    def _decode_split(self, tokens, positions, slots, block_tables, context_lens, max_context):
+        """Two half-batches on two streams (TP = 1, N >= DECODE_SPLIT_MIN): the halves are
+        independent (own rows, own K/V slots), so while one half's paged attention streams its
+        K/V (HBM-bound) the other half's projection GEMMs (latency / L2-bound at these M) run
+        beside it.  The second half starts after the first half's first q|k|v projection, so
+        the two settle half a layer apart.  Costs one more read of the weights per step.
+        Captured in the decode graph like the single-stream path (fork / join by events)."""
+        N = tokens.shape[0]
+        hN = N // 2
+        cur = torch.cuda.current_stream(self.device)
+        side = getattr(self, "_split_stream", None)
+        if side is None:
+            side = self._split_stream = torch.cuda.Stream(device=self.device)
+        first = torch.cuda.Event()
+        self._split_mark = first
+        outs = [None, None]
+        a = slice(0, hN)
+        outs[0] = self._decode_rows(tokens[a], positions[a], slots[a], block_tables[a],
+                                    context_lens[a], max_context, None, True, mark=first)
+        side.wait_event(first)
+        with torch.cuda.stream(side):
+            b = slice(hN, N)
+            outs[1] = self._decode_rows(tokens[b], positions[b], slots[b], block_tables[b],
+                                        context_lens[b], max_context, None, True)
+        cur.wait_stream(side)
+        return torch.cat(outs, 0)
+
+    def _decode_rows(self, tokens, positions, slots, block_tables, context_lens, max_context,
+                     lora_ids=None, gather: bool = True, mark=None):
         h = embedding(tokens, self.w.embed)
         N = tokens.shape[0]
         nh, D = self.w.nh, self.cfg.head_dim
@@ -314,7 +359,7 @@ class ModelRunner:
             return paged_decode(q, self.k_cache[i], self.v_cache[i], block_tables, context_lens,
                                 max_context, self.scale, self.decode_partition(N)).view(N, nh * D)
 
-        h, res = self._layers(h, positions, slots, attn, lora_ids)
+        h, res = self._layers(h, positions, slots, attn, lora_ids, mark=mark)
         y, _ = rms_norm(h, self.w.norm, self.cfg.rms_norm_eps, res)
         logits = linear_nt(y, self.w.lm_head)
         return self._vocab_gather(logits) if gather else logits
