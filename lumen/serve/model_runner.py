@@ -327,7 +327,12 @@ class ModelRunner:
         K/V (HBM-bound) the other half's projection GEMMs (latency / L2-bound at these M) run
         beside it.  The second half starts after the first half's first q|k|v projection, so
         the two settle half a layer apart.  Costs one more read of the weights per step.
-        Captured in the decode graph like the single-stream path (fork / join by events)."""
+        Captured in the decode graph like the single-stream path (fork / join by events).
+        Measured NEGATIVE on Llama-2-7B at 256 rows x ~600 context (profiles/r5_decode):
+        21.1-21.2 vs 19.55 ms per step -- side by side the halves' paged attention ran at 222 us
+        per 128-row call (444 per layer vs 400 alone) and the M = 128 projections cost 9.2 ms
+        per step for both halves, so the overlap never paid for the doubled weight reads.  Off
+        by default (LUMEN_DECODE_SPLIT=0)."""
         N = tokens.shape[0]
         hN = N // 2
         cur = torch.cuda.current_stream(self.device)
