@@ -119,7 +119,8 @@ class Linear(nn.Module):
         is partitioned); otherwise also of the weight as currently bound."""
         lo, W = self.lora, self.weight
         if (not lora_ops.FOLD or lo is None or not self.lora_enabled or W.requires_grad
-                or not W.is_cuda or W.dtype not in (torch.bfloat16, torch.float16)):
+                or not W.is_cuda or W.dtype not in (torch.bfloat16, torch.float16)
+                or not lora_ops.use_native(W)):
             return 0
         if not static:
             if W.dim() != 2 or W.numel() == 0:

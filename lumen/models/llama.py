@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
+from ..ops._native import use_native
 from ..ops.embedding import embedding
 from ..ops.lora import arena_reset
 from ..ops.activation import recompute_mlp, swiglu
@@ -46,7 +47,10 @@ class LlamaAttention(nn.Module):
         c = self.cfg
         nh, nkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
         cos, sin = rope_tables(D, c.max_position_embeddings, c.rope_theta, x2d.device)
-        if x2d.is_cuda and D == 128 and USE_FLASH:
+        # the HIP flash / fused-RoPE path takes 16-bit activations; an fp32 model on the GPU
+        # (--dtype fp32) or the explicit torch fallback runs the portable path below
+        if (x2d.is_cuda and D == 128 and USE_FLASH and x2d.dtype != torch.float32
+                and use_native(x2d)):
             # HIP path: RoPE in place on the fused buffer (inside the adapter write-back when
             # q|k are adapted), flash attention reads q/k/v from it and writes O token-major
             # (no split / transpose copies)

@@ -585,7 +585,21 @@ def lora_linear(x: torch.Tensor, weight_fn, bias: Optional[torch.Tensor], A: tor
                               torch.is_grad_enabled(), rope, fold)
     else:
         y = lora_linear_ref(x2d, _frozen(weight_fn()), bias, A, B, segs, r, scale, p, seed)
+        if rope is not None:   # the caller expects rotated q|k columns back
+            y = _rope_ref_cols(y, rope)
     return y if x.dim() == 2 else y.view(*shp[:-1], y.shape[-1])
+
+
+def _rope_ref_cols(y: torch.Tensor, rope) -> torch.Tensor:
+    """Torch RoPE over columns [0, ncols) (128-wide heads) at positions ``pos`` (out of place)."""
+    from .rope import _rotate_ref
+
+    pos, cos_t, sin_t, ncols = rope
+    T = y.shape[0]
+    p = pos.long()
+    head = y[:, :ncols].reshape(T, ncols // 128, 128).transpose(0, 1)
+    rot = _rotate_ref(head, cos_t[p], sin_t[p]).transpose(0, 1).reshape(T, ncols)
+    return torch.cat([rot, y[:, ncols:]], 1)
 
 
 def lora_linear_ref(x2d, W, bias, A, B, segs, r, scale, p, seed):

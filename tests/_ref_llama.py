@@ -74,8 +74,10 @@ def lin(x, W, lora=None, p: float = 0.0, seed: int = 0):
     return torch.cat(parts, 1)
 
 
-def attention(q, k, v, lens: List[int]):
-    """Causal attention of packed sequences: q [T, nh, D], k/v [T, nkv, D]."""
+def attention(q, k, v, lens: List[int], kv_last=None):
+    """Causal attention of packed sequences: q [T, nh, D], k/v [T, nkv, D].  ``kv_last``: a
+    function applied to the K / V the LAST query row of each sequence reads (a decode row
+    attending to a quantized cache), the other rows reading them as given."""
     nh, nkv, D = q.shape[1], k.shape[1], q.shape[2]
     outs, s0 = [], 0
     for L in lens:
@@ -85,46 +87,68 @@ def attention(q, k, v, lens: List[int]):
         sc = (qs @ ks.transpose(1, 2)) / math.sqrt(D)
         mask = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
         sc = sc.masked_fill(mask, float("-inf"))
-        outs.append((sc.softmax(-1) @ vs).transpose(0, 1).reshape(L, nh * D))
+        o = sc.softmax(-1) @ vs
+        if kv_last is not None:
+            kq, vq = kv_last(ks), kv_last(vs)
+            sl = (qs[:, -1:] @ kq.transpose(1, 2)) / math.sqrt(D)
+            o = torch.cat([o[:, :-1], sl.softmax(-1) @ vq], 1)
+        outs.append(o.transpose(0, 1).reshape(L, nh * D))
         s0 += L
     return torch.cat(outs, 0)
 
 
+def _identity(t):
+    return t
+
+
+def bf16_round(t):
+    """Round to bf16 and back (the storage precision of every activation of a bf16 model)."""
+    return t.to(torch.bfloat16).float()
+
+
+def fp8_round(t):
+    """Round to OCP e4m3fn and back (the fp8 KV cache's element type)."""
+    return t.to(torch.float8_e4m3fn).float()
+
+
 def ref_hidden(P: Dict, cfg, ids: torch.Tensor, lens: List[int], p: float = 0.0,
-               seeds: Optional[List[int]] = None) -> torch.Tensor:
+               seeds: Optional[List[int]] = None, store=_identity,
+               kv_last=None) -> torch.Tensor:
     """Final-norm hidden states [T, H] of packed sequences ``ids`` [T] with lengths ``lens``.
     ``seeds``: the dropout seed of every adapted linear call, in call order (q|k|v then o per
-    layer -- the order lumen draws them from torch's CPU generator)."""
+    layer -- the order lumen draws them from torch's CPU generator).  ``store``: rounding
+    applied to every activation between ops (``bf16_round``: the bf16 noise floor of the same
+    math, each op itself in fp32); ``kv_last``: see ``attention``."""
     nh, nkv, D, Fd = (cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
                       cfg.intermediate_size)
     eps, theta = cfg.rms_norm_eps, cfg.rope_theta
     pos = torch.cat([torch.arange(L, device=ids.device) for L in lens])
-    h = P["embed"][ids]
+    h = store(P["embed"][ids])
     it = iter(seeds or [])
 
     def call(x, L, key):
         lo = L.get(key + "_lora")
         seed = next(it) if (lo is not None and p > 0) else 0
-        return lin(x, L[key], lo, p, seed)
+        return store(lin(x, L[key], lo, p, seed))
 
     for L in P["layers"]:
-        x = rms(h, L["ln1"], eps)
+        x = store(rms(h, L["ln1"], eps))
         qkv = call(x, L, "qkv")
         q, k, v = qkv.split([nh * D, nkv * D, nkv * D], 1)
         T = q.shape[0]
-        q = rope(q.reshape(T, nh, D), pos, theta)
-        k = rope(k.reshape(T, nkv, D), pos, theta)
-        o = attention(q, k, v.reshape(T, nkv, D), lens)
-        h = h + call(o, L, "o")
-        x = rms(h, L["ln2"], eps)
+        q = store(rope(q.reshape(T, nh, D), pos, theta))
+        k = store(rope(k.reshape(T, nkv, D), pos, theta))
+        o = store(attention(q, k, v.reshape(T, nkv, D), lens, kv_last))
+        h = store(h + call(o, L, "o"))
+        x = store(rms(h, L["ln2"], eps))
         gu = call(x, L, "gu")
-        h = h + call(F.silu(gu[:, :Fd]) * gu[:, Fd:], L, "down")
+        h = store(h + call(store(F.silu(gu[:, :Fd]) * gu[:, Fd:]), L, "down"))
     return rms(h, P["norm"], eps)
 
 
 def ref_loss(P: Dict, cfg, ids: torch.Tensor, labels: torch.Tensor, lens: List[int],
-             p: float = 0.0, seeds: Optional[List[int]] = None) -> torch.Tensor:
+             p: float = 0.0, seeds: Optional[List[int]] = None, store=_identity) -> torch.Tensor:
     """Mean next-token cross-entropy over labels != -100 (labels already shifted)."""
-    h = ref_hidden(P, cfg, ids, lens, p, seeds)
+    h = ref_hidden(P, cfg, ids, lens, p, seeds, store)
     logits = h @ P["head"].t()
     return F.cross_entropy(logits, labels, ignore_index=-100)

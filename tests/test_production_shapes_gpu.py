@@ -18,7 +18,7 @@ import os
 import pytest
 import torch
 
-from _ref_llama import ref_hidden, ref_loss, ref_params
+from _ref_llama import bf16_round, fp8_round, ref_hidden, ref_loss, ref_params
 
 pytestmark = pytest.mark.gpu
 
@@ -75,23 +75,37 @@ def test_llama2_7b_shaped_training_step_matches_fp32():
     assert all(mod.fold_ext() for _, mod in m.lora_modules())     # the fold is what ran
     got = {n: prm.grad.float().clone() for n, prm in m.named_parameters() if prm.requires_grad}
 
-    # oracle: the same dropout seeds, drawn in the same order from the CPU generator
+    # oracle: the same dropout seeds, drawn in the same order from the CPU generator; run in
+    # fp32, and again with every activation rounded to bf16 between ops (the noise floor any
+    # bf16 implementation of this math has against fp32)
     torch.manual_seed(7)
     seeds = [int(torch.randint(0, 2**62, (1,)).item()) for _ in range(2 * cfg.num_hidden_layers)]
-    lref = ref_loss(P, cfg, ids.reshape(-1).to(DEV), labels.reshape(-1).to(DEV), [S] * B, p,
-                    seeds)
-    lref.backward()
-    assert abs(loss.item() - lref.item()) < 2e-3 * abs(lref.item()), (loss.item(), lref.item())
-    n = 0
-    for i, L in enumerate(P["layers"]):
-        for key, name in (("qkv", "self_attn.qkv_proj"), ("o", "self_attn.o_proj")):
-            A, Bm = L[key + "_lora"][:2]
-            for leaf, which in ((A, "lora_A"), (Bm, "lora_B")):
-                gname = f"layers.{i}.{name}.lora.{which}"
-                e = rel(got[gname], leaf.grad)
-                assert e < 2e-2, (gname, e)
-                n += 1
-    assert n == 4 * cfg.num_hidden_layers
+    grads = {}
+    for tag, store in (("fp32", None), ("bf16", bf16_round)):
+        for L in P["layers"]:
+            for key in ("qkv", "o"):
+                for leaf in L[key + "_lora"][:2]:
+                    leaf.grad = None
+        kw = {"store": store} if store is not None else {}
+        lref = ref_loss(P, cfg, ids.reshape(-1).to(DEV), labels.reshape(-1).to(DEV), [S] * B, p,
+                        seeds, **kw)
+        lref.backward()
+        grads[tag] = (lref.item(), {
+            f"layers.{i}.{name}.lora.{which}": leaf.grad.clone()
+            for i, L in enumerate(P["layers"])
+            for key, name in (("qkv", "self_attn.qkv_proj"), ("o", "self_attn.o_proj"))
+            for leaf, which in zip(L[key + "_lora"][:2], ("lora_A", "lora_B"))})
+    l32, g32 = grads["fp32"]
+    l16, g16 = grads["bf16"]
+    assert abs(loss.item() - l32) < 2e-3 * abs(l32), (loss.item(), l32)
+    report = {}
+    for gname, ref in g32.items():
+        e, floor = rel(got[gname], ref), rel(g16[gname], ref)
+        report[gname] = (round(e, 4), round(floor, 4))
+        # within the bf16 floor of the same math (x 1.5), or 1.5e-2 when the floor is tiny
+        assert e < max(1.5e-2, 1.5 * floor), (gname, e, floor)
+    print("lumen vs fp32 oracle, bf16-rounded oracle vs fp32:", report)
+    assert len(report) == 4 * cfg.num_hidden_layers
 
 
 @pytest.mark.parametrize("kv", ["auto", "fp8"])
@@ -134,19 +148,23 @@ def test_llama2_7b_shaped_decode_step_matches_fp32(kv):
     rows, logits = full[0]
     assert logits.shape == (256, cfg.vocab_size)
     # oracle: fp32 forward of prompt + first token, logits at the last position
+    # (fp8: the decode row reads every K / V through the e4m3 cache, the prompt rows -- which
+    # built the cache by whole-prompt prefill -- read them unrounded, as the engine does)
     ref = []
     with torch.no_grad():
         for c in range(0, 256, 32):
             chunk = rows[c:c + 32]
             ids = [s.prompt_ids + s.output_ids[:1] for s in chunk]
-            h = ref_hidden(P, cfg, torch.tensor(sum(ids, []), device=DEV), [len(x) for x in ids])
+            h = ref_hidden(P, cfg, torch.tensor(sum(ids, []), device=DEV), [len(x) for x in ids],
+                           kv_last=fp8_round if kv == "fp8" else None)
             ends = torch.tensor([len(x) for x in ids], device=DEV).cumsum(0) - 1
             ref.append(h[ends] @ P["head"].t())
     ref = torch.cat(ref, 0)
     e = rel(logits, ref)
     per_row = ((logits - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
     agree = (logits.argmax(1) == ref.argmax(1)).float().mean().item()
-    tol = 2e-2 if kv == "auto" else 6e-2
+    tol = 2e-2 if kv == "auto" else 3e-2
+    print(kv, "decode logits vs fp32 oracle: rel", e, "worst row", per_row, "argmax", agree)
     assert e < tol and per_row < 2 * tol, (kv, e, per_row)
     assert agree >= 0.9, agree
     assert [s.output_ids[1] for s in rows] == logits.argmax(1).tolist()
