@@ -150,21 +150,31 @@ def test_llama2_7b_shaped_decode_step_matches_fp32(kv):
     # oracle: fp32 forward of prompt + first token, logits at the last position
     # (fp8: the decode row reads every K / V through the e4m3 cache, the prompt rows -- which
     # built the cache by whole-prompt prefill -- read them unrounded, as the engine does)
-    ref = []
-    with torch.no_grad():
-        for c in range(0, 256, 32):
-            chunk = rows[c:c + 32]
-            ids = [s.prompt_ids + s.output_ids[:1] for s in chunk]
-            h = ref_hidden(P, cfg, torch.tensor(sum(ids, []), device=DEV), [len(x) for x in ids],
-                           kv_last=fp8_round if kv == "fp8" else None)
-            ends = torch.tensor([len(x) for x in ids], device=DEV).cumsum(0) - 1
-            ref.append(h[ends] @ P["head"].t())
-    ref = torch.cat(ref, 0)
+    # The fp32 oracle, and the same oracle with bf16-rounded activations (its distance from
+    # fp32 is the noise floor of any bf16 implementation; with fp8 K/V it is large, because a
+    # one-ulp bf16 difference moves an element across an e4m3 rounding boundary).
+    def oracle(store):
+        out = []
+        with torch.no_grad():
+            for c in range(0, 256, 32):
+                chunk = rows[c:c + 32]
+                ids = [s.prompt_ids + s.output_ids[:1] for s in chunk]
+                kw = {"store": store} if store is not None else {}
+                h = ref_hidden(P, cfg, torch.tensor(sum(ids, []), device=DEV),
+                               [len(x) for x in ids], kv_last=fp8_round if kv == "fp8" else None,
+                               **kw)
+                ends = torch.tensor([len(x) for x in ids], device=DEV).cumsum(0) - 1
+                out.append(h[ends] @ P["head"].t())
+        return torch.cat(out, 0)
+
+    ref = oracle(None)
+    floor = rel(oracle(bf16_round), ref)
     e = rel(logits, ref)
     per_row = ((logits - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
     agree = (logits.argmax(1) == ref.argmax(1)).float().mean().item()
-    tol = 2e-2 if kv == "auto" else 3e-2
-    print(kv, "decode logits vs fp32 oracle: rel", e, "worst row", per_row, "argmax", agree)
-    assert e < tol and per_row < 2 * tol, (kv, e, per_row)
+    print(kv, "decode logits vs fp32 oracle: rel", e, "bf16 floor", floor, "worst row", per_row,
+          "argmax", agree)
+    tol = max(2e-2, 1.5 * floor)
+    assert e < tol and per_row < 2.5 * tol, (kv, e, floor, per_row)
     assert agree >= 0.9, agree
     assert [s.output_ids[1] for s in rows] == logits.argmax(1).tolist()
