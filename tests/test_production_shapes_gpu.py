@@ -168,13 +168,16 @@ def test_llama2_7b_shaped_decode_step_matches_fp32(kv):
         return torch.cat(out, 0)
 
     ref = oracle(None)
-    floor = rel(oracle(bf16_round), ref)
+    r16 = oracle(bf16_round)
+    floor = rel(r16, ref)
+    floor_agree = (r16.argmax(1) == ref.argmax(1)).float().mean().item()
     e = rel(logits, ref)
     per_row = ((logits - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
     agree = (logits.argmax(1) == ref.argmax(1)).float().mean().item()
     print(kv, "decode logits vs fp32 oracle: rel", e, "bf16 floor", floor, "worst row", per_row,
-          "argmax", agree)
+          "argmax", agree, "floor argmax", floor_agree)
     tol = max(2e-2, 1.5 * floor)
     assert e < tol and per_row < 2.5 * tol, (kv, e, floor, per_row)
-    assert agree >= 0.9, agree
+    # greedy choices of a random-init model are often near-ties: as often right as the floor's
+    assert agree >= min(0.9, floor_agree - 0.05), (agree, floor_agree)
     assert [s.output_ids[1] for s in rows] == logits.argmax(1).tolist()
