@@ -183,7 +183,7 @@ class CustomAllReduce:
                 t = torch.ones(nb // 2, dtype=torch.bfloat16, device=self.device)
                 row = {"bytes": int(nb)}
                 for name, two in (("one", False), ("two", True)):
-                    _, blocks = self.plan(nb, t.numel())
+                    blocks = self._blocks(t.numel(), two)
                     row[name] = self._time_us(
                         lambda: self.C.car_allreduce(self.data, self.sig, self.rank, t, t, two,
                                                      blocks, self.timeout_s, self._flag_dev),
@@ -225,15 +225,17 @@ class CustomAllReduce:
         return (t.is_cuda and t.dtype in _DTYPES and t.is_contiguous()
                 and t.numel() % 8 == 0 and 0 < t.numel() * t.element_size() <= self.max_bytes)
 
-    def plan(self, nbytes: int, numel: int):
-        """(two_shot, blocks) for a message: ~2 units of 8 elements per thread (256 threads)
-        up to the kernel's block limit."""
-        two = nbytes > self.one_shot_max
+    def _blocks(self, numel: int, two: bool) -> int:
+        """~2 units of 8 elements per thread (256 threads) up to the kernel's block limit; a
+        two-shot block splits its span over the W ranks, so at most units / W blocks."""
         units = numel // 8
         blocks = max(1, min(self.max_blocks, -(-units // 512)))
-        if two:
-            blocks = max(1, min(blocks, units // self.world))
-        return two, blocks
+        return max(1, min(blocks, units // self.world)) if two else blocks
+
+    def plan(self, nbytes: int, numel: int):
+        """(two_shot, blocks) for a message."""
+        two = nbytes > self.one_shot_max
+        return two, self._blocks(numel, two)
 
     def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None,
                    two_shot: Optional[bool] = None, blocks: Optional[int] = None) -> torch.Tensor:
