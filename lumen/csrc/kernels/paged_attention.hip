@@ -304,12 +304,51 @@ __device__ __forceinline__ R pa_ld_nt(const void* p) {
   return r;
 }
 
+// inline-asm form of pa_ld_nt (the PF kernel counts its own waits: see there)
+template <typename R>
+__device__ __forceinline__ R pa_ld_nt_asm(const void* p) {
+  R r;
+  if constexpr (sizeof(R) == 16) {
+    pa_u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+    __builtin_memcpy(&r, &v, 16);
+  } else {
+    pa_u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+    __builtin_memcpy(&r, &v, 8);
+  }
+  return r;
+}
+
+// orders every later use of these registers after the preceding asm wait
+template <typename R>
+__device__ __forceinline__ void pa_fence_reg(R& a, R& b) {
+  if constexpr (sizeof(R) == 16) {
+    pa_u32x4 x, y;
+    __builtin_memcpy(&x, &a, 16);
+    __builtin_memcpy(&y, &b, 16);
+    asm volatile("" : "+v"(x), "+v"(y));
+    __builtin_memcpy(&a, &x, 16);
+    __builtin_memcpy(&b, &y, 16);
+  } else {
+    pa_u32x2 x, y;
+    __builtin_memcpy(&x, &a, 8);
+    __builtin_memcpy(&y, &b, 8);
+    asm volatile("" : "+v"(x), "+v"(y));
+    __builtin_memcpy(&a, &x, 8);
+    __builtin_memcpy(&b, &y, 8);
+  }
+}
+
 // UNI (block_size == rows per workgroup step, the launcher checks): row t = base + u * NGR + grp
 // of an iteration lies in block (base / BS + u) at offset grp, so the block ids are
 // workgroup-uniform -- scalar loads issued one iteration ahead -- instead of a per-lane block
 // table load feeding every K / V address (a dependent L2 round trip per iteration); the K / V
 // pieces are non-temporal loads.
-template <typename T, int D, int G, typename KT = T, bool UNI = false>
+// PF (with UNI): software-pipelined -- iteration i+1's K / V pieces are issued before iteration
+// i's softmax / P.V work, so every wave keeps two iterations of loads in flight (a pure nt read
+// stream reaches 7.1 TB/s on this chip with 8 x 16 B per lane in flight, profiles/r5_decode)
+template <typename T, int D, int G, typename KT = T, bool UNI = false, bool PF = false>
 __global__ void __launch_bounds__(256) pa_decode1_kernel(
     T* __restrict__ out, const T* __restrict__ q, const KT* __restrict__ kc,
     const KT* __restrict__ vc, const int* __restrict__ block_tables,
@@ -351,42 +390,8 @@ __global__ void __launch_bounds__(256) pa_decode1_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
   }
-  int nbid[U];
-  if constexpr (UNI) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) nbid[u] = start + u * NGR < end ? bt[start / NGR + u] : 0;
-  }
-  for (int base = start; base < end; base += NGR * U) {
-    const int t0 = base + grp;
-    Raw kraw[U], vraw[U];
-    if constexpr (UNI) {
-      int bid[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) bid[u] = nbid[u];
-      const int nb = base + NGR * U;
-#pragma unroll
-      for (int u = 0; u < U; ++u) nbid[u] = nb + u * NGR < end ? bt[nb / NGR + u] : 0;
-      const KT* kr0 = kc + head_off + static_cast<size_t>(grp) * D + d0;
-      const KT* vr0 = vc + head_off + static_cast<size_t>(grp) * D + d0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (t0 + u * NGR < end) {
-          const size_t off = static_cast<size_t>(bid[u]) * blk_stride;
-          kraw[u] = pa_ld_nt<Raw>(kr0 + off);
-          vraw[u] = pa_ld_nt<Raw>(vr0 + off);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int t = t0 + u * NGR;
-        if (t < end) {
-          const size_t off = bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
-          kraw[u] = *reinterpret_cast<const Raw*>(kc + off);
-          vraw[u] = *reinterpret_cast<const Raw*>(vc + off);
-        }
-      }
-    }
+  // one iteration's online-softmax update from its raw K / V pieces (rows t0 + u * NGR)
+  const auto consume = [&](int t0, const Raw (&kraw)[U], const Raw (&vraw)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = t0 + u * NGR;
@@ -410,6 +415,97 @@ __global__ void __launch_bounds__(256) pa_decode1_kernel(
         }
       }
     }
+  };
+  int nbid[U];
+  if constexpr (UNI) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) nbid[u] = start + u * NGR < end ? bt[start / NGR + u] : 0;
+  }
+  if constexpr (UNI && PF) {
+    // Two register sets, the loop unrolled by two so they swap roles without copies (a copy of
+    // the freshly issued set would wait for it); the loads are inline asm and the waits counted
+    // by hand -- the compiler cannot see them, so it neither drains the set in flight before
+    // the set being consumed nor waits before the branch joins.  Rows past the context read
+    // their (allocated) block's slot or block 0; consume() skips them.
+    const KT* kr0 = kc + head_off + static_cast<size_t>(grp) * D + d0;
+    const KT* vr0 = vc + head_off + static_cast<size_t>(grp) * D + d0;
+    constexpr int NL = 2 * U;  // loads per set
+    const int step = NGR * U;
+    const auto ids = [&](int b, int (&o)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) o[u] = b + u * NGR < end ? bt[b / NGR + u] : 0;
+    };
+    const auto issue = [&](const int (&id)[U], Raw (&kk)[U], Raw (&vv)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t off = static_cast<size_t>(id[u]) * blk_stride;
+        kk[u] = pa_ld_nt_asm<Raw>(kr0 + off);
+        vv[u] = pa_ld_nt_asm<Raw>(vr0 + off);
+      }
+    };
+    // wait until the OLDER set landed (NEWER loads may stay in flight), then fence its registers
+    const auto landed = [&](bool newer_in_flight, Raw (&kk)[U], Raw (&vv)[U]) {
+      if (newer_in_flight) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < U; ++u) pa_fence_reg(kk[u], vv[u]);
+    };
+    // q must land before the first asm load issues: a later compiler-inserted wait for it
+    // would be vmcnt(0) and drain the prefetched set too
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(qv[h][j]));
+    Raw kA[U], vA[U], kB[U], vB[U];
+    issue(nbid, kA, vA);
+    ids(start + step, nbid);
+    for (int base = start; base < end; base += 2 * step) {
+      const int b1 = base + step;
+      const bool more1 = b1 < end;
+      if (more1) issue(nbid, kB, vB);
+      ids(b1 + step, nbid);
+      landed(more1, kA, vA);
+      consume(base + grp, kA, vA);
+      if (!more1) break;
+      const int b2 = b1 + step;
+      const bool more2 = b2 < end;
+      if (more2) issue(nbid, kA, vA);
+      ids(b2 + step, nbid);
+      landed(more2, kB, vB);
+      consume(b1 + grp, kB, vB);
+    }
+  } else
+  for (int base = start; base < end; base += NGR * U) {
+    const int t0 = base + grp;
+    Raw kraw[U], vraw[U];
+    if constexpr (UNI) {
+      int bid[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) bid[u] = nbid[u];
+      const int nb = base + NGR * U;
+#pragma unroll
+      for (int u = 0; u < U; ++u) nbid[u] = nb + u * NGR < end ? bt[nb / NGR + u] : 0;
+      const KT* kr0 = kc + head_off + static_cast<size_t>(grp) * D + d0;
+      const KT* vr0 = vc + head_off + static_cast<size_t>(grp) * D + d0;
+      // unconditional (see the PF form): all 2U pieces in flight before the first use
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t off = static_cast<size_t>(bid[u]) * blk_stride;
+        kraw[u] = pa_ld_nt<Raw>(kr0 + off);
+        vraw[u] = pa_ld_nt<Raw>(vr0 + off);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int t = t0 + u * NGR;
+        if (t < end) {
+          const size_t off = bt[t / BS] * blk_stride + head_off + (t % BS) * D + d0;
+          kraw[u] = *reinterpret_cast<const Raw*>(kc + off);
+          vraw[u] = *reinterpret_cast<const Raw*>(vc + off);
+        }
+      }
+    }
+    consume(t0, kraw, vraw);
   }
   // merge the 64 / LPT row groups of each wave (lanes d0-aligned at xor 16, 32, ...)
 #pragma unroll
@@ -594,9 +690,18 @@ static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out
                         float* tm,
                         float* tl, void* to, int PART, unsigned* cnt, int one_pass, bool fp8kv) {
   // one_pass 2: the uniform-block-id variant where the block size equals the rows per step
-  const bool uni = one_pass == 2 && BS == 256 / (D / 8) && PART % BS == 0;
+  const bool uni = one_pass >= 2 && BS == 256 / (D / 8) && PART % BS == 0;
+  const bool pf = uni && one_pass == 3;
 #define LUMEN_PA_G(GG)                                                                         \
-  if (fp8kv && uni)                                                                             \
+  if (fp8kv && pf)                                                                              \
+    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8, true, true>), grid, dim3(256), 0, st,  \
+                       (T*)out, (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh,    \
+                       nkv, BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);         \
+  else if (pf)                                                                                  \
+    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, T, true, true>), grid, dim3(256), 0, st,    \
+                       (T*)out, (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, qldh, nkv,   \
+                       BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);              \
+  else if (fp8kv && uni)                                                                        \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8, true>), grid, dim3(256), 0, st,        \
                        (T*)out, (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh,    \
                        nkv, BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);         \

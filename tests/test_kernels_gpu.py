@@ -304,9 +304,11 @@ def test_paged_decode(nh, nkv, D, ctx_max):
     for part in (512, 64):
         o = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part)
         assert rel(o, o2) < 1e-2
-        for one in (True, False):  # single-pass (online softmax) and two-pass kernels
+        # two-pass (0), single-pass (1), single-pass with uniform block ids + nt loads (2),
+        # and its software-pipelined form (3); 2 / 3 fall back to 1 where block size != 16
+        for one in (0, 1, 2, 3):
             assert rel(paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part,
-                                    one_pass=one), o2) < 1e-2
+                                    one_pass=one), o2) < 1e-2, (one, part)
         # fused merge (arrival counters, last partition merges) == two-kernel merge, and the
         # counters reset themselves: a repeat call gives the same bits
         o_f = paged_decode(q, kc, vc, bt, cl, int(lens.max()), scale, part, fused_merge=True,
@@ -926,7 +928,9 @@ def test_fp8_kv_cache_kernels(nh, nkv, D):
     scale = 1 / math.sqrt(D)
     o2 = paged_decode_ref(q, kc, vc, perm, cl, scale)
     for part in (512, 64):
-        assert rel(paged_decode(q, kc, vc, perm, cl, ctx, scale, part), o2) < 1e-2
+        for one in (1, 2, 3):
+            assert rel(paged_decode(q, kc, vc, perm, cl, ctx, scale, part, one_pass=one),
+                       o2) < 1e-2, (one, part)
     if D == 128:  # chunked prefill over the fp8 cache (dequantised into the 16-bit scratch)
         cu, kl = [0, 20, 37, 137, 138], [300, 17, 200, 129]
         qr = (torch.randn(cu[-1], (nh + 2 * nkv) * D, device=DEV) * 0.5).to(torch.bfloat16)
