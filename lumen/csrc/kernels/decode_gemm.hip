@@ -146,7 +146,7 @@ template <typename T, int BM, int BN, int WM, int WN, bool XT = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
 dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y,
              float* __restrict__ ws, int* __restrict__ cnt, int M, int N, int K, long long ldx,
-             long long ldy, int tiles_n, int S, int kt_total, int rot) {
+             long long ldy, int tiles_n, int S, int kt_total, int rot, int skip) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NI = BN / WN / 16, MJ = BM / WM / 16;
@@ -196,7 +196,7 @@ dgemm_kernel(const T* __restrict__ x, const T* __restrict__ W, T* __restrict__ y
       stage<T, BM, BN, NW, XT>(lds + nbuf * STAGE_B, Wt, K, nvalid, x, ldx, M, kat(t + 2), wid,
                                lane);
     }
-    compute<T, NI, MJ>(lds + buf * STAGE_B, nrow0, mrow0, acc, lane);
+    if (!skip) compute<T, NI, MJ>(lds + buf * STAGE_B, nrow0, mrow0, acc, lane);
     buf = buf == 2 ? 0 : buf + 1;
   }
 
@@ -274,11 +274,12 @@ hipError_t launch(const void* x, const void* W, void* y, float* ws, int* cnt, in
   const int tiles_n = (N + BN - 1) / BN;
   const int kt = K / BK;
   const int rot = (flags & 1) ? 1 : 0;
+  const int skip = (flags >> 2) & 1;  // cost probe: the k loop without its MFMA work
   dim3 grid(tiles_n * S), block(64 * NW);
 #define LUMEN_DG_CASE(bm, bn, wm, wn)                                                          \
   if (BM == bm && BN == bn && NW == wm * wn && !(flags & 2)) {                                 \
     hipLaunchKernelGGL((dgemm_kernel<T, bm, bn, wm, wn>), grid, block, 0, st, (const T*)x,     \
-                       (const T*)W, (T*)y, ws, cnt, M, N, K, ldx, ldy, tiles_n, S, kt, rot);  \
+                       (const T*)W, (T*)y, ws, cnt, M, N, K, ldx, ldy, tiles_n, S, kt, rot, skip);  \
     return hipGetLastError();                                                                  \
   }
   LUMEN_DG_VARIANTS(LUMEN_DG_CASE)
@@ -287,7 +288,7 @@ hipError_t launch(const void* x, const void* W, void* y, float* ws, int* cnt, in
   if (BM == bm && BN == bn && NW == wm * wn && (flags & 2)) {                                  \
     hipLaunchKernelGGL((dgemm_kernel<T, bm, bn, wm, wn, true>), grid, block, 0, st,            \
                        (const T*)x, (const T*)W, (T*)y, ws, cnt, M, N, K, ldx, ldy, tiles_n, S, \
-                       kt, rot);                                                               \
+                       kt, rot, skip);                                                         \
     return hipGetLastError();                                                                  \
   }
   LUMEN_DG_XT_VARIANTS(LUMEN_DG_XT_CASE)
@@ -303,7 +304,8 @@ hipError_t launch(const void* x, const void* W, void* y, float* ws, int* cnt, in
 // ceil(N / BN) * S * 256 * (BM * BN / 256) floats and ``cnt`` ceil(N / BN) zeroed ints (the last
 // slice of each tile re-zeroes its counter, so they stay zero between launches).
 // flags: bit 0 = per-tile k rotation; bit 1 = x in the k-tiled layout [K / 64][BM][64]
-// (ldx ignored; BM = 256 variants only)
+// (ldx ignored; BM = 256 variants only); bit 2 = cost probe, the k loop without its ds_reads and
+// MFMAs (the output is garbage)
 extern "C" hipError_t lumen_decode_gemm(int dtype, const void* x, const void* W, void* y,
                                         float* ws, int* cnt, int M, int N, int K, long long ldx,
                                         long long ldy, int BM, int BN, int NW, int S, int flags,

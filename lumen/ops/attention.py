@@ -44,8 +44,10 @@ _merge_counters: dict = {}
 # 3.857 vs 3.865 ms ITL, profiles/r02_serve); callers may still ask for it (``fused_merge``).
 # decode kernel: 0 = two-pass; 1 = single-pass (K and V streamed together, online softmax per
 # row group); 2 = single-pass with workgroup-uniform block ids and non-temporal K / V loads
-# (used where the block size equals the kernel's rows per step, else 1)
-PA_ONE_PASS = int(os.environ.get("LUMEN_PA_1PASS", "2"))
+# (used where the block size equals the kernel's rows per step, else 1); 3 = 2 software-pipelined
+# (two register sets, the next iteration's K / V loads in flight while one is consumed; default,
+# profiles/r5_decode)
+PA_ONE_PASS = int(os.environ.get("LUMEN_PA_1PASS", "3"))
 
 
 def _pa_counters(device: torch.device, n: int) -> torch.Tensor:
