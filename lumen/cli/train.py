@@ -34,6 +34,16 @@ VARIANTS = {
 }
 
 
+def _ckpt_arg(v: str) -> str:
+    """--gradient_checkpointing value: auto | true | false | selective | full, optionally ':N'."""
+    base, _, n = v.partition(":")
+    if base not in ("auto", "true", "false", "selective", "full") or (
+            n and (base not in ("selective", "full") or not n.isdigit())):
+        raise argparse.ArgumentTypeError(
+            f"invalid choice {v!r}: auto, true, false, selective, full, selective:N or full:N")
+    return v
+
+
 def build_parser(variant: str) -> argparse.ArgumentParser:
     v = VARIANTS[variant]
     ap = argparse.ArgumentParser(description=f"LoRA fine-tuning on MI355X ({variant})")
@@ -79,13 +89,14 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--save_strategy", default=v["save"], choices=["steps", "epoch", "no"])
     ap.add_argument("--warmup_steps", type=int, default=0)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--gradient_checkpointing", default="auto",
-                    choices=["auto", "true", "false", "selective", "full"],
-                    help="activation recompute (the reference always enables it).  true = the "
+    ap.add_argument("--gradient_checkpointing", default="auto", type=_ckpt_arg,
+                    help="activation recompute (the reference always enables it): auto | true | "
+                         "false | selective | full | selective:N | full:N.  true = the "
                          "model's default policy (Llama: 'selective', the gate|up output "
                          "recomputed; layers whose MLP is trainable or adapted are recomputed "
-                         "whole, as 'full'); full = per-layer recompute like HF; auto: on only "
-                         "when the estimated activations do not fit in free HBM (logged)")
+                         "whole, as 'full'); full = per-layer recompute like HF; ':N' = only the "
+                         "first N layers recompute; auto: only as much recompute as the "
+                         "estimated activations need to fit in free HBM (logged)")
     ap.add_argument("--no_gradient_checkpointing", action="store_true",
                     help="same as --gradient_checkpointing false")
     ap.add_argument("--no_fuse_accumulation", action="store_true",

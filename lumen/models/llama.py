@@ -95,6 +95,25 @@ def _positions(B: int, S: int, device) -> torch.Tensor:
     return t
 
 
+def parse_ckpt_policy(v, policies=("none", "selective", "full")):
+    """``"policy"`` or ``"policy:N"`` (the first N layers recompute) -> (policy, N or None)."""
+    n = None
+    if isinstance(v, str) and ":" in v:
+        v, ns = v.split(":", 1)
+        try:
+            n = int(ns)
+        except ValueError:
+            n = -1
+        if n < 0:
+            raise ValueError(f"gradient checkpointing layer count must be an integer >= 0: {ns!r}")
+    if v not in policies:
+        raise ValueError(f"gradient checkpointing policy must be one of {policies} "
+                         "(optionally ':N' for the first N layers)")
+    if n == 0:
+        v, n = "none", None
+    return v, (None if v == "none" else n)
+
+
 class LlamaMLP(nn.Module):
     def __init__(self, cfg: ModelConfig, dtype=None, device=None):
         super().__init__()
@@ -150,6 +169,7 @@ class LlamaForCausalLM(nn.Module):
         self.norm = RMSNorm(H, cfg.rms_norm_eps, dtype, device)
         self.lm_head = Linear(H, V, dtype=dtype, device=device, seg_names=["lm_head"])
         self._ckpt = "none"
+        self._ckpt_layers: Optional[int] = None  # recompute only the first N layers (None: all)
         self.unit_gate = None    # engine hook run before each unit (async optimizer offload)
         self.coordinator = None  # ZeRO-3 parameter coordinator (lumen.parallel.zero)
 
@@ -164,17 +184,24 @@ class LlamaForCausalLM(nn.Module):
         projection GEMM per layer); ``"full"`` -- the reference's per-layer recompute (HF
         ``gradient_checkpointing=True``: the layer input only, the whole forward re-run).
         Assigning True picks ``LUMEN_CKPT_POLICY`` (default ``selective``), False ``none``.
+        ``"selective:N"`` / ``"full:N"``: only the first N layers recompute, the others keep
+        their activations (Megatron's recompute-num-layers): recompute cost and activation
+        saving both scale with N, so ``--gradient_checkpointing auto`` recomputes just the
+        layers the HBM budget needs (``memory_plan.pick_checkpointing``).
 
         A layer whose MLP cannot use the selective recompute (trainable gate|up / down weights,
         or adapters on them) is checkpointed whole instead (``full`` for that layer), so asking
         for checkpointing never silently keeps every activation."""
-        return self._ckpt
+        n = self._ckpt_layers
+        return self._ckpt if n is None or self._ckpt == "none" else f"{self._ckpt}:{n}"
 
     def selective_eligible(self) -> bool:
         """True when every layer can run the ``selective`` policy as such."""
         return all(l.mlp.recompute_eligible for l in self.layers)
 
-    def _layer_policy(self, layer) -> str:
+    def _layer_policy(self, layer, i: int = 0) -> str:
+        if self._ckpt_layers is not None and i >= self._ckpt_layers:
+            return "none"
         if self._ckpt == "selective" and not layer.mlp.recompute_eligible:
             if not getattr(self, "_warned_selective", False):
                 self._warned_selective = True
@@ -192,11 +219,13 @@ class LlamaForCausalLM(nn.Module):
             v = os.environ.get("LUMEN_CKPT_POLICY", "selective")
         elif v is False or v is None or v == "false":
             v = "none"
-        if v not in self.CKPT_POLICIES:
-            raise ValueError(f"gradient checkpointing policy must be one of {self.CKPT_POLICIES}")
-        self._ckpt = v
-        for layer in self.layers:
-            layer.mlp.recompute = v == "selective"
+        v, n = parse_ckpt_policy(v, self.CKPT_POLICIES)
+        L = len(self.layers)
+        if n is not None and n >= L:
+            n = None
+        self._ckpt, self._ckpt_layers = v, n
+        for i, layer in enumerate(self.layers):
+            layer.mlp.recompute = v == "selective" and (n is None or i < n)
 
     # --- ZeRO-3 units, in execution order ------------------------------------------------------
     def zero_units(self) -> List[List[nn.Module]]:
@@ -245,7 +274,7 @@ class LlamaForCausalLM(nn.Module):
         res = None
         for i, layer in enumerate(self.layers):
             if (self._ckpt != "none" and self.training and torch.is_grad_enabled()
-                    and self._layer_policy(layer) == "full"):
+                    and self._layer_policy(layer, i) == "full"):
                 fn = lambda h_, r_, L=layer: cp.checkpoint(L, h_, r_, B, S, pos, cu, use_reentrant=False)  # noqa: E731
             else:
                 fn = lambda h_, r_, L=layer: L(h_, r_, B, S, pos, cu)  # noqa: E731

@@ -304,8 +304,11 @@ def _rope_covered(segs, ncols: int) -> bool:
 
 
 def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed,
-                    need_dA=True, need_dB=True):
-    """Returns (dA, dB); adds dZ A into dx in place."""
+                    need_dA=True, need_dB=True, dx_fn=None):
+    """Returns (dA, dB); adds dZ A into dx in place.  ``dx_fn`` (with dx None): produces the
+    frozen path's input gradient (a fresh contiguous [T, K] tensor) when the adapter pass is
+    ready for it -- with ``LUMEN_LORA_BWD_OVERLAP=1`` the dZ / dB pass runs on a side stream
+    beside that GEMM."""
     T, K = x2d.shape
     R = A.shape[0]
     Ntot = dy.shape[1]
@@ -319,7 +322,10 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
     # gradient buffer) when they exist: no zero-filled temporaries and no autograd add kernels
     direct = v2 and DIRECT_GRAD and _direct_ok(A) and _direct_ok(B)
     if v3:
-        return _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, direct)
+        return _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, direct,
+                          dx_fn)
+    if dx_fn is not None:
+        dx = dx_fn()
     nA = R * K if need_dA and not direct else 0
     nB = B.shape[0] * r if need_dB and not direct else 0
     ws = _zeros(T * R + nA + nB, device=dev)
@@ -373,7 +379,8 @@ def lora_bwd_native(dy, x2d, A, B, Z, dx, segs: Sequence[Seg], r, scale, p, seed
     return dA, dB
 
 
-def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, direct):
+def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, direct,
+               dx_fn=None):
     """v3 backward: ONE pass over dY for dZ and dB (lora3_dy), dA from the dropped-out input
     (v2 WGRAD), dx += drop'(dZ A) lane-local (lora3_up mode 5)."""
     T, K = x2d.shape
@@ -386,10 +393,27 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     dZ = ws[:T * R].view(T, R)
     dB = B.grad if (direct and need_dB) else ws[T * R + nA:].view(B.shape[0], r)
 
-    for i in range(0, len(segs), 4):  # one pass over dY: dZ and dB (f32 atomics)
-        ch = segs[i:i + 4]
-        nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
-                     [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+    def dy_pass():
+        for i in range(0, len(segs), 4):  # one pass over dY: dZ and dB (f32 atomics)
+            ch = segs[i:i + 4]
+            nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
+                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+
+    if dx_fn is not None and BWD_OVERLAP and dy.is_cuda:
+        # the dY pass (memory-bound, f32 atomics) beside the input-gradient GEMM (MFMA-bound):
+        # every operand was produced on the main stream before the fork, and the main stream
+        # waits for the side stream before anything reads dZ / dB or frees them
+        main = torch.cuda.current_stream(dev)
+        side = _side_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            dy_pass()
+        dx = dx_fn()
+        main.wait_stream(side)
+    else:
+        dy_pass()
+        if dx_fn is not None:
+            dx = dx_fn()
     dA = None
     if need_dA:
         dA = A.grad if direct else ws[T * R:T * R + nA].view(R, K)
@@ -423,6 +447,16 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
 
 
 DIRECT_GRAD = _os.environ.get("LUMEN_LORA_DIRECT_GRAD", "1") != "0"
+# the backward's dZ / dB pass on a side stream beside the input-gradient GEMM (opt-in A/B)
+BWD_OVERLAP = _os.environ.get("LUMEN_LORA_BWD_OVERLAP", "0") == "1"
+_side_streams: dict = {}
+
+
+def _side_stream(dev) -> "torch.cuda.Stream":
+    s = _side_streams.get(dev)
+    if s is None:
+        s = _side_streams[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def _direct_ok(prm: torch.Tensor) -> bool:
@@ -489,15 +523,22 @@ class _LoraLinear(torch.autograd.Function):
             if not getattr(dy, "_lumen_scratch", False):
                 dy = dy.clone()
             _rope_(dy, ctx.rope, inverse=True)
-        dx = _input_grad(ctx, dy) if ctx.needs_input_grad[0] else None
+        got = {}
+
+        def dx_fn():
+            got["dx"] = _input_grad(ctx, dy)
+            return got["dx"]
+
         _IN_BACKWARD[0] = True
         _DELTA_SLOT[0] = ctx.delta_slot
         try:
-            dA, dB = lora_bwd_native(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed,
-                                     ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+            dA, dB = lora_bwd_native(dy, x2d, A, B, Z, None, segs, r, scale, p, seed,
+                                     ctx.needs_input_grad[3], ctx.needs_input_grad[4],
+                                     dx_fn=dx_fn if ctx.needs_input_grad[0] else None)
         finally:
             _IN_BACKWARD[0] = False
             _DELTA_SLOT[0] = None
+        dx = got.get("dx")
         dw =torch.matmul(dy.t(), x2d) if ctx.w_grad else None
         db = dy.sum(0) if ctx.b_grad else None
         return dx, None, db, dA, dB, None, None, None, None, None, dw, None, None, None, None

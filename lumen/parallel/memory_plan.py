@@ -52,25 +52,51 @@ def transposes_fit(need_bytes: float, gathered_bytes: float, free_bytes: float,
     return need_bytes + gathered_bytes <= free_bytes - activation_reserve(total_bytes)
 
 
+def _act_fraction(policy: str, k: int, L: int) -> float:
+    """Activations kept under ``policy`` on the first k of L layers, as a fraction of none."""
+    if policy == "selective":
+        return 1.0 - k * (1.0 - SELECTIVE_FRACTION) / L
+    # full on k layers: their inputs only, plus one layer's activations during its recompute
+    return (L - k) / L + k / (ACT_ROWS_PER_LAYER * L) + (1.0 / L if k else 0.0)
+
+
+def _split_policy(policy):
+    if isinstance(policy, str) and ":" in policy:
+        p, n = policy.split(":", 1)
+        return p, int(n)
+    return policy, None
+
+
 def activation_bytes(cfg, tokens: int, policy: str = "none") -> float:
     """Activations a micro-step of ``tokens`` keeps for its backward under a recompute policy
-    (``full``: the layer inputs plus one layer's activations during its recompute)."""
+    (``full``: the layer inputs plus one layer's activations during its recompute;
+    ``"selective:N"`` / ``"full:N"``: that policy on the first N layers only)."""
     L, H = cfg.num_hidden_layers, cfg.hidden_size
     full = tokens * L * ACT_ROWS_PER_LAYER * H * 2
     if policy in ("none", False, None):
         return float(full)
-    if policy == "selective":
-        return SELECTIVE_FRACTION * full
-    return float(tokens * H * 2 * (L + ACT_ROWS_PER_LAYER))
+    if policy is True:
+        policy = "selective"
+    p, n = _split_policy(policy)
+    return float(full * _act_fraction(p, L if n is None else min(n, L), L))
 
 
-def pick_checkpointing(est_bytes: float, free_bytes: float, selective_ok: bool):
+def pick_checkpointing(est_bytes: float, free_bytes: float, selective_ok: bool,
+                       n_layers: Optional[int] = None):
     """``--gradient_checkpointing auto``: none when the activations fit twice, else selective
-    (where every layer can run it), else full per-layer recompute."""
+    (where every layer can run it), else full per-layer recompute.  With ``n_layers`` (the
+    model takes ``"policy:N"``) only as many layers recompute as the budget needs: the
+    recompute cost grows with N, so the fewest that fit."""
     if 2 * est_bytes <= free_bytes:
         return False
-    if selective_ok and 2 * SELECTIVE_FRACTION * est_bytes <= free_bytes:
-        return "selective"
+    L = n_layers
+    for pol in (("selective", "full") if selective_ok else ("full",)):
+        if L:
+            for k in range(1, L + 1):
+                if 2 * est_bytes * _act_fraction(pol, k, L) <= free_bytes:
+                    return pol if k == L else f"{pol}:{k}"
+        elif pol == "selective" and 2 * SELECTIVE_FRACTION * est_bytes <= free_bytes:
+            return "selective"
     return "full"
 
 
@@ -170,7 +196,8 @@ def plan_zero3(cfg, world: int, hbm_bytes: float, tokens: int, checkpointing="au
     est = activation_bytes(cfg, tokens, "none")
     if checkpointing == "auto":
         policy = pick_checkpointing(est, left, selective_ok=not any(
-            t in lora_targets for t in ("gate_proj", "up_proj", "down_proj")))
+            t in lora_targets for t in ("gate_proj", "up_proj", "down_proj")),
+            n_layers=cfg.num_hidden_layers)
     else:
         policy = checkpointing
     act = activation_bytes(cfg, tokens, policy or "none")

@@ -161,8 +161,11 @@ class Trainer:
         # selective only where every layer's MLP can recompute (frozen, unadapted gate|up/down)
         sel_ok = bool(pols and "selective" in pols
                       and getattr(self.model, "selective_eligible", lambda: False)())
-        pick = pick_checkpointing(est, free, sel_ok)
-        if pick == "full" and not (pols and "full" in pols):
+        # per-layer granularity ("selective:N") where the model takes it: recompute only the
+        # layers the budget needs
+        n_layers = cfg.num_hidden_layers if pols else None
+        pick = pick_checkpointing(est, free, sel_ok, n_layers=n_layers)
+        if isinstance(pick, str) and pick.split(":")[0] == "full" and not (pols and "full" in pols):
             pick = True
         self.print(f"[lumen] activation checkpointing {pick or 'off'} (auto): "
                    f"~{est / 1e9:.1f} GB of activations per micro-step vs {free / 1e9:.1f} GB "

@@ -230,17 +230,19 @@ def test_adamw_device_hf_linear_schedule():
 
 @pytest.mark.parametrize("segs_kind", ["qkv", "o", "gqa_sparse"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
-@pytest.mark.parametrize("impl", ["v3", "v2", "f32"])
+@pytest.mark.parametrize("impl", ["v3", "v3_overlap", "v2", "f32"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_lora_linear_fwd_bwd(segs_kind, p_drop, impl, monkeypatch, dtype):
     """impl v3 (shipped default): one-shot DOWN / fused dY pass / fused dA + dx (lora_v3.hip)
-    with the v2 UP write-back; v2: 16-bit MFMA kernels (lora_v2.hip, the fallback for
-    unaligned segments); f32: exact-f32 MFMA kernel (lora.hip, other ranks)."""
+    with the v2 UP write-back; v3_overlap: the same with the dY pass on a side stream beside
+    the input-gradient GEMM (LUMEN_LORA_BWD_OVERLAP); v2: 16-bit MFMA kernels (lora_v2.hip, the
+    fallback for unaligned segments); f32: exact-f32 MFMA kernel (lora.hip, other ranks)."""
     import lumen.ops.lora as lora_mod
     from lumen.ops.lora import lora_linear, lora_linear_ref
 
     monkeypatch.setattr(lora_mod, "USE_V2", impl != "f32")
-    monkeypatch.setattr(lora_mod, "USE_V3", impl == "v3")
+    monkeypatch.setattr(lora_mod, "USE_V3", impl.startswith("v3"))
+    monkeypatch.setattr(lora_mod, "BWD_OVERLAP", impl == "v3_overlap")
 
     T, K, r = 512 + 64, 1024, 16
     if segs_kind == "qkv":

@@ -2,6 +2,7 @@
 import json
 import os
 
+import pytest
 import torch
 
 from lumen.lora import (LoraConfig, adapter_state_dict, apply_lora, count_parameters,
@@ -132,3 +133,47 @@ def test_checkpointing_true_never_silently_off(monkeypatch):
         # eligible: the MLP recomputes its gate|up itself, no whole-layer checkpoint;
         # not eligible: one whole-layer checkpoint per layer
         assert len(calls) == (0 if eligible else m.config.num_hidden_layers)
+
+
+def test_partial_layer_checkpointing_matches_no_recompute(monkeypatch):
+    """``"selective:N"`` / ``"full:N"``: only the first N layers recompute; the loss and every
+    adapter gradient equal the run without recompute."""
+    import lumen.models.llama as L
+
+    calls = []
+    real = L.cp.checkpoint
+
+    def counting(fn, *a, **k):
+        calls.append(fn)
+        return real(fn, *a, **k)
+
+    monkeypatch.setattr(L.cp, "checkpoint", counting)
+    torch.manual_seed(0)
+    ids = torch.randint(0, 100, (2, 16))
+    labels = ids.clone()
+    ref = None
+    for pol in ("none", "selective:1", "full:1", "full"):
+        torch.manual_seed(1)  # identical weights and adapter init for every policy
+        m = build_model("tiny-llama", dtype=torch.float32, init="random")
+        apply_lora(m, LoraConfig(r=4, target_modules=["q_proj", "v_proj"]))
+        m.gradient_checkpointing = pol
+        m.train()
+        nl = m.config.num_hidden_layers
+        assert m.gradient_checkpointing == (pol if pol != f"full:{nl}" else "full")
+        recomputing = [l.mlp.recompute for l in m.layers]
+        assert recomputing == [pol == "selective:1" and i == 0 for i in range(nl)]
+        calls.clear()
+        loss = m(ids, labels)
+        loss.backward()
+        assert len(calls) == {"none": 0, "selective:1": 0, "full:1": 1, "full": nl}[pol]
+        grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        if ref is None:
+            ref = (loss.item(), grads)
+        else:
+            assert abs(loss.item() - ref[0]) < 1e-6
+            for n, g in grads.items():
+                assert torch.allclose(g, ref[1][n], atol=1e-6, rtol=1e-5), (pol, n)
+    m.gradient_checkpointing = "selective:0"
+    assert m.gradient_checkpointing == "none"
+    with pytest.raises(ValueError):
+        m.gradient_checkpointing = "selective:x"

@@ -20,7 +20,8 @@ def test_llama70b_world8_plan_keeps_one_copy_with_headroom():
                                 (4096, "auto", "selective")):
         p = plan_zero3(cfg, 8, HBM, tokens, ck)
         assert p["schedule"] == "keep", p            # one gathered copy, resident
-        assert p["checkpointing"] == want_ck, p
+        # auto recomputes only as many layers as the budget needs ("selective:N")
+        assert p["checkpointing"].split(":")[0] == want_ck, p
         assert p["headroom"] >= 0.10, p               # >= 10% of the 288 GB left over
         # W^T of the 70B projections (129 GB) does not fit next to the gathered copy: the
         # backward runs the NN input-gradient GEMMs instead of over-committing HBM
@@ -64,3 +65,29 @@ def test_runtime_budget_helpers_are_the_planners():
     units = [u["stored"] for u in llama_units(get_config("llama2-70b"))]
     s, _ = ParamCoordinator.auto_schedule(sum(units), live_budget_elems(free, total, 2), 8, units)
     assert s == "keep"
+
+
+def test_partial_recompute_picks_fewest_layers():
+    """``auto`` with per-layer granularity: the fewest recomputed layers whose activations fit
+    twice; selective before full; all layers -> the plain policy name."""
+    from lumen.parallel.memory_plan import (SELECTIVE_FRACTION, activation_bytes,
+                                            pick_checkpointing)
+
+    L, est = 32, 100.0
+    assert pick_checkpointing(est, 200, True, L) is False
+    pol = pick_checkpointing(est, 150, True, L)
+    k = int(pol.split(":")[1])
+    frac = lambda k: 1 - k * (1 - SELECTIVE_FRACTION) / L  # noqa: E731
+    assert pol.startswith("selective:") and 2 * est * frac(k) <= 150 < 2 * est * frac(k - 1)
+    assert pick_checkpointing(est, 2 * SELECTIVE_FRACTION * est, True, L) == "selective"
+    assert pick_checkpointing(est, 110, True, L).startswith("full:")   # selective cannot fit
+    assert pick_checkpointing(est, 150, False, L).startswith("full:")  # MLP not eligible
+    assert pick_checkpointing(est, 1, True, L) == "full"
+    assert pick_checkpointing(est, 150, True) == "selective"           # no granularity: as before
+    assert pick_checkpointing(est, 110, True) == "full"
+    cfg = get_config("llama2-7b")
+    none = activation_bytes(cfg, 4096, "none")
+    assert activation_bytes(cfg, 4096, "selective:16") == pytest.approx(
+        none * (1 - 16 * (1 - SELECTIVE_FRACTION) / 32))
+    assert activation_bytes(cfg, 4096, "selective:32") == activation_bytes(cfg, 4096, "selective")
+    assert activation_bytes(cfg, 4096, "full:32") == pytest.approx(activation_bytes(cfg, 4096, "full"))
