@@ -137,7 +137,7 @@ def dg_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple]:
 # views of one buffer (ldc = full width, no copies).  scripts/probes/split_gemm_probe.py measures it.
 GEMM_SPLIT = os.environ.get("LUMEN_GEMM_SPLIT", "1") != "0"
 SPLIT_TILE, SPLIT_CUS = 256, 256
-SPLIT_MAX_TAIL = float(os.environ.get("LUMEN_GEMM_SPLIT_MAX_TAIL", "0.5"))
+SPLIT_MAX_TAIL = float(os.environ.get("LUMEN_GEMM_SPLIT_MAX_TAIL", "0.75"))
 
 
 def split_cols(M: int, N: int) -> int:
@@ -218,7 +218,9 @@ def linear_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     p = dg_plan(x, w)
     if p is not None:
         return decode_gemm(x, w, *p)
-    return torch.matmul(x, w.t())
+    # prefill / mixed steps (M = 2048-4096 tokens): the whole-wave column split where both
+    # parts are tuned, as in training (profiles/r5_serve_split)
+    return mm_nt(x, w)
 
 
 def swiglu_linear_nt(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

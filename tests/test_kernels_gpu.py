@@ -1146,3 +1146,22 @@ def test_fp32_model_matches_cpu(name):
         assert rel(gg[n].grad, p.grad.to(DEV)) < 1e-3, n
         n_checked += 1
     assert n_checked > 0
+
+
+def test_serving_prefill_projection_wave_split():
+    """Serving prefill / mixed-step projections (``linear_nt`` at M = 2048 tokens) take the
+    whole-wave column split where both parts are in the shipped TunableOp table (q|k|v 8192 +
+    4096, gate|up 16384 + 5632 columns) and equal the single GEMM."""
+    import lumen.ops.gemm as G
+    from lumen.utils.gemm_tuning import load_tuned_gemms
+
+    assert load_tuned_gemms(), "shipped TunableOp table did not load"
+    G._plans.clear()
+    for N, n1 in ((12288, 8192), (22016, 16384)):
+        x = torch.randn(2048, 4096, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, 4096, device=DEV, dtype=torch.bfloat16) * 0.02
+        assert G._split_plan(x, w) == n1, N
+        y = G.linear_nt(x, w)
+        ref = x.float() @ w.float().t()
+        assert rel(y, ref) < 1e-2
+        assert torch.equal(y, G.mm_nt(x, w))

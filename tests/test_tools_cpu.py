@@ -367,15 +367,17 @@ def test_bench_contract_torchrun(world):
 
 
 def test_gemm_wave_split_plan():
-    """Whole-wave column split of the training GEMMs (lumen/ops/gemm.py): only where the last
-    wave of 256x256 tiles on 256 CUs is at most half full, at a column-tile boundary."""
+    """Whole-wave column split of the training and serving-prefill GEMMs (lumen/ops/gemm.py):
+    only where the last wave of 256x256 tiles on 256 CUs is at most 3/4 full, at a column-tile
+    boundary (taken at run time only where both parts are in the tuned table)."""
     from lumen.ops.gemm import mm_nt, split_cols
 
     assert split_cols(4096, 22016) == 20480      # gate|up fwd: 1376 tiles -> 1280 + 96
     assert split_cols(1024, 22016) == 16384      # 344 tiles -> 256 + 88
-    for M, N in [(4096, 4096), (4096, 12288), (4096, 11008), (4096, 32000), (4000, 22016),
-                 (256, 1024)]:
-        assert split_cols(M, N) == 0, (M, N)     # whole waves, >half-full tail, or ragged M
+    assert split_cols(2048, 12288) == 8192       # serving mixed step q|k|v: 384 -> 256 + 128
+    assert split_cols(2048, 22016) == 16384      # serving mixed step gate|up: 688 -> 512 + 176
+    for M, N in [(4096, 4096), (4096, 12288), (4096, 32000), (4000, 22016), (256, 1024)]:
+        assert split_cols(M, N) == 0, (M, N)     # whole waves, >3/4-full tail, or ragged M
     x, w = torch.randn(8, 16), torch.randn(24, 16)
     assert torch.allclose(mm_nt(x, w), x @ w.t())  # CPU: plain matmul
 
