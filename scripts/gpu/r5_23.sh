@@ -4,10 +4,10 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/r5_10; mkdir -p $O
+O=$GRAFT_REPO_ROOT/gpurun_out/r5_23; mkdir -p $O
 export LUMEN_SHARED_GPU_REHEARSAL=1 LUMEN_DIST_TIMEOUT=300
 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
-  --master-port 29631 bench.py --gpus 8 --model llama2-7b-2l --steps 3 --warmup 1 --seq_len 256 \
+  --master-port 29641 bench.py --gpus 8 --model llama2-7b-2l --steps 3 --warmup 1 --seq_len 256 \
   --micro_batch 2 --partitioned_steps 2 > $O/bench_w8.json 2> $O/bench_w8.err || { tail -30 $O/bench_w8.err; exit 1; }
 echo "json lines: $(grep -c '^{' $O/bench_w8.json)"
 python3 - <<EOF
