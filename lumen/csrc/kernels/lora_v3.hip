@@ -95,6 +95,23 @@ __global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
                         ? *reinterpret_cast<const uint4*>(x + (long long)t * a.ldx + c)
                         : make_uint4(0, 0, 0, 0);
       }
+    // the A operand (f32 rows, L2-resident) is loaded right behind the x tile and
+    // unconditionally (clamped addresses, out-of-range columns zeroed by a select after the
+    // load): guarded loads made hipcc wait for every pair of them in turn -- 12 dependent L2
+    // round trips after the x tile had landed -- instead of one wait for both
+    float4 af[4][NJ][2];
+    if (!(a.probe & 2)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = min(k0 + 32 * i + 8 * g, a.K - 8);
+#pragma unroll
+        for (int jt = 0; jt < NJ; ++jt) {
+          const float* ap = a.A + (long long)(jt * 16 + L) * a.lda + c;
+          af[i][jt][0] = *reinterpret_cast<const float4*>(ap);
+          af[i][jt][1] = *reinterpret_cast<const float4*>(ap + 4);
+        }
+      }
+    }
     if (DROP && !(a.probe & 1)) {
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt)
@@ -109,11 +126,15 @@ __global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = k0 + 32 * i + 8 * g;
+      const bool cok = k0 + 32 * i + 8 * g < a.K;
       uint4 bop[NJ];
 #pragma unroll
-      for (int jt = 0; jt < NJ; ++jt)
-        bop[jt] = (a.probe & 2) ? xv[jt & 3][i] : ld_f32x8<T>(a.A + (long long)(jt * 16 + L) * a.lda + c, c < a.K);
+      for (int jt = 0; jt < NJ; ++jt) {
+        const float4 u = af[i][jt][0], v = af[i][jt][1];
+        const uint4 w = make_uint4(pk2<T>(u.x, u.y), pk2<T>(u.z, u.w), pk2<T>(v.x, v.y),
+                                   pk2<T>(v.z, v.w));
+        bop[jt] = (a.probe & 2) ? xv[jt & 3][i] : (cok ? w : make_uint4(0, 0, 0, 0));
+      }
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
@@ -584,11 +605,22 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, L = lane & 15, g = lane >> 4;
   const T* x = reinterpret_cast<const T*>(a.x);
   T* dx = reinterpret_cast<T*>(a.dx);
-  // A^T slice for the dx products: s2[c][j] = A[j][c0 + c] (zero beyond R / K)
-  for (int idx = threadIdx.x; idx < 32 * KJ; idx += 256) {
-    const int j = idx / 32, c = (idx % 32) * 4;
-    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (j < a.R && c0 + c < a.K) f = *reinterpret_cast<const float4*>(a.A + (long long)j * a.lda + c0 + c);
+  // A^T slice for the dx products: s2[c][j] = A[j][c0 + c] (zero beyond R / K).  Every load is
+  // issued before the first LDS store (clamped addresses, zeroed by a select): a guarded load
+  // per loop trip made hipcc wait for each in turn, KJ / 8 serial L2 round trips per block
+  constexpr int NS2 = 32 * KJ / 256;
+  float4 f2[NS2];
+#pragma unroll
+  for (int q = 0; q < NS2; ++q) {
+    const int idx = threadIdx.x + q * 256, j = idx / 32, c = (idx % 32) * 4;
+    const int jj = min(j, a.R - 1), cc = min(c0 + c, a.K - 4);
+    f2[q] = *reinterpret_cast<const float4*>(a.A + (long long)jj * a.lda + cc);
+  }
+#pragma unroll
+  for (int q = 0; q < NS2; ++q) {
+    const int idx = threadIdx.x + q * 256, j = idx / 32, c = (idx % 32) * 4;
+    const bool ok = j < a.R && c0 + c < a.K;
+    const float4 f = ok ? f2[q] : make_float4(0.f, 0.f, 0.f, 0.f);
     s2[(c + 0) * SP + j] = from_f32<T>(f.x);
     s2[(c + 1) * SP + j] = from_f32<T>(f.y);
     s2[(c + 2) * SP + j] = from_f32<T>(f.z);
@@ -603,20 +635,24 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
   // staging registers: x tile (4 x 16 B per thread) and dZ tile (J / 4 float4 per row)
   uint4 xv[4];
   float4 zv[(64 * J / 4 + 255) / 256];
+  // every staging / row load is unconditional (clamped address) and out-of-range values are
+  // zeroed by a select afterwards: with per-lane guarded loads hipcc could not count the loads
+  // in flight across the branches and drained the whole prefetch with vmcnt(0)
   const auto load_stage = [&](int t0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = threadIdx.x + i * 256;
       const int r = t0 + (idx >> 4), c = c0 + (idx & 15) * 8;
-      xv[i] = (r < te && c < a.K) ? *reinterpret_cast<const uint4*>(x + (long long)r * a.ldx + c)
-                                  : make_uint4(0, 0, 0, 0);
+      const uint4 u = *reinterpret_cast<const uint4*>(x + (long long)min(r, te - 1) * a.ldx +
+                                                       min(c, a.K - 8));
+      xv[i] = (r < te && c < a.K) ? u : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < (64 * J / 4 + 255) / 256; ++i) {
       const int idx = threadIdx.x + i * 256;
       const int r = idx / (J / 4), j = (idx % (J / 4)) * 4;
-      zv[i] = (r < 64 && t0 + r < te) ? *reinterpret_cast<const float4*>(a.dZ + (long long)(t0 + r) * a.R + j)
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 u = *reinterpret_cast<const float4*>(a.dZ + (long long)min(t0 + r, te - 1) * a.R + j);
+      zv[i] = (r < 64 && t0 + r < te) ? u : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   const auto store_stage = [&](int t0, int b) {
@@ -645,28 +681,34 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
   };
   // dx operands of a wave's 16 rows (dZ row, the dx row, O for the delta dot), loaded one
   // sub-tile ahead: loaded right before use they left one HBM round trip exposed per 64 rows
-  uint4 nbop[NKS], ndv[4];
+  // (dZ rows as f32 pairs, loaded unconditionally from clamped addresses and zeroed / packed
+  // at use: the guarded form made hipcc wait for each pair right after issuing it)
+  float4 nbf[NKS][2];
+  uint4 ndv[4];
   uint4 nov[DELTA ? 4 : 1];  // O (un-dropped x) in the dx lane layout, for the delta dot
   const auto load_rows = [&](int t0) {
     const int t = t0 + wid * 16 + L;
     const bool tok = t < te;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      const int j = ks * 32 + g * 8;
-      nbop[ks] = ld_f32x8<T>(a.dZ + (long long)t * a.R + j, tok && j < a.R);
+      const int j = min(ks * 32 + g * 8, a.R - 8);
+      const float* zp = a.dZ + (long long)min(t, te - 1) * a.R + j;
+      nbf[ks][0] = *reinterpret_cast<const float4*>(zp);
+      nbf[ks][1] = *reinterpret_cast<const float4*>(zp + 4);
     }
+    const long long tc = min(t, te - 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = c0 + 32 * i + 8 * g;
-      ndv[i] = (tok && c < a.K) ? *reinterpret_cast<const uint4*>(dx + (long long)t * a.lddx + c)
-                                : make_uint4(0, 0, 0, 0);
+      const uint4 u = *reinterpret_cast<const uint4*>(dx + tc * a.lddx + min(c, a.K - 8));
+      ndv[i] = (tok && c < a.K) ? u : make_uint4(0, 0, 0, 0);
     }
     if constexpr (DELTA) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = c0 + 32 * i + 8 * g;
-        nov[i] = (tok && c < a.K) ? *reinterpret_cast<const uint4*>(x + (long long)t * a.ldx + c)
-                                  : make_uint4(0, 0, 0, 0);
+        const uint4 u = *reinterpret_cast<const uint4*>(x + tc * a.ldx + min(c, a.K - 8));
+        nov[i] = (tok && c < a.K) ? u : make_uint4(0, 0, 0, 0);
       }
     }
   };
@@ -676,19 +718,26 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
   for (int t0 = tb; t0 < te; t0 += 64, buf ^= 1) {
     store_stage(t0, buf);
     __syncthreads();
-    if (t0 + 64 < te) load_stage(t0 + 64);
+    // unconditional (the last trip re-reads clamped rows it never stores): a branch around
+    // the loads made hipcc drain the prefetch with vmcnt(0) at the join
+    load_stage(t0 + 64);
     const int t = t0 + wid * 16 + L;
     const bool tok = t < te;
     uint4 bop[NKS], dv[4], ov[DELTA ? 4 : 1];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) bop[ks] = nbop[ks];
+    for (int ks = 0; ks < NKS; ++ks) {
+      const float4 u = nbf[ks][0], v = nbf[ks][1];
+      bop[ks] = (tok && ks * 32 + g * 8 < a.R)
+                    ? make_uint4(pk2<T>(u.x, u.y), pk2<T>(u.z, u.w), pk2<T>(v.x, v.y), pk2<T>(v.z, v.w))
+                    : make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) dv[i] = ndv[i];
     if constexpr (DELTA) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) ov[i] = nov[i];
     }
-    if (t0 + 64 < te) load_rows(t0 + 64);
+    load_rows(t0 + 64);
     // dA: D[j][k] += dZ^T[j][t] x[t][k] over the sub-tile's 64 rows
     const char* im = img[buf];
     const T* sz = st[buf];
