@@ -21,6 +21,20 @@
 
 namespace lumen {
 
+// 8 elements of T kept packed in registers as 16-byte words: one for 16-bit T, two for f32.
+// (Declared as uint4 words and loaded word by word: a struct of T[8] compiled to per-element
+// flat loads plus scratch on the bf16 path, 26 -> 39 us per training-shape call.)
+template <typename T> struct Pack8 {
+  static constexpr int W = 8 * sizeof(T) / 16;
+  uint4 w[W];
+  __device__ __forceinline__ void load(const T* p, bool ok) {
+#pragma unroll
+    for (int i = 0; i < W; ++i)
+      w[i] = ok ? reinterpret_cast<const uint4*>(p)[i] : make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ const T* v() const { return reinterpret_cast<const T*>(w); }
+};
+
 template <typename T, int VPL, int WPR = 1>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
     const T* __restrict__ x, const T* __restrict__ residual, const T* __restrict__ w,
@@ -34,21 +48,34 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
   const int row = blockIdx.x * (4 / WPR) + wid / WPR;
   const bool rok = row < rows;  // no early return: the waves of a block meet at a barrier
   const size_t base = static_cast<size_t>(rok ? row : 0) * H;
-  float v[VPL][8];
+  // every row load (x, residual, weight) is issued up front, packed, from a clamped address and
+  // zeroed afterwards when out of range: loads guarded by `if (rok && c < H)` (and the residual
+  // load behind its own branch) compiled to a vmcnt(0) per 16-byte load, serial round trips
+  Pack8<T> xr[VPL], rr[VPL], wr[VPL];
+  const T* rp = residual ? residual : x;  // a valid row either way; added only with a residual
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int cc = min(((i * WPR + ws) * 64 + lane) * 8, H - 8);
+    xr[i].load(x + base + cc, true);
+    rr[i].load(rp + base + cc, true);
+    wr[i].load(w + cc, true);
+  }
+  float v[VPL][8], wv[VPL][8];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = ((i * WPR + ws) * 64 + lane) * 8;
-    if (rok && c < H) {
-      load8(x + base + c, v[i]);
-      if (residual) {
-        float r[8];
-        load8(residual + base + c, r);
+    const bool ok = rok && c < H;
+    const T* xe = xr[i].v();
+    const T* re = rr[i].v();
+    const T* we = wr[i].v();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] += r[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    for (int j = 0; j < 8; ++j) {
+      float t = to_f32(xe[j]);
+      if (residual) t += to_f32(re[j]);
+      v[i][j] = ok ? t : 0.f;
+      wv[i][j] = to_f32(we[j]);
+      ss += v[i][j] * v[i][j];
     }
   }
   ss = wave_sum(ss);
@@ -73,10 +100,9 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
         for (int j = 0; j < 8; ++j) sr[j] = to_f32(from_f32<T>(v[i][j]));
         store8(s_out + base + c, sr);
       }
-      float wv[8], o[8];
-      load8(w + c, wv);
+      float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[j];
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rs * wv[i][j];
       store8(y + static_cast<size_t>((rok ? row : 0)) * ldy + c, o);
     }
   }
@@ -94,22 +120,31 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_row_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row = blockIdx.x;
   const size_t base = static_cast<size_t>(row) * H;
+  // all loads up front, unconditional from clamped addresses (see rmsnorm_fwd_kernel)
+  Pack8<T> xr[VPT], rr[VPT], wr[VPT];
+  const T* rp = residual ? residual : x;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int cc = min((tid + i * 256) * 8, H - 8);
+    xr[i].load(x + base + cc, true);
+    rr[i].load(rp + base + cc, true);
+    wr[i].load(w + cc, true);
+  }
   float v[VPT][8], wv[VPT][8];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int c = (tid + i * 256) * 8;
-    if (c < H) {
-      load8(w + c, wv[i]);
-      load8(x + base + c, v[i]);
-      if (residual) {
-        float r[8];
-        load8(residual + base + c, r);
+    const bool ok = (tid + i * 256) * 8 < H;
+    const T* xe = xr[i].v();
+    const T* re = rr[i].v();
+    const T* we = wr[i].v();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] += r[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    for (int j = 0; j < 8; ++j) {
+      float t = to_f32(xe[j]);
+      if (residual) t += to_f32(re[j]);
+      v[i][j] = ok ? t : 0.f;
+      wv[i][j] = to_f32(we[j]);
+      ss += v[i][j] * v[i][j];
     }
   }
   ss = wave_sum(ss);
@@ -136,20 +171,6 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_row_kernel(
   }
 }
 
-// 8 elements of T kept packed in registers as 16-byte words: one for 16-bit T, two for f32.
-// (Declared as uint4 words and loaded word by word: a struct of T[8] compiled to per-element
-// flat loads plus scratch on the bf16 path, 26 -> 39 us per training-shape call.)
-template <typename T> struct Pack8 {
-  static constexpr int W = 8 * sizeof(T) / 16;
-  uint4 w[W];
-  __device__ __forceinline__ void load(const T* p, bool ok) {
-#pragma unroll
-    for (int i = 0; i < W; ++i)
-      w[i] = ok ? reinterpret_cast<const uint4*>(p)[i] : make_uint4(0, 0, 0, 0);
-  }
-  __device__ __forceinline__ const T* v() const { return reinterpret_cast<const T*>(w); }
-};
-
 template <typename T, int VPL, int WPR>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ s, const T* __restrict__ w,
@@ -167,7 +188,9 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
   const bool rok = row < rows;  // no early return: the waves of a block meet at a barrier
   const size_t base = static_cast<size_t>(rok ? row : 0) * H;
   const float rs = rok ? rstd[row] : 0.f;
-  Pack8<T> dyr[VPL], sr[VPL], rr[VPL];
+  // the norm weight is loaded with the rows (it was a guarded load8 in both passes below: four
+  // serial L2 round trips per wave after the rows had landed)
+  Pack8<T> dyr[VPL], sr[VPL], rr[VPL], wr[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = ((i * WPR + ws) * 64 + lane) * 8;
@@ -175,6 +198,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     dyr[i].load(dy + base + c, ok);
     sr[i].load(s + base + c, ok);
     rr[i].load(ds_res + base + c, ok && ds_res);
+    wr[i].load(w + min(c, H - 8), true);
   }
   float dot = 0.f;
 #pragma unroll
@@ -183,10 +207,9 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     if (rok && c < H) {
       const T* dyv = dyr[i].v();
       const T* sv = sr[i].v();
-      float wv[8];
-      load8(w + c, wv);
+      const T* wv = wr[i].v();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dot += to_f32(dyv[j]) * wv[j] * (to_f32(sv[j]) * rs);
+      for (int j = 0; j < 8; ++j) dot += to_f32(dyv[j]) * to_f32(wv[j]) * (to_f32(sv[j]) * rs);
       if (dw) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) atomicAdd(dw + c + j, to_f32(dyv[j]) * to_f32(sv[j]) * rs);
@@ -209,11 +232,11 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
       const T* dyv = dyr[i].v();
       const T* sv = sr[i].v();
       const T* rv = rr[i].v();
-      float wv[8], o[8];
-      load8(w + c, wv);
+      const T* wv = wr[i].v();
+      float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        o[j] = rs * (to_f32(dyv[j]) * wv[j] - to_f32(sv[j]) * rs * dot);
+        o[j] = rs * (to_f32(dyv[j]) * to_f32(wv[j]) - to_f32(sv[j]) * rs * dot);
         if (ds_res) o[j] += to_f32(rv[j]);
       }
       store8(dx + base + c, o);
