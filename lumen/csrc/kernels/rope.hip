@@ -87,13 +87,15 @@ __global__ void __launch_bounds__(256) rope_inplace_kernel(
   const int h = static_cast<int>((tid / chunks) % nheads);
   const int t = static_cast<int>(tid / (static_cast<long long>(chunks) * nheads));
   const int half = D / 2, i0 = c * 8;
-  const int p = pos[t];
   T* row = x + static_cast<size_t>(t) * row_stride + static_cast<size_t>(h) * D;
   float cs[8], sn[8], a[8], bb[8], oa[8], ob[8];
-  load8(cos_t + static_cast<size_t>(p) * half + i0, cs);
-  load8(sin_t + static_cast<size_t>(p) * half + i0, sn);
+  // the row loads go out first: they do not depend on the position, whose load the cos / sin
+  // loads wait for
   load8(row + i0, a);
   load8(row + i0 + half, bb);
+  const int p = pos[t];
+  load8(cos_t + static_cast<size_t>(p) * half + i0, cs);
+  load8(sin_t + static_cast<size_t>(p) * half + i0, sn);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     oa[j] = a[j] * cs[j] - bb[j] * sn[j];
