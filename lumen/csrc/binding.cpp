@@ -62,6 +62,8 @@ hipError_t lumen_lora3_dy(int, const void*, long long, const float*, int, const 
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, const float*, void*,
                             void*, const long long*, int, int, int, int, int, int, hipStream_t);
+hipError_t lumen_skinny_swiglu_gemm(int, const void*, const void*, void*, int, int, int, long long,
+                                    long long, hipStream_t);
 hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int, long long,
                              long long, hipStream_t);
 hipError_t lumen_decode_gemm(int, const void*, const void*, void*, float*, int*, int, int, int,
@@ -197,6 +199,22 @@ void swiglu(bool bwd, const at::Tensor& gu, const std::optional<at::Tensor>& dac
   check(lumen_swiglu(dcode(gu), bwd ? 1 : 0, gu.data_ptr(), ptr(dact), out.data_ptr(), rows, F,
                      cur_stream()),
         "swiglu");
+}
+
+// y [M, N] = swiglu(gu [M, 2K]) @ w [N, K]^T, M <= 4 (batch-1..4 decode down projection)
+void skinny_swiglu_gemm(const at::Tensor& gu, const at::Tensor& w, at::Tensor& y) {
+  if (!gu.is_cuda() || !y.is_cuda()) throw std::invalid_argument("lumen: skinny_swiglu_gemm needs GPU tensors");
+  need_cuda(w, "w");
+  if (gu.dim() != 2 || w.dim() != 2 || y.dim() != 2 || gu.stride(1) != 1 || y.stride(1) != 1 ||
+      !w.is_contiguous() || gu.size(1) != 2 * w.size(1) || y.size(0) != gu.size(0) ||
+      y.size(1) != w.size(0) || gu.scalar_type() != w.scalar_type() ||
+      y.scalar_type() != w.scalar_type())
+    throw std::invalid_argument("lumen: skinny_swiglu_gemm shape/layout mismatch");
+  check(lumen_skinny_swiglu_gemm(dcode(w), gu.data_ptr(), w.data_ptr(), y.data_ptr(),
+                                 static_cast<int>(gu.size(0)), static_cast<int>(w.size(0)),
+                                 static_cast<int>(w.size(1)), gu.stride(0), y.stride(0),
+                                 cur_stream()),
+        "skinny_swiglu_gemm");
 }
 
 void skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y) {
@@ -892,6 +910,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora2", &lora2);
   m.def("transpose2d", &transpose2d);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_swiglu_gemm", &skinny_swiglu_gemm);
   m.def("decode_gemm", &decode_gemm);
   m.def("lora3_w_tail_batch", &lora3_w_tail_batch);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });

@@ -327,6 +327,33 @@ hipError_t launch_gemv(const void* x, const void* W, void* y, int M, int N, int 
 // M == 1 kernel form: 1 = rows-per-lane (gemv_r4_kernel), 0 = row-group form (gemv_kernel)
 extern "C" void lumen_set_gemv_form(int form) { g_gemv_form = form; }
 
+// y[M, N] = (silu(gu[:, :K]) * gu[:, K:]) @ W[N, K]^T for M <= 4 (decode batches): the SwiGLU
+// activation formed in registers inside the rows-per-lane weight stream (gu rows at stride ldgu
+// >= 2K), so the batch-1 down projection needs no separate activation launch.
+extern "C" hipError_t lumen_skinny_swiglu_gemm(int dtype, const void* gu, const void* W, void* y,
+                                               int M, int N, int K, long long ldgu,
+                                               long long ldy, hipStream_t st) {
+  if (M < 1 || M > 4 || N % 4 != 0 || K % 8 != 0 || ldgu < 2LL * K || ldgu % 8 != 0)
+    return hipErrorInvalidValue;
+  dim3 grid(N / 4), block(256);
+#define LUMEN_SWG(TT, MM)                                                                       \
+  hipLaunchKernelGGL((lumen::sk::gemv_r4_kernel<TT, true, MM>), grid, block, 0, st,            \
+                     (const TT*)gu, (const TT*)W, (TT*)y, N, K, M, ldgu, ldy)
+  if (dtype == lumen::kBF16) {
+    if (M == 1) LUMEN_SWG(lumen::bf16, 1);
+    else if (M == 2) LUMEN_SWG(lumen::bf16, 2);
+    else LUMEN_SWG(lumen::bf16, 4);
+  } else if (dtype == lumen::kF16) {
+    if (M == 1) LUMEN_SWG(lumen::fp16, 1);
+    else if (M == 2) LUMEN_SWG(lumen::fp16, 2);
+    else LUMEN_SWG(lumen::fp16, 4);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef LUMEN_SWG
+  return hipGetLastError();
+}
+
 extern "C" hipError_t lumen_skinny_gemm(int dtype, const void* x, const void* W, void* y, int M,
                                         int N, int K, long long ldx, long long ldy,
                                         hipStream_t st) {

@@ -223,10 +223,24 @@ def linear_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return mm_nt(x, w)
 
 
+# batch <= 4 decode, opt-in (LUMEN_SWIGLU_GEMV=1): SwiGLU formed inside the rows-per-lane weight
+# stream, one launch fewer per layer.  Measured slower both ways: the row-group GEMV form 21.4 vs
+# 18.5 us per call, the rows-per-lane form 3.085 vs 2.99-3.01 ms per batch-1 decode step (gpurun
+# r5_35) -- every workgroup re-reads and re-activates the whole 2 x 11008 gate|up row
+SWIGLU_GEMV = os.environ.get("LUMEN_SWIGLU_GEMV", "0") == "1"
+
+
 def swiglu_linear_nt(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """(silu(gu[:, :F]) * gu[:, F:]) @ w[N, F]^T, the MLP down projection: SwiGLU kernel +
-    ``linear_nt`` (forming the activation inside the batch-1 weight stream measured slower:
-    21.4 vs 18.5 us, every workgroup re-activates the whole gate|up vector)."""
+    """(silu(gu[:, :F]) * gu[:, F:]) @ w[N, F]^T, the MLP down projection."""
     from .activation import swiglu
 
+    M, F = gu.shape[0], gu.shape[1] // 2
+    if (SWIGLU_GEMV and 0 < M <= 4 and gu.dim() == 2 and gu.shape[1] == 2 * F
+            and gu.stride(1) == 1 and gu.stride(0) % 8 == 0 and use_native(gu)
+            and w.dim() == 2 and w.shape[1] == F and w.is_contiguous() and gu.dtype == w.dtype
+            and gu.dtype in (torch.bfloat16, torch.float16) and w.shape[0] % 4 == 0
+            and F % 8 == 0 and skinny_ok(gu[:, :F], w)):
+        y = torch.empty(M, w.shape[0], device=gu.device, dtype=gu.dtype)
+        native().skinny_swiglu_gemm(gu, w, y)
+        return y
     return linear_nt(swiglu(gu), w)

@@ -1165,3 +1165,27 @@ def test_serving_prefill_projection_wave_split():
         ref = x.float() @ w.float().t()
         assert rel(y, ref) < 1e-2
         assert torch.equal(y, G.mm_nt(x, w))
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("K", [11008, 1024])
+def test_skinny_swiglu_gemm(M, K, monkeypatch):
+    """Batch <= 4 decode down projection with SwiGLU formed inside the weight stream
+    (kernels/skinny_gemm.hip, gemv_r4_kernel<SWIGLU>; opt-in LUMEN_SWIGLU_GEMV) vs an f32
+    reference of swiglu + matmul."""
+    import lumen.ops.gemm as G
+
+    monkeypatch.setattr(G, "SWIGLU_GEMV", True)
+    import torch.nn.functional as F
+    from lumen.ops._native import native
+    from lumen.ops.gemm import swiglu_linear_nt
+
+    N = 4096
+    gu = torch.randn(M, 2 * K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    act = (F.silu(gu[:, :K].float()) * gu[:, K:].float()).to(torch.bfloat16).float()
+    ref = act @ w.float().t()
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    native().skinny_swiglu_gemm(gu, w, y)
+    assert rel(y, ref) < 1e-2
+    assert rel(swiglu_linear_nt(gu, w), ref) < 1e-2
