@@ -192,15 +192,26 @@ class CustomAllReduce:
                     row["rccl"] = self._time_us(lambda: dist.all_reduce(t, group=rccl_group),
                                                 iters, warmup)
                 table.append(row)
-            self.poll()
+            # a barrier timeout on any rank is decided collectively, AFTER the max-reduction
+            # every rank takes part in: raising on one rank before it would leave its peers
+            # waiting in that reduction
+            torch.cuda.synchronize(self.device)
+            timed_out = bool(self._flag_host and self.C.car_host_flag_read(self._flag_host))
             keys = ["one", "two"] + (["rccl"] if rccl_group is not None else [])
-            vals = torch.tensor([[r[k] for k in keys] for r in table], dtype=torch.float64)
+            vals = torch.tensor([[r[k] for k in keys] + [float(timed_out)] for r in table]
+                                or [[0.0] * len(keys) + [float(timed_out)]],
+                                dtype=torch.float64)
             if dist.get_backend(self.group) == "nccl":
                 dv = vals.to(self.device)
                 dist.all_reduce(dv, op=dist.ReduceOp.MAX, group=self.group)
                 vals = dv.cpu()
             else:
                 dist.all_reduce(vals, op=dist.ReduceOp.MAX, group=self.group)
+        if vals[:, -1].max().item() > 0:
+            self.poll()  # this rank's own timeout, with its diagnostics
+            raise CollectiveTimeout(f"custom all-reduce rank {self.rank}: a peer's barrier "
+                                    "timed out during calibration")
+        vals = vals[:, :-1]
         for r, v in zip(table, vals.tolist()):
             for k, x in zip(keys, v):
                 r[k] = round(float(x), 2)
