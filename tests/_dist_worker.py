@@ -442,3 +442,40 @@ def rccl_probe_worker(rank, world, port, outdir):
     rccl_probe.main()
     with open(os.path.join(outdir, f"probe_ok_{rank}"), "w") as f:
         f.write("ok")
+
+
+def car_calibrate_worker(rank, world, port, outdir, delay_s, timeout_s):
+    """``CustomAllReduce.calibrate`` on every rank; with ``delay_s`` > 0 the last rank starts it
+    late, so an early rank's first barrier times out: every rank must then raise (collectively,
+    after the shared max-reduction) instead of one raising and its peers hanging."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import json
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lumen.parallel.custom_ar import CollectiveTimeout, CustomAllReduce
+
+    dev = torch.device("cuda", 0)
+    car = CustomAllReduce(dist.group.WORLD, dev, max_bytes=1 << 20, timeout_s=timeout_s)
+    dist.barrier()
+    if rank == world - 1 and delay_s > 0:
+        time.sleep(delay_s)
+    res = {"rank": rank}
+    t0 = time.perf_counter()
+    try:
+        cal = car.calibrate(rccl_group=None, sizes=(8 << 10, 256 << 10), iters=3, warmup=1,
+                            apply=False)
+        res["table"], res["plan"], res["error"] = cal["table"], cal["plan"], None
+    except CollectiveTimeout as e:
+        res["error"] = str(e)
+    res["wall_s"] = time.perf_counter() - t0
+    with open(os.path.join(outdir, f"cal_{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    car.close()
+    dist.destroy_process_group()

@@ -220,6 +220,29 @@ def test_custom_allreduce_late_peer(delay_s, timeout_s, tmp_path):
         assert d["timed_out"] and d["missing_peer"] == world - 1 and d["barrier"] == 0, d
 
 
+@pytest.mark.parametrize("delay_s,timeout_s", [(0.0, 20.0), (3.0, 1.0)])
+def test_custom_allreduce_calibration_collective(delay_s, timeout_s, tmp_path):
+    """``calibrate`` gives every rank the same max-over-ranks table and plan; when a barrier
+    times out on any rank (here the last rank starts 3 s late against a 1 s deadline) every
+    rank raises, after the shared reduction, and none is left waiting in it."""
+    import json
+
+    from tests._dist_worker import car_calibrate_worker
+
+    world = 2
+    mp.start_processes(car_calibrate_worker,
+                       args=(world, _port(), str(tmp_path), delay_s, timeout_s),
+                       nprocs=world, join=True, start_method="spawn")
+    r = [json.loads((tmp_path / f"cal_{k}.json").read_text()) for k in range(world)]
+    print(r)
+    if delay_s == 0:
+        assert all(x["error"] is None for x in r), r
+        assert r[0]["table"] == r[1]["table"] and r[0]["plan"] == r[1]["plan"]
+        assert [row["bytes"] for row in r[0]["table"]] == [8 << 10, 256 << 10]
+    else:
+        assert all(x["error"] and "timed out" in x["error"] for x in r), r
+
+
 def test_tp2_serving_rccl_on_one_gpu(tmp_path):
     """TP=2 serving with the step broadcast and vocab gather on RCCL (custom IPC all-reduce for
     the row-parallel sums): same greedy tokens as the gloo-broadcast TP run."""
