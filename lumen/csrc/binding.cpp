@@ -22,7 +22,7 @@ hipError_t lumen_qkv_rope(int, int, void*, void*, void*, void*, const int*, cons
                           const float*, int, int, int, int, int, hipStream_t);
 hipError_t lumen_rope_inplace(int, void*, const int*, const float*, const float*, int, int, int,
                               int, hipStream_t);
-hipError_t lumen_swiglu(int, int, const void*, const void*, void*, int, int, hipStream_t);
+hipError_t lumen_swiglu(int, int, const void*, const void*, void*, int, int, int, int, hipStream_t);
 hipError_t lumen_cross_entropy(int, void*, const int64_t*, float*, float*, int, int, int, float,
                                int, const float*, hipStream_t);
 hipError_t lumen_grad_norm_sq(int, const void*, long long, float*, hipStream_t);
@@ -192,12 +192,19 @@ void rope_inplace(at::Tensor& x, const at::Tensor& pos, const at::Tensor& cos_t,
         "rope_inplace");
 }
 
-void swiglu(bool bwd, const at::Tensor& gu, const std::optional<at::Tensor>& dact, at::Tensor& out) {
+// c1 < 0: the whole row; else columns [c0, c1) of the activation (contiguous gu / dact / out)
+void swiglu(bool bwd, const at::Tensor& gu, const std::optional<at::Tensor>& dact, at::Tensor& out,
+            int64_t c0, int64_t c1) {
   need_cuda(gu, "gate_up"); need_cuda(out, "out");
   const int F = static_cast<int>(gu.size(-1) / 2);
   const int rows = static_cast<int>(gu.numel() / (2 * F));
+  if (!gu.is_contiguous() || !out.is_contiguous() || (dact && !dact->is_contiguous()) ||
+      out.numel() != static_cast<int64_t>(rows) * (bwd ? 2 * F : F) ||
+      (dact && dact->numel() != static_cast<int64_t>(rows) * F))
+    throw std::invalid_argument("lumen: swiglu shape/layout mismatch");
+  if (c1 < 0) { c0 = 0; c1 = F; }
   check(lumen_swiglu(dcode(gu), bwd ? 1 : 0, gu.data_ptr(), ptr(dact), out.data_ptr(), rows, F,
-                     cur_stream()),
+                     static_cast<int>(c0), static_cast<int>(c1), cur_stream()),
         "swiglu");
 }
 
@@ -902,7 +909,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("qkv_rope", &qkv_rope);
   m.def("rope_inplace", &rope_inplace);
-  m.def("swiglu", &swiglu);
+  m.def("swiglu", &swiglu, py::arg("bwd"), py::arg("gu"), py::arg("dact"), py::arg("out"),
+        py::arg("c0") = 0, py::arg("c1") = -1);
   m.def("cross_entropy", &cross_entropy);
   m.def("grad_norm_sq", &grad_norm_sq);
   m.def("adamw", &adamw);

@@ -21,6 +21,7 @@
 //        tile (loops over key tiles); the softmax row statistics come from the forward's LSE
 //        and delta = rowsum(dO * O) (preprocess kernel).
 #include "common.h"
+#include <cstdlib>
 
 namespace lumen {
 namespace fa {
@@ -747,7 +748,7 @@ __device__ __forceinline__ float xor32_sum(float v) {
   return a + b;
 }
 
-template <typename T, bool CAUSAL, bool MASK>
+template <typename T, bool CAUSAL, bool MASK, int PR = 0>
 __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, const Off32& off,
                                            const uint4 (&qf)[8], f32x16 (&acc)[4], float& m_i,
                                            float& l_i, int kv0, int L, int qrow, int hi,
@@ -783,6 +784,17 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
     vr[1][n] = tr32a<1>(vb, off, n);
     vr[2][n] = tr32a<2>(vb, off, n);
     vr[3][n] = tr32a<3>(vb, off, n);
+  }
+  if (PR == 5) {  // cost probe: no softmax
+    const uint4 pb[4] = {pack8<T>(st[0], 0), pack8<T>(st[0], 1), pack8<T>(st[1], 0),
+                         pack8<T>(st[1], 1)};
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      lgkm_wait(vr[sl][0], vr[sl][1], vr[sl][2], vr[sl][3]);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[n] = Mfma32<T>::run(as_u4(vr[sl][n]), pb[sl], acc[n]);
+    }
+    return;
   }
   float mx = -INFINITY;
 #pragma unroll
@@ -833,7 +845,10 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
   }
 }
 
-template <typename T, bool CAUSAL, bool PAGED = false>
+// PROBE (cost split, LUMEN_FA_PROBE; never the default): 1 = key loop without the tile math
+// (loads, waits and barriers only), 2 = key loop without the K / V loads (math on stale LDS),
+// 3 = no key loop (Q load, first K / V tile, O / LSE stores), 5 = tile math without the softmax
+template <typename T, bool CAUSAL, bool PAGED = false, int PROBE = 0>
 __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   constexpr int BM = 128;
   // Two SEPARATE LDS objects for the ping-pong K|V buffers, with the loop unrolled by two so
@@ -903,25 +918,26 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   }
   // one K/V tile: prefetch the next into `nxt`, wait for `cur`, compute, release `cur`
   auto tile = [&](char* cur, char* nxt, int kv0) {
-    if (kv0 + BN < kv_end) {
+    if (PROBE == 2) {
+    } else if (kv0 + BN < kv_end) {
       stage(nxt, kv0 + BN);
       wait_vm_8();
     } else {
       wait_vm_all();
     }
     lds_fence_barrier();
-    if (kv0 < w_end) {  // (causal: tiles entirely above this wave's rows are skipped)
+    if (PROBE != 1 && kv0 < w_end) {  // (causal: tiles entirely above this wave's rows are skipped)
       const bool need_mask = (kv0 + BN > Lk) || (CAUSAL && kv0 + BN - 1 > wq0 + qoff);
       if (need_mask)
-        fwd32_tile<T, CAUSAL, true>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos, hi,
-                                    a.scale_log2);
+        fwd32_tile<T, CAUSAL, true, PROBE>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos,
+                                           hi, a.scale_log2);
       else
-        fwd32_tile<T, CAUSAL, false>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos, hi,
-                                     a.scale_log2);
+        fwd32_tile<T, CAUSAL, false, PROBE>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos,
+                                            hi, a.scale_log2);
     }
     lds_fence_barrier();  // every wave is done with `cur` before it is refilled
   };
-  for (int kv0 = 0; kv0 < kv_end; kv0 += 2 * BN) {
+  for (int kv0 = 0; kv0 < (PROBE == 3 ? 0 : kv_end); kv0 += 2 * BN) {
     tile(bufA, bufB, kv0);
     if (kv0 + BN < kv_end) tile(bufB, bufA, kv0 + BN);
   }
@@ -1239,7 +1255,12 @@ static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& 
     if (mt != 20) return hipErrorInvalidValue;
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
     if (a.nitems > 0) grid = dim3(std::min(a.nitems, (causal ? 2 : 1) * cu_count()), 1);
-    if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
+    static const int probe = [] { const char* e = std::getenv("LUMEN_FA_PROBE"); return e ? std::atoi(e) : 0; }();
+    if (causal && probe == 1) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 1>), grid, block, 0, st, a);
+    else if (causal && probe == 2) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 2>), grid, block, 0, st, a);
+    else if (causal && probe == 3) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 3>), grid, block, 0, st, a);
+    else if (causal && probe == 5) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 5>), grid, block, 0, st, a);
+    else if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((fwd32_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 1) {
     dim3 grid((unsigned)((a.T + 3) / 4));

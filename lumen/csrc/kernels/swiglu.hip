@@ -11,11 +11,13 @@ namespace lumen {
 template <typename T, bool BWD>
 __global__ void __launch_bounds__(256) swiglu_kernel(const T* __restrict__ gu,
                                                      const T* __restrict__ dact,
-                                                     T* __restrict__ out, int rows, int F) {
-  const int vpr = F / 8;  // vectors per row
+                                                     T* __restrict__ out, int rows, int F,
+                                                     int c0, int nc) {
+  // columns [c0, c0 + nc) of the F-wide activation (the whole row: c0 = 0, nc = F)
+  const int vpr = nc / 8;  // vectors per row
   const long long tid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (tid >= static_cast<long long>(rows) * vpr) return;
-  const int r = static_cast<int>(tid / vpr), c = static_cast<int>(tid % vpr) * 8;
+  const int r = static_cast<int>(tid / vpr), c = c0 + static_cast<int>(tid % vpr) * 8;
   const T* g_p = gu + static_cast<size_t>(r) * 2 * F + c;
   float g[8], u[8];
   load8(g_p, g);
@@ -43,26 +45,31 @@ __global__ void __launch_bounds__(256) swiglu_kernel(const T* __restrict__ gu,
 
 template <typename T>
 static hipError_t launch(bool bwd, const void* gu, const void* dact, void* out, int rows, int F,
-                         hipStream_t st) {
-  const long long total = static_cast<long long>(rows) * (F / 8);
+                         int c0, int nc, hipStream_t st) {
+  const long long total = static_cast<long long>(rows) * (nc / 8);
   if (total == 0) return hipSuccess;
   dim3 grid(static_cast<unsigned>((total + 255) / 256)), block(256);
   if (bwd)
     hipLaunchKernelGGL((swiglu_kernel<T, true>), grid, block, 0, st, (const T*)gu,
-                       (const T*)dact, (T*)out, rows, F);
+                       (const T*)dact, (T*)out, rows, F, c0, nc);
   else
     hipLaunchKernelGGL((swiglu_kernel<T, false>), grid, block, 0, st, (const T*)gu, nullptr,
-                       (T*)out, rows, F);
+                       (T*)out, rows, F, c0, nc);
   return hipGetLastError();
 }
 
 }  // namespace lumen
 
+// columns [c0, c1) of the activation only (c0 = 0, c1 = F: the whole row).  The column range
+// lets the MLP run the activation of the columns a split gate|up GEMM (or down-projection dX)
+// has already produced while the GEMM's last-wave tail computes the rest on a side stream.
 extern "C" hipError_t lumen_swiglu(int dtype, int bwd, const void* gu, const void* dact, void* out,
-                                   int rows, int F, hipStream_t st) {
-  if (F % 8 != 0) return hipErrorInvalidValue;
-  if (dtype == lumen::kBF16) return lumen::launch<lumen::bf16>(bwd, gu, dact, out, rows, F, st);
-  if (dtype == lumen::kF16) return lumen::launch<lumen::fp16>(bwd, gu, dact, out, rows, F, st);
-  if (dtype == lumen::kF32) return lumen::launch<float>(bwd, gu, dact, out, rows, F, st);
+                                   int rows, int F, int c0, int c1, hipStream_t st) {
+  if (F % 8 != 0 || c0 % 8 != 0 || c1 % 8 != 0 || c0 < 0 || c1 > F || c0 > c1)
+    return hipErrorInvalidValue;
+  const int nc = c1 - c0;
+  if (dtype == lumen::kBF16) return lumen::launch<lumen::bf16>(bwd, gu, dact, out, rows, F, c0, nc, st);
+  if (dtype == lumen::kF16) return lumen::launch<lumen::fp16>(bwd, gu, dact, out, rows, F, c0, nc, st);
+  if (dtype == lumen::kF32) return lumen::launch<float>(bwd, gu, dact, out, rows, F, c0, nc, st);
   return hipErrorInvalidValue;
 }

@@ -22,7 +22,7 @@ import torch.utils.checkpoint as cp
 from ..ops._native import use_native
 from ..ops.embedding import embedding
 from ..ops.lora import arena_reset
-from ..ops.activation import recompute_mlp, swiglu
+from ..ops.activation import overlap_mlp, overlap_mlp_plan, recompute_mlp, swiglu
 from ..ops.attention import causal_attention, flash_attention_qkv, prepare_varlen
 from ..ops.loss import lm_head_cross_entropy
 from ..ops.rope import qkv_rope_split, rope_qkv_, rope_tables
@@ -135,6 +135,10 @@ class LlamaMLP(nn.Module):
         gu, dn = self.gate_up_proj, self.down_proj
         if self.recompute and self.training and torch.is_grad_enabled() and self.recompute_eligible:
             return recompute_mlp(x2d, gu, dn)
+        if self.recompute_eligible:
+            n1 = overlap_mlp_plan(x2d, gu, dn)
+            if n1:
+                return overlap_mlp(x2d, gu, dn, n1)
         return dn(swiglu(gu(x2d)))
 
 

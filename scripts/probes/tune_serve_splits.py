@@ -16,7 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 SHAPES = (("qkv", 12288, 4096), ("o", 4096, 4096), ("gate_up", 22016, 4096),
-          ("down", 4096, 11008))
+          ("down", 4096, 11008),
+          # training: the down projection's input gradient dY @ W (TN against the cached W^T)
+          ("down_dx", 11008, 4096))
 
 
 def _time(fn, n_w, iters=20):
@@ -49,11 +51,12 @@ def main():
     ap.add_argument("--ms", default="2048,4096")
     ap.add_argument("--max_tail", type=float, default=0.75)
     ap.add_argument("--phase", default="both", choices=["both", "tune", "time"])
+    ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
     a = ap.parse_args()
     if a.phase == "both":  # TunableOp writes its file at process exit: tune in a child first
         import subprocess
         rc = subprocess.call([sys.executable, "-u", __file__, "--out", a.out, "--ms", a.ms,
-                              "--max_tail", str(a.max_tail), "--phase", "tune"])
+                              "--max_tail", str(a.max_tail), "--phase", "tune", "--only", a.only])
         if rc:
             sys.exit(rc)
         a.phase = "time"
@@ -65,6 +68,8 @@ def main():
     ms = [int(m) for m in a.ms.split(",")]
     cases = []
     for name, N, K in SHAPES:
+        if a.only and name not in a.only.split(","):
+            continue
         for M in ms:
             cases.append((name, N, K, M, G.split_cols(M, N)))
     if a.phase == "tune":

@@ -115,6 +115,61 @@ def test_swiglu(dtype):
     assert rel(gu.grad, gu2.grad) < 1e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_swiglu_column_ranges(dtype):
+    """The column-range entry (used beside a split GEMM's tail): two ranges == the whole row,
+    forward and backward, and columns outside the range stay untouched."""
+    from lumen.ops._native import native
+
+    T, F, c = 129, 1024, 392
+    gu = torch.randn(T, 2 * F, device=DEV, dtype=dtype)
+    d = torch.randn(T, F, device=DEV, dtype=dtype)
+    whole, parts = torch.empty(T, F, device=DEV, dtype=dtype), torch.full((T, F), 7.0, device=DEV, dtype=dtype)
+    native().swiglu(False, gu, None, whole)
+    native().swiglu(False, gu, None, parts, 0, c)
+    assert torch.equal(parts[:, :c], whole[:, :c]) and bool((parts[:, c:] == 7).all())
+    native().swiglu(False, gu, None, parts, c, F)
+    assert torch.equal(parts, whole)
+    dw, dp = torch.empty_like(gu), torch.empty_like(gu)
+    native().swiglu(True, gu, d, dw)
+    native().swiglu(True, gu, d, dp, 0, c)
+    native().swiglu(True, gu, d, dp, c, F)
+    assert torch.equal(dp, dw)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_overlap_mlp(mode, monkeypatch):
+    """The frozen MLP with its split GEMMs' tails on a side stream beside the SwiGLU of the
+    columns already produced (``_OverlapMLP``, both issue orders) vs the fp32 reference and the
+    unfused path: output and input gradient."""
+    import lumen.ops.activation as act
+    import lumen.ops.gemm as G
+    from lumen.models.layers import Linear
+
+    T, H, F = 512, 512, 1376
+    monkeypatch.setattr(act, "MLP_OVERLAP", mode)
+    monkeypatch.setattr(G, "_split_plan", lambda x, w: 1024 if w.shape[0] == F else 0)
+    gu_l = Linear(H, 2 * F, dtype=torch.bfloat16, device=DEV)
+    dn_l = Linear(F, H, dtype=torch.bfloat16, device=DEV)
+    for m in (gu_l, dn_l):
+        m.weight.requires_grad_(False)
+        m.weight.copy_(torch.randn_like(m.weight) * 0.05)
+        m.transpose_bwd = True
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    out = act.overlap_mlp(x, gu_l, dn_l, F + 256)
+    g = torch.randn_like(out)
+    out.backward(g)
+    x2 = x.detach().clone().requires_grad_(True)
+    out2 = dn_l(act.swiglu(gu_l(x2)))
+    out2.backward(g)
+    x3 = x.detach().float().requires_grad_(True)
+    out3 = act.swiglu_ref(x3 @ gu_l.weight.float().t()) @ dn_l.weight.float().t()
+    out3.backward(g.float())
+    assert rel(out, out2) < 2e-3 and rel(x.grad, x2.grad) < 2e-3
+    assert rel(out, out3) < 1e-2 and rel(x.grad, x3.grad) < 1e-2
+    assert act.overlap_mlp_plan(x.cpu(), gu_l, dn_l) == 0  # CPU: never
+
+
 @pytest.mark.parametrize("V", [32000, 50272])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 def test_lm_head_cross_entropy(V, dtype):

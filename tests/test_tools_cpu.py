@@ -448,3 +448,14 @@ def test_custom_allreduce_crossover_selection():
     assert pick_plan(t3) == {"one_shot_max": 64 * KB, "rccl_from": None}
     # two-shot wins from the smallest size
     assert pick_plan([dict(bytes=8 * KB, one=20, two=10)])["one_shot_max"] == 0
+
+
+def test_overlap_mlp_plan_cpu_is_off():
+    """The side-stream MLP (``_OverlapMLP``) never plans on CPU tensors; the unfused path runs."""
+    import torch
+
+    from lumen.models.layers import Linear
+    from lumen.ops.activation import overlap_mlp_plan
+
+    gu, dn = Linear(64, 2 * 96), Linear(96, 64)
+    assert overlap_mlp_plan(torch.randn(8, 64), gu, dn) == 0
