@@ -25,3 +25,7 @@ for (n, dur), p in zip(kt, pm):
     ga = p.get("GRBM_GUI_ACTIVE", 0)
     print(f"{dur/1e3:8.1f} us  clk~{ga / dur:5.2f} GHz  mfma_busy {p.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / (1024 * max(ga, 1)):5.2f}  {n[:70]}")
 PY
+# serving burst (in-process engine, prefill-first 4096, the bench's settings): GPU busy / idle
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/serve -o serve -- python3 -m lumen.bench.serve_bench --mode engine --scheduling-policy prefill_first --max-batched-tokens 4096 --max-model-len 1024 > $O/serve.json 2> $O/serve.err || { tail -20 $O/serve.err; exit 1; }
+tail -2 $O/serve.json
+python3 scripts/tools/busy_timeline.py $O/serve 3.9
