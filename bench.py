@@ -499,6 +499,8 @@ def main():
     model.train()
     n_tr, n_all = count_parameters(model)
     engine = ZeroEngine(model, ds, env)
+    # overlapped reduce-scatter buckets of the LoRA gradients (16 MiB over xGMI at N > 1)
+    dp_buckets = len(engine.flat.buckets)
     on_gpu = env.device.type == "cuda"
     if on_gpu:
         torch.cuda.synchronize()
@@ -702,6 +704,7 @@ def main():
                 "gather_group_world": gather_world,
                 "backend": env.backend,
                 "zero3": zstats,
+                "dp_grad_buckets": dp_buckets,
                 # keep schedule: the frozen weights are gathered once (warm-up), 0 per timed step
                 "zero3_gathered_mb_total": round(gathered_total_mb, 1),
                 "zero3_gathered_mb_per_step": round(gathered_mb, 1),

@@ -100,6 +100,25 @@ class Bucket:
     work: Optional[object] = None
 
 
+# Gradient buckets of the overlapped (ZeRO-2/3) reduce-scatter.  A LoRA-sized trainable set fits
+# one DeepSpeed-sized bucket (16.8 M elements against reduce_bucket_size 5e7), and that single
+# reduce-scatter can only start once the whole backward has finished.  Over xGMI, buckets of
+# ~16 MiB of fp32 gradients let every bucket but the last reduce under the
+# remaining layers' backward.  At that size each collective still moves enough per link to stay
+# bandwidth-bound.  LUMEN_DP_BUCKET_MB = 0 keeps the config's bucket size.
+DP_BUCKET_MB = float(os.environ.get("LUMEN_DP_BUCKET_MB", "16"))
+
+
+def overlap_bucket_numel(cfg_numel: int, world: int, overlapped: bool,
+                         cap_mb: Optional[float] = None) -> int:
+    """Bucket size (fp32 elements) for the flat gradient buffer: the config's, capped at
+    ``cap_mb`` MiB when world > 1 and the reduce-scatter overlaps the backward."""
+    cap_mb = DP_BUCKET_MB if cap_mb is None else cap_mb
+    if world <= 1 or not overlapped or cap_mb <= 0:
+        return cfg_numel
+    return min(cfg_numel, max(int(cap_mb * 2**20) // 4, 1))
+
+
 class FlatTrainable:
     def __init__(self, params: Sequence[nn.Parameter], env: DistEnv, bucket_numel: int,
                  device: torch.device):

@@ -24,7 +24,7 @@ import torch.nn as nn
 
 from ..parallel.dist import DistEnv
 from ..parallel.zero import (AsyncOffloadStep, DynamicLossScaler, FlatTrainable,
-                             ParamCoordinator, ShardAdamW, grad_norm_sq)
+                             ParamCoordinator, ShardAdamW, grad_norm_sq, overlap_bucket_numel)
 from .config import DSConfig, warmup_lr
 
 
@@ -129,6 +129,8 @@ class ZeroEngine:
                     [m.weight for m in model.modules() if isinstance(m, Linear)
                      and m.transpose_bwd and getattr(m.weight, "_lumen_gathered", False)])
         bucket = cfg.reduce_bucket_size if self.stage >= 1 else int(2.5e7)
+        bucket = overlap_bucket_numel(bucket, W, self.sharded and self.stage >= 2
+                                      and cfg.overlap_comm)
         self.flat = FlatTrainable(trainable, env, max(bucket, 1), self.device)
         # broadcast adapter init from rank 0 (only the trainable 32 MiB, not 13.5 GB)
         if W > 1:
