@@ -100,13 +100,20 @@ class Bucket:
     work: Optional[object] = None
 
 
-# Gradient buckets of the overlapped (ZeRO-2/3) reduce-scatter.  A LoRA-sized trainable set fits
-# one DeepSpeed-sized bucket (16.8 M elements against reduce_bucket_size 5e7), and that single
-# reduce-scatter can only start once the whole backward has finished.  Over xGMI, buckets of
-# ~16 MiB of fp32 gradients let every bucket but the last reduce under the
-# remaining layers' backward.  At that size each collective still moves enough per link to stay
-# bandwidth-bound.  LUMEN_DP_BUCKET_MB = 0 keeps the config's bucket size.
-DP_BUCKET_MB = float(os.environ.get("LUMEN_DP_BUCKET_MB", "16"))
+# Gradient buckets of the overlapped (ZeRO-2/3) reduce-scatter (opt-in, LUMEN_DP_BUCKET_MB > 0).
+# A LoRA-sized trainable set fits one DeepSpeed-sized bucket (16.8 M elements against
+# reduce_bucket_size 5e7), and that single reduce-scatter can only start once the whole
+# backward has finished.  Buckets of e.g. 16 MiB of fp32 gradients let every
+# bucket but the last reduce under the remaining layers' backward.
+# Off by default, because it is unmeasured on an 8-GPU node:
+# * on this chip, concurrent kernels have so far cost the compute kernel more than they hid
+#   (profiles/r5_mlp_overlap: a tail GEMM beside the SwiGLU ran 2x longer);
+# * an RCCL kernel holding CUs during a one-wave backward GEMM can push that GEMM's tiles into a
+#   second wave;
+# * the single reduce-scatter it would hide is ~0.3 % of the step.
+# The bench records dp_grad_buckets, and extra.comm records the reduce-scatter size sweep, so
+# the node's own numbers can decide this.
+DP_BUCKET_MB = float(os.environ.get("LUMEN_DP_BUCKET_MB", "0"))
 
 
 def overlap_bucket_numel(cfg_numel: int, world: int, overlapped: bool,

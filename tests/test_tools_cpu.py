@@ -462,10 +462,10 @@ def test_overlap_mlp_plan_cpu_is_off():
 
 
 def test_overlap_bucket_cap():
-    """The overlapped ZeRO-2/3 gradient buckets: the LoRA set of Llama-2-7B (16.8 M fp32
-    elements, one 5e7 DeepSpeed bucket) splits into 16 MiB buckets at world > 1, so all but the
-    last reduce-scatter run under the backward; world 1, non-overlapped stages and a cap of 0
-    keep the config's size."""
+    """The overlapped ZeRO-2/3 gradient buckets (opt-in LUMEN_DP_BUCKET_MB): the LoRA set of
+    Llama-2-7B (16.8 M fp32 elements, one 5e7 DeepSpeed bucket) splits into 16 MiB buckets at
+    world > 1, so all but the last reduce-scatter run under the backward; world 1,
+    non-overlapped stages and a cap of 0 (the default) keep the config's size."""
     from lumen.parallel.zero import overlap_bucket_numel
 
     assert overlap_bucket_numel(int(5e7), 8, True, 16) == 4 * 2**20
@@ -474,3 +474,4 @@ def test_overlap_bucket_cap():
     assert overlap_bucket_numel(int(5e7), 1, True, 16) == int(5e7)
     assert overlap_bucket_numel(int(5e7), 8, False, 16) == int(5e7)
     assert overlap_bucket_numel(int(5e7), 8, True, 0) == int(5e7)
+    assert overlap_bucket_numel(int(5e7), 8, True) == int(5e7)  # default: off
