@@ -637,8 +637,9 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     load8(row + i0 + half, b);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      oa[j] = a[j] * cs[j] - b[j] * sn[j];
-      ob[j] = b[j] * cs[j] + a[j] * sn[j];
+      // explicit fmas: bit-identical to rope_inplace (kernels/rope.hip), whatever the contraction
+      oa[j] = fmaf(a[j], cs[j], -(b[j] * sn[j]));
+      ob[j] = fmaf(b[j], cs[j], a[j] * sn[j]);
     }
     store8(row + i0, oa);
     store8(row + i0 + half, ob);

@@ -85,11 +85,12 @@ def test_qkv_rope_split(nh, nkv, D, dtype):
     assert rel(qp, qr) < 1e-2 and rel(kp, kr) < 1e-2
 
 
+@pytest.mark.parametrize("nh", [4, 16])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-def test_rope_inplace(dtype):
+def test_rope_inplace(dtype, nh):
     from lumen.ops.rope import rope_inplace, rope_tables, _rotate_ref
 
-    T, nh, D = 37, 4, 128
+    T, D = 37, 128
     cos, sin = rope_tables(D, 4096, 10000.0, DEV)
     x = torch.randn(T, 3 * nh * D, device=DEV, dtype=dtype)
     pos = torch.randint(0, 2000, (T,), device=DEV)
