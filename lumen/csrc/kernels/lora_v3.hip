@@ -599,6 +599,11 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
   __shared__ __attribute__((aligned(16))) char img[2][64 * 256];
   __shared__ __attribute__((aligned(16))) T st[2][J * kDxST];
   __shared__ __attribute__((aligned(16))) T s2[128 * SP];
+  // the sub-tile's dropout keep-masks (one byte per 8 elements, [row][chunk]), hashed once in
+  // store_stage for the dA image and re-read by the dx update of the same elements (it hashed
+  // them a second time: the dropout hash, four 32-bit multiplies per element pair, was the
+  // kernel's largest VALU cost)
+  __shared__ uint8_t mk[DROP ? 2 : 1][DROP ? 64 * 16 : 1];
   const int c0 = blockIdx.x * 128;
   const int tb = blockIdx.y * a.TW, te = min(a.T, tb + a.TW);
   if (c0 >= a.K || tb >= a.T) return;
@@ -661,10 +666,14 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
       const int idx = threadIdx.x + i * 256;
       const int row = idx >> 4, ch = idx & 15;
       uint4 u = xv[i];
-      if (DROP)
-        u = mask8(u, dropout_keep8(a.drop.seed,
-                                   (unsigned long long)((long long)(t0 + row) * a.drop.ld + a.drop.col0 + c0 + ch * 8),
-                                   a.drop.thresh));
+      if (DROP) {
+        const uint32_t keep = dropout_keep8(
+            a.drop.seed,
+            (unsigned long long)((long long)(t0 + row) * a.drop.ld + a.drop.col0 + c0 + ch * 8),
+            a.drop.thresh);
+        u = mask8(u, keep);
+        mk[b][row * 16 + ch] = static_cast<uint8_t>(keep);
+      }
       *reinterpret_cast<uint4*>(img[b] + img_off(row, ch)) = u;
     }
 #pragma unroll
@@ -771,9 +780,10 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
         if (c >= a.K) continue;
         float y[8];
         unpack8<T>(dv[i], y);
-        const uint32_t keep = DROP ? dropout_keep8(a.drop.seed,
-                                                   (unsigned long long)((long long)t * a.drop.ld + a.drop.col0 + c),
-                                                   a.drop.thresh)
+        // row t = t0 + 16 wid + L, chunk (c - c0) / 8 = 4 i + g: the mask store_stage hashed
+        // (hashing these masks a second time here measured 35.9 / 32.5 against 34.9 / 31.4 us
+        // per q|k|v / o call, gpurun r5_49)
+        const uint32_t keep = DROP ? static_cast<uint32_t>(mk[buf][(wid * 16 + L) * 16 + 4 * i + g])
                                    : 0xFFu;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
