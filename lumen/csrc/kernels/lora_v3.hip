@@ -417,10 +417,13 @@ __device__ __forceinline__ void dy_load(uint4 (&v)[4], const T* base, long long 
                                         int c0, int cmax) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    // unconditional from a clamped address, zeroed by a select: a guarded load here made hipcc
+    // drain every load in flight at the branch join (rmax > r0, cmax >= 8)
     const int idx = threadIdx.x + i * 256;
     const int r = r0 + (idx >> 4), c = c0 + (idx & 15) * 8;
-    v[i] = (r < rmax && c < cmax) ? *reinterpret_cast<const uint4*>(base + (long long)r * ld + c)
-                                  : make_uint4(0, 0, 0, 0);
+    const uint4 u = *reinterpret_cast<const uint4*>(base + (long long)min(r, rmax - 1) * ld +
+                                                     min(c, cmax - 8));
+    v[i] = (r < rmax && c < cmax) ? u : make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -458,9 +461,10 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
       for (int jt = 0; jt < NJ; ++jt) {
         float f[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < 8; ++e) {  // unconditional (clamped column), zeroed after
           const int c = cb + cc * 128 + 32 * i + 8 * g + e;
-          f[e] = c < NL ? B[(long long)c * a.r + jt * 16 + L] : 0.f;
+          const float u = B[(long long)min(c, NL - 1) * a.r + jt * 16 + L];
+          f[e] = c < NL ? u : 0.f;
         }
         bop[cc][i][jt] = pack8<T>(f);
       }
@@ -484,28 +488,29 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
     const int t0 = tb + ts * 64, cbase = cb + cc * 128;
     dy_store(img[buf], v);
     __syncthreads();
-    if (s + 1 < nstage) {
-      const int ts1 = (s + 1) / nch, cc1 = (s + 1) % nch;
+    // dB B-operand: lane (L, g) <- Z[t0 + 32 ks + 8 g + e][16 jt + L], loaded every stage (the
+    // chunks of a sub-tile reload the same L2-resident rows) and BEFORE the next stage's dY
+    // prefetch, all unconditional from clamped rows: the wait for them is then a counted
+    // vmcnt that leaves the prefetch in flight.  (Loaded after it behind `if (cc == 0)`, with
+    // guarded loads, hipcc drained the prefetch with vmcnt(0) before the dB products.)
+    float zf[2][NJ][8];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int t = t0 + 32 * ks + 8 * g + e;
+          zf[ks][jt][e] = Z[(long long)min(t, te - 1) * a.ldz + jt * 16 + L];
+        }
+    {  // the last stage reloads itself (results unused): no branch around the prefetch
+      const int s1 = min(s + 1, nstage - 1);
+      const int ts1 = s1 / nch, cc1 = s1 % nch;
       dy_load<T>(v, dy, a.ldy, tb + ts1 * 64, te, cb + cc1 * 128, NL);
     }
     if (cc == 0) {
 #pragma unroll
       for (int jt = 0; jt < NJ; ++jt) dzacc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // dB B-operand: lane (L, g) <- Z[t0 + 32 ks + 8 g + e][16 jt + L]
-      // (loading these one sub-tile ahead measured neutral: 29.7 -> 30.1 us, one fewer wave per
-      // SIMD from the extra registers; profiles/r3d/lora)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int jt = 0; jt < NJ; ++jt) {
-          float f[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int t = t0 + 32 * ks + 8 * g + e;
-            f[e] = t < te ? Z[(long long)t * a.ldz + jt * 16 + L] : 0.f;
-          }
-          zop[ks][jt] = pack8<T>(f);
-        }
     }
     const char* im = img[buf];
     // dZ: rows 16 wid + L, k = chunk columns
@@ -520,6 +525,15 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
         }
     }
     // dB: columns 32 wid + 16 m + (4 g + r), k = sub-tile rows
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt) {
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = t0 + 32 * ks + 8 * g + e < te ? zf[ks][jt][e] : 0.f;
+        zop[ks][jt] = pack8<T>(f);
+      }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
