@@ -23,6 +23,7 @@ hipError_t lumen_qkv_rope(int, int, void*, void*, void*, void*, const int*, cons
 hipError_t lumen_rope_inplace(int, void*, const int*, const float*, const float*, int, int, int,
                               int, hipStream_t);
 hipError_t lumen_swiglu(int, int, const void*, const void*, void*, int, int, int, int, hipStream_t);
+hipError_t lumen_scale_dev(int, void*, long long, const float*, const float*, hipStream_t);
 hipError_t lumen_cross_entropy(int, void*, const int64_t*, float*, float*, int, int, int, float,
                                int, const float*, hipStream_t);
 hipError_t lumen_grad_norm_sq(int, const void*, long long, float*, hipStream_t);
@@ -284,6 +285,17 @@ void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::opti
                             static_cast<int>(ignore_index), static_cast<float>(scale),
                             write_grad ? 1 : 0, ptr<const float>(gscale), cur_stream()),
         "cross_entropy");
+}
+
+// x *= num / den (device f32 scalars; den optional), in place, contiguous x
+void scale_dev(at::Tensor& x, const at::Tensor& num, const std::optional<at::Tensor>& den) {
+  need_cuda(x, "x"); need_cuda(num, "num");
+  if (!x.is_contiguous() || num.scalar_type() != at::kFloat || num.numel() < 1 ||
+      (den && (den->scalar_type() != at::kFloat || den->numel() < 1)))
+    throw std::invalid_argument("lumen: scale_dev needs a contiguous x and f32 scalars");
+  check(lumen_scale_dev(dcode(x), x.data_ptr(), x.numel(), num.data_ptr<float>(),
+                        ptr<const float>(den), cur_stream()),
+        "scale_dev");
 }
 
 void grad_norm_sq(const at::Tensor& g, at::Tensor& out) {
@@ -912,6 +924,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu", &swiglu, py::arg("bwd"), py::arg("gu"), py::arg("dact"), py::arg("out"),
         py::arg("c0") = 0, py::arg("c1") = -1);
   m.def("cross_entropy", &cross_entropy);
+  m.def("scale_dev", &scale_dev);
   m.def("grad_norm_sq", &grad_norm_sq);
   m.def("adamw", &adamw);
   m.def("lora_gemm", &lora_gemm);

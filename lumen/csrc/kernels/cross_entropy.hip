@@ -68,7 +68,41 @@ __global__ void __launch_bounds__(NT) xent_kernel(T* __restrict__ logits, const 
   }
 }
 
+// x *= num[0] / den[0] (den optional), f32 math on 16-bit rows, 16 bytes per thread: the LM
+// head's dH times the upstream device scalar (as torch's mixed-dtype in-place mul it ran the
+// generic unrolled elementwise kernel: 53 us for 32 MiB at Llama-2-7B's 8 x 512 tokens)
+template <typename T>
+__global__ void __launch_bounds__(256) scale_dev_kernel(T* __restrict__ x, long long n8,
+                                                        const float* __restrict__ num,
+                                                        const float* __restrict__ den) {
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const float s = den ? num[0] / den[0] : num[0];
+  float v[8];
+  load8(x + i * 8, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= s;
+  store8(x + i * 8, v);
+}
+
 }  // namespace lumen
+
+extern "C" hipError_t lumen_scale_dev(int dtype, void* x, long long n, const float* num,
+                                      const float* den, hipStream_t st) {
+  if (n % 8 != 0) return hipErrorInvalidValue;
+  const long long n8 = n / 8;
+  if (n8 == 0) return hipSuccess;
+  dim3 grid(static_cast<unsigned>((n8 + 255) / 256)), block(256);
+  if (dtype == lumen::kBF16)
+    hipLaunchKernelGGL(lumen::scale_dev_kernel<lumen::bf16>, grid, block, 0, st, (lumen::bf16*)x, n8, num, den);
+  else if (dtype == lumen::kF16)
+    hipLaunchKernelGGL(lumen::scale_dev_kernel<lumen::fp16>, grid, block, 0, st, (lumen::fp16*)x, n8, num, den);
+  else if (dtype == lumen::kF32)
+    hipLaunchKernelGGL(lumen::scale_dev_kernel<float>, grid, block, 0, st, (float*)x, n8, num, den);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
 
 extern "C" hipError_t lumen_cross_entropy(int dtype, void* logits, const int64_t* labels,
                                           float* loss_sum, float* row_loss, int rows, int V,

@@ -48,7 +48,11 @@ class _LMHeadCE(torch.autograd.Function):
         # upstream grad (a 0-dim f32 tensor): multiplied in f32 math, never cast to 16 bits
         # first (2^16, the initial fp16 loss scale, is not representable in fp16); dlogits that
         # already carry the hinted scale are divided by it (ratio 1 on the engine's path)
-        dh.mul_(g / ctx.hint if ctx.hint is not None else g)
+        if (g.dtype == torch.float32 and g.is_cuda and dh.is_contiguous() and dh.numel() % 8 == 0
+                and (ctx.hint is None or (ctx.hint.dtype == torch.float32 and ctx.hint.is_cuda))):
+            native().scale_dev(dh, g.reshape(1), ctx.hint)  # one vectorized pass
+        else:
+            dh.mul_(g / ctx.hint if ctx.hint is not None else g)
         dw = None
         if ctx.w_grad:
             dw = torch.matmul(dlogits.t(), h)

@@ -192,6 +192,24 @@ def test_lm_head_cross_entropy(V, dtype):
     assert rel(h.grad, h2.grad) < 3e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_scale_dev(dtype):
+    """x *= num / den with device f32 scalars (the LM head's dH times the upstream gradient and
+    the fp16 loss-scale hint), f32 math, vs torch."""
+    from lumen.ops._native import native
+
+    x = torch.randn(1000, 24, device=DEV).to(dtype)
+    num = torch.tensor([65536.0 * 3], device=DEV)
+    den = torch.tensor([65536.0], device=DEV)
+    ref = (x.float() * 3).to(dtype)
+    y = x.clone()
+    native().scale_dev(y, num, den)
+    assert torch.equal(y, ref)
+    y = x.clone()
+    native().scale_dev(y, torch.tensor([0.37], device=DEV), None)
+    assert torch.equal(y, (x.float() * 0.37).to(dtype))
+
+
 def test_grad_norm_and_adamw():
     from lumen.ops._native import native
     from lumen.parallel.zero import _adamw_torch
