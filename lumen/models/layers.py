@@ -283,7 +283,10 @@ def configure_backward_layout(model: nn.Module, policy=None) -> int:
     n = 0
     for name, m in model.named_modules():
         if isinstance(m, Linear):
-            on = not name.endswith("lm_head") and (names is None or m.seg_names[0] in names)
+            # the LM head too (LUMEN_LMHEAD_WT=0: not): its dH = dlogits @ W measured 874 -> 778 us
+            # as the TN GEMM against W^T (Llama-2-7B, 8 x 512 tokens, gpurun r5_55)
+            head_ok = not name.endswith("lm_head") or os.environ.get("LUMEN_LMHEAD_WT", "1") != "0"
+            on = head_ok and (names is None or m.seg_names[0] in names)
             gathered = getattr(m.weight, "_lumen_gathered", False)
             if on and not gathered:  # persistent copies must fit the HBM budget
                 need = m.weight.numel() * m.weight.element_size()

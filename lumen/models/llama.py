@@ -301,7 +301,7 @@ class LlamaForCausalLM(nn.Module):
                 return torch.matmul(y, self.lm_head.weight.t())
             nv = int(n_valid) if n_valid is not None else int((labels != -100).sum())
             return lm_head_cross_entropy(y, labels.reshape(-1), self.lm_head.weight_fn, nv,
-                                         self.lm_head.weight)
+                                         self.lm_head.weight, self.lm_head._wt_fn())
 
         return self._run_unit(last, head, h, res)
 

@@ -190,6 +190,11 @@ def test_lm_head_cross_entropy(V, dtype):
     (loss * 3).backward()
     (loss2 * 3).backward()
     assert rel(h.grad, h2.grad) < 3e-2
+    # TN input gradient against a cached W^T (the frozen head's weight_t_fn)
+    Wt = W.t().contiguous()
+    h3 = h.detach().clone().requires_grad_(True)
+    (lm_head_cross_entropy(h3, labels, lambda: W, n_valid, None, lambda: Wt) * 3).backward()
+    assert rel(h3.grad, h2.grad) < 3e-2 and rel(h3.grad, h.grad) < 1e-2
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])

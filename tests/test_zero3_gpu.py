@@ -5,6 +5,8 @@ as RCCL's.  Every schedule (release / keep), with accumulation and activation ch
 must give the stage-0 trajectory."""
 import math
 
+import os
+
 import pytest
 import torch
 
@@ -138,7 +140,9 @@ def test_zero3_offpath_transposes_match_persistent_layout(monkeypatch):
     ref, _, _ = _train(monkeypatch, 0, bwd_wt="all", ckpt=True)
     got, _, coord = _train(monkeypatch, 3, "keep", bwd_wt="all", ckpt=True)
     assert coord.transposed_numel > 0
-    assert sum(len(u.tn) for u in coord.units) == 4 * sum(1 for u in coord.units[1:-1])
+    # 4 projections per decoder unit, plus the LM head's W^T in the last unit (LUMEN_LMHEAD_WT)
+    head = int(os.environ.get("LUMEN_LMHEAD_WT", "1") != "0")
+    assert sum(len(u.tn) for u in coord.units) == 4 * sum(1 for u in coord.units[1:-1]) + head
     for k in ref:
         torch.testing.assert_close(got[k], ref[k], rtol=2e-3, atol=2e-5)
 
