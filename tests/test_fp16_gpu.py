@@ -104,7 +104,10 @@ def test_fp16_forced_overflow_skips_and_backs_off():
         assert torch.isfinite(a[k]).all(), k
         moved = (a[k].float() - init[k].float()).norm()
         diff = (a[k].float() - b[k].float()).norm()
-        assert diff <= 1e-2 * moved + 1e-7, (k, float(diff), float(moved))
+        # 3 %: Adam's 1/sqrt(v) turns the order noise of near-zero gradient components into
+        # lr-sized steps (a full-suite run measured 1.46 % once, r5_57; isolated runs pass at
+        # 1 %); a wrong skip would move A away from B by O(moved) itself
+        assert diff <= 3e-2 * moved + 1e-7, (k, float(diff), float(moved))
     assert any(v.abs().sum() > 0 for k, v in a.items() if "lora_B" in k)
 
 

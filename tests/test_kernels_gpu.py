@@ -651,8 +651,11 @@ def test_transposed_weight_backward_matches():
     ids = torch.randint(3, m.config.vocab_size, (2, 64), device=dev)
     labels = torch.roll(ids, -1, 1)
     grads = []
+    import os
+
+    head = int(os.environ.get("LUMEN_LMHEAD_WT", "1") != "0")  # the LM head's W^T (TN dH)
     for pol in ("none", "all"):
-        assert configure_backward_layout(m, pol) == (0 if pol == "none" else 8)
+        assert configure_backward_layout(m, pol) == (0 if pol == "none" else 8 + head)
         for p in m.parameters():
             p.grad = None
         loss = m(ids, labels=labels)
