@@ -215,6 +215,20 @@ def test_scale_dev(dtype):
     assert torch.equal(y, (x.float() * 0.37).to(dtype))
 
 
+@pytest.mark.parametrize("n", [1, 7, 8, 1000003, 16777216 + 5])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_grad_norm_sq_sizes(n, dtype):
+    """Sum of squares (the global grad-norm pass): ragged tails and the LoRA-set size, vs torch
+    in f64 (it accumulates into a pre-zeroed scalar)."""
+    from lumen.ops._native import native
+
+    g = (torch.randn(n, device=DEV) * 3).to(dtype)
+    out = torch.zeros(1, device=DEV)
+    native().grad_norm_sq(g, out)
+    ref = (g.double() ** 2).sum().item()
+    assert abs(out.item() - ref) <= 1e-4 * ref + 1e-6
+
+
 def test_grad_norm_and_adamw():
     from lumen.ops._native import native
     from lumen.parallel.zero import _adamw_torch
