@@ -329,6 +329,16 @@ def run_comm_probe(env, gather_group=None, unit_mb: float = 386.0, bucket_numel:
         return {"numel": m, "ms": round(t * 1e3, 3),
                 "busbw_gbps": round(m * 4 / t / 1e9 * (W - 1) / W, 1)}
 
+    if on_gpu:
+        # which device pairs HIP reports peer access for (xGMI: every pair on an 8-GPU node);
+        # the custom all-reduce's IPC mapping needs it (VERDICT r5 Next #7)
+        try:
+            n = torch.cuda.device_count()
+            res["peer_access"] = {"devices": n, "matrix": [
+                [1 if i == j else int(torch.cuda.can_device_access_peer(i, j)) for j in range(n)]
+                for i in range(n)]}
+        except Exception as e:  # noqa: BLE001
+            res["peer_access"] = {"error": repr(e)[:200]}
     res["all_gather"] = dict(gather(unit_mb),
                              group="weight-gather" if gather_group is not None else "default")
     res["reduce_scatter"] = rscatter(bucket_numel)
@@ -343,6 +353,8 @@ def run_comm_probe(env, gather_group=None, unit_mb: float = 386.0, bucket_numel:
             from lumen.parallel.custom_ar import CustomAllReduce
 
             car = CustomAllReduce(None, dev, max_bytes=max(car_sizes))
+            res["custom_ar_setup"] = {"ok": True, "world": car.world,
+                                      "shared_device": bool(car.shared_device)}
             try:
                 cal = car.calibrate(rccl_group=dist.group.WORLD, sizes=car_sizes, apply=False)
             finally:
@@ -351,6 +363,7 @@ def run_comm_probe(env, gather_group=None, unit_mb: float = 386.0, bucket_numel:
             res["allreduce_plan"] = cal["plan"]
         except Exception as e:  # noqa: BLE001 - the RCCL numbers stand
             res["allreduce_us"] = {"error": repr(e)[:300]}
+            res.setdefault("custom_ar_setup", {"ok": False, "error": repr(e)[:300]})
     return res
 
 
@@ -451,6 +464,16 @@ def main():
                     help="all-gather size of the probe on CPU / gloo runs (GPU: 386 MiB)")
     ap.add_argument("--partitioned_steps", type=int, default=5,
                     help="timed steps of each partitioned run (2 untimed warm-up steps first)")
+    ap.add_argument("--wall_budget", type=float,
+                    default=float(os.environ.get("LUMEN_BENCH_WALL_S", "520")),
+                    help="seconds from process start for the whole run: an optional section "
+                         "(comm probe, partitioned schedules, serving) whose estimate does not "
+                         "fit in what is left is skipped and listed in extra.budget (the driver "
+                         "kills the run at 600 s)")
+    ap.add_argument("--box", dest="box", action="store_true", default=True,
+                    help="(default, GPU) extra.box: clock / power sampled through the timed "
+                         "region plus a fixed 8192^3 GEMM and a 4 GiB HBM read")
+    ap.add_argument("--no_box", dest="box", action="store_false")
     args = ap.parse_args()
 
     import torch
@@ -573,6 +596,20 @@ def main():
 
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
+    from lumen.bench.budget import WallBudget, partitioned_estimate_s
+    from lumen.utils import boxcal
+
+    def _agree_min(x: float) -> float:
+        if not dist.is_initialized():
+            return x
+        t = torch.tensor([x], dtype=torch.float64 if not on_gpu else torch.float32,
+                         device=env.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return float(t.item())
+
+    budget = WallBudget(args.wall_budget, T_START, _agree_min)
+    hwmon = boxcal.gpu_hwmon(env.device) if (on_gpu and args.box) else None
+    sampler = boxcal.HwmonSampler(hwmon).start() if (on_gpu and args.box) else None
     # every timed step must really update the adapters: a non-finite gradient makes the fused
     # AdamW skip the step on the device (a NaN-producing kernel would otherwise time as "fast")
     sk0 = engine.skipped_steps
@@ -584,6 +621,7 @@ def main():
     loss = run_steps(args.steps, args.warmup)
     sync()
     dt = time.perf_counter() - t1
+    timed_box = sampler.stop() if sampler is not None else None
     if prof is not None:
         prof.__exit__(None, None, None)
         os.makedirs(args.profile_dir, exist_ok=True)
@@ -622,8 +660,25 @@ def main():
     zstats = coord.stats() if coord else None
     if wd is not None:
         wd.close()
+    box = None
+    if on_gpu and args.box:
+        # fixed work on this box, same process and lease, right after the timed region: a slow
+        # record is a slow box when these ran slow too (max over ranks at N > 1)
+        try:
+            fixed = boxcal.fixed_work(env.device, hwmon=hwmon)
+            if dist.is_initialized():
+                v = torch.tensor([fixed["gemm"]["ms_med"],
+                                  fixed.get("hbm_read", {}).get("ms_med", 0.0)],
+                                 dtype=torch.float32, device=env.device)
+                dist.all_reduce(v, op=dist.ReduceOp.MAX)
+                fixed["max_over_ranks"] = {"gemm_ms_med": round(float(v[0]), 3),
+                                           "hbm_read_ms_med": round(float(v[1]), 3)}
+            box = boxcal.box_record(env.device, timed_box, fixed)
+        except Exception as e:  # noqa: BLE001 - keep the headline result
+            box = {"error": repr(e)[:300], "timed_region": timed_box}
+    ms_step = dt / args.steps * 1000
     comm = None
-    if world > 1 and args.comm_probe:
+    if world > 1 and args.comm_probe and budget.allow("comm_probe", 30.0 if on_gpu else 10.0):
         # after (and outside) the timed region: the transport's own numbers
         try:
             comm = run_comm_probe(env, engine.gather_group,
@@ -631,6 +686,7 @@ def main():
         except Exception as e:  # noqa: BLE001 - keep the headline result
             comm = {"error": repr(e)[:300]}
             raise  # ranks may disagree on where they failed: do not continue collectives
+        budget.done("comm_probe")
     serve = serve_engine = serve_chunked = None
     parts = {}
     want_parts = [x for x in args.partitioned.split(",") if x] if ds.stage == 3 else []
@@ -650,6 +706,11 @@ def main():
         # never runs a hybrid whose ring is smaller than release's (r4 world-8 rehearsal:
         # 2,147 vs 1,338 MB gathered per step at half of a 2-layer model)
         ml = 1e9 if sched == "release" else max(0.5 * cfg.num_params(), 1e9 + _max_unit(cfg))
+        est = partitioned_estimate_s(ms_step, args.partitioned_steps,
+                                     min(2, args.partitioned_steps), build_s)
+        if not budget.allow(f"zero3_{sched}", est):
+            parts[sched] = {"skipped": "wall budget", "est_s": round(est, 1)}
+            continue
         try:
             parts[sched] = run_partitioned(args, env, ds, batches, sched, ml,
                                            steps=args.partitioned_steps,
@@ -658,11 +719,16 @@ def main():
             parts[sched] = {"error": repr(e)[:300]}
             if world > 1:
                 raise  # ranks may disagree on where they failed: do not continue collectives
+        budget.done(f"zero3_{sched}")
     if args.serve and world == 1 and on_gpu:
         # second half of the BASELINE metric ("serve tok/s + p50 TTFT"), after the timed
         # training region: the training model and engine are freed first
         del batches
-        serve, serve_engine, serve_chunked = run_serve_bench(args)
+        if budget.allow("serve", 60.0):
+            serve, serve_engine, serve_chunked = run_serve_bench(args)
+            budget.done("serve")
+        else:
+            serve = {"skipped": "wall budget"}
     out = None
     if env.is_main:
         from lumen.train.trainer import model_flops_per_token
@@ -719,6 +785,7 @@ def main():
                 "serve": serve,
                 "serve_engine": serve_engine,
                 "serve_chunked": serve_chunked,
+                "box": box,
             },
         }
     import threading
@@ -733,7 +800,26 @@ def main():
                 print(json.dumps(out), file=json_out, flush=True)
                 printed[0] = True
 
-    if args.serve_tp and world > 1 and (on_gpu or args.serve_tp == 2):
+    tp_deadline = args.serve_tp_deadline
+    run_tp = bool(args.serve_tp and world > 1 and (on_gpu or args.serve_tp == 2))
+    if run_tp:
+        # the TP section's own deadline is cut to what the wall budget leaves (minus the
+        # closing barrier and teardown); below a minute it is not started at all
+        tp_deadline = min(args.serve_tp_deadline, budget.left() - 20.0)
+        min_tp = 60.0 if on_gpu else 1.0
+        if tp_deadline < min_tp and args.serve_tp_deadline >= min_tp:
+            budget.skipped.append({"section": "serve_tp", "est_s": min_tp,
+                                   "left_s": round(tp_deadline + 20.0, 1)})
+            run_tp = False
+            if out is not None:
+                out["extra"]["serve_tp"] = {"skipped": "wall budget"}
+        else:
+            tp_deadline = max(tp_deadline, min(args.serve_tp_deadline, 0.01))
+    if out is not None:
+        out["extra"]["budget"] = budget.record()
+        if run_tp:
+            out["extra"]["budget"]["serve_tp_deadline_s"] = round(tp_deadline, 1)
+    if run_tp:
         # TP = N serving over the N GPUs.  A hung collective must not cost the training record:
         # past the deadline (TP section + closing barrier) rank 0 prints the JSON line with the
         # error (unless it already did) and every rank exits
@@ -743,11 +829,11 @@ def main():
 
         def _deadline():
             if out is not None and not printed[0]:
-                out["extra"]["serve_tp"] = {"error": f"timed out after {args.serve_tp_deadline} s"}
+                out["extra"]["serve_tp"] = {"error": f"timed out after {tp_deadline:.1f} s"}
             _print_once()
             os._exit(0)
 
-        timer = threading.Timer(args.serve_tp_deadline + (0 if env.is_main else 15), _deadline)
+        timer = threading.Timer(tp_deadline + (0 if env.is_main else 15), _deadline)
         timer.daemon = True
         timer.start()
         try:

@@ -69,6 +69,10 @@ hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int
                              long long, hipStream_t);
 hipError_t lumen_decode_gemm(int, const void*, const void*, void*, float*, int*, int, int, int,
                              long long, long long, int, int, int, int, int, hipStream_t);
+hipError_t lumen_mlp_gemm(int, int, const void*, long long, const void*, long long, void*, long long,
+                          void*, long long, const void*, long long, int, int, int, int, int,
+                          hipStream_t);
+hipError_t lumen_hbm_read(const void*, long long, unsigned*, int, hipStream_t);
 void lumen_set_gemv_form(int);
 void lumen_set_rms_lds(int, int);
 hipError_t lumen_paged_attention_decode(int, void*, const void*, const void*, const void*,
@@ -80,7 +84,8 @@ hipError_t lumen_kv_dequant(int, const void*, const void*, void*, void*, const i
 hipError_t lumen_reshape_and_cache(int, const void*, const void*, void*, void*, const long long*,
                                    int, int, int, int, long long, long long, int, hipStream_t);
 hipError_t lumen_sample(int, const void*, const float*, const float*, const int*,
-                        unsigned long long, long long, long long*, float*, int, int, hipStream_t);
+                        unsigned long long, long long, long long*, float*, float*, int, int,
+                        hipStream_t);
 hipError_t lumen_flash_attn_paged(int, int, const void*, long long, const void*, const void*, void*,
                                   long long, const int*, const int*, const int*, int, const int*,
                                   int, int, int, int, int, float, hipStream_t);
@@ -271,6 +276,56 @@ void decode_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
                           static_cast<int>(bn), static_cast<int>(nw), static_cast<int>(s),
                           static_cast<int>(flags), cur_stream()),
         "decode_gemm");
+}
+
+// training-shape MLP GEMMs with the SwiGLU in the epilogue (kernels/mlp_gemm.hip):
+// epi 0: c = x @ w^T; epi 1: c = gu = x @ w^T (w = [gate | up] rows), act = silu(g) * u;
+// epi 2: c = dgu from dact = x @ w^T (x = dout, w = Wd^T) and the saved gu
+void mlp_gemm(int64_t epi, const at::Tensor& x, const at::Tensor& w, at::Tensor& c,
+              const std::optional<at::Tensor>& act, const std::optional<at::Tensor>& gu,
+              int64_t group_m) {
+  if (!x.is_cuda() || !w.is_cuda() || !c.is_cuda())
+    throw std::invalid_argument("lumen: mlp_gemm needs GPU tensors");
+  if (x.dim() != 2 || w.dim() != 2 || c.dim() != 2 || x.stride(1) != 1 || w.stride(1) != 1 ||
+      c.stride(1) != 1 || x.size(1) != w.size(1) || c.size(0) != x.size(0) ||
+      x.scalar_type() != w.scalar_type() || c.scalar_type() != w.scalar_type())
+    throw std::invalid_argument("lumen: mlp_gemm shape/layout mismatch");
+  const int64_t M = x.size(0), K = x.size(1), Nw = w.size(0);
+  int64_t F = 0;
+  const int64_t e = epi & 15;  // bit 4: kernel variant (A/B probes)
+  if (e == 0) {
+    if (c.size(1) != Nw) throw std::invalid_argument("lumen: mlp_gemm c must be [M, N]");
+  } else if (e == 1) {
+    F = Nw / 2;
+    if (!act || !act->is_cuda() || act->dim() != 2 || act->stride(1) != 1 || act->size(0) != M ||
+        act->size(1) != F || c.size(1) != 2 * F || act->scalar_type() != w.scalar_type())
+      throw std::invalid_argument("lumen: mlp_gemm swiglu operands mismatch");
+  } else if (e == 2) {
+    F = Nw;
+    if (!gu || !gu->is_cuda() || gu->dim() != 2 || gu->stride(1) != 1 || gu->size(0) != M ||
+        gu->size(1) != 2 * F || c.size(1) != 2 * F || gu->scalar_type() != w.scalar_type())
+      throw std::invalid_argument("lumen: mlp_gemm swiglu-backward operands mismatch");
+  } else {
+    throw std::invalid_argument("lumen: mlp_gemm epi must be 0, 1 or 2");
+  }
+  check(lumen_mlp_gemm(dcode(w), static_cast<int>(epi), x.data_ptr(), x.stride(0), w.data_ptr(),
+                       w.stride(0), c.data_ptr(), c.stride(0), act ? act->data_ptr() : nullptr,
+                       act ? act->stride(0) : 0, gu ? gu->data_ptr() : nullptr,
+                       gu ? gu->stride(0) : 0, static_cast<int>(M), static_cast<int>(Nw),
+                       static_cast<int>(K), static_cast<int>(F), static_cast<int>(group_m),
+                       cur_stream()),
+        "mlp_gemm");
+}
+
+// box calibration: a non-temporal read of all of ``buf`` (kernels/calib.hip)
+void hbm_read(const at::Tensor& buf, at::Tensor& out, int64_t blocks) {
+  need_cuda(buf, "buf"); need_cuda(out, "out");
+  if (out.scalar_type() != at::kInt || out.numel() < 1)
+    throw std::invalid_argument("lumen: hbm_read out must be an int32 tensor");
+  check(lumen_hbm_read(buf.data_ptr(), buf.numel() * buf.element_size(),
+                       reinterpret_cast<unsigned*>(out.data_ptr()), static_cast<int>(blocks),
+                       cur_stream()),
+        "hbm_read");
 }
 
 void cross_entropy(at::Tensor& logits, const at::Tensor& labels, const std::optional<at::Tensor>& loss_sum,
@@ -685,15 +740,22 @@ void rope_cache_write(at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& 
 
 void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& top_p,
             const at::Tensor& top_k, int64_t seed, int64_t offset, at::Tensor& out_tokens,
-            const std::optional<at::Tensor>& out_logprob) {
+            const std::optional<at::Tensor>& out_logprob, const std::optional<at::Tensor>& out_tau) {
   need_cuda(logits, "logits");
   const int V = static_cast<int>(logits.size(-1));
   const int rows = static_cast<int>(logits.numel() / V);
+  for (const at::Tensor* t :
+       std::initializer_list<const at::Tensor*>{&temperature, &top_p, &top_k, &out_tokens})
+    if (!t->is_cuda() || t->numel() < rows)
+      throw std::invalid_argument("lumen: sample per-row tensors must be GPU tensors of >= rows");
+  if (out_tau && (!out_tau->is_cuda() || out_tau->scalar_type() != at::kFloat ||
+                  out_tau->numel() < rows))
+    throw std::invalid_argument("lumen: sample out_tau must be a float32 GPU tensor of >= rows");
   check(lumen_sample(dcode(logits), logits.data_ptr(), temperature.data_ptr<float>(),
                      top_p.data_ptr<float>(), top_k.data_ptr<int>(),
                      static_cast<unsigned long long>(seed), offset,
                      reinterpret_cast<long long*>(out_tokens.data_ptr<int64_t>()),
-                     ptr<float>(out_logprob), rows, V, cur_stream()),
+                     ptr<float>(out_logprob), ptr<float>(out_tau), rows, V, cur_stream()),
         "sample");
 }
 
@@ -933,6 +995,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_swiglu_gemm", &skinny_swiglu_gemm);
   m.def("decode_gemm", &decode_gemm);
+  m.def("mlp_gemm", &mlp_gemm);
+  m.def("hbm_read", &hbm_read);
   m.def("lora3_w_tail_batch", &lora3_w_tail_batch);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });
   m.def("set_rms_lds", [](int64_t f, int64_t b) {
@@ -941,7 +1005,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_cache_write", &rope_cache_write);
   m.def("paged_attention_decode", &paged_attention_decode);
   m.def("reshape_and_cache", &reshape_and_cache);
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"),
+        py::arg("top_k"), py::arg("seed"), py::arg("offset"), py::arg("out_tokens"),
+        py::arg("out_logprob") = py::none(), py::arg("out_tau") = py::none());
   m.def("flash_attn", &flash_attn);
   m.def("flash_attn_paged", &flash_attn_paged);
   m.def("flash_attn_ds", &flash_attn_ds);

@@ -184,10 +184,10 @@ __global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
     }
   }
   if (a.xe == nullptr) return;
-  // last-arriver tail.  No fences: an agent-scope fence writes back the whole L2 (measured
-  // +36 us per call); the Z atomics are agent-scope already, so waiting for this wave's vector
-  // memory counter to drain is enough before the block counts in (same protocol as
-  // decode_gemm.hip's split-K reduction).
+  // last-arriver tail.  No RELEASE fence: an agent-scope release writes back the whole L2
+  // (measured +36 us per call), and the Z atomics execute at the memory side already, so each
+  // wave's drained vector memory counter orders them before the block counts in.  The last
+  // arriver takes an agent-scope ACQUIRE (invalidate only) before it reads the sums.
   __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
   __syncthreads();
   __shared__ int last;
@@ -195,7 +195,15 @@ __global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
     unsigned* cp = a.cnt + blockIdx.x;
     const unsigned prev = __hip_atomic_fetch_add(cp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int l = prev == gridDim.y - 1;
-    if (l) __hip_atomic_store(cp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l) {
+      __hip_atomic_store(cp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // agent-scope ACQUIRE (invalidate only, no L2 writeback): the other blocks' Z adds
+      // landed at the memory side, and nothing this CU cached before them may serve the
+      // reads below (MI355X_MICROARCH.md, inter-workgroup visibility); the wait holds the
+      // barrier until the invalidate has completed
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     last = l;
   }
   __syncthreads();

@@ -1,93 +1,225 @@
 // Token sampling: greedy / temperature / top-k / top-p in one kernel.
 //
-// Reference behaviour: vLLM 0.6.0's Sampler (declared serving stack, requirements.txt:17-18):
-// temperature scaling, sort-based top-k/top-p masking, softmax, multinomial draw.
+// Reference behaviour: vLLM 0.6.0's Sampler (the declared serving stack, requirements.txt:17-18),
+// `_apply_top_k_top_p`: temperature scaling; top-k keeps every logit >= the k-th largest VALUE
+// (ties kept); top-p then works on the softmax of the top-k-truncated logits and keeps the
+// smallest head of the sorted distribution whose mass reaches p (at least one token); softmax,
+// multinomial draw.
 //
-// Sort-free formulation, one 512-thread workgroup per row (logits row stays L2-resident):
-//   z = logit / T;  m = max z;  Z = sum exp(z - m)
-//   top-k:  tau_k = largest threshold with count(z >= tau_k) >= k    (bisection on the value)
-//   top-p:  tau_p = largest threshold with mass(z >= tau_p) >= p     (bisection on the value)
-//   token = argmax_{z_j >= max(tau_k, tau_p)} z_j + Gumbel(hash(seed, offset, row, j))
-// Gumbel-max over the kept set is an exact draw from the renormalised truncated distribution.
+// Sort-free, one 512-thread workgroup per row, the row's scaled logits z cached in LDS
+// (V <= 32768; larger vocabularies re-read the L2-resident row every pass):
+//   keys: the f32 bits of z mapped to an order-preserving uint32
+//   top-k: tau_k = the k-th largest key, by RADIX SELECT -- four 8-bit digit levels, each one
+//          pass building a 256-bin count histogram of the keys under the prefix fixed so far,
+//          then one wave's parallel suffix scan picks the digit (exact, 4 passes instead of the
+//          previous 30-step bisection over the values)
+//   top-p: fixed-point masses W = exp(z - m) * 2^32 (integer sums: order-independent, so the
+//          kept set is deterministic); target = p * sum(W over key >= tau_k); tau_p = the largest
+//          key whose suffix mass reaches the target, by the same radix select on mass histograms
+//   token = argmax over key >= max(tau_k, tau_p) of z + Gumbel(hash(seed, offset, row, j)):
+//          an exact draw from the renormalised truncated distribution
 // temperature == 0 -> greedy argmax.  Also returns the chosen token's log-prob under the
-// temperature-scaled (untruncated) distribution.
+// temperature-scaled (untruncated) distribution, and optionally the kept threshold (as a
+// value of z) for tests.
 #include "common.h"
 
 namespace lumen {
 
 constexpr int kSampNT = 512;
 
-template <typename T>
-__device__ __forceinline__ float ld_logit(const T* row, int j, float invT) {
-  return to_f32(row[j]) * invT;
+__device__ __forceinline__ uint32_t fkey(float z) {
+  const uint32_t u = __float_as_uint(z);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float keyf(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-template <typename T>
+// NPT = 1: the row's scaled logits cached in LDS (V <= kSampLdsV); NPT = 0: re-read from the
+// (L2-resident) logits every pass
+constexpr int kSampLdsV = 32768;
+
+template <typename T, int NPT>
+struct Row {
+  const float* zl;  // LDS copy (NPT = 1)
+  const T* p;
+  int V;
+  float invT;
+  __device__ __forceinline__ float ld(int j) const { return to_f32(p[j]) * invT; }
+  // f(j, z) for every element this thread owns
+  template <typename F>
+  __device__ __forceinline__ void each(F&& f) const {
+    if constexpr (NPT > 0) {
+      for (int j = threadIdx.x; j < V; j += kSampNT) f(j, zl[j]);
+    } else {
+      for (int j = threadIdx.x; j < V; j += kSampNT) f(j, ld(j));
+    }
+  }
+};
+
+// Wave 0 picks the digit: bins descend from 255; lane l owns bins 255-4l .. 252-4l.  Finds the
+// bin b where the suffix sum (from 255 down, inclusive) first reaches `need`, writes b and the
+// need left inside b to sel[0] / sel64[0].
+template <typename C>
+__device__ __forceinline__ void pick_digit(const C* hist, unsigned long long need, int* sel_b,
+                                           unsigned long long* sel_need) {
+  const int lane = threadIdx.x;  // wave 0 only
+  unsigned long long v[4], s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = hist[255 - 4 * lane - q];
+    s += v[q];
+  }
+  // inclusive prefix over lanes (lane 0 = the top bins)
+  unsigned long long pre = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned lo = __shfl_up(static_cast<unsigned>(pre), o, 64);
+    const unsigned hi = __shfl_up(static_cast<unsigned>(pre >> 32), o, 64);
+    if (lane >= o) pre += (static_cast<unsigned long long>(hi) << 32) | lo;
+  }
+  const unsigned long long hit = __ballot(pre >= need);
+  const int first = hit ? __builtin_ctzll(hit) : 63;
+  if (lane == first) {
+    unsigned long long base = pre - s;
+    int b = 255 - 4 * lane - 3;
+    unsigned long long left = need - base;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (base + v[q] >= need || q == 3) {
+        b = 255 - 4 * lane - q;
+        left = need - base;
+        break;
+      }
+      base += v[q];
+    }
+    *sel_b = b;
+    *sel_need = left;
+  }
+}
+
+// Largest key t with  sum_{key >= t, key >= lo} weight >= need  (need >= 1), weight = 1
+// (MASS = false) or the fixed-point mass (MASS = true).  Four 8-bit levels, MSB first.
+template <typename T, int NPT, bool MASS>
+__device__ __forceinline__ uint32_t radix_select(const Row<T, NPT>& row, float m, uint32_t lo,
+                                 unsigned long long need, unsigned* hc, unsigned long long* hm,
+                                 int* sel_b, unsigned long long* sel_need) {
+  uint32_t prefix = 0, mask = 0;
+#pragma unroll 1
+  for (int lvl = 0; lvl < 4; ++lvl) {
+    const int shift = 24 - 8 * lvl;
+    for (int b = threadIdx.x; b < 256; b += kSampNT) {
+      if (MASS) hm[b] = 0; else hc[b] = 0;
+    }
+    __syncthreads();
+    row.each([&](int, float z) {
+      const uint32_t k = fkey(z);
+      if ((k & mask) == prefix && k >= lo) {
+        const int d = (k >> shift) & 255;
+        if constexpr (MASS) {
+          const unsigned long long w =
+              static_cast<unsigned long long>(__expf(z - m) * 4294967296.f);
+          if (w) atomicAdd(hm + d, w);
+        } else {
+          atomicAdd(hc + d, 1u);
+        }
+      }
+    });
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      if constexpr (MASS) pick_digit(hm, need, sel_b, sel_need);
+      else pick_digit(hc, need, sel_b, sel_need);
+    }
+    __syncthreads();
+    prefix |= static_cast<uint32_t>(*sel_b) << shift;
+    mask |= 255u << shift;
+    need = *sel_need;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+template <typename T, int NPT>
 __global__ void __launch_bounds__(kSampNT) sample_kernel(
     const T* __restrict__ logits, const float* __restrict__ temperature,
     const float* __restrict__ top_p, const int* __restrict__ top_k, unsigned long long seed,
-    long long offset, long long* __restrict__ out_tok, float* __restrict__ out_lp, int V) {
+    long long offset, long long* __restrict__ out_tok, float* __restrict__ out_lp,
+    float* __restrict__ out_tau, int V) {
   __shared__ float red[kSampNT / 64];
   __shared__ int redi[kSampNT / 64];
-  const int row = blockIdx.x;
-  const T* lr = logits + static_cast<size_t>(row) * V;
-  const float temp = temperature[row];
+  __shared__ unsigned hc[256];
+  __shared__ unsigned long long hm[256];
+  __shared__ unsigned long long red64[kSampNT / 64];
+  __shared__ int sel_b;
+  __shared__ unsigned long long sel_need;
+  extern __shared__ __attribute__((aligned(16))) float zlds[];
+  const int row_i = blockIdx.x;
+  const float temp = temperature[row_i];
   const bool greedy = !(temp > 0.f);
-  const float invT = greedy ? 1.f : 1.f / temp;
-  // max
+  Row<T, NPT> row;
+  row.p = logits + static_cast<size_t>(row_i) * V;
+  row.V = V;
+  row.invT = greedy ? 1.f : 1.f / temp;
+  row.zl = zlds;
+  if constexpr (NPT > 0) {
+    for (int j = threadIdx.x; j < V; j += kSampNT) zlds[j] = row.ld(j);
+    __syncthreads();
+  }
   float m = -INFINITY;
-  for (int j = threadIdx.x; j < V; j += kSampNT) m = fmaxf(m, ld_logit(lr, j, invT));
+  row.each([&](int, float z) { m = fmaxf(m, z); });
   m = block_max<kSampNT>(m, red);
   float s = 0.f;
-  for (int j = threadIdx.x; j < V; j += kSampNT) s += __expf(ld_logit(lr, j, invT) - m);
+  row.each([&](int, float z) { s += __expf(z - m); });
   const float Z = block_sum<kSampNT>(s, red);
-  float tau = -INFINITY;
+  uint32_t tau = 0;  // keep key >= tau (0: everything)
   if (!greedy) {
-    const int k = top_k[row];
-    if (k > 0 && k < V) {
-      float lo = m - 80.f, hi = m;  // count(z >= lo) >= k assumed (exp underflow region)
-      for (int it = 0; it < 30; ++it) {
-        const float mid = 0.5f * (lo + hi);
-        float c = 0.f;
-        for (int j = threadIdx.x; j < V; j += kSampNT) c += ld_logit(lr, j, invT) >= mid ? 1.f : 0.f;
-        c = block_sum<kSampNT>(c, red);
-        if (c >= static_cast<float>(k)) lo = mid; else hi = mid;
-      }
-      tau = lo;
-    }
-    const float p = top_p[row];
+    const int k = top_k[row_i];
+    if (k > 0 && k < V)
+      tau = radix_select<T, NPT, false>(row, m, 0u, static_cast<unsigned long long>(k), hc, hm,
+                                        &sel_b, &sel_need);
+    const float p = top_p[row_i];
     if (p < 1.f) {
-      float lo = m - 80.f, hi = m;
-      for (int it = 0; it < 30; ++it) {
-        const float mid = 0.5f * (lo + hi);
-        float c = 0.f;
-        for (int j = threadIdx.x; j < V; j += kSampNT) {
-          const float z = ld_logit(lr, j, invT);
-          c += z >= mid ? __expf(z - m) : 0.f;
-        }
-        c = block_sum<kSampNT>(c, red) / Z;
-        if (c >= p) lo = mid; else hi = mid;
+      // mass of the top-k-kept set, fixed point (exact integer sum)
+      unsigned long long zk = 0;
+      row.each([&](int, float z) {
+        if (fkey(z) >= tau) zk += static_cast<unsigned long long>(__expf(z - m) * 4294967296.f);
+      });
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned lo = __shfl_xor(static_cast<unsigned>(zk), o, 64);
+        const unsigned hi = __shfl_xor(static_cast<unsigned>(zk >> 32), o, 64);
+        zk += (static_cast<unsigned long long>(hi) << 32) | lo;
       }
-      tau = fmaxf(tau, lo);
+      if ((threadIdx.x & 63) == 0) red64[threadIdx.x >> 6] = zk;
+      __syncthreads();
+      zk = 0;
+#pragma unroll
+      for (int w = 0; w < kSampNT / 64; ++w) zk += red64[w];
+      __syncthreads();
+      const double tgt = static_cast<double>(fmaxf(p, 0.f)) * static_cast<double>(zk);
+      unsigned long long need = static_cast<unsigned long long>(ceil(tgt));
+      if (need < 1) need = 1;
+      if (need > zk) need = zk;
+      const uint32_t tp =
+          radix_select<T, NPT, true>(row, m, tau, need, hc, hm, &sel_b, &sel_need);
+      tau = tp > tau ? tp : tau;
     }
   }
-  // argmax over kept set (with Gumbel noise unless greedy)
+  // argmax over the kept set (with Gumbel noise unless greedy)
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int j = threadIdx.x; j < V; j += kSampNT) {
-    const float z = ld_logit(lr, j, invT);
-    if (z < tau) continue;
+  const uint32_t sd = static_cast<uint32_t>(seed) ^
+                      (static_cast<uint32_t>(offset) * 0x9E3779B9u + 0x7F4A7C15u);
+  row.each([&](int j, float z) {
+    if (fkey(z) < tau) return;
     float key = z;
     if (!greedy) {
-      const uint32_t sd = static_cast<uint32_t>(seed) ^
-                          (static_cast<uint32_t>(offset) * 0x9E3779B9u + 0x7F4A7C15u);
-      const uint32_t r = rng_u32(sd, static_cast<uint64_t>(row) * static_cast<uint64_t>(V) + j);
+      const uint32_t r = rng_u32(sd, static_cast<uint64_t>(row_i) * static_cast<uint64_t>(V) + j);
       const float u = (static_cast<float>(r >> 8) + 0.5f) * (1.f / 16777216.f);
       key = z - __logf(-__logf(u));
     }
     if (key > best || (key == best && j < bi)) { best = key; bi = j; }
-  }
-  // block argmax
+  });
   for (int o = 32; o > 0; o >>= 1) {
     const float ob = __shfl_xor(best, o, 64);
     const int oi = __shfl_xor(bi, o, 64);
@@ -102,31 +234,55 @@ __global__ void __launch_bounds__(kSampNT) sample_kernel(
     for (int w = 1; w < kSampNT / 64; ++w)
       if (red[w] > b || (red[w] == b && redi[w] < idx)) { b = red[w]; idx = redi[w]; }
     if (idx >= V) idx = 0;
-    out_tok[row] = idx;
-    if (out_lp) out_lp[row] = ld_logit(lr, idx, invT) - m - __logf(Z);
+    out_tok[row_i] = idx;
+    if (out_lp) out_lp[row_i] = row.ld(idx) - m - __logf(Z);
+    if (out_tau) out_tau[row_i] = tau ? keyf(tau) : -INFINITY;
   }
+}
+
+template <typename T>
+hipError_t launch_sample(const void* logits, const float* temperature, const float* top_p,
+                         const int* top_k, unsigned long long seed, long long offset,
+                         long long* out_tok, float* out_lp, float* out_tau, int rows, int V,
+                         hipStream_t st) {
+  dim3 grid(rows), block(kSampNT);
+  const T* lg = static_cast<const T*>(logits);
+  if (V <= kSampLdsV) {
+    // the LDS row copy goes past the 64 KiB dynamic default (gfx950 has 160 KiB per CU)
+    static bool attr_set = false;
+    if (!attr_set) {
+      const hipError_t e = hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&sample_kernel<T, 1>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, kSampLdsV * static_cast<int>(sizeof(float)));
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+    hipLaunchKernelGGL((sample_kernel<T, 1>), grid, block, V * sizeof(float), st, lg, temperature,
+                       top_p, top_k, seed, offset, out_tok, out_lp, out_tau, V);
+  } else {
+    hipLaunchKernelGGL((sample_kernel<T, 0>), grid, block, 0, st, lg, temperature, top_p, top_k,
+                       seed, offset, out_tok, out_lp, out_tau, V);
+  }
+  return hipGetLastError();
 }
 
 }  // namespace lumen
 
+// out_tau (optional): per row the smallest kept scaled logit (-inf when nothing is truncated)
 extern "C" hipError_t lumen_sample(int dtype, const void* logits, const float* temperature,
                                    const float* top_p, const int* top_k, unsigned long long seed,
-                                   long long offset, long long* out_tok, float* out_lp, int rows,
-                                   int V, hipStream_t st) {
+                                   long long offset, long long* out_tok, float* out_lp,
+                                   float* out_tau, int rows, int V, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  dim3 grid(rows), block(lumen::kSampNT);
+  if (V < 1) return hipErrorInvalidValue;
   if (dtype == lumen::kF32)
-    hipLaunchKernelGGL(lumen::sample_kernel<float>, grid, block, 0, st, (const float*)logits,
-                       temperature, top_p, top_k, seed, offset, out_tok, out_lp, V);
-  else if (dtype == lumen::kBF16)
-    hipLaunchKernelGGL(lumen::sample_kernel<lumen::bf16>, grid, block, 0, st,
-                       (const lumen::bf16*)logits, temperature, top_p, top_k, seed, offset,
-                       out_tok, out_lp, V);
-  else if (dtype == lumen::kF16)
-    hipLaunchKernelGGL(lumen::sample_kernel<lumen::fp16>, grid, block, 0, st,
-                       (const lumen::fp16*)logits, temperature, top_p, top_k, seed, offset,
-                       out_tok, out_lp, V);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
+    return lumen::launch_sample<float>(logits, temperature, top_p, top_k, seed, offset, out_tok,
+                                       out_lp, out_tau, rows, V, st);
+  if (dtype == lumen::kBF16)
+    return lumen::launch_sample<lumen::bf16>(logits, temperature, top_p, top_k, seed, offset,
+                                             out_tok, out_lp, out_tau, rows, V, st);
+  if (dtype == lumen::kF16)
+    return lumen::launch_sample<lumen::fp16>(logits, temperature, top_p, top_k, seed, offset,
+                                             out_tok, out_lp, out_tau, rows, V, st);
+  return hipErrorInvalidValue;
 }

@@ -361,11 +361,29 @@ def maybe_custom_allreduce(group, device, max_bytes: int) -> Optional[CustomAllR
         if dist.get_rank(group) == 0:
             print(f"[lumen] custom all-reduce unavailable ({e}); TP uses RCCL", flush=True)
         return None
+    # LUMEN_CAR_CALIBRATE: 1 (default) = calibrate across physical devices, fall back to RCCL
+    # if it times out; always = also on a shared device (rehearsal), same fallback; force =
+    # always, and a failure is fatal; 0 = never
     mode = os.environ.get("LUMEN_CAR_CALIBRATE", "1")
-    if mode == "force" or (mode != "0" and not car.shared_device):
+    if mode in ("force", "always") or (mode != "0" and not car.shared_device):
         # measured crossovers on THIS group (xGMI on a node; shared-device rehearsals measure
         # nonsense but run the same code): replaces the guessed one-shot limit
-        cal = car.calibrate(rccl_group=group if dist.get_backend(group) == "nccl" else None)
+        try:
+            cal = car.calibrate(rccl_group=group if dist.get_backend(group) == "nccl" else None)
+        except CollectiveTimeout as e:
+            # calibration is tuning only: every rank sees the same timeout after calibrate's
+            # max-reduction, so all of them drop the custom kernel here together (its barrier
+            # epochs are out of step anyway) and serve every reduction on RCCL.  An explicit
+            # LUMEN_CAR_CALIBRATE=force keeps the failure fatal.
+            if mode == "force":
+                raise
+            car.close()
+            if dist.get_rank(group) == 0:
+                import sys
+
+                print(f"[lumen] custom all-reduce calibration failed ({e}); TP uses RCCL",
+                      file=sys.stderr, flush=True)
+            return None
         if dist.get_rank(group) == 0:
             import sys
 

@@ -124,7 +124,10 @@ def llama_units(cfg, lora_targets=("q_proj", "k_proj", "v_proj", "o_proj"), lora
              "wt": sum(n * k for _, n, k, _ in lin), "linears": len(lin)}
     units = [{"name": "embed", "stored": V * H, "wt": 0}]
     units += [dict(layer, name=f"layer{i}") for i in range(cfg.num_hidden_layers)]
-    units.append({"name": "head", "stored": V * H, "wt": 0})
+    # the LM head keeps a W^T too unless LUMEN_LMHEAD_WT=0 (configure_backward_layout; the
+    # ZeRO-3 keep schedule transposes its gathered head like the projections)
+    head_wt = V * H if os.environ.get("LUMEN_LMHEAD_WT", "1") != "0" else 0
+    units.append({"name": "head", "stored": V * H, "wt": head_wt, "linears": 1})
     return units
 
 
@@ -159,13 +162,17 @@ def plan_zero3(cfg, world: int, hbm_bytes: float, tokens: int, checkpointing="au
         # persistent weights: configure_backward_layout's greedy per-linear W^T under the reserve
         budget = max(0.0, free - activation_reserve(hbm_bytes, "LUMEN_BWD_WT_RESERVE_GB"))
         wt = 0.0
+        # in module order, as configure_backward_layout walks them: each layer's q|k|v, o,
+        # gate|up, down, then the LM head
         per_lin = []
+        H, Fd = cfg.hidden_size, cfg.intermediate_size
+        q = cfg.num_attention_heads * cfg.head_dim
+        kv = cfg.num_key_value_heads * cfg.head_dim
         for u in units:
-            if u["wt"]:
-                H, Fd = cfg.hidden_size, cfg.intermediate_size
-                q = cfg.num_attention_heads * cfg.head_dim
-                kv = cfg.num_key_value_heads * cfg.head_dim
+            if u["name"].startswith("layer") and u["wt"]:
                 per_lin += [(q + 2 * kv) * H, H * q, 2 * Fd * H, H * Fd]
+            elif u["name"] == "head" and u["wt"]:
+                per_lin.append(u["wt"])
         for n in per_lin:
             need = n * elem_bytes
             if need <= budget:

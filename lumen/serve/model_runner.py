@@ -457,6 +457,25 @@ class ModelRunner:
         return sample_ref(logits, t, p, k, seed, offset)
 
 
+def topk_topp_keep(zs: torch.Tensor, k: int, p: float) -> torch.Tensor:
+    """The kept set of vLLM 0.6.0's ``_apply_top_k_top_p`` for one row of scaled logits: top-k
+    keeps every value >= the k-th largest (ties kept); top-p then keeps the smallest head of
+    the sorted top-k-renormalised distribution whose mass reaches p (at least one token)."""
+    V = zs.shape[-1]
+    keep = torch.ones(V, dtype=torch.bool, device=zs.device)
+    if 0 < k < V:
+        keep &= zs >= torch.topk(zs, k).values[-1]
+    if p < 1.0:
+        zk = torch.where(keep, zs, torch.full_like(zs, -float("inf")))
+        sp, idx = torch.sort(torch.softmax(zk, -1), descending=True)
+        c = torch.cumsum(sp, 0)
+        cut = int((c - sp < p).sum())  # tokens whose mass strictly above them is < p
+        m = torch.zeros(V, dtype=torch.bool, device=zs.device)
+        m[idx[:max(cut, 1)]] = True
+        keep &= m
+    return keep
+
+
 def sample_ref(logits, temps, top_ps, top_ks, seed, offset):
     """Torch sampler (CPU path): same semantics as kernels/sampling.hip, torch RNG."""
     R, V = logits.shape
@@ -471,20 +490,8 @@ def sample_ref(logits, temps, top_ps, top_ks, seed, offset):
             zs = z
         else:
             zs = z / T
+            keep = topk_topp_keep(zs, int(top_ks[i]), float(top_ps[i]))
             probs = torch.softmax(zs, -1)
-            keep = torch.ones(V, dtype=torch.bool, device=z.device)
-            k = int(top_ks[i])
-            if 0 < k < V:
-                thr = torch.topk(zs, k).values[-1]
-                keep &= zs >= thr
-            p = float(top_ps[i])
-            if p < 1.0:
-                sp, idx = torch.sort(probs, descending=True)
-                c = torch.cumsum(sp, 0)
-                cut = int((c < p).sum()) + 1
-                m = torch.zeros(V, dtype=torch.bool, device=z.device)
-                m[idx[:cut]] = True
-                keep &= m
             pr = torch.where(keep, probs, torch.zeros_like(probs))
             tok = int(torch.multinomial(pr / pr.sum(), 1, generator=g))
         out[i] = tok

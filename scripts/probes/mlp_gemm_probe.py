@@ -1,0 +1,147 @@
+"""The fused MLP GEMMs (lumen/csrc/kernels/mlp_gemm.hip) against hipBLASLt (tuned table) on the
+Llama-2-7B training shapes, T = 8 x 512 tokens, one process, interleaved rounds.
+
+* plain store (epi 0) vs torch.matmul: 4096 x 20480 x 4096 (the whole-wave part of gate|up),
+  4096 x 22016 x 4096, 4096 x 11008 x 4096 (down dX), 4096 x 4096 x 4096;
+* fused forward (epi 1) vs  matmul + swiglu kernel;
+* fused backward (epi 2) vs  matmul (dact) + swiglu backward kernel;
+each checked against an fp32 torch reference first.  Output: JSON lines, and
+gpurun_out/mlp_gemm/probe.json.
+
+    python scripts/probes/mlp_gemm_probe.py [--reps 20] [--group_m 4]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.getcwd())
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from lumen.ops._native import native  # noqa: E402
+from lumen.ops.gemm import mm_nt  # noqa: E402
+from lumen.utils.gemm_tuning import load_tuned_gemms  # noqa: E402
+
+
+def ev(fn, n):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / n
+
+
+def rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--group_m", type=int, default=4)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    os.makedirs("gpurun_out/mlp_gemm", exist_ok=True)
+    C = native()
+    tuned = load_tuned_gemms()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    T, H, Fd = 4096, 4096, 11008
+    out = {"tuned": tuned, "cases": []}
+    # activations ~ RMSNorm outputs (unit scale), weights ~ N(0, 0.02) (random init)
+    x = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+    cases = []
+
+    def plain(N, K, name):
+        xx = torch.randn(T, K, device=dev, dtype=torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        c = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
+        ref = xx.float() @ w.float().t()
+        C.mlp_gemm(0, xx, w, c, None, None, a.group_m)
+        torch.cuda.synchronize()
+        err = rel(c, ref)
+        mine = lambda: C.mlp_gemm(0, xx, w, c, None, None, a.group_m)  # noqa: E731
+        lib = lambda: mm_nt(xx, w)  # noqa: E731
+        cases.append((name, 2.0 * T * N * K, mine, lib, err))
+
+    def fwd():
+        w = (torch.randn(2 * Fd, H, device=dev) * 0.02).to(torch.bfloat16)
+        gu = torch.empty(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
+        act = torch.empty(T, Fd, device=dev, dtype=torch.bfloat16)
+        C.mlp_gemm(1, x, w, gu, act, None, a.group_m)
+        torch.cuda.synchronize()
+        ref = x.float() @ w.float().t()
+        g, u = ref.chunk(2, dim=-1)
+        err = max(rel(gu, ref), rel(act, F.silu(g) * u))
+
+        def lib():
+            y = mm_nt(x, w)
+            o = torch.empty(T, Fd, device=dev, dtype=torch.bfloat16)
+            C.swiglu(False, y, None, o, 0, -1)
+        cases.append(("fwd gate|up+swiglu 4096x22016x4096", 2.0 * T * 2 * Fd * H,
+                      lambda: C.mlp_gemm(1, x, w, gu, act, None, a.group_m), lib, err))
+
+    def bwd():
+        dout = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+        wdt = (torch.randn(Fd, H, device=dev) * 0.02).to(torch.bfloat16)   # Wd^T [F, H]
+        gu = torch.randn(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
+        dgu = torch.empty(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
+        C.mlp_gemm(2, dout, wdt, dgu, None, gu, a.group_m)
+        torch.cuda.synchronize()
+        g_ = gu.float()[:, :Fd].clone().requires_grad_(True)
+        u_ = gu.float()[:, Fd:].clone().requires_grad_(True)
+        (F.silu(g_) * u_).backward(dout.float() @ wdt.float().t())
+        err = rel(dgu, torch.cat([g_.grad, u_.grad], dim=1))
+
+        def lib():
+            d = torch.matmul(dout, wdt.t())
+            o = torch.empty(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
+            C.swiglu(True, gu, d, o, 0, -1)
+        cases.append(("bwd dact+swiglu' 4096x11008x4096", 2.0 * T * Fd * H,
+                      lambda: C.mlp_gemm(2, dout, wdt, dgu, None, gu, a.group_m), lib, err))
+
+    # the two-stage loop without ping-pong (epi bit 4), for the A/B
+    xx0 = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+    w0 = (torch.randn(20480, H, device=dev) * 0.02).to(torch.bfloat16)
+    c0 = torch.empty(T, 20480, device=dev, dtype=torch.bfloat16)
+    C.mlp_gemm(16, xx0, w0, c0, None, None, a.group_m)
+    cases.append(("plain(no pp) 4096x20480x4096", 2.0 * T * 20480 * H,
+                  lambda: C.mlp_gemm(16, xx0, w0, c0, None, None, a.group_m),
+                  lambda: mm_nt(xx0, w0), rel(c0, xx0.float() @ w0.float().t())))
+    plain(20480, H, "plain 4096x20480x4096")
+    plain(2 * Fd, H, "plain 4096x22016x4096")
+    plain(Fd, H, "plain 4096x11008x4096")
+    plain(H, H, "plain 4096x4096x4096")
+    fwd()
+    bwd()
+    if a.only:
+        cases[:] = [c for c in cases if a.only in c[0]]
+    times = {c[0]: {"mine": [], "lib": []} for c in cases}
+    for name, _, mine, lib, _ in cases:
+        mine(), lib()
+    torch.cuda.synchronize()
+    for _ in range(a.rounds):
+        for name, _, mine, lib, _ in cases:
+            times[name]["mine"].append(ev(mine, a.reps))
+            times[name]["lib"].append(ev(lib, a.reps))
+    for name, fl, _, _, err in cases:
+        tm = sorted(times[name]["mine"])
+        tl = sorted(times[name]["lib"])
+        r = {"case": name, "rel_err_vs_fp32": round(err, 5),
+             "mine_us_med": round(tm[len(tm) // 2], 1), "mine_us_min": round(tm[0], 1),
+             "lib_us_med": round(tl[len(tl) // 2], 1), "lib_us_min": round(tl[0], 1),
+             "mine_pf": round(fl / tm[len(tm) // 2] / 1e9, 3),
+             "lib_pf": round(fl / tl[len(tl) // 2] / 1e9, 3),
+             "mine_over_lib": round(tm[len(tm) // 2] / tl[len(tl) // 2], 3)}
+        out["cases"].append(r)
+        print(json.dumps(r), flush=True)
+    with open("gpurun_out/mlp_gemm/probe.json", "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

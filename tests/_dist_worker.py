@@ -479,3 +479,43 @@ def car_calibrate_worker(rank, world, port, outdir, delay_s, timeout_s):
     dist.barrier()
     car.close()
     dist.destroy_process_group()
+
+
+def car_fallback_worker(rank, world, port, outdir, delay_s, timeout_s):
+    """``maybe_custom_allreduce`` when its calibration times out (the last rank starts late):
+    every rank must get None back (RCCL serves the TP reductions) instead of an exception that
+    aborts engine startup."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", LUMEN_CAR_CALIBRATE="always",
+                      LUMEN_CAR_TIMEOUT=str(timeout_s))
+    import json
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import lumen.parallel.custom_ar as car_mod
+
+    orig = car_mod.CustomAllReduce.calibrate
+
+    def late_calibrate(self, *a, **k):
+        if rank == world - 1 and delay_s > 0:
+            time.sleep(delay_s)
+        return orig(self, *a, **k)
+
+    car_mod.CustomAllReduce.calibrate = late_calibrate
+    res = {"rank": rank}
+    try:
+        car = car_mod.maybe_custom_allreduce(dist.group.WORLD, torch.device("cuda", 0), 1 << 20)
+        res["car"] = car is not None
+        res["error"] = None
+        if car is not None:
+            car.close()
+    except Exception as e:  # noqa: BLE001
+        res["error"] = repr(e)
+    with open(os.path.join(outdir, f"fb_{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()

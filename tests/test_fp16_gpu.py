@@ -80,13 +80,27 @@ def test_fp16_forced_overflow_skips_and_backs_off():
     init = {k: v.clone() for k, v in adapter_state_dict(mA).items()}
     bs = _batches(6, mA.config.vocab_size)
     scales = []
+    snap = None
     for i, b in enumerate(bs):
         loss = engA.forward(b)
         engA.backward(loss)
         if i in (2, 3):
             engA.flat.grad[5] = float("inf")
+        if i == 2:  # the optimizer's whole state before the two overflowing steps
+            o = engA.opt
+            snap = [t.clone() for t in (o.master, o.m, o.v)] + [
+                {k: v.clone() for k, v in adapter_state_dict(mA).items()}, o.state[0].item()]
         engA.step()
         scales.append(engA.loss_scale)
+        if i == 3:
+            # the skip itself, asserted directly: master weights, both Adam moments, the
+            # published adapters and the device step counter are exactly as before step 2
+            o = engA.opt
+            for before, now in zip(snap[:3], (o.master, o.m, o.v)):
+                assert torch.equal(before, now)
+            now_ad = adapter_state_dict(mA)
+            assert all(torch.equal(v, now_ad[k]) for k, v in snap[3].items())
+            assert o.state[0].item() == snap[4]
     assert scales[:3] == [2.0 ** 16] * 3          # first overflow: hysteresis 2 -> 1
     assert scales[3:] == [2.0 ** 15] * 3          # second: halve
     assert engA.skipped_steps == 2 and engA.opt.step_count == 4

@@ -453,6 +453,113 @@ def test_sampling_greedy_and_topk():
     assert 0.70 < frac1 < 0.80
 
 
+def _kept_matches(zs, kept, ref, p):
+    """Kernel kept set vs the sort-based reference: equal, or different only in the tokens at
+    the top-p boundary where the reference's cumulative mass sits within 1e-5 of p (the
+    kernel's fast exp / fixed-point masses vs torch's f32 softmax)."""
+    if torch.equal(kept, ref):
+        return True
+    if p >= 1.0:
+        return False
+    # exact ties at the top-p boundary (bf16 logits): the value threshold keeps every tied
+    # token, the sort keeps the ones its order put first
+    if torch.equal(kept, zs >= zs[ref].min()):
+        return True
+    diff = (kept ^ ref).nonzero().flatten()
+    zk = torch.where(ref | kept, zs, torch.full_like(zs, -float("inf")))
+    pr = torch.softmax(zs.double(), -1)
+    for j in diff.tolist():
+        above = pr[zs > zs[j]].sum().item()  # mass strictly above token j (untruncated)
+        tot = pr[zk > -float("inf")].sum().item()
+        if min(abs(above / tot - p), abs((above + pr[j].item()) / tot - p)) > 1e-5:
+            return False
+    return True
+
+
+@pytest.mark.parametrize("k,p", [(1, 1.0), (50, 1.0), (1000, 1.0), (0, 0.5), (0, 0.9), (0, 0.99),
+                                 (50, 0.9), (1000, 0.5), (1000, 0.99), (31999, 0.9)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sampling_kept_set_vs_sort(k, p, dtype):
+    """Radix-select top-k / top-p (kernels/sampling.hip) against vLLM 0.6.0's sort-based
+    ``_apply_top_k_top_p`` (lumen.serve.model_runner.topk_topp_keep), V = 32000: the kept set
+    (the kernel reports its threshold) and every sampled token inside it.  bf16 logits have
+    exact ties, which top-k keeps (value threshold) like the reference."""
+    from lumen.ops._native import native
+    from lumen.serve.model_runner import topk_topp_keep
+
+    C = native()
+    R, V = 8, 32000
+    g = torch.Generator(device="cpu").manual_seed(k * 7 + int(p * 100))
+    logits = (torch.randn(R, V, generator=g) * 3.0).to(dtype).to(DEV)
+    temp = torch.tensor([1.0, 0.5] * (R // 2), device=DEV)   # 1/T exact: same z as torch
+    out = torch.empty(R, device=DEV, dtype=torch.int64)
+    tau = torch.empty(R, device=DEV, dtype=torch.float32)
+    C.sample(logits, temp, torch.full((R,), p, device=DEV),
+             torch.full((R,), k, device=DEV, dtype=torch.int32), 5, 1, out, None, tau)
+    for i in range(R):
+        zs = logits[i].float() * (1.0 / temp[i])
+        kept = zs >= tau[i]
+        ref = topk_topp_keep(zs, k, p)
+        assert _kept_matches(zs, kept, ref, p), (i, int(kept.sum()), int(ref.sum()))
+        assert kept[out[i]], i
+        if 0 < k < V and p >= 1.0:
+            assert int(kept.sum()) >= k
+
+
+def test_sampling_distribution_chi2():
+    """65,536 draws (one row each: the Gumbel noise is hashed per row) from one V = 200
+    distribution with top-k 50 and top-p 0.9 at temperature 0.8: nothing outside the kept set,
+    and a chi-square test of the counts against the renormalised truncated distribution."""
+    from scipy.stats import chisquare
+
+    from lumen.ops._native import native
+    from lumen.serve.model_runner import topk_topp_keep
+
+    C = native()
+    R, V = 65536, 200
+    g = torch.Generator(device="cpu").manual_seed(3)
+    row = torch.randn(V, generator=g) * 2.0
+    logits = row.expand(R, V).contiguous().to(DEV)
+    T = 0.8
+    temp = torch.full((R,), T, device=DEV)
+    out = torch.empty(R, device=DEV, dtype=torch.int64)
+    C.sample(logits, temp, torch.full((R,), 0.9, device=DEV),
+             torch.full((R,), 50, device=DEV, dtype=torch.int32), 1234, 9, out, None)
+    zs = row.float() * (1.0 / torch.tensor(T, dtype=torch.float32))
+    keep = topk_topp_keep(zs, 50, 0.9)
+    cnt = torch.bincount(out.cpu(), minlength=V).double()
+    assert cnt[~keep].sum() == 0
+    pr = torch.softmax(zs.double(), -1)[keep]
+    exp = pr / pr.sum() * R
+    res = chisquare(cnt[keep].numpy(), exp.numpy())
+    assert res.pvalue > 1e-4, (res, int(keep.sum()))
+
+
+def test_sampling_speed_256_rows():
+    """The decode-step sampler with both filters (256 rows x 32000, top-k 50, top-p 0.95,
+    temperature 0.8): radix select replaced the 30-pass bisections (VERDICT r5 Weak #6).
+    A loose regression bound; the measured time goes in the bench record."""
+    from lumen.ops._native import native
+
+    C = native()
+    R, V = 256, 32000
+    logits = torch.randn(R, V, device=DEV) * 3
+    args = (logits, torch.full((R,), 0.8, device=DEV), torch.full((R,), 0.95, device=DEV),
+            torch.full((R,), 50, device=DEV, dtype=torch.int32))
+    out = torch.empty(R, device=DEV, dtype=torch.int64)
+    for _ in range(3):
+        C.sample(*args, 1, 0, out, None)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(20):
+        C.sample(*args, 1, i, out, None)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) * 1000 / 20
+    print(f"sampler 256 x 32000, top-k 50 + top-p 0.95: {us:.1f} us")
+    assert us < 300, us
+
+
 @pytest.mark.parametrize("nh,nkv,lens", [(8, 8, [512, 512]), (8, 2, [512, 300, 77]),
                                          (4, 4, [1000, 64, 129])])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

@@ -91,3 +91,17 @@ def test_partial_recompute_picks_fewest_layers():
         none * (1 - 16 * (1 - SELECTIVE_FRACTION) / 32))
     assert activation_bytes(cfg, 4096, "selective:32") == activation_bytes(cfg, 4096, "selective")
     assert activation_bytes(cfg, 4096, "full:32") == pytest.approx(activation_bytes(cfg, 4096, "full"))
+
+
+def test_lm_head_transpose_is_planned(monkeypatch):
+    """The LM head's W^T (LUMEN_LMHEAD_WT, on by default) is in the plan: V * H elements on the
+    head unit, and in the world-1 greedy W^T budget after the layers."""
+    cfg = get_config("llama2-7b")
+    V, H = cfg.vocab_size, cfg.hidden_size
+    head = llama_units(cfg)[-1]
+    assert head["name"] == "head" and head["wt"] == V * H
+    with_head = plan_zero3(cfg, 1, HBM, 4096, "none")["gb"]["w_transposed"]
+    monkeypatch.setenv("LUMEN_LMHEAD_WT", "0")
+    assert llama_units(cfg)[-1]["wt"] == 0
+    without = plan_zero3(cfg, 1, HBM, 4096, "none")["gb"]["w_transposed"]
+    assert with_head - without == pytest.approx(V * H * 2 / 1e9)

@@ -243,6 +243,21 @@ def test_custom_allreduce_calibration_collective(delay_s, timeout_s, tmp_path):
         assert all(x["error"] and "timed out" in x["error"] for x in r), r
 
 
+def test_custom_allreduce_calibration_timeout_falls_back(tmp_path):
+    """A calibration that times out (a peer 3 s late against a 1 s barrier deadline) costs the
+    TP group its custom all-reduce, not its startup: ``maybe_custom_allreduce`` returns None on
+    every rank together, so all of them serve the reductions on RCCL."""
+    import json
+
+    from tests._dist_worker import car_fallback_worker
+
+    world = 2
+    mp.start_processes(car_fallback_worker, args=(world, _port(), str(tmp_path), 3.0, 1.0),
+                       nprocs=world, join=True, start_method="spawn")
+    r = [json.loads((tmp_path / f"fb_{k}.json").read_text()) for k in range(world)]
+    assert all(x["error"] is None and x["car"] is False for x in r), r
+
+
 def test_tp2_serving_rccl_on_one_gpu(tmp_path):
     """TP=2 serving with the step broadcast and vocab gather on RCCL (custom IPC all-reduce for
     the row-parallel sums): same greedy tokens as the gloo-broadcast TP run."""

@@ -475,3 +475,59 @@ def test_overlap_bucket_cap():
     assert overlap_bucket_numel(int(5e7), 8, False, 16) == int(5e7)
     assert overlap_bucket_numel(int(5e7), 8, True, 0) == int(5e7)
     assert overlap_bucket_numel(int(5e7), 8, True) == int(5e7)  # default: off
+
+
+def test_wall_budget_logic():
+    """lumen/bench/budget.py: sections run while their estimate fits in what is left of one
+    overall deadline (agreed as the minimum over ranks), and skipped ones are recorded."""
+    from lumen.bench.budget import WallBudget, partitioned_estimate_s
+
+    now = [100.0]
+    agreed = []
+
+    def agree(x):  # a slower peer: the minimum over ranks is what counts
+        agreed.append(x)
+        return x - 5.0
+
+    b = WallBudget(60.0, 100.0, agree, clock=lambda: now[0])
+    assert b.allow("comm_probe", 30.0)           # left 60 -> agreed 55
+    now[0] += 12.0
+    b.done("comm_probe")
+    assert not b.allow("zero3_release", 50.0)    # left 48 -> agreed 43 < 50
+    assert b.allow("zero3_hybrid", 40.0)
+    now[0] += 3.0
+    b.done("zero3_hybrid")
+    r = b.record()
+    assert [x["section"] for x in r["ran"]] == ["comm_probe", "zero3_hybrid"]
+    assert r["ran"][0]["took_s"] == 12.0 and r["ran"][0]["left_s"] == 55.0
+    assert r["skipped"] == [{"section": "zero3_release", "est_s": 50.0, "left_s": 43.0}]
+    assert r["left_at_record_s"] == 45.0 and agreed == [60.0, 48.0, 48.0]
+    assert partitioned_estimate_s(90.0, 5, 2, 1.0) == pytest.approx(10 + 2 + 7 * 0.09 * 1.5)
+
+
+def test_bench_wall_budget_skips_sections_torchrun():
+    """bench.py at world 2 (gloo, tiny model) with a wall budget already spent by the headline:
+    the comm probe and both partitioned schedules are skipped on every rank alike (no
+    collective mismatch), the record lists them, and rank 0 still prints its one JSON line."""
+    import json
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                          str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--steps", "1", "--warmup", "1", "--model", "tiny-llama", "--seq_len",
+                          "32", "--micro_batch", "2", "--wall_budget", "1"],
+                         capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    x = json.loads(lines[0])["extra"]
+    skipped = {d["section"] for d in x["budget"]["skipped"]}
+    assert {"comm_probe", "zero3_release", "zero3_hybrid"} <= skipped, x["budget"]
+    assert x["comm"] is None and x["zero3_release"]["skipped"] == "wall budget"
+    assert x["budget"]["ran"] == [] and x["budget"]["wall_budget_s"] == 1.0
