@@ -70,8 +70,9 @@ hipError_t lumen_skinny_gemm(int, const void*, const void*, void*, int, int, int
 hipError_t lumen_decode_gemm(int, const void*, const void*, void*, float*, int*, int, int, int,
                              long long, long long, int, int, int, int, int, hipStream_t);
 hipError_t lumen_mlp_gemm(int, int, const void*, long long, const void*, long long, void*, long long,
-                          void*, long long, const void*, long long, int, int, int, int, int,
-                          hipStream_t);
+                          void*, long long, const void*, long long, int, int, int, int, int, float*,
+                          int*, int, hipStream_t);
+int lumen_mlp_gemm_split(int, int, int, int, int);
 hipError_t lumen_hbm_read(const void*, long long, unsigned*, int, hipStream_t);
 void lumen_set_gemv_form(int);
 void lumen_set_rms_lds(int, int);
@@ -281,9 +282,16 @@ void decode_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
 // training-shape MLP GEMMs with the SwiGLU in the epilogue (kernels/mlp_gemm.hip):
 // epi 0: c = x @ w^T; epi 1: c = gu = x @ w^T (w = [gate | up] rows), act = silu(g) * u;
 // epi 2: c = dgu from dact = x @ w^T (x = dout, w = Wd^T) and the saved gu
+// tiles of the last wave that would run split in two k halves (0: none)
+int64_t mlp_gemm_split(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t cus) {
+  return lumen_mlp_gemm_split(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
+                              static_cast<int>(epi), static_cast<int>(cus));
+}
+
 void mlp_gemm(int64_t epi, const at::Tensor& x, const at::Tensor& w, at::Tensor& c,
               const std::optional<at::Tensor>& act, const std::optional<at::Tensor>& gu,
-              int64_t group_m) {
+              int64_t group_m, const std::optional<at::Tensor>& ws,
+              const std::optional<at::Tensor>& cnt, int64_t split) {
   if (!x.is_cuda() || !w.is_cuda() || !c.is_cuda())
     throw std::invalid_argument("lumen: mlp_gemm needs GPU tensors");
   if (x.dim() != 2 || w.dim() != 2 || c.dim() != 2 || x.stride(1) != 1 || w.stride(1) != 1 ||
@@ -308,11 +316,17 @@ void mlp_gemm(int64_t epi, const at::Tensor& x, const at::Tensor& w, at::Tensor&
   } else {
     throw std::invalid_argument("lumen: mlp_gemm epi must be 0, 1 or 2");
   }
+  if (split > 0 && (!ws || !cnt || !ws->is_cuda() || !cnt->is_cuda() ||
+                    ws->scalar_type() != at::kFloat || cnt->scalar_type() != at::kInt ||
+                    ws->numel() < split * 2 * 65536 || cnt->numel() < split))
+    throw std::invalid_argument("lumen: mlp_gemm split workspace too small");
   check(lumen_mlp_gemm(dcode(w), static_cast<int>(epi), x.data_ptr(), x.stride(0), w.data_ptr(),
                        w.stride(0), c.data_ptr(), c.stride(0), act ? act->data_ptr() : nullptr,
                        act ? act->stride(0) : 0, gu ? gu->data_ptr() : nullptr,
                        gu ? gu->stride(0) : 0, static_cast<int>(M), static_cast<int>(Nw),
                        static_cast<int>(K), static_cast<int>(F), static_cast<int>(group_m),
+                       split > 0 ? ws->data_ptr<float>() : nullptr,
+                       split > 0 ? cnt->data_ptr<int>() : nullptr, static_cast<int>(split),
                        cur_stream()),
         "mlp_gemm");
 }
@@ -995,7 +1009,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_swiglu_gemm", &skinny_swiglu_gemm);
   m.def("decode_gemm", &decode_gemm);
-  m.def("mlp_gemm", &mlp_gemm);
+  m.def("mlp_gemm", &mlp_gemm, py::arg("epi"), py::arg("x"), py::arg("w"), py::arg("c"),
+        py::arg("act") = py::none(), py::arg("gu") = py::none(), py::arg("group_m") = 4,
+        py::arg("ws") = py::none(), py::arg("cnt") = py::none(), py::arg("split") = 0);
+  m.def("mlp_gemm_split", &mlp_gemm_split);
   m.def("hbm_read", &hbm_read);
   m.def("lora3_w_tail_batch", &lora3_w_tail_batch);
   m.def("set_gemv_form", [](int64_t f) { lumen_set_gemv_form(static_cast<int>(f)); });

@@ -67,7 +67,20 @@ struct Args {
   long long ldx, ldw, ldc, ldact, ldgu;
   int M, N, K, F;  // N: GEMM output columns (EPI 1: 2F)
   int tiles_m, tiles_n, group_m;
+  // last-wave split: tiles [full, full + split) run as two k halves each (blocks full + 2u,
+  // full + 2u + 1), f32 partial slabs in ws, the last-arriving half (ticket in cnt[u]) sums
+  // both and runs the epilogue
+  int full, split;
+  float* ws;
+  int* cnt;
 };
+
+// W image row r -> output column within its 32-row group: image row 16 i' + 4 g + e (fragment
+// i' of a pair, lane group g, accumulator e) holds column 8 g + 4 i' + e, so a lane's
+// accumulators of the two fragments of a pair are 8 CONSECUTIVE columns: 16-byte stores
+__device__ __forceinline__ int colperm(int r) {
+  return (r & ~31) | (((r >> 2) & 3) << 3) | (((r >> 4) & 1) << 2) | (r & 3);
+}
 
 // 16-byte chunk c of image row r lives at chunk c ^ swz(r) (see decode_gemm.hip: a ds_read_b128
 // fragment read -- 16 rows at one chunk -- touches 16 distinct bank slots)
@@ -112,9 +125,9 @@ __device__ __forceinline__ void stage(char* img, const Args& a, const T* xb, int
         // wave slot wn = r / 64: rows 0..31 gate, 32..63 up, of activation columns
         // 128 tn + 32 wn + (r % 32)
         const int w = r & 63;
-        wrow = (w < 32 ? 0 : a.F) + tn * 128 + (r >> 6) * 32 + (w & 31);
+        wrow = (w < 32 ? 0 : a.F) + tn * 128 + (r >> 6) * 32 + colperm(w & 31);
       } else {
-        wrow = tn * BN + r;
+        wrow = tn * BN + colperm(r);
       }
       const unsigned off =
           (unsigned)(((long long)wrow * a.ldw + k0 + 8 * ch) * (long long)sizeof(T));
@@ -126,6 +139,45 @@ __device__ __forceinline__ void stage(char* img, const Args& a, const T* xb, int
       const unsigned off = (unsigned)(((long long)m * a.ldx + k0 + 8 * ch) * (long long)sizeof(T));
       dma16(xb, off, img + p * 8 * ROWB);
     }
+  }
+}
+
+// The W image rows of wave slot wn (rows 64 wn .. 64 wn + 63 = pieces 8 wn .. 8 wn + 7), issued by
+// one wave (ping-pong loop)
+template <typename T, int EPI>
+__device__ __forceinline__ void stage_w(char* img, const Args& a, int tn, int k0, int wn,
+                                        int lane) {
+  const int rr = lane >> 3, c = lane & 7;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = 8 * wn + q;
+    const int r = 8 * p + rr;
+    const int ch = c ^ swz(r);
+    int wrow;
+    if constexpr (EPI == kSwiGLU) {
+      const int w = r & 63;
+      wrow = (w < 32 ? 0 : a.F) + tn * 128 + (r >> 6) * 32 + colperm(w & 31);
+    } else {
+      wrow = tn * BN + colperm(r);
+    }
+    const unsigned off = (unsigned)(((long long)wrow * a.ldw + k0 + 8 * ch) * (long long)sizeof(T));
+    dma16(a.w, off, img + p * 8 * ROWB);
+  }
+}
+
+// The whole x image (32 pieces), issued by the 4 waves of one group: wave wl issues wl + 4q
+template <typename T>
+__device__ __forceinline__ void stage_x(char* img, const Args& a, const T* xb, int mvalid, int k0,
+                                        int wl, int lane) {
+  const int rr = lane >> 3, c = lane & 7;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = wl + 4 * q;
+    const int r = 8 * p + rr;
+    const int ch = c ^ swz(r);
+    const int m = min(r, mvalid - 1);
+    const unsigned off = (unsigned)(((long long)m * a.ldx + k0 + 8 * ch) * (long long)sizeof(T));
+    dma16(xb, off, img + IMG + p * 8 * ROWB);
   }
 }
 
@@ -156,13 +208,6 @@ __device__ __forceinline__ void compute(const char* img, int nrow0, int mrow0,
 
 __device__ __forceinline__ float bf_round(float v, bf16*) { return __bfloat162float(__float2bfloat16(v)); }
 __device__ __forceinline__ float bf_round(float v, fp16*) { return __half2float(__float2half(v)); }
-
-template <typename T>
-__device__ __forceinline__ void unpack4(uint2 v, float (&o)[4]) {
-  const T* e = reinterpret_cast<const T*>(&v);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) o[k] = to_f32(e[k]);
-}
 
 // Fragments of one k-step (both 32-deep halves) for one wave: W rows nrow0 + [0, 64), x rows
 // mrow0 + [0, 128)
@@ -201,6 +246,19 @@ __device__ __forceinline__ void mfma_step(const uint4 (&fa)[2][NI], const uint4 
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// keeps fragment registers alive in a probe build without MFMAs (no DCE of the reads)
+__device__ __forceinline__ void keep_live(uint4 (&fa)[2][NI], uint4 (&fb)[2][MJ]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      asm volatile("" : "+v"(fa[s][i].x), "+v"(fa[s][i].y), "+v"(fa[s][i].z), "+v"(fa[s][i].w));
+#pragma unroll
+    for (int j = 0; j < MJ; ++j)
+      asm volatile("" : "+v"(fb[s][j].x), "+v"(fb[s][j].y), "+v"(fb[s][j].z), "+v"(fb[s][j].w));
+  }
+}
+
 __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -211,16 +269,150 @@ __device__ __forceinline__ void wait_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-template <typename T, int EPI, bool PP>
+// ---- ring variant: 5 slots of one 32-deep k half-step each (the whole 160 KiB LDS) ---------
+// A slot holds [W image 256 rows x 64 B | x image 256 rows x 64 B]; with 64-byte rows the 16-byte
+// chunk c of row r lives at chunk c ^ swz64(r), conflict-free for the ds_read_b128 lane groups
+// (searched over the bank model: rows r and r + 4 would otherwise share a bank slot).
+constexpr int SROWB = 64, SIMG = 256 * SROWB, SLOT_B = 2 * SIMG, NSLOT = 5;
+__device__ __forceinline__ int swz64(int r) { return (r >> 1) & 2; }
+
+// one slot (k range [k0, k0 + 32)) issued by one wave group: its wave wl (0-3) issues pieces wl,
+// wl + 4, ... of 16 rows x 64 B; pieces 0-15 = W image, 16-31 = x image
+template <typename T, int EPI>
+__device__ __forceinline__ void stage_slot(char* img, const Args& a, const T* xb, int mvalid,
+                                           int tn, int k0, int wl, int lane) {
+  const int rr = lane >> 2, c = lane & 3;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = wl + 4 * q;
+    if (q < 4) {
+      const int r = 16 * p + rr;
+      const int ch = c ^ swz64(r);
+      int wrow;
+      if constexpr (EPI == kSwiGLU) {
+        const int w = r & 63;
+        wrow = (w < 32 ? 0 : a.F) + tn * 128 + (r >> 6) * 32 + colperm(w & 31);
+      } else {
+        wrow = tn * BN + colperm(r);
+      }
+      const unsigned off =
+          (unsigned)(((long long)wrow * a.ldw + k0 + 8 * ch) * (long long)sizeof(T));
+      dma16(a.w, off, img + p * 16 * SROWB);
+    } else {
+      const int r = 16 * (p - 16) + rr;
+      const int ch = c ^ swz64(r);
+      const int m = min(r, mvalid - 1);
+      const unsigned off = (unsigned)(((long long)m * a.ldx + k0 + 8 * ch) * (long long)sizeof(T));
+      dma16(xb, off, img + p * 16 * SROWB);
+    }
+  }
+}
+
+// fragments of one k-step from its two slots (half-step s from slot s)
+template <typename T>
+__device__ __forceinline__ void read_frags_ring(const char* s0, const char* s1, int nrow0,
+                                                int mrow0, uint4 (&fa)[2][NI], uint4 (&fb)[2][MJ],
+                                                int lane) {
+  const int lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const char* img = s ? s1 : s0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = nrow0 + 16 * i + lr;
+      fa[s][i] = *reinterpret_cast<const uint4*>(img + r * SROWB + ((lg ^ swz64(r)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const int r = mrow0 + 16 * j + lr;
+      fb[s][j] = *reinterpret_cast<const uint4*>(img + SIMG + r * SROWB + ((lg ^ swz64(r)) << 4));
+    }
+  }
+}
+
+__device__ __forceinline__ int slot_next(int h) { return h == NSLOT - 1 ? 0 : h + 1; }
+
+// PROBE (cost split, plain store only; the output is garbage): bit 0 = no LDS-DMA after the
+// prologue, bit 1 = no fragment reads, bit 2 = no MFMAs.  LOOP: 0 plain two-stage loop, 1
+// ping-pong over two 64-deep stages, 2 ping-pong over the 5-slot ring
+// ---- quarter ring (LOOP 3): 10 slots of 128 rows x 128 B (16 KiB), the whole LDS ----------
+// stage k's quarters j = 0..3 are [x rows 0-127 | W rows 0-127 | W rows 128-255 | x rows 128-255]
+// in slots (4k + j) mod 10; a wave group's share of one quarter: its wave wl issues pieces
+// wl, wl + 4, wl + 8, wl + 12 (8 rows each)
+constexpr int QB = 128 * ROWB, NQ = 10;
+
+template <typename T, int EPI>
+__device__ __forceinline__ void stage_quarter(char* img, int j, const Args& a, const T* xb,
+                                              int mvalid, int tn, int k0, int wl, int lane) {
+  const int rr = lane >> 3, c = lane & 7;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = wl + 4 * q;
+    const int r = 8 * p + rr;  // row within the quarter
+    const int ch = c ^ swz(r);
+    unsigned off;
+    const void* base;
+    if (j == 1 || j == 2) {
+      const int rw = r + (j == 2 ? 128 : 0);  // W image row
+      int wrow;
+      if constexpr (EPI == kSwiGLU) {
+        const int w = rw & 63;
+        wrow = (w < 32 ? 0 : a.F) + tn * 128 + (rw >> 6) * 32 + colperm(w & 31);
+      } else {
+        wrow = tn * BN + colperm(rw);
+      }
+      off = (unsigned)(((long long)wrow * a.ldw + k0 + 8 * ch) * (long long)sizeof(T));
+      base = a.w;
+    } else {
+      const int m = min(r + (j == 3 ? 128 : 0), mvalid - 1);
+      off = (unsigned)(((long long)m * a.ldx + k0 + 8 * ch) * (long long)sizeof(T));
+      base = xb;
+    }
+    dma16(base, off, img + p * 8 * ROWB);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void read_frags_q(const char* xq, const char* wq, int wrow0,
+                                             uint4 (&fa)[2][NI], uint4 (&fb)[2][MJ], int lane) {
+  const int lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = wrow0 + 16 * i + lr;
+      fa[s][i] = *reinterpret_cast<const uint4*>(wq + r * ROWB + (((4 * s + lg) ^ swz(r)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const int r = 16 * j + lr;
+      fb[s][j] = *reinterpret_cast<const uint4*>(xq + r * ROWB + (((4 * s + lg) ^ swz(r)) << 4));
+    }
+  }
+}
+
+__device__ __forceinline__ int qslot(int k, int j) { return (4 * k + j) % NQ; }
+
+template <typename T, int EPI, int LOOP, int PROBE = 0>
 __global__ void __launch_bounds__(NT, 1) mlp_gemm_kernel(Args a) {
-  __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE_B];
+  constexpr bool PP = LOOP == 1;
+  __shared__ __attribute__((aligned(16))) char lds[LOOP == 2 ? NSLOT * SLOT_B
+                                                   : LOOP == 3 ? NQ * QB : NSTAGE * STAGE_B];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // XCD-aware bijective remap: blocks are dealt round-robin over the 8 XCDs, so XCD x gets the
   // consecutive virtual ids [x * nb / 8, (x + 1) * nb / 8)
-  const int nb = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
-  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int bid = blockIdx.x;
+  int v, slice = -1;
+  if (bid < a.full) {
+    const int nb = a.full;
+    const int xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
+    v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  } else {  // the split last wave: dispatched last, dealt over every XCD in block order
+    const int u = bid - a.full;
+    v = a.full + (u >> 1);
+    slice = u & 1;
+  }
   // grouped order: GROUP_M row tiles x every column tile, row tile fastest
   const int gsz = a.group_m * a.tiles_n;
   const int g = v / gsz, first_m = g * a.group_m;
@@ -237,8 +429,155 @@ __global__ void __launch_bounds__(NT, 1) mlp_gemm_kernel(Args a) {
 #pragma unroll
     for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.K / BK;
-  if constexpr (!PP) {
+  // k-steps of this block: all of K, or one half of it for a split tile
+  const int nk_all = a.K / BK;
+  const int kb = slice == 1 ? nk_all / 2 : 0;
+  const int nk = slice < 0 ? nk_all : slice == 0 ? nk_all / 2 : nk_all - nk_all / 2;
+  const int kofs = kb * BK;
+  if constexpr (LOOP == 3) {
+    // Ping-pong (as LOOP 1) over the quarter ring.  A quarter is refilled only after the
+    // barrier that follows every wave's reads of it: x0 (read by group 0 in interval 2k) and W0
+    // (read by both groups by the end of 2k + 1) ... Stage k + 2 goes into slots freed at:
+    // x0, W0 -> stage k - 1's W1 / x1 slots (free from interval 2k), W1 -> stage k's x0 slot
+    // (free from 2k + 1), x1 -> stage k's W0 slot (free from 2k + 2).  Issuers: group 0 issues
+    // x0 + W0 of stage k + 2 at the start of interval 2k; group 1 W1 at the start of 2k + 1 and
+    // x1 at the start of 2k + 2.  Each group's vmcnt(8) before a barrier retires its quarters
+    // issued one step earlier: 3-4 intervals of load latency cover instead of 1.5-2.
+    uint4 fa[2][NI], fb[2][MJ];
+    const bool g1 = wid >= 4;
+    const int wl = wid & 3;
+    const int wq_j = 1 + (wn >> 1), wrow0 = (wn & 1) * 64;  // this wave's W quarter and rows
+    const int xq_j = g1 ? 3 : 0;
+    // prologue: stages 0 and 1; group 0 x0 / W0, group 1 W1 / x1 of each
+    for (int st = 0; st < 2 && st < nk; ++st) {
+      for (int j = 0; j < 4; ++j)
+        if ((j < 2) != g1)
+          stage_quarter<T, EPI>(lds + qslot(st, j) * QB, j, a, xb, mvalid, tn, st * BK, wl, lane);
+    }
+    wait_vm<0>();
+    bar();
+    if (!g1) {
+      for (int k = 0; k < nk; ++k) {
+        // interval 2k: issue x0 / W0 of stage k + 2; load step k
+        const bool more = k + 2 < nk && !(PROBE & 1);
+        if (more) {
+          stage_quarter<T, EPI>(lds + qslot(k + 2, 0) * QB, 0, a, xb, mvalid, tn, (k + 2) * BK,
+                                wl, lane);
+          stage_quarter<T, EPI>(lds + qslot(k + 2, 1) * QB, 1, a, xb, mvalid, tn, (k + 2) * BK,
+                                wl, lane);
+        }
+        if (!(PROBE & 2))
+          read_frags_q<T>(lds + qslot(k, xq_j) * QB, lds + qslot(k, wq_j) * QB, wrow0, fa, fb,
+                          lane);
+        wait_lds();
+        bar();
+        // interval 2k + 1: compute step k; x0 / W0 of stage k + 1 have landed
+        if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
+        if (more) wait_vm<8>(); else wait_vm<0>();
+        bar();
+      }
+    } else {
+      // after the prologue (all retired) this group issues W1(s) in interval 2s - 3 and x1(s)
+      // in 2s - 2 (s >= 2); it retires x1(k) before the barrier ending interval 2k (it reads it
+      // in 2k + 1) and W1(k + 1) before the barrier ending 2k + 1 (group 0 reads it in 2k + 2)
+      for (int k = 0; k < nk; ++k) {
+        // interval 2k: issue x1 of stage k + 1 (its slot, stage k - 1's W0, is free now);
+        // compute step k - 1
+        const bool x1_next = k >= 1 && k + 1 < nk && !(PROBE & 1);
+        if (x1_next)
+          stage_quarter<T, EPI>(lds + qslot(k + 1, 3) * QB, 3, a, xb, mvalid, tn, (k + 1) * BK,
+                                wl, lane);
+        if (k > 0) {
+          if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
+        }
+        if (x1_next) wait_vm<8>(); else wait_vm<0>();  // x1(k) landed (younger: W1, x1 of k+1)
+        bar();
+        // interval 2k + 1: issue W1 of stage k + 2 (its slot, stage k's x0, is free now);
+        // load step k; retire W1(k + 1)
+        const bool w1_next = k + 2 < nk && !(PROBE & 1);
+        if (w1_next)
+          stage_quarter<T, EPI>(lds + qslot(k + 2, 2) * QB, 2, a, xb, mvalid, tn, (k + 2) * BK,
+                                wl, lane);
+        if (!(PROBE & 2))
+          read_frags_q<T>(lds + qslot(k, xq_j) * QB, lds + qslot(k, wq_j) * QB, wrow0, fa, fb,
+                          lane);
+        wait_lds();
+        // younger than W1(k + 1): x1(k + 1) (issued in 2k when k >= 1) and W1(k + 2)
+        if (w1_next) {
+          if (x1_next) wait_vm<8>(); else wait_vm<4>();
+        } else if (x1_next) {
+          wait_vm<4>();
+        } else {
+          wait_vm<0>();
+        }
+        bar();
+      }
+      if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
+    }
+  } else if constexpr (LOOP == 2) {
+    // Ping-pong as LOOP 1, over a ring of 5 half-step slots: step k reads slots 2k, 2k + 1
+    // (mod 5) in intervals 2k (group 0) and 2k + 1 (group 1).  Group 0 issues slot 2k + 4 at
+    // the start of interval 2k (that slot was last read in interval 2k - 1), group 1 slot
+    // 2k + 5 at the end of interval 2k + 1 after its own reads; each group waits (counted
+    // vmcnt: the slot it issued one step earlier) before the barrier that ends interval 2k + 1,
+    // so 1.5 steps of loads (96 KiB per CU) stay in flight instead of one.
+    uint4 fa[2][NI], fb[2][MJ];
+    const bool g1 = wid >= 4;
+    const int wl = wid & 3;
+    const int nh = 2 * nk;  // half-steps
+    // prologue: group 0 issues slots 0 and 2, group 1 slots 1 and 3; slots 0 and 1 land first
+    stage_slot<T, EPI>(lds + (g1 ? 1 : 0) * SLOT_B, a, xb, mvalid, tn, (g1 ? 1 : 0) * 32, wl, lane);
+    if ((g1 ? 3 : 2) < nh) {
+      stage_slot<T, EPI>(lds + (g1 ? 3 : 2) * SLOT_B, a, xb, mvalid, tn, (g1 ? 3 : 2) * 32, wl,
+                         lane);
+      wait_vm<8>();
+    } else {
+      wait_vm<0>();
+    }
+    bar();
+    int h0 = 0;  // slot of half-step 2k
+    if (!g1) {
+      for (int k = 0; k < nk; ++k) {
+        const int h1 = slot_next(h0), h2 = slot_next(h1), h3 = slot_next(h2), h4 = slot_next(h3);
+        // interval 2k: load step k; issue half-step 2k + 4
+        if (!(PROBE & 2))
+          read_frags_ring<T>(lds + h0 * SLOT_B, lds + h1 * SLOT_B, nrow0, mrow0, fa, fb, lane);
+        const bool more = 2 * k + 4 < nh;
+        if (more && !(PROBE & 1))
+          stage_slot<T, EPI>(lds + h4 * SLOT_B, a, xb, mvalid, tn, (2 * k + 4) * 32, wl, lane);
+        wait_lds();
+        bar();
+        // interval 2k + 1: compute step k; half-step 2k + 2 (this group's) must have landed
+        if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
+        if (more && !(PROBE & 1)) wait_vm<8>(); else wait_vm<0>();
+        bar();
+        h0 = h2;
+      }
+    } else {
+      for (int k = 0; k < nk; ++k) {
+        const int h1 = slot_next(h0), h2 = slot_next(h1);
+        // interval 2k: compute step k - 1
+        if (k > 0) {
+          if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
+        }
+        bar();
+        // interval 2k + 1: load step k; issue half-step 2k + 5 into slot h0 (= 2k + 5 mod 5)
+        if (!(PROBE & 2))
+          read_frags_ring<T>(lds + h0 * SLOT_B, lds + h1 * SLOT_B, nrow0, mrow0, fa, fb, lane);
+        wait_lds();
+        const bool more = 2 * k + 5 < nh;
+        if (more && !(PROBE & 1)) {
+          stage_slot<T, EPI>(lds + h0 * SLOT_B, a, xb, mvalid, tn, (2 * k + 5) * 32, wl, lane);
+          wait_vm<8>();  // half-step 2k + 3 landed
+        } else {
+          wait_vm<0>();
+        }
+        bar();
+        h0 = h2;
+      }
+      if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
+    }
+  } else if constexpr (!PP) {
     stage<T, EPI>(lds, a, xb, mvalid, tn, 0, wid, lane);
     for (int kt = 0; kt < nk; ++kt) {
       wait_vm<0>();   // this wave's pieces of stage kt have landed
@@ -250,100 +589,150 @@ __global__ void __launch_bounds__(NT, 1) mlp_gemm_kernel(Args a) {
   } else {
     // Ping-pong: wave group 0 (waves 0-3, output rows 0-127) and group 1 (waves 4-7, rows
     // 128-255) alternate between a LOAD interval (this k-step's fragments LDS -> registers, plus
-    // its share of a later stage's LDS-DMA) and a COMPUTE interval (64 MFMAs on the fragments in
-    // registers), one barrier between intervals, group 1 one interval behind group 0: on every
-    // SIMD (one wave of each group) one wave's MFMAs cover the other's LDS reads and DMA issue.
-    // Stage k (buffer k & 1) is read in intervals 2k (group 0) and 2k + 1 (group 1).  Its buffer
-    // is refilled with stage k + 2 by group 1 at the end of interval 2k + 1 (after its own reads
-    // completed) and by group 0 at the start of 2k + 2; both halves are waited for (counted
-    // vmcnt) before the barrier that ends interval 2k + 3.
+    // LDS-DMA of a later stage) and a COMPUTE interval (64 MFMAs on the fragments in registers),
+    // one barrier between intervals, group 1 one interval behind group 0: on every SIMD (one
+    // wave of each group) one wave's MFMAs cover the other's LDS reads and DMA issue.  DMA is
+    // issued only in load intervals (issued before its MFMAs it delays the MFMA cluster: measured
+    // 1.22x slower).
+    // Stage k (buffer k & 1) is read in intervals 2k (group 0) and 2k + 1 (group 1).  Refills,
+    // race-free by construction:
+    //  * W image of stage k + 2: group 1 wave wn, right after its own reads of stage k complete,
+    //    writes exactly the 64 W rows only it (and group 0's wave wn, one interval earlier) reads;
+    //  * x image of stage k + 1: group 0 at the start of interval 2k, after the barrier that
+    //    follows group 1's last reads of that buffer (interval 2k - 1).
+    // Each group retires its pieces (counted vmcnt) before the barrier ahead of their first
+    // reader: ~2 intervals of load latency covered.
     uint4 fa[2][NI], fb[2][MJ];
     const bool g1 = wid >= 4;
-    stage<T, EPI>(lds, a, xb, mvalid, tn, 0, wid, lane);
-    if (g1) {
+    const int wl = wid & 3;
+    if (!g1) {
+      stage_x<T>(lds, a, xb, mvalid, kofs, wl, lane);
+      wait_vm<0>();
+    } else {
+      stage_w<T, EPI>(lds, a, tn, kofs, wn, lane);
       if (nk > 1) {
-        stage<T, EPI>(lds + STAGE_B, a, xb, mvalid, tn, BK, wid, lane);
+        stage_w<T, EPI>(lds + STAGE_B, a, tn, kofs + BK, wn, lane);
         wait_vm<8>();
       } else {
         wait_vm<0>();
       }
-    } else {
-      wait_vm<0>();
     }
     bar();
     if (!g1) {
       for (int k = 0; k < nk; ++k) {
-        // interval 2k: load step k, issue this group's half of stage k + 1
-        read_frags<T>(lds + (k & 1) * STAGE_B, nrow0, mrow0, fa, fb, lane);
-        if (k + 1 < nk)
-          stage<T, EPI>(lds + ((k + 1) & 1) * STAGE_B, a, xb, mvalid, tn, (k + 1) * BK, wid, lane);
+        // interval 2k: x image of stage k + 1; load step k
+        if (k + 1 < nk && !(PROBE & 1))
+          stage_x<T>(lds + ((k + 1) & 1) * STAGE_B, a, xb, mvalid, kofs + (k + 1) * BK, wl, lane);
+        if (!(PROBE & 2)) read_frags<T>(lds + (k & 1) * STAGE_B, nrow0, mrow0, fa, fb, lane);
         wait_lds();
         bar();
-        // interval 2k + 1: compute step k; stage k + 1 (this group's half) must have landed
-        mfma_step<T>(fa, fb, acc);
+        // interval 2k + 1: compute step k; the x image of stage k + 1 must have landed
+        if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
         if (k + 1 < nk) wait_vm<0>();
         bar();
       }
     } else {
       for (int k = 0; k < nk; ++k) {
         // interval 2k: compute step k - 1
-        if (k > 0) mfma_step<T>(fa, fb, acc);
+        if (k > 0) {
+          if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
+        }
         bar();
-        // interval 2k + 1: load step k; refill its buffer with stage k + 2; stage k + 1 landed
-        read_frags<T>(lds + (k & 1) * STAGE_B, nrow0, mrow0, fa, fb, lane);
+        // interval 2k + 1: load step k; then this wave's W rows of stage k + 2; W of stage
+        // k + 1 landed
+        if (!(PROBE & 2)) read_frags<T>(lds + (k & 1) * STAGE_B, nrow0, mrow0, fa, fb, lane);
         wait_lds();
-        if (k + 2 < nk) {
-          stage<T, EPI>(lds + (k & 1) * STAGE_B, a, xb, mvalid, tn, (k + 2) * BK, wid, lane);
+        if (k + 2 < nk && !(PROBE & 1)) {
+          stage_w<T, EPI>(lds + (k & 1) * STAGE_B, a, tn, kofs + (k + 2) * BK, wn, lane);
           wait_vm<8>();
         } else {
           wait_vm<0>();
         }
         bar();
       }
-      mfma_step<T>(fa, fb, acc);  // interval 2 nk: the last step
+      if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);  // the last step
     }
   }
 
-  // lane holds C[m = mrow0 + 16 j + (lane & 15)][n = nrow0 + 16 i + 4 (lane >> 4) + 0..3]
+  if (slice >= 0) {
+    // split tile: publish this half's partial sums, take a ticket; the second half to arrive
+    // adds the other's slab and runs the epilogue (decode_gemm.hip's protocol: plain slab
+    // stores, agent-scope release before the ticket, acquire by the last arriver)
+    const int u = v - a.full;
+    float* mine = a.ws + ((long long)u * 2 + slice) * (NT * NI * MJ * 4);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < MJ; ++j)
+        *reinterpret_cast<f32x4*>(mine + ((i * MJ + j) * NT + threadIdx.x) * 4) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(a.cnt + u, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == 1;
+      if (last) {
+        __hip_atomic_store(a.cnt + u, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const float* other = a.ws + ((long long)u * 2 + (slice ^ 1)) * (NT * NI * MJ * 4);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < MJ; ++j)
+        acc[i][j] += *reinterpret_cast<const f32x4*>(other + ((i * MJ + j) * NT + threadIdx.x) * 4);
+  }
+
+  // lane (lr, lg) holds, for the fragment pair h (fragments 2h, 2h + 1), row
+  // m = mrow0 + 16 j + lr and the 8 consecutive columns nrow0 + 32 h + 8 lg + [0, 8) (colperm):
+  // v[0..3] = acc[2h][j][0..3], v[4..7] = acc[2h + 1][j][0..3]
   const int lr = lane & 15, lg = lane >> 4;
   T* c = reinterpret_cast<T*>(a.c);
+  const auto pack8 = [&](const f32x4& x, const f32x4& y) {
+    return make_uint4(pk2<T>(x[0], x[1]), pk2<T>(x[2], x[3]), pk2<T>(y[0], y[1]),
+                      pk2<T>(y[2], y[3]));
+  };
   if constexpr (EPI == kStore) {
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
       const int m = mrow0 + 16 * j + lr;
       if (m >= mvalid) continue;
-      T* row = c + (long long)(m0 + m) * a.ldc + tn * BN + nrow0 + 4 * lg;
+      T* row = c + (long long)(m0 + m) * a.ldc + tn * BN + nrow0 + 8 * lg;
 #pragma unroll
-      for (int i = 0; i < NI; ++i)
-        *reinterpret_cast<uint2*>(row + 16 * i) =
-            make_uint2(pk2<T>(acc[i][j][0], acc[i][j][1]), pk2<T>(acc[i][j][2], acc[i][j][3]));
+      for (int h = 0; h < NI / 2; ++h)
+        *reinterpret_cast<uint4*>(row + 32 * h) = pack8(acc[2 * h][j], acc[2 * h + 1][j]);
     }
   } else if constexpr (EPI == kSwiGLU) {
-    // fragments 0, 1: gate of activation columns 128 tn + 32 wn + 16 i + 4 lg + e; 2, 3: up
+    // pair 0 (fragments 0, 1): gate of activation columns 128 tn + 32 wn + 8 lg + [0, 8);
+    // pair 1 (fragments 2, 3): up of the same columns
     T* act = reinterpret_cast<T*>(a.act);
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
       const int m = mrow0 + 16 * j + lr;
       if (m >= mvalid) continue;
       const long long row = m0 + m;
+      const int na = tn * 128 + wn * 32 + 8 * lg;
+      float o[8];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int na = tn * 128 + wn * 32 + 16 * i + 4 * lg;
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          // the activation of the ROUNDED g / u: the values the backward reads back
-          const float gg = bf_round(acc[i][j][e], (T*)nullptr);
-          const float uu = bf_round(acc[i + 2][j][e], (T*)nullptr);
-          o[e] = silu(gg) * uu;
-        }
-        *reinterpret_cast<uint2*>(c + row * a.ldc + na) =
-            make_uint2(pk2<T>(acc[i][j][0], acc[i][j][1]), pk2<T>(acc[i][j][2], acc[i][j][3]));
-        *reinterpret_cast<uint2*>(c + row * a.ldc + a.F + na) = make_uint2(
-            pk2<T>(acc[i + 2][j][0], acc[i + 2][j][1]), pk2<T>(acc[i + 2][j][2], acc[i + 2][j][3]));
-        *reinterpret_cast<uint2*>(act + row * a.ldact + na) =
-            make_uint2(pk2<T>(o[0], o[1]), pk2<T>(o[2], o[3]));
+      for (int e = 0; e < 8; ++e) {
+        // the activation of the ROUNDED g / u: the values the backward reads back
+        const float gg = bf_round(acc[e >> 2][j][e & 3], (T*)nullptr);
+        const float uu = bf_round(acc[2 + (e >> 2)][j][e & 3], (T*)nullptr);
+        o[e] = silu(gg) * uu;
       }
+      *reinterpret_cast<uint4*>(c + row * a.ldc + na) = pack8(acc[0][j], acc[1][j]);
+      *reinterpret_cast<uint4*>(c + row * a.ldc + a.F + na) = pack8(acc[2][j], acc[3][j]);
+      *reinterpret_cast<uint4*>(act + row * a.ldact + na) =
+          make_uint4(pk2<T>(o[0], o[1]), pk2<T>(o[2], o[3]), pk2<T>(o[4], o[5]),
+                     pk2<T>(o[6], o[7]));
     }
   } else {
     // dact = acc (f32, never rounded); g / u from the saved gu; writes dg | du
@@ -352,45 +741,55 @@ __global__ void __launch_bounds__(NT, 1) mlp_gemm_kernel(Args a) {
     for (int j = 0; j < MJ; ++j) {
       const int m = mrow0 + 16 * j + lr;
       const long long row = m0 + min(m, mvalid - 1);  // clamped: loads stay unconditional
-      uint2 gv[NI], uv[NI];
+      uint4 gv[NI / 2], uv[NI / 2];
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int n = tn * BN + nrow0 + 16 * i + 4 * lg;
-        gv[i] = *reinterpret_cast<const uint2*>(gu + row * a.ldgu + n);
-        uv[i] = *reinterpret_cast<const uint2*>(gu + row * a.ldgu + a.F + n);
+      for (int h = 0; h < NI / 2; ++h) {
+        const int n = tn * BN + nrow0 + 32 * h + 8 * lg;
+        gv[h] = *reinterpret_cast<const uint4*>(gu + row * a.ldgu + n);
+        uv[h] = *reinterpret_cast<const uint4*>(gu + row * a.ldgu + a.F + n);
       }
       if (m >= mvalid) continue;
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int n = tn * BN + nrow0 + 16 * i + 4 * lg;
-        float g[4], u[4], dg[4], du[4];
-        unpack4<T>(gv[i], g);
-        unpack4<T>(uv[i], u);
+      for (int h = 0; h < NI / 2; ++h) {
+        const int n = tn * BN + nrow0 + 32 * h + 8 * lg;
+        float g[8], u[8], dg[8], du[8];
+        const T* ge = reinterpret_cast<const T*>(&gv[h]);
+        const T* ue = reinterpret_cast<const T*>(&uv[h]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float d = acc[i][j][e];
+        for (int e = 0; e < 8; ++e) {
+          g[e] = to_f32(ge[e]);
+          u[e] = to_f32(ue[e]);
+          const float d = acc[2 * h + (e >> 2)][j][e & 3];
           const float sg = 1.f / (1.f + __expf(-g[e]));
           du[e] = d * g[e] * sg;
           dg[e] = d * u[e] * sg * (1.f + g[e] * (1.f - sg));
         }
-        *reinterpret_cast<uint2*>(c + row * a.ldc + n) =
-            make_uint2(pk2<T>(dg[0], dg[1]), pk2<T>(dg[2], dg[3]));
-        *reinterpret_cast<uint2*>(c + row * a.ldc + a.F + n) =
-            make_uint2(pk2<T>(du[0], du[1]), pk2<T>(du[2], du[3]));
+        store8(c + row * a.ldc + n, dg);
+        store8(c + row * a.ldc + a.F + n, du);
       }
     }
   }
 }
 
-template <typename T, bool PP>
+template <typename T, int LOOP>
 hipError_t launch(int epi, const Args& a, hipStream_t st) {
-  dim3 grid(a.tiles_m * a.tiles_n), block(NT);
+  dim3 grid(a.full + 2 * a.split), block(NT);
+  const int probe = (epi >> 5) & 7;
+  epi &= 15;
+  if (probe && LOOP && epi == kStore) {
+#define LUMEN_MG_PROBE(P) \
+    if (probe == P) hipLaunchKernelGGL((mlp_gemm_kernel<T, kStore, LOOP, P>), grid, block, 0, st, a);
+    LUMEN_MG_PROBE(1) LUMEN_MG_PROBE(2) LUMEN_MG_PROBE(3) LUMEN_MG_PROBE(4) LUMEN_MG_PROBE(5)
+    LUMEN_MG_PROBE(6)
+#undef LUMEN_MG_PROBE
+    return hipGetLastError();
+  }
   if (epi == kStore)
-    hipLaunchKernelGGL((mlp_gemm_kernel<T, kStore, PP>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((mlp_gemm_kernel<T, kStore, LOOP>), grid, block, 0, st, a);
   else if (epi == kSwiGLU)
-    hipLaunchKernelGGL((mlp_gemm_kernel<T, kSwiGLU, PP>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((mlp_gemm_kernel<T, kSwiGLU, LOOP>), grid, block, 0, st, a);
   else if (epi == kSwiGLUBwd)
-    hipLaunchKernelGGL((mlp_gemm_kernel<T, kSwiGLUBwd, PP>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((mlp_gemm_kernel<T, kSwiGLUBwd, LOOP>), grid, block, 0, st, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -405,12 +804,27 @@ hipError_t launch(int epi, const Args& a, hipStream_t st) {
 //        (N == F, F % 256 == 0)
 // K % 64 == 0; row strides in elements: ldx, ldw % 8 == 0, ldc / ldact / ldgu % 4 == 0; every
 // base 16-byte aligned; group_m: row tiles per tile group (L2 reuse order), >= 1.
+// ws / cnt (optional, both or neither): when the last wave of tiles fills at most half the CUs
+// it runs split in two k halves (ws: split * 2 * 65536 floats, cnt: split zeroed ints, which
+// the launch leaves zeroed); lumen_mlp_gemm_split() says how many tiles that is
+extern "C" int lumen_mlp_gemm_split(int M, int N, int K, int epi, int cus) {
+  const int tm = (M + lumen::mg::BM - 1) / lumen::mg::BM;
+  const int tn = (epi & 15) == lumen::mg::kSwiGLU ? N / 256 : N / lumen::mg::BN;
+  const int total = tm * tn, rem = cus > 0 ? total % cus : 0;
+  if ((epi & 16) || total < cus || rem == 0 || 2 * rem > cus || K / lumen::mg::BK < 4) return 0;
+  return rem;
+}
+
 extern "C" hipError_t lumen_mlp_gemm(int dtype, int epi, const void* x, long long ldx,
                                      const void* w, long long ldw, void* c, long long ldc,
                                      void* act, long long ldact, const void* gu, long long ldgu,
-                                     int M, int N, int K, int F, int group_m, hipStream_t st) {
+                                     int M, int N, int K, int F, int group_m, float* ws, int* cnt,
+                                     int split, hipStream_t st) {
   using namespace lumen::mg;
-  const bool pp = (epi & 16) == 0;  // bit 4: the plain two-stage loop (A/B probe)
+  // bit 4: the plain two-stage loop; bit 8: ping-pong over the quarter ring; bit 9: ping-pong
+  // over the half-step ring (A/B probes); default: ping-pong over two stages
+  const int loop = (epi & 16) ? 0 : (epi & 256) ? 3 : (epi & 512) ? 2 : 1;
+  const int probe_bits = epi & (7 << 5);  // bits 5-7: cost-split probe builds (plain store)
   epi &= 15;
   if (M < 1 || K < BK || K % BK || group_m < 1 || ldx < K || ldw < K || ldx % 8 || ldw % 8 ||
       ldc % 4 || x == nullptr || w == nullptr || c == nullptr)
@@ -434,11 +848,20 @@ extern "C" hipError_t lumen_mlp_gemm(int dtype, int epi, const void* x, long lon
   // every 32-bit lane offset of the DMAs stays below 2^32 bytes
   if (wrows * ldw * 2 >= (1LL << 32) || (long long)BM * ldx * 2 >= (1LL << 32))
     return hipErrorInvalidValue;
-  Args a{x, w, c, act, gu, ldx, ldw, ldc, ldact, ldgu, M, N, K, F, (M + BM - 1) / BM,
-         epi == kSwiGLU ? F / 128 : N / BN, group_m};
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = epi == kSwiGLU ? F / 128 : N / BN;
+  if (split < 0 || split > tiles_m * tiles_n || (split > 0 && (ws == nullptr || cnt == nullptr)) ||
+      (split > 0 && loop != 1))
+    return hipErrorInvalidValue;
+  Args a{x, w, c, act, gu, ldx, ldw, ldc, ldact, ldgu, M, N, K, F, tiles_m, tiles_n, group_m,
+         tiles_m * tiles_n - split, split, ws, cnt};
   if (dtype == lumen::kBF16)
-    return pp ? launch<lumen::bf16, true>(epi, a, st) : launch<lumen::bf16, false>(epi, a, st);
+    return loop == 3   ? launch<lumen::bf16, 3>(epi | probe_bits, a, st)
+           : loop == 2 ? launch<lumen::bf16, 2>(epi | probe_bits, a, st)
+           : loop == 1 ? launch<lumen::bf16, 1>(epi | probe_bits, a, st)
+                       : launch<lumen::bf16, 0>(epi, a, st);
   if (dtype == lumen::kF16)
-    return pp ? launch<lumen::fp16, true>(epi, a, st) : launch<lumen::fp16, false>(epi, a, st);
+    return loop == 3   ? launch<lumen::fp16, 3>(epi, a, st)
+           : loop == 2 ? launch<lumen::fp16, 2>(epi, a, st)
+           : loop == 1 ? launch<lumen::fp16, 1>(epi, a, st) : launch<lumen::fp16, 0>(epi, a, st);
   return hipErrorInvalidValue;
 }

@@ -22,7 +22,8 @@ import torch.utils.checkpoint as cp
 from ..ops._native import use_native
 from ..ops.embedding import embedding
 from ..ops.lora import arena_reset
-from ..ops.activation import overlap_mlp, overlap_mlp_plan, recompute_mlp, swiglu
+from ..ops.activation import (fused_mlp, fused_mlp_ok, overlap_mlp, overlap_mlp_plan,
+                              recompute_mlp, swiglu)
 from ..ops.attention import causal_attention, flash_attention_qkv, prepare_varlen
 from ..ops.loss import lm_head_cross_entropy
 from ..ops.rope import qkv_rope_split, rope_qkv_, rope_tables
@@ -136,6 +137,8 @@ class LlamaMLP(nn.Module):
         if self.recompute and self.training and torch.is_grad_enabled() and self.recompute_eligible:
             return recompute_mlp(x2d, gu, dn)
         if self.recompute_eligible:
+            if fused_mlp_ok(x2d, gu, dn):
+                return fused_mlp(x2d, gu, dn)
             n1 = overlap_mlp_plan(x2d, gu, dn)
             if n1:
                 return overlap_mlp(x2d, gu, dn, n1)

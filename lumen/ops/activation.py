@@ -197,6 +197,90 @@ def overlap_mlp(y: torch.Tensor, gate_up, down, n1: int) -> torch.Tensor:
                              down.weight_fn, down._wt_fn(), n1)
 
 
+# LUMEN_FUSED_MLP: the frozen MLP's gate|up GEMM with the SwiGLU in its epilogue, and the
+# down projection's input-gradient GEMM with the SwiGLU backward in its epilogue (hand-written
+# gfx950 GEMM, kernels/mlp_gemm.hip; VERDICT r5 Next #1).  1 = both, fwd / bwd = one of them,
+# 0 = off (library GEMMs + the separate SwiGLU passes).
+FUSED_MLP = _os.environ.get("LUMEN_FUSED_MLP", "0")
+
+
+def _mlp_gemm_ok(x: torch.Tensor, w: torch.Tensor, col_mult: int) -> bool:
+    return (x.dim() == 2 and w.dim() == 2 and x.stride(1) == 1 and w.stride(1) == 1
+            and x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and x.shape[1] == w.shape[1]
+            and x.shape[1] % 64 == 0 and x.dtype == w.dtype
+            and x.dtype in (torch.bfloat16, torch.float16) and w.shape[0] % col_mult == 0
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
+class _FusedMLP(torch.autograd.Function):
+    """down(swiglu(gate_up(y))) for frozen, adapter-free weights with the activation inside the
+    GEMM epilogues (kernels/mlp_gemm.hip):
+
+    * forward: ONE launch writes gu (saved for the backward) and act = silu(g) * u; the down
+      projection is the library GEMM;
+    * backward: dact = dout @ Wd (against the cached Wd^T) in ONE launch whose epilogue reads
+      g / u and writes dg | du -- dact never reaches HBM; dX = dgu @ W_gu is the library GEMM.
+    Each half falls back to the separate passes where the kernel does not take the layout."""
+
+    @staticmethod
+    def forward(ctx, y, gu_w, gu_wt, dn_w, dn_wt, mode):
+        from .gemm import mm_nt
+
+        w = gu_w()
+        T, F = y.shape[0], w.shape[0] // 2
+        if mode in ("1", "fwd") and _mlp_gemm_ok(y, w, 256):
+            gu = torch.empty(T, 2 * F, device=y.device, dtype=y.dtype)
+            act = torch.empty(T, F, device=y.device, dtype=y.dtype)
+            from .mlp_gemm import mlp_gemm
+
+            mlp_gemm(1, y, w, gu, act)
+        else:
+            gu = mm_nt(y, w)
+            act = torch.empty(T, F, device=y.device, dtype=y.dtype)
+            native().swiglu(False, gu, None, act, 0, -1)
+        out = mm_nt(act, dn_w())
+        ctx.save_for_backward(gu)
+        ctx.fns = (gu_w, gu_wt, dn_w, dn_wt)
+        ctx.mode = mode
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        gu_w, gu_wt, dn_w, dn_wt = ctx.fns
+        dout = dout.contiguous()
+        F = gu.shape[1] // 2
+        wdt = dn_wt() if dn_wt is not None else None   # Wd^T [F, H]
+        dgu = torch.empty_like(gu)
+        if (ctx.mode in ("1", "bwd") and wdt is not None and F % 256 == 0
+                and _mlp_gemm_ok(dout, wdt, 256)):
+            from .mlp_gemm import mlp_gemm
+
+            mlp_gemm(2, dout, wdt, dgu, None, gu)
+        else:
+            dact = _dx(dout, dn_w, dn_wt)
+            native().swiglu(True, gu, dact, dgu, 0, -1)
+            del dact
+        return _dx(dgu, gu_w, gu_wt), None, None, None, None, None
+
+
+def fused_mlp_ok(y: torch.Tensor, gate_up, down) -> bool:
+    """The fused-epilogue MLP applies: LUMEN_FUSED_MLP on, GPU native kernels, 16-bit 2-D
+    activations, frozen adapter-free bias-free weights, F a multiple of 256."""
+    if FUSED_MLP in ("0", "") or not (y.is_cuda and y.dim() == 2 and use_native(y)):
+        return False
+    if gate_up.bias is not None or down.bias is not None:
+        return False
+    w = gate_up.weight
+    return (w.dim() == 2 and w.shape[0] % 512 == 0 and y.dtype in (torch.bfloat16, torch.float16)
+            and hasattr(native(), "mlp_gemm"))
+
+
+def fused_mlp(y: torch.Tensor, gate_up, down) -> torch.Tensor:
+    return _FusedMLP.apply(y.contiguous(), gate_up.weight_fn, gate_up._wt_fn(), down.weight_fn,
+                           down._wt_fn(), FUSED_MLP)
+
+
 def recompute_mlp(y: torch.Tensor, gate_up, down) -> torch.Tensor:
     """Selective-recompute MLP over two frozen, adapter-free ``Linear`` modules (see
     ``_RecomputeMLP``)."""

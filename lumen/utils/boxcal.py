@@ -110,23 +110,23 @@ def summarize(sclk: List[float], power: List[float], hwmon: Optional[str]) -> Di
     return out
 
 
-def _ev_ms(fn, n: int) -> List[float]:
-    ts = []
+def _batch_ms(fn, n: int) -> float:
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
     for _ in range(n):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
         fn()
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e))
-    return ts
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / n
 
 
-def fixed_work(device, gemm_n: int = 8192, hbm_gib: int = 4, reps: int = 10,
-               hwmon: Optional[str] = None) -> Dict:
+def fixed_work(device, gemm_n: int = 8192, hbm_gib: int = 4, reps: int = 5,
+               hwmon: Optional[str] = None, batch: int = 60) -> Dict:
     """The fixed calibration work on ``device``: an n^3 bf16 GEMM (hipBLASLt, uniform [-1, 1)
-    operands: the power-hungry case) and a ``hbm_gib`` GiB non-temporal read.  Medians over
-    ``reps`` after 3 warm-ups; the clock sampled during the GEMM runs."""
+    operands: the power-hungry case) and a ``hbm_gib`` GiB non-temporal read.  Each is run in
+    back-to-back batches of ``batch`` launches (~55 ms for the GEMM, long enough for the clock
+    and power to settle as they do in a training step) after a ~0.2 s warm-up; the medians of
+    ``reps`` batches, with the clock / power sampled during the GEMM batches."""
     out: Dict = {}
     g = torch.Generator(device=device).manual_seed(7)
     a = torch.rand(gemm_n, gemm_n, device=device, generator=g, dtype=torch.float32).mul_(2).sub_(1)
@@ -135,9 +135,9 @@ def fixed_work(device, gemm_n: int = 8192, hbm_gib: int = 4, reps: int = 10,
     b = b.to(torch.bfloat16)
     c = torch.empty(gemm_n, gemm_n, device=device, dtype=torch.bfloat16)
     fn = lambda: torch.mm(a, b, out=c)  # noqa: E731
-    _ev_ms(fn, 3)
-    smp = HwmonSampler(hwmon).start()
-    ts = sorted(_ev_ms(fn, reps))
+    _batch_ms(fn, 4 * batch)
+    smp = HwmonSampler(hwmon, period_s=0.005).start()
+    ts = sorted(_batch_ms(fn, batch) for _ in range(reps))
     clk = smp.stop()
     med = ts[len(ts) // 2]
     out["gemm"] = {"shape": f"{gemm_n}^3 bf16 (uniform [-1, 1))", "ms_med": round(med, 3),
@@ -157,8 +157,8 @@ def fixed_work(device, gemm_n: int = 8192, hbm_gib: int = 4, reps: int = 10,
         sink = torch.zeros(1, dtype=torch.int32, device=device)
         blocks = 4096
         fn = lambda: C.hbm_read(buf, sink, blocks)  # noqa: E731
-        _ev_ms(fn, 3)
-        ts = sorted(_ev_ms(fn, reps))
+        _batch_ms(fn, batch)
+        ts = sorted(_batch_ms(fn, batch) for _ in range(reps))
         med = ts[len(ts) // 2]
         out["hbm_read"] = {"gib": hbm_gib, "ms_med": round(med, 3), "ms_min": round(ts[0], 3),
                            "tbps": round(nbytes / (med * 1e-3) / 1e12, 3), "nontemporal": True}

@@ -21,6 +21,7 @@ import torch.nn.functional as F  # noqa: E402
 
 from lumen.ops._native import native  # noqa: E402
 from lumen.ops.gemm import mm_nt  # noqa: E402
+from lumen.ops.mlp_gemm import mlp_gemm  # noqa: E402
 from lumen.utils.gemm_tuning import load_tuned_gemms  # noqa: E402
 
 
@@ -44,6 +45,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--group_m", type=int, default=4)
     ap.add_argument("--only", default="")
+    ap.add_argument("--gms", default="", help="extra group_m values for the 20480 case")
+    ap.add_argument("--probes", default="", help="cost-split probe builds (1, 2, 4, ...)")
     a = ap.parse_args()
     os.makedirs("gpurun_out/mlp_gemm", exist_ok=True)
     C = native()
@@ -61,10 +64,10 @@ def main():
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
         c = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
         ref = xx.float() @ w.float().t()
-        C.mlp_gemm(0, xx, w, c, None, None, a.group_m)
+        mlp_gemm(0, xx, w, c)
         torch.cuda.synchronize()
         err = rel(c, ref)
-        mine = lambda: C.mlp_gemm(0, xx, w, c, None, None, a.group_m)  # noqa: E731
+        mine = lambda: mlp_gemm(0, xx, w, c)  # noqa: E731
         lib = lambda: mm_nt(xx, w)  # noqa: E731
         cases.append((name, 2.0 * T * N * K, mine, lib, err))
 
@@ -72,7 +75,7 @@ def main():
         w = (torch.randn(2 * Fd, H, device=dev) * 0.02).to(torch.bfloat16)
         gu = torch.empty(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
         act = torch.empty(T, Fd, device=dev, dtype=torch.bfloat16)
-        C.mlp_gemm(1, x, w, gu, act, None, a.group_m)
+        mlp_gemm(1, x, w, gu, act)
         torch.cuda.synchronize()
         ref = x.float() @ w.float().t()
         g, u = ref.chunk(2, dim=-1)
@@ -83,14 +86,16 @@ def main():
             o = torch.empty(T, Fd, device=dev, dtype=torch.bfloat16)
             C.swiglu(False, y, None, o, 0, -1)
         cases.append(("fwd gate|up+swiglu 4096x22016x4096", 2.0 * T * 2 * Fd * H,
-                      lambda: C.mlp_gemm(1, x, w, gu, act, None, a.group_m), lib, err))
+                      lambda: mlp_gemm(1, x, w, gu, act), lib, err))
+        cases.append(("fwd nosplit 4096x22016x4096", 2.0 * T * 2 * Fd * H,
+                      lambda: mlp_gemm(1, x, w, gu, act, split=False), lib, err))
 
     def bwd():
         dout = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
         wdt = (torch.randn(Fd, H, device=dev) * 0.02).to(torch.bfloat16)   # Wd^T [F, H]
         gu = torch.randn(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
         dgu = torch.empty(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
-        C.mlp_gemm(2, dout, wdt, dgu, None, gu, a.group_m)
+        mlp_gemm(2, dout, wdt, dgu, None, gu)
         torch.cuda.synchronize()
         g_ = gu.float()[:, :Fd].clone().requires_grad_(True)
         u_ = gu.float()[:, Fd:].clone().requires_grad_(True)
@@ -102,17 +107,34 @@ def main():
             o = torch.empty(T, 2 * Fd, device=dev, dtype=torch.bfloat16)
             C.swiglu(True, gu, d, o, 0, -1)
         cases.append(("bwd dact+swiglu' 4096x11008x4096", 2.0 * T * Fd * H,
-                      lambda: C.mlp_gemm(2, dout, wdt, dgu, None, gu, a.group_m), lib, err))
+                      lambda: mlp_gemm(2, dout, wdt, dgu, None, gu), lib, err))
 
     # the two-stage loop without ping-pong (epi bit 4), for the A/B
     xx0 = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
     w0 = (torch.randn(20480, H, device=dev) * 0.02).to(torch.bfloat16)
     c0 = torch.empty(T, 20480, device=dev, dtype=torch.bfloat16)
-    C.mlp_gemm(16, xx0, w0, c0, None, None, a.group_m)
-    cases.append(("plain(no pp) 4096x20480x4096", 2.0 * T * 20480 * H,
-                  lambda: C.mlp_gemm(16, xx0, w0, c0, None, None, a.group_m),
-                  lambda: mm_nt(xx0, w0), rel(c0, xx0.float() @ w0.float().t())))
+    for flag, nm in ((16, "plain(no pp)"), (256, "quarter ring")):
+        C.mlp_gemm(flag, xx0, w0, c0, None, None, a.group_m)
+        cases.append((f"{nm} 4096x20480x4096", 2.0 * T * 20480 * H,
+                      lambda flag=flag: C.mlp_gemm(flag, xx0, w0, c0, None, None, a.group_m),
+                      lambda: mm_nt(xx0, w0), rel(c0, xx0.float() @ w0.float().t())))
     plain(20480, H, "plain 4096x20480x4096")
+    for gm in [int(v) for v in a.gms.split(",") if v]:
+        xx1 = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+        w1 = (torch.randn(20480, H, device=dev) * 0.02).to(torch.bfloat16)
+        c1 = torch.empty(T, 20480, device=dev, dtype=torch.bfloat16)
+        cases.append((f"plain gm{gm} 4096x20480x4096", 2.0 * T * 20480 * H,
+                      lambda gm=gm, xx1=xx1, w1=w1, c1=c1: C.mlp_gemm(0, xx1, w1, c1, None, None, gm),
+                      lambda xx1=xx1, w1=w1: mm_nt(xx1, w1), 0.0))
+    for pb in [int(v) for v in a.probes.split(",") if v]:
+        # cost split (garbage output): 1 no DMA in the loop, 2 no fragment reads, 4 no MFMAs
+        xx2 = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+        w2 = (torch.randn(20480, H, device=dev) * 0.02).to(torch.bfloat16)
+        c2 = torch.empty(T, 20480, device=dev, dtype=torch.bfloat16)
+        cases.append((f"probe{pb} 4096x20480x4096", 2.0 * T * 20480 * H,
+                      lambda pb=pb, xx2=xx2, w2=w2, c2=c2: C.mlp_gemm(pb << 5, xx2, w2, c2, None,
+                                                                    None, a.group_m),
+                      lambda xx2=xx2, w2=w2: mm_nt(xx2, w2), 0.0))
     plain(2 * Fd, H, "plain 4096x22016x4096")
     plain(Fd, H, "plain 4096x11008x4096")
     plain(H, H, "plain 4096x4096x4096")

@@ -1421,3 +1421,105 @@ def test_skinny_swiglu_gemm(M, K, monkeypatch):
     native().skinny_swiglu_gemm(gu, w, y)
     assert rel(y, ref) < 1e-2
     assert rel(swiglu_linear_nt(gu, w), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,dtype", [(4096, 22016, 4096, torch.bfloat16),
+                                         (4096, 11008, 4096, torch.bfloat16),
+                                         (300, 1024, 512, torch.bfloat16),
+                                         (512, 2048, 1024, torch.float16)])
+def test_mlp_gemm_plain_vs_fp32(M, N, K, dtype):
+    """kernels/mlp_gemm.hip epi 0 (ping-pong LDS-DMA MFMA GEMM; the 22016 shape runs its last
+    wave split in two k halves) against an fp32 matmul; partial last row tile at M = 300."""
+    from lumen.ops.mlp_gemm import mlp_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(dtype).to(DEV)
+    w = (torch.randn(N, K, generator=g) * 0.02).to(dtype).to(DEV)
+    c = torch.empty(M, N, device=DEV, dtype=dtype)
+    mlp_gemm(0, x, w, c)
+    ref = x.float() @ w.float().t()
+    err = ((c.float() - ref).norm() / ref.norm()).item()
+    assert err < 4e-3, err
+
+
+@pytest.mark.parametrize("T,H,F", [(4096, 4096, 11008), (384, 512, 768)])
+def test_mlp_gemm_swiglu_fwd_bwd_vs_fp32(T, H, F):
+    """The fused SwiGLU epilogues against fp32 torch: forward gu = y @ [Wg | Wu]^T and
+    act = silu(g) * u in one launch; backward dact = dout @ Wd (against Wd^T) with dg | du
+    formed in the epilogue from the saved gu."""
+    import torch.nn.functional as Fn
+
+    from lumen.ops.mlp_gemm import mlp_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(T + F)
+    y = torch.randn(T, H, generator=g).to(torch.bfloat16).to(DEV)
+    wgu = (torch.randn(2 * F, H, generator=g) * 0.02).to(torch.bfloat16).to(DEV)
+    gu = torch.empty(T, 2 * F, device=DEV, dtype=torch.bfloat16)
+    act = torch.empty(T, F, device=DEV, dtype=torch.bfloat16)
+    mlp_gemm(1, y, wgu, gu, act)
+    ref = y.float() @ wgu.float().t()
+    gr, ur = ref.chunk(2, dim=-1)
+    assert ((gu.float() - ref).norm() / ref.norm()).item() < 4e-3
+    ra = Fn.silu(gr) * ur
+    assert ((act.float() - ra).norm() / ra.norm()).item() < 8e-3
+    # backward from the kernel's own (bf16) gu, as training does
+    dout = torch.randn(T, H, generator=g).to(torch.bfloat16).to(DEV)
+    wdt = (torch.randn(F, H, generator=g) * 0.02).to(torch.bfloat16).to(DEV)   # Wd^T
+    dgu = torch.empty(T, 2 * F, device=DEV, dtype=torch.bfloat16)
+    mlp_gemm(2, dout, wdt, dgu, None, gu)
+    g_ = gu.float()[:, :F].clone().requires_grad_(True)
+    u_ = gu.float()[:, F:].clone().requires_grad_(True)
+    (Fn.silu(g_) * u_).backward(dout.float() @ wdt.float().t())
+    rd = torch.cat([g_.grad, u_.grad], dim=1)
+    assert ((dgu.float() - rd).norm() / rd.norm()).item() < 8e-3
+
+
+def test_mlp_gemm_split_tail_matches_unsplit():
+    """The split last wave (two k halves, f32 slabs, last-arriver sum) gives the unsplit result
+    up to f32 summation order, and leaves its ticket counters zeroed for the next launch."""
+    from lumen.ops import mlp_gemm as mg
+
+    M, N, K = 4096, 22016, 4096
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    a = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    b = torch.empty_like(a)
+    mg.mlp_gemm(0, x, w, a, split=True)
+    mg.mlp_gemm(0, x, w, b, split=False)
+    assert int(mg.native().mlp_gemm_split(M, N, K, 0, mg._cu_count(x.device))) > 0
+    d = (a.float() - b.float()).abs().max().item()
+    assert d <= 2e-2 * b.float().abs().max().item(), d
+    for ws, cnt in mg._ws.values():
+        assert int(cnt.abs().sum()) == 0
+
+
+def test_fused_mlp_autograd_matches_unfused(monkeypatch):
+    """LlamaMLP through _FusedMLP (LUMEN_FUSED_MLP=1: both fused GEMMs) against the default
+    path (library GEMMs + SwiGLU passes): output and input gradient agree to bf16 rounding."""
+    import dataclasses
+
+    import lumen.ops.activation as act_mod
+    import lumen.ops.mlp_gemm as mg
+    from lumen.models.config import get_config
+    from lumen.models.llama import LlamaMLP
+
+    cfg = dataclasses.replace(get_config("small-llama"), intermediate_size=1536)
+    torch.manual_seed(0)
+    mlp = LlamaMLP(cfg, dtype=torch.bfloat16, device=DEV)
+    for p in mlp.parameters():
+        torch.nn.init.normal_(p, std=0.02)
+    mlp.gate_up_proj.transpose_bwd = mlp.down_proj.transpose_bwd = True   # W^T, as in training
+    x = torch.randn(512, cfg.hidden_size, device=DEV, dtype=torch.bfloat16)
+    calls = []
+    real = mg.mlp_gemm
+    monkeypatch.setattr(mg, "mlp_gemm", lambda epi, *a, **k: (calls.append(epi), real(epi, *a, **k))[1])
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(act_mod, "FUSED_MLP", mode)
+        xi = x.clone().requires_grad_(True)
+        y = mlp(xi)
+        y.float().square().sum().backward()
+        outs[mode] = (y.detach().float(), xi.grad.float())
+    assert calls == [1, 2], calls   # both fused kernels ran in mode 1, none in mode 0
+    for a, b in zip(outs["1"], outs["0"]):
+        assert ((a - b).norm() / b.norm()).item() < 1e-2
