@@ -79,7 +79,7 @@ def run_serve_bench(args) -> dict:
         eng = make_engine(a)
         r = bench_engine(a, eng)
     except Exception as e:  # noqa: BLE001 - keep the training result
-        return {"error": repr(e)[:500]}, None, None
+        return {"error": repr(e)[:500]}, None, None, None
     e_out = {k: r[k] for k in keep if k in r}
     e_out["bench_s"] = round(time.time() - t0, 1)
     e_out["config"] = dict(conf, async_scheduling=r.get("async_scheduling"),
@@ -89,7 +89,7 @@ def run_serve_bench(args) -> dict:
         h = bench_http(a, eng)
     except Exception as e:  # noqa: BLE001 - the engine-mode number stands
         eng.shutdown()
-        return {"error": "http: " + repr(e)[:500], "engine_fallback": e_out}, e_out, None
+        return {"error": "http: " + repr(e)[:500], "engine_fallback": e_out}, e_out, None, None
     h_out = {k: h[k] for k in keep if k in h}
     h_out["bench_s"] = round(time.time() - t1, 1)
     h_out["vs_engine"] = round(h["output_tok_s"] / max(r["output_tok_s"], 1e-9), 3)
@@ -111,8 +111,24 @@ def run_serve_bench(args) -> dict:
                                    mode="in-process engine")
         except Exception as e:  # noqa: BLE001
             c_out = {"error": repr(e)[:500]}
+    # the same burst with vLLM's non-greedy sampler settings (temperature 0.8, top-p 0.95,
+    # top-k 50: the radix-select top-k / top-p kernel, kernels/sampling.hip), prefill-first
+    s_out = None
+    t3 = time.time()
+    try:
+        eng.scheduler.cfg.policy = "prefill_first"
+        eng.scheduler.cfg.max_num_batched_tokens = a.max_batched_tokens
+        asm = types.SimpleNamespace(**dict(vars(a), temperature=0.8, top_p=0.95, top_k=50))
+        sm = bench_engine(asm, eng)
+        s_out = {k: sm[k] for k in keep if k in sm}
+        s_out["bench_s"] = round(time.time() - t3, 1)
+        s_out["vs_greedy_engine"] = round(sm["output_tok_s"] / max(r["output_tok_s"], 1e-9), 3)
+        s_out["config"] = dict(conf, sampling="temperature 0.8, top_p 0.95, top_k 50, ignore_eos",
+                               mode="in-process engine")
+    except Exception as e:  # noqa: BLE001
+        s_out = {"error": repr(e)[:500]}
     eng.shutdown()
-    return h_out, e_out, c_out
+    return h_out, e_out, c_out, s_out
 
 
 def run_serve_tp(args, env) -> dict:
@@ -608,6 +624,19 @@ def main():
         return float(t.item())
 
     budget = WallBudget(args.wall_budget, T_START, _agree_min)
+    # heartbeat on stderr once a minute (which section, how long): a long section over a slow
+    # transport (a shared-GPU rehearsal's loopback RCCL) reads as progress, not as a hang
+    import threading as _th
+
+    def _heartbeat():
+        while True:
+            time.sleep(60)
+            o = budget._open
+            print(f"[bench] rank {env.rank}: {time.time() - T_START:.0f} s, section "
+                  f"{o['section'] if o else 'headline / between sections'}", file=sys.stderr,
+                  flush=True)
+
+    _th.Thread(target=_heartbeat, daemon=True, name="bench-heartbeat").start()
     hwmon = boxcal.gpu_hwmon(env.device) if (on_gpu and args.box) else None
     sampler = boxcal.HwmonSampler(hwmon).start() if (on_gpu and args.box) else None
     # every timed step must really update the adapters: a non-finite gradient makes the fused
@@ -687,7 +716,7 @@ def main():
             comm = {"error": repr(e)[:300]}
             raise  # ranks may disagree on where they failed: do not continue collectives
         budget.done("comm_probe")
-    serve = serve_engine = serve_chunked = None
+    serve = serve_engine = serve_chunked = serve_sampled = None
     parts = {}
     want_parts = [x for x in args.partitioned.split(",") if x] if ds.stage == 3 else []
     if want_parts or (args.serve and world == 1 and on_gpu):
@@ -725,7 +754,7 @@ def main():
         # training region: the training model and engine are freed first
         del batches
         if budget.allow("serve", 60.0):
-            serve, serve_engine, serve_chunked = run_serve_bench(args)
+            serve, serve_engine, serve_chunked, serve_sampled = run_serve_bench(args)
             budget.done("serve")
         else:
             serve = {"skipped": "wall budget"}
@@ -785,6 +814,7 @@ def main():
                 "serve": serve,
                 "serve_engine": serve_engine,
                 "serve_chunked": serve_chunked,
+                "serve_sampled": serve_sampled,
                 "box": box,
             },
         }

@@ -76,6 +76,10 @@ def bench_engine(a, eng=None) -> dict:
     mk = lambda n: [rng.randrange(3, V) for _ in range(n)]  # noqa: E731
     _warm(eng, a, rng)
     params = dict(max_tokens=a.max_tokens, temperature=a.temperature, ignore_eos=True)
+    if getattr(a, "top_p", None) is not None:
+        params["top_p"] = a.top_p
+    if getattr(a, "top_k", None) is not None:
+        params["top_k"] = a.top_k
     # --shared-prefix N: every prompt starts with the same N tokens (a shared system prompt)
     shared = mk(min(getattr(a, "shared_prefix", 0), a.prompt_len))
     prompts = [shared + mk(a.prompt_len - len(shared)) for _ in range(a.num_requests)]
@@ -260,6 +264,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=512)
     ap.add_argument("--max-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--top-p", type=float, default=None)
+    ap.add_argument("--top-k", type=int, default=None)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=2048)

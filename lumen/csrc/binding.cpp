@@ -8,6 +8,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -47,11 +48,12 @@ hipError_t lumen_lora3_w_tail(int, void*, long long, int, const float*, int, int
                               const long long*, const int*, const int*, float, hipStream_t);
 hipError_t lumen_lora3_dxa(int, const void*, long long, void*, long long, const float*, const float*,
                            long long, float*, long long, int, int, int, int, unsigned long long,
-                           unsigned int, float, long long, long long, float*, hipStream_t);
+                           unsigned int, float, long long, long long, float*, float*, unsigned*,
+                           hipStream_t);
 hipError_t lumen_embedding(const void*, const long long*, void*, int, int, int, hipStream_t);
 hipError_t lumen_lora3_down(int, const void*, long long, const float*, long long, float*, long long,
                             int, int, int, float, unsigned long long, unsigned int, float, long long,
-                            long long, void*, long long, int, int, unsigned*, hipStream_t);
+                            long long, void*, long long, int, int, unsigned*, float*, hipStream_t);
 hipError_t lumen_lora3_up(int, int, void*, long long, const float*, long long, const float*,
                           long long, int, int, float, unsigned long long, unsigned int, float,
                           long long, long long, int, const long long*, const long long*,
@@ -59,7 +61,8 @@ hipError_t lumen_lora3_up(int, int, void*, long long, const float*, long long, c
                           int, hipStream_t);
 hipError_t lumen_lora3_dy(int, const void*, long long, const float*, int, const float*, long long,
                           float*, long long, float*, int, int, float, int, const long long*,
-                          const long long*, const long long*, const int*, hipStream_t);
+                          const long long*, const long long*, const int*, float*, float*,
+                          unsigned*, unsigned*, hipStream_t);
 hipError_t lumen_transpose(int, const void*, void*, int, int, long long, long long, hipStream_t);
 hipError_t lumen_rope_cache(int, void*, long long, const int*, const float*, const float*, void*,
                             void*, const long long*, int, int, int, int, int, int, hipStream_t);
@@ -474,7 +477,7 @@ void lora3_down(const at::Tensor& x, int64_t ldx, const at::Tensor& A, at::Tenso
                 int64_t T, int64_t K, int64_t R, double alpha, int64_t seed, int64_t thresh,
                 double drop_scale, int64_t drop_ld, int64_t drop_col0,
                 const c10::optional<at::Tensor>& xe, int64_t xk, int64_t KP,
-                const c10::optional<at::Tensor>& cnt) {
+                const c10::optional<at::Tensor>& cnt, const c10::optional<at::Tensor>& slab) {
   if (!x.is_cuda()) throw std::invalid_argument("lumen: lora3_down needs GPU tensors");
   need_cuda_f32(A, "lora3_down A");
   need_cuda_f32(Z, "lora3_down Z");
@@ -493,12 +496,22 @@ void lora3_down(const at::Tensor& x, int64_t ldx, const at::Tensor& A, at::Tenso
     ldxe = xe->stride(0);
     cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
   }
+  float* sp = nullptr;
+  if (slab && slab->defined()) {
+    // deterministic K-block sum: slab f32 >= ceil(T / 64) * ceil(K / 1024) * 64 * R, cnt zeroed
+    if (!cnt || !cnt->defined() || cnt->scalar_type() != at::kInt || !cnt->is_cuda() ||
+        cnt->numel() < (T + 63) / 64 || slab->scalar_type() != at::kFloat || !slab->is_cuda() ||
+        slab->numel() < ((T + 63) / 64) * ((K + 1023) / 1024) * 64 * R)
+      throw std::invalid_argument("lumen: lora3_down slab / cnt too small");
+    sp = slab->data_ptr<float>();
+    cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+  }
   check(lumen_lora3_down(dcode(x), x.data_ptr(), ldx, A.data_ptr<float>(), A.stride(0),
                          Z.data_ptr<float>(), ldz, static_cast<int>(T), static_cast<int>(K),
                          static_cast<int>(R), static_cast<float>(alpha),
                          static_cast<unsigned long long>(seed), static_cast<unsigned int>(thresh),
                          static_cast<float>(drop_scale), drop_ld, drop_col0, xp, ldxe,
-                         static_cast<int>(xk), static_cast<int>(KP), cp, cur_stream()),
+                         static_cast<int>(xk), static_cast<int>(KP), cp, sp, cur_stream()),
         "lora3_down");
 }
 
@@ -535,7 +548,8 @@ void lora3_up(int64_t fwd, at::Tensor& out, int64_t ldo, const at::Tensor& s1, i
 // segs: (n_off, r_off, b_off, n_len)
 void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r, const at::Tensor& Z,
               int64_t ldz, at::Tensor& dZ, int64_t lddz, at::Tensor& dB, int64_t T, int64_t tw,
-              double alpha, const std::vector<std::vector<int64_t>>& segs) {
+              double alpha, const std::vector<std::vector<int64_t>>& segs,
+              const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& cnt) {
   if (!dy.is_cuda()) throw std::invalid_argument("lumen: lora3_dy needs GPU tensors");
   need_cuda_f32(B, "lora3_dy B");
   need_cuda_f32(Z, "lora3_dy Z");
@@ -549,10 +563,28 @@ void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r,
     if (segs[i].size() != 4) throw std::invalid_argument("lumen: lora3_dy segment = (n_off, r_off, b_off, n_len)");
     no[i] = segs[i][0]; ro[i] = segs[i][1]; bo[i] = segs[i][2]; nl[i] = static_cast<int>(segs[i][3]);
   }
+  // deterministic sums (ws f32, cnt int32 zeroed): dZ partials [nseg][gy][gx][tw][r], then dB
+  // partials [nseg][gx][gy][256][r]; counters: dZ [nseg][gy], then dB [nseg][gx]
+  float *sz = nullptr, *sb = nullptr;
+  unsigned *cz = nullptr, *cb = nullptr;
+  if (ws && ws->defined()) {
+    int maxl = 0;
+    for (int i = 0; i < nseg; ++i) maxl = std::max(maxl, nl[i]);
+    const long long gx = (maxl + 255) / 256, gy = (T + tw - 1) / tw;
+    const long long nz = nseg * gy * gx * tw * r, nb = nseg * gx * gy * 256 * r;
+    if (!cnt || !cnt->defined() || !ws->is_cuda() || ws->scalar_type() != at::kFloat ||
+        !cnt->is_cuda() || cnt->scalar_type() != at::kInt || ws->numel() < nz + nb ||
+        cnt->numel() < nseg * (gx + gy))
+      throw std::invalid_argument("lumen: lora3_dy deterministic workspace too small");
+    sz = ws->data_ptr<float>();
+    sb = sz + nz;
+    cz = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+    cb = cz + nseg * gy;
+  }
   check(lumen_lora3_dy(dcode(dy), dy.data_ptr(), ldy, B.data_ptr<float>(), static_cast<int>(r),
                        Z.data_ptr<float>(), ldz, dZ.data_ptr<float>(), lddz, dB.data_ptr<float>(),
                        static_cast<int>(T), static_cast<int>(tw), static_cast<float>(alpha), nseg,
-                       no, ro, bo, nl, cur_stream()),
+                       no, ro, bo, nl, sz, sb, cz, cb, cur_stream()),
         "lora3_dy");
 }
 
@@ -617,7 +649,8 @@ void lora3_w_tail_batch(const at::Tensor& desc, int64_t dtype, int64_t max_chunk
 // fused x-side LoRA backward (kernels/lora_v3.hip dxa3_kernel)
 void lora3_dxa(const at::Tensor& x, at::Tensor& dx, const at::Tensor& dZ, const at::Tensor& A,
                at::Tensor& dA, int64_t tw, int64_t seed, int64_t thresh, double drop_scale,
-               int64_t drop_ld, int64_t drop_col0, const c10::optional<at::Tensor>& delta) {
+               int64_t drop_ld, int64_t drop_col0, const c10::optional<at::Tensor>& delta,
+               const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& cnt) {
   need_cuda_f32(dZ, "lora3_dxa dZ");
   float* dp = nullptr;
   if (delta && delta->defined()) {
@@ -636,13 +669,24 @@ void lora3_dxa(const at::Tensor& x, at::Tensor& dx, const at::Tensor& dZ, const 
       A.size(0) != dZ.size(1) || dA.size(0) != dZ.size(1) || A.size(1) != x.size(1) ||
       dA.size(1) != x.size(1))
     throw std::invalid_argument("lumen: lora3_dxa: x/dx [T, K] 16-bit, dZ [T, R] f32, A/dA [R, K] f32");
+  float* sp = nullptr;
+  unsigned* cp = nullptr;
+  if (ws && ws->defined()) {  // deterministic dA: partials [gx][gy][R][128], counters [gx]
+    const long long gx = (x.size(1) + 127) / 128, gy = (x.size(0) + tw - 1) / tw;
+    if (!cnt || !cnt->defined() || !ws->is_cuda() || ws->scalar_type() != at::kFloat ||
+        !cnt->is_cuda() || cnt->scalar_type() != at::kInt ||
+        ws->numel() < gx * gy * 128 * dZ.size(1) || cnt->numel() < gx)
+      throw std::invalid_argument("lumen: lora3_dxa deterministic workspace too small");
+    sp = ws->data_ptr<float>();
+    cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+  }
   check(lumen_lora3_dxa(dcode(x), x.data_ptr(), x.stride(0), dx.data_ptr(), dx.stride(0),
                         dZ.data_ptr<float>(), A.data_ptr<float>(), A.stride(0),
                         dA.data_ptr<float>(), dA.stride(0), static_cast<int>(x.size(0)),
                         static_cast<int>(x.size(1)), static_cast<int>(dZ.size(1)),
                         static_cast<int>(tw), static_cast<unsigned long long>(seed),
                         static_cast<unsigned int>(thresh), static_cast<float>(drop_scale), drop_ld,
-                        drop_col0, dp, cur_stream()),
+                        drop_col0, dp, sp, cp, cur_stream()),
         "lora3_dxa");
 }
 
@@ -982,14 +1026,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ldz"), py::arg("T"), py::arg("K"), py::arg("R"), py::arg("alpha"), py::arg("seed"),
         py::arg("thresh"), py::arg("drop_scale"), py::arg("drop_ld"), py::arg("drop_col0"),
         py::arg("xe") = py::none(), py::arg("xk") = 0, py::arg("KP") = 0,
-        py::arg("cnt") = py::none());
+        py::arg("cnt") = py::none(), py::arg("slab") = py::none());
   m.def("embedding", &embedding);
   m.def("lora3_dy", &lora3_dy, py::arg("dy"), py::arg("ldy"), py::arg("B"), py::arg("r"),
         py::arg("Z"), py::arg("ldz"), py::arg("dZ"), py::arg("lddz"), py::arg("dB"), py::arg("T"),
-        py::arg("tw"), py::arg("alpha"), py::arg("segs"));
+        py::arg("tw"), py::arg("alpha"), py::arg("segs"), py::arg("ws") = py::none(),
+        py::arg("cnt") = py::none());
   m.def("lora3_dxa", &lora3_dxa, py::arg("x"), py::arg("dx"), py::arg("dZ"), py::arg("A"),
         py::arg("dA"), py::arg("tw"), py::arg("seed"), py::arg("thresh"), py::arg("drop_scale"),
-        py::arg("drop_ld"), py::arg("drop_col0"), py::arg("delta") = py::none());
+        py::arg("drop_ld"), py::arg("drop_col0"), py::arg("delta") = py::none(),
+        py::arg("ws") = py::none(), py::arg("cnt") = py::none());
   m.def("lora3_z_tail", &lora3_z_tail);
   m.def("lora3_w_tail", &lora3_w_tail);
   m.def("kv_dequant", &kv_dequant);

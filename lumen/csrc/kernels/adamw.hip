@@ -14,6 +14,7 @@
 //    step needs no device->host synchronisation at all; optionally it writes a 16-bit copy of the
 //    updated parameters in the same pass (the "fp32 master -> bf16 model" copy-out).
 #include "common.h"
+#include "det.h"
 
 #include <algorithm>
 
@@ -71,6 +72,12 @@ __device__ __forceinline__ float sched_lr(const OptSched& s, float it) {
   return s.lr_min + (s.lr_max - s.lr_min) * gamma;
 }
 
+// deterministic block sum (det.h): one partial per workgroup, the last arriver adds them to *out
+// in block order (at most 512 workgroups; one norm_sq launch at a time, as the engine issues it)
+constexpr int kNormMaxBlocks = 512;
+__device__ float g_norm_slab[kNormMaxBlocks];
+__device__ unsigned g_norm_cnt;
+
 template <typename G>
 __global__ void __launch_bounds__(256) norm_sq_kernel(const G* __restrict__ g, long long n,
                                                       float* __restrict__ out) {
@@ -99,7 +106,15 @@ __global__ void __launch_bounds__(256) norm_sq_kernel(const G* __restrict__ g, l
     acc += t * t;
   }
   acc = block_sum<256>(acc, red);
-  if (threadIdx.x == 0) atomicAdd(out, acc);
+  if (threadIdx.x == 0) det::st_wt(g_norm_slab + blockIdx.x, acc);
+  __shared__ int lastf;
+  if (!det::last_arriver(&g_norm_cnt, gridDim.x, &lastf)) return;
+  if (threadIdx.x < 64) {
+    float v = 0.f;
+    for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += 64) v += det::ld_wt(g_norm_slab + b);
+    v = wave_sum(v);  // fixed butterfly order
+    if (threadIdx.x == 0) *out += v;
+  }
 }
 
 template <typename G, typename O>

@@ -21,6 +21,7 @@
 // Dropout is the same counter hash as lora_v2 (common.h dropout_keep8), so masks regenerate
 // bit-identically across kernels and against lumen.ops.lora.dropout_mask_ref.
 #include "tile128.h"
+#include "det.h"
 
 namespace lumen {
 namespace lv3 {
@@ -68,6 +69,10 @@ struct DownArgs {
   // z_tail launch.  cnt[blockIdx.x] arrival counters: zero on entry, left at zero.
   void* xe; long long ldxe; int xk, KP;
   unsigned* cnt;
+  // deterministic sum (slab != nullptr, cnt required): each K-block's [64 x J] partial goes to
+  // slab[(blockIdx.x * gridDim.y + blockIdx.y) * 64 * J] (write-through), the last K-block of the
+  // row tile sums them in K order and writes Z (det.h) -- no f32 atomics
+  float* slab;
 };
 
 template <typename T, bool DROP, int NJ>
@@ -174,6 +179,36 @@ __global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
   }
   __syncthreads();
   const float alpha = DROP ? a.alpha * a.drop.scale : a.alpha;
+  if (a.slab != nullptr) {
+    float* mine = a.slab + ((long long)blockIdx.x * gridDim.y + blockIdx.y) * (64 * J);
+    for (int i = threadIdx.x; i < 64 * J; i += 512) {
+      const int o = (i / J) * JP + i % J;
+      det::st_wt(mine + i, alpha * (red[0][o] + red[1][o] + red[2][o] + red[3][o]));
+    }
+    __shared__ int lastf;
+    if (!det::last_arriver(a.cnt + blockIdx.x, gridDim.y, &lastf)) return;
+    // the row tile's sum in K-block order; Z written once, the fold tail straight from it
+    const float* base = a.slab + (long long)blockIdx.x * gridDim.y * (64 * J);
+    T* xe = reinterpret_cast<T*>(a.xe);
+    for (int i = threadIdx.x; i < 32 * J; i += 512) {  // pairs of columns
+      const int row = (2 * i) / J, j = (2 * i) % J, t = t0 + row;
+      const float2 v = det::sum_pairs(base + 2 * i, 64LL * J, gridDim.y);
+      if (t < a.T) {
+        *reinterpret_cast<float2*>(a.Z + (long long)t * a.ldz + j) = v;
+        if (xe != nullptr) {
+          xe[(long long)t * a.ldxe + a.xk + j] = from_f32<T>(v.x);
+          xe[(long long)t * a.ldxe + a.xk + j + 1] = from_f32<T>(v.y);
+        }
+      }
+    }
+    if (xe != nullptr) {  // zero tail columns J .. KP
+      for (int i = threadIdx.x; i < 64 * (a.KP - J); i += 512) {
+        const int row = i / (a.KP - J), c = J + i % (a.KP - J), t = t0 + row;
+        if (t < a.T) xe[(long long)t * a.ldxe + a.xk + c] = from_f32<T>(0.f);
+      }
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < 64 * J; i += 512) {
     const int row = i / J, j = i % J, t = t0 + row;
     const int o = row * JP + j;
@@ -416,6 +451,11 @@ struct DyArgs {
   float alpha;
   DySeg seg;
   int probe;  // cost probes (0 in production): 16 dZ atomics, 32 dB atomics only when v == 1234.5
+  // deterministic sums (slab_z != nullptr; det.h): dZ partials per (segment, row block, column
+  // block) [TW][r], dB partials per (segment, column block, row block) [256][r]; the last
+  // column block of a row block sums dZ, the last row block of a column block sums dB
+  float* slab_z; float* slab_b;
+  unsigned* cnt_z; unsigned* cnt_b;
 };
 
 constexpr int kDyCC = 2;
@@ -556,15 +596,74 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
       }
     if (cc == nch - 1) {
       // flush this sub-tile's dZ rows: accumulator row 4 g + r, column 16 jt + L
+      if (a.slab_z != nullptr) {
+        float* sz = a.slab_z + (((long long)seg * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) *
+                                   ((long long)a.TW * a.r);
 #pragma unroll
-      for (int jt = 0; jt < NJ; ++jt)
+        for (int jt = 0; jt < NJ; ++jt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int t = t0 + wid * 16 + g * 4 + r;
-          if (t < te && (!(a.probe & 16) || dzacc[jt][r] == 1234.5f))
-            atomicAdd(dZ + (long long)t * a.lddz + jt * 16 + L, a.alpha * dzacc[jt][r]);
-        }
+          for (int r = 0; r < 4; ++r) {
+            const int t = t0 + wid * 16 + g * 4 + r;
+            if (t < te) det::st_wt(sz + (long long)(t - tb) * a.r + jt * 16 + L, dzacc[jt][r]);
+          }
+      } else {
+#pragma unroll
+        for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = t0 + wid * 16 + g * 4 + r;
+            if (t < te && (!(a.probe & 16) || dzacc[jt][r] == 1234.5f))
+              atomicAdd(dZ + (long long)t * a.lddz + jt * 16 + L, a.alpha * dzacc[jt][r]);
+          }
+      }
     }
+  }
+  if (a.slab_z != nullptr) {
+    // dB partials of this (segment, column block, row block), then the two last-arriver sums
+    float* sb = a.slab_b + (((long long)seg * gridDim.x + blockIdx.x) * gridDim.y + blockIdx.y) *
+                               (256LL * a.r);
+#pragma unroll
+    for (int cc = 0; cc < kDyCC; ++cc) {
+      if (cc >= nch) break;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int cl = cc * 128 + wid * 32 + m * 16 + g * 4 + r;
+            if (cb + cl < NL) det::st_wt(sb + (long long)cl * a.r + jt * 16 + L, dbacc[cc][m][jt][r]);
+          }
+    }
+    __shared__ int lastf;
+    const int ncb = (NL + 128 * kDyCC - 1) / (128 * kDyCC);  // column blocks of this segment
+    const int J = NJ * 16;
+    if (det::last_arriver(a.cnt_z + (long long)seg * gridDim.y + blockIdx.y, ncb, &lastf)) {
+      // dZ rows [tb, te) of this segment: column blocks summed in order
+      const float* base = a.slab_z + ((long long)seg * gridDim.y + blockIdx.y) * gridDim.x *
+                                         ((long long)a.TW * a.r);
+      for (int i = threadIdx.x; i < (te - tb) * (J / 2); i += 256) {
+        const int tl = i / (J / 2), j = (i % (J / 2)) * 2;
+        const float2 v = det::sum_pairs(base + (long long)tl * a.r + j, (long long)a.TW * a.r, ncb);
+        float* o = dZ + (long long)(tb + tl) * a.lddz + j;
+        o[0] = a.alpha * v.x;
+        o[1] = a.alpha * v.y;
+      }
+    }
+    if (det::last_arriver(a.cnt_b + (long long)seg * gridDim.x + blockIdx.x, gridDim.y, &lastf)) {
+      // dB rows [cb, cb + 256) of this segment: row blocks summed in order, added to dB
+      const float* base = a.slab_b + ((long long)seg * gridDim.x + blockIdx.x) * gridDim.y *
+                                         (256LL * a.r);
+      const int nc = min(256, NL - cb);
+      for (int i = threadIdx.x; i < nc * (J / 2); i += 256) {
+        const int cl = i / (J / 2), j = (i % (J / 2)) * 2;
+        const float2 v = det::sum_pairs(base + (long long)cl * a.r + j, 256LL * a.r, gridDim.y);
+        float* o = dB + (long long)(cb + cl) * a.r + j;
+        o[0] += a.alpha * v.x;
+        o[1] += a.alpha * v.y;
+      }
+    }
+    return;
   }
 #pragma unroll
   for (int cc = 0; cc < kDyCC; ++cc) {
@@ -607,6 +706,9 @@ struct DxaArgs {
   float da_scale, dx_scale;   // dA: keep-scale; dx: keep-scale (dZ already carries s)
   Drop drop;
   int probe;  // cost probe (0 in production): 64 dA atomics only when v == 1234.5
+  // deterministic dA sum (slab != nullptr; det.h): partials per (column block, row block)
+  // [R][128], the last row block of a column block adds their in-order sum into dA
+  float* slab; unsigned* cnt;
   // flash-attention delta hand-off (DELTA instantiation; x = the attention output O, dx = dO
   // once updated, 128-column blocks = heads): delta[c0 / 128][t] = sum_c dO[t][c] O[t][c] over
   // the block, written here so the attention backward skips its delta pass.
@@ -829,6 +931,30 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
     }
   }
   // dA flush: accumulator (row j = 16 jt + 4 g + r, column k = c0 + 32 wid + 16 m + L)
+  if (a.slab != nullptr) {
+    float* sp = a.slab + ((long long)blockIdx.x * gridDim.y + blockIdx.y) * (128LL * a.R);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kl = wid * 32 + m * 16 + L, j = jt * 16 + g * 4 + r;
+          if (c0 + kl < a.K && j < a.R) det::st_wt(sp + (long long)j * 128 + kl, da[m][jt][r]);
+        }
+    __shared__ int lastf;
+    if (!det::last_arriver(a.cnt + blockIdx.x, gridDim.y, &lastf)) return;
+    const float* base = a.slab + (long long)blockIdx.x * gridDim.y * (128LL * a.R);
+    for (int i = threadIdx.x; i < a.R * 64; i += 256) {  // pairs of columns
+      const int j = i / 64, kl = (i % 64) * 2;
+      if (c0 + kl >= a.K) continue;
+      const float2 v = det::sum_pairs(base + (long long)j * 128 + kl, 128LL * a.R, gridDim.y);
+      float* o = a.dA + (long long)j * a.ldda + c0 + kl;
+      o[0] += a.da_scale * v.x;
+      if (c0 + kl + 1 < a.K) o[1] += a.da_scale * v.y;
+    }
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -942,14 +1068,16 @@ extern "C" hipError_t lumen_lora3_down(int dtype, const void* x, long long ldx, 
                                        float alpha, unsigned long long seed, unsigned int thresh,
                                        float drop_scale, long long drop_ld, long long drop_col0,
                                        void* xe, long long ldxe, int xk, int KP, unsigned* cnt,
-                                       hipStream_t st) {
+                                       float* slab, hipStream_t st) {
   if (T <= 0 || K <= 0 || R < 16 || R > 64 || (R & 15) || (K & 7) || (ldx & 7) || (lda & 3))
     return hipErrorInvalidValue;
   if (xe != nullptr && (cnt == nullptr || (KP & 7) || KP < R || (ldxe & 7) || (xk & 7)))
     return hipErrorInvalidValue;
+  if (slab != nullptr && (cnt == nullptr || (ldz & 1)))
+    return hipErrorInvalidValue;
   lv3::DownArgs a{x, ldx, A, lda, Z, ldz, T, K, alpha,
                   {static_cast<unsigned>(seed) ^ static_cast<unsigned>(seed >> 32), thresh, drop_scale,
-                   drop_ld, drop_col0}, lv3_probe(), xe, ldxe, xk, KP, cnt};
+                   drop_ld, drop_col0}, lv3_probe(), xe, ldxe, xk, KP, cnt, slab};
   const dim3 grid((T + 63) / 64, (K + 1023) / 1024), block(512);
   const bool drop = thresh != 0;
 #define LV3_DOWN(TT, NJ)                                                                           \
@@ -1024,7 +1152,9 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
                                      const float* Z, long long ldz, float* dZ, long long lddz,
                                      float* dB, int T, int tw, float alpha, int nseg,
                                      const long long* n_off, const long long* r_off,
-                                     const long long* b_off, const int* n_len, hipStream_t st) {
+                                     const long long* b_off, const int* n_len, float* slab_z,
+                                     float* slab_b, unsigned* cnt_z, unsigned* cnt_b,
+                                     hipStream_t st) {
   if (T <= 0 || nseg < 1 || nseg > 4 || (r != 16 && r != 32 && r != 64) || tw < 64 || (tw & 63) ||
       (ldy & 7))
     return hipErrorInvalidValue;
@@ -1032,6 +1162,10 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
   a.probe = lv3_probe();
   a.dy = dy; a.ldy = ldy; a.B = B; a.r = r; a.Z = Z; a.ldz = ldz; a.dZ = dZ; a.lddz = lddz;
   a.dB = dB; a.T = T; a.TW = tw; a.alpha = alpha;
+  a.slab_z = slab_z; a.slab_b = slab_b; a.cnt_z = cnt_z; a.cnt_b = cnt_b;
+  if (slab_z != nullptr && (slab_b == nullptr || cnt_z == nullptr || cnt_b == nullptr ||
+                            (lddz & 1)))
+    return hipErrorInvalidValue;
   a.seg.nseg = nseg;
   int maxl = 0;
   for (int i = 0; i < 4; ++i) {
@@ -1101,7 +1235,7 @@ extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, v
                                       long long lda, float* dA, long long ldda, int T, int K,
                                       int R, int tw, unsigned long long seed, unsigned int thresh,
                                       float drop_scale, long long drop_ld, long long drop_col0,
-                                      float* delta, hipStream_t st) {
+                                      float* delta, float* slab, unsigned* cnt, hipStream_t st) {
   if (T <= 0 || K <= 0 || R < 16 || R > 64 || (R & 15) || (K & 7) || (ldx & 7) || (lddx & 7) ||
       (lda & 3) || tw < 64 || (tw & 63))
     return hipErrorInvalidValue;
@@ -1110,6 +1244,8 @@ extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, v
   a.probe = lv3_probe();
   a.x = x; a.ldx = ldx; a.dx = dx; a.lddx = lddx; a.dZ = dZ; a.A = A; a.lda = lda; a.dA = dA;
   a.ldda = ldda; a.T = T; a.K = K; a.R = R; a.TW = tw; a.delta = delta;
+  a.slab = slab; a.cnt = cnt;
+  if (slab != nullptr && (cnt == nullptr || (ldda & 1))) return hipErrorInvalidValue;
   const bool drop = thresh != 0;
   a.da_scale = drop ? drop_scale : 1.f;
   a.dx_scale = drop ? drop_scale : 1.f;

@@ -193,6 +193,28 @@ DELTA_HANDOFF = _os.environ.get("LUMEN_FA_DELTA_HANDOFF", "1") != "0"
 _DELTA_SLOT = [None]
 
 
+# Deterministic adapter reductions (VERDICT r5 Next #4; kernels/det.h): the v3 down / dY / dA
+# passes sum their cross-workgroup partials through write-through slabs and a last-arriver fixed
+# order instead of f32 atomics, so two runs with the same seed give bit-identical adapter
+# gradients.  Opt-in (LUMEN_LORA_DETERMINISTIC=1): it costs step time (profiles/r6_det).
+DETERMINISTIC = _os.environ.get("LUMEN_LORA_DETERMINISTIC", "0") == "1"
+_det: dict = {}
+
+
+def _det_ws(dev, nfloat: int, ncnt: int):
+    """(f32 slab workspace, zeroed int32 ticket counters) of the current stream on ``dev``;
+    counters are left zeroed by every launch, so they are shared by the kernels in stream order."""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    got = _det.get(key)
+    if got is None or got[0].numel() < nfloat or got[1].numel() < ncnt:
+        nf = max(nfloat, got[0].numel() if got is not None else 0, 1 << 20)
+        nc = max(ncnt, got[1].numel() if got is not None else 0, 4096)
+        got = (torch.empty(nf, dtype=torch.float32, device=dev),
+               torch.zeros(nc, dtype=torch.int32, device=dev))
+        _det[key] = got
+    return got
+
+
 def _v3_ok(r: int, R: int, segs, *mats) -> bool:
     """kernels/lora_v3.hip: ranks 16/32/64, up to 64 stacked adapter rows, 8-element aligned
     rows and segments, contiguous f32 adapter weights (checked by the caller)."""
@@ -205,9 +227,13 @@ def _lora3_down(x2d, A, Z, p, seed):
     """Z += drop(x) A^T (f32 [T, R])."""
     T, K = x2d.shape
     R = A.shape[0]
+    cnt = slab = None
+    if DETERMINISTIC and x2d.is_cuda:
+        slab, cnt = _det_ws(x2d.device, math.ceil(T / 64) * math.ceil(K / 1024) * 64 * R,
+                            math.ceil(T / 64))
     native().lora3_down(x2d, x2d.stride(0), A, Z, R, T, K, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
                         drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0,
-                        None, 0, 0, None)
+                        None, 0, 0, cnt, slab)
 
 
 def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope):
@@ -394,10 +420,19 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     dB = B.grad if (direct and need_dB) else ws[T * R + nA:].view(B.shape[0], r)
 
     def dy_pass():
-        for i in range(0, len(segs), 4):  # one pass over dY: dZ and dB (f32 atomics)
+        for i in range(0, len(segs), 4):  # one pass over dY: dZ and dB
             ch = segs[i:i + 4]
-            nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, _dy_tw(ch, T), scale,
-                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch])
+            tw_ = _dy_tw(ch, T)
+            ws = cnt = None
+            if DETERMINISTIC:
+                gx = math.ceil(max(sg[1] for sg in ch) / 256)
+                gy = math.ceil(T / tw_)
+                ns = len(ch)
+                ws, cnt = _det_ws(dev, ns * gy * gx * tw_ * r + ns * gx * gy * 256 * r,
+                                  ns * (gx + gy))
+            nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, tw_, scale,
+                         [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
+                         ws, cnt)
 
     if dx_fn is not None and BWD_OVERLAP and dy.is_cuda:
         # the dY pass (memory-bound, f32 atomics) beside the input-gradient GEMM (MFMA-bound):
@@ -417,6 +452,11 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
     dA = None
     if need_dA:
         dA = A.grad if direct else ws[T * R:T * R + nA].view(R, K)
+    if need_dA and dx is None and DXA and DETERMINISTIC and x2d.is_cuda:
+        # no input gradient wanted (the first layer): the fused pass still computes dA, its
+        # deterministic sum, and updates a throwaway dx (the atomic WGRAD fallback below would
+        # make dA order-dependent)
+        dx = torch.empty_like(x2d)
     if need_dA and dx is not None and DXA:
         # one pass over the [T, K] rows: dA from the staged x tiles, dx updated lane-locally
         tw = 256 if math.ceil(K / 128) * math.ceil(T / 256) >= 512 else 128
@@ -424,8 +464,12 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
         delta = None
         if slot is not None and R == 16 and K % 128 == 0 and dx.shape == x2d.shape:
             delta = torch.empty(K // 128, T, device=dev, dtype=torch.float32)
+        ws = cnt = None
+        if DETERMINISTIC:
+            ws, cnt = _det_ws(dev, math.ceil(K / 128) * math.ceil(T / tw) * 128 * R,
+                              math.ceil(K / 128))
         nat.lora3_dxa(x2d, dx, dZ, A, dA, tw, int(seed) & 0x7FFFFFFFFFFFFFFF, drop_threshold(p),
-                      1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, delta)
+                      1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, delta, ws, cnt)
         if delta is not None:
             slot["delta"], slot["key"] = delta, (dx.data_ptr(), dx._version)
     else:
