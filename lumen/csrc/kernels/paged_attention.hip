@@ -684,6 +684,33 @@ __global__ void __launch_bounds__(256) kv_dequant_kernel(
   }
 }
 
+// The PF kernel's inline-asm K / V loads are invisible to hipcc's register allocator, so a spill
+// or copy of a result before its counted wait would read stale data (scripts/tools/
+// check_asm_loads.py audits the code object).  The audit passes for D = 128 (every G) and G = 1
+// (every D); under the register pressure of D = 32 / 64 / 256 with G > 1 hipcc spills the loaded
+// registers right after the issue, so those shapes run the compiler-visible UNI kernel -- and
+// the PF form is not even instantiated for them.
+template <int D, int G>
+constexpr bool pa_pf_ok() { return D == 128 || G == 1; }
+
+template <typename T, int D, int G, typename KT>
+static void launch_pa_uni(bool pf, dim3 grid, hipStream_t st, void* out, const void* q,
+                          const void* kc, const void* vc, const int* bt, const int* cl, int nh,
+                          int qldh, int nkv, int BS, int max_blocks, int max_parts, float scale,
+                          float* tm, float* tl, void* to, int PART) {
+  if constexpr (pa_pf_ok<D, G>()) {
+    if (pf) {
+      hipLaunchKernelGGL((pa_decode1_kernel<T, D, G, KT, true, true>), grid, dim3(256), 0, st,
+                         (T*)out, (const T*)q, (const KT*)kc, (const KT*)vc, bt, cl, nh, qldh, nkv,
+                         BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((pa_decode1_kernel<T, D, G, KT, true>), grid, dim3(256), 0, st, (T*)out,
+                     (const T*)q, (const KT*)kc, (const KT*)vc, bt, cl, nh, qldh, nkv, BS,
+                     max_blocks, max_parts, scale, tm, tl, (float*)to, PART);
+}
+
 template <typename T, int D>
 static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out, const void* q,
                         const void* kc, const void* vc, const int* bt, const int* cl, int nh,
@@ -694,26 +721,16 @@ static void launch_pa_g(int G, dim3 grid, size_t smem, hipStream_t st, void* out
   const bool uni = one_pass >= 2 && BS == 256 / (D / 8) && PART % BS == 0;
   const bool pf = uni && one_pass == 3;
 #define LUMEN_PA_G(GG)                                                                         \
-  if (fp8kv && pf)                                                                              \
-    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8, true, true>), grid, dim3(256), 0, st,  \
-                       (T*)out, (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh,    \
-                       nkv, BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);         \
-  else if (pf)                                                                                  \
-    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, T, true, true>), grid, dim3(256), 0, st,    \
-                       (T*)out, (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, qldh, nkv,   \
-                       BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);              \
-  else if (fp8kv && uni)                                                                        \
-    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8, true>), grid, dim3(256), 0, st,        \
-                       (T*)out, (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh,    \
-                       nkv, BS, max_blocks, max_parts, scale, tm, tl, (float*)to, PART);         \
+  if (fp8kv && uni)                                                                             \
+    launch_pa_uni<T, D, GG, fp8>(pf, grid, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS,        \
+                                 max_blocks, max_parts, scale, tm, tl, to, PART);                \
   else if (fp8kv)                                                                               \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, fp8>), grid, dim3(256), 0, st, (T*)out,     \
                        (const T*)q, (const fp8*)kc, (const fp8*)vc, bt, cl, nh, qldh, nkv, BS,        \
                        max_blocks, max_parts, scale, tm, tl, (float*)to, PART);                 \
   else if (uni)                                                                                 \
-    hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG, T, true>), grid, dim3(256), 0, st, (T*)out, \
-                       (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, qldh, nkv, BS,          \
-                       max_blocks, max_parts, scale, tm, tl, (float*)to, PART);                 \
+    launch_pa_uni<T, D, GG, T>(pf, grid, st, out, q, kc, vc, bt, cl, nh, qldh, nkv, BS,          \
+                               max_blocks, max_parts, scale, tm, tl, to, PART);                  \
   else if (one_pass)                                                                            \
     hipLaunchKernelGGL((pa_decode1_kernel<T, D, GG>), grid, dim3(256), 0, st, (T*)out,          \
                        (const T*)q, (const T*)kc, (const T*)vc, bt, cl, nh, qldh, nkv, BS, max_blocks, \

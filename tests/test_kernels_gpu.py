@@ -1523,3 +1523,40 @@ def test_fused_mlp_autograd_matches_unfused(monkeypatch):
     assert calls == [1, 2], calls   # both fused kernels ran in mode 1, none in mode 0
     for a, b in zip(outs["1"], outs["0"]):
         assert ((a - b).norm() / b.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("D", [32, 64, 128, 256])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_paged_decode_uniform_variants_all_shapes(D, G):
+    """The uniform-block-id decode (LUMEN_PA_1PASS 2) and its pipelined inline-asm form (3) at
+    the block size that enables them (256 / (D / 8) rows), every head size and GQA group: the
+    pipelined form runs where scripts/tools/check_asm_loads.py passes (D = 128 or G = 1) and
+    falls back to variant 2 elsewhere -- both must match the fp32 reference at several
+    partition sizes."""
+    from lumen.ops.attention import paged_decode, paged_decode_ref, write_kv_cache
+
+    torch.manual_seed(D * 10 + G)
+    bs = 256 // (D // 8)
+    nkv = 2
+    nh = nkv * G
+    lens = torch.tensor([5 * bs + 3, 1, bs, 17 * bs - 1])
+    nseq, ctx = len(lens), int(lens.max())
+    maxb = (ctx + bs - 1) // bs
+    nblocks = nseq * maxb + 2
+    kc = torch.zeros(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    perm = torch.randperm(nblocks)[: nseq * maxb].view(nseq, maxb).int()
+    for i in range(nseq):
+        L = int(lens[i])
+        t = torch.arange(L)
+        slots = (perm[i, t // bs].long() * bs + t % bs).to(DEV)
+        write_kv_cache(torch.randn(L, nkv, D, device=DEV, dtype=torch.bfloat16),
+                       torch.randn(L, nkv, D, device=DEV, dtype=torch.bfloat16), kc, vc, slots)
+    q = torch.randn(nseq, nh, D, device=DEV, dtype=torch.bfloat16)
+    bt, cl = perm.to(DEV), lens.int().to(DEV)
+    scale = 1 / math.sqrt(D)
+    ref = paged_decode_ref(q, kc, vc, bt, cl, scale)
+    for part in (bs, 4 * bs, 512 if 512 % bs == 0 else 8 * bs):
+        for one in (2, 3):
+            got = paged_decode(q, kc, vc, bt, cl, ctx, scale, part, one_pass=one)
+            assert rel(got, ref) < 1e-2, (one, part)
