@@ -269,135 +269,14 @@ __device__ __forceinline__ void wait_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-// ---- ring variant: 5 slots of one 32-deep k half-step each (the whole 160 KiB LDS) ---------
-// A slot holds [W image 256 rows x 64 B | x image 256 rows x 64 B]; with 64-byte rows the 16-byte
-// chunk c of row r lives at chunk c ^ swz64(r), conflict-free for the ds_read_b128 lane groups
-// (searched over the bank model: rows r and r + 4 would otherwise share a bank slot).
-constexpr int SROWB = 64, SIMG = 256 * SROWB, SLOT_B = 2 * SIMG, NSLOT = 5;
-__device__ __forceinline__ int swz64(int r) { return (r >> 1) & 2; }
-
-// one slot (k range [k0, k0 + 32)) issued by one wave group: its wave wl (0-3) issues pieces wl,
-// wl + 4, ... of 16 rows x 64 B; pieces 0-15 = W image, 16-31 = x image
-template <typename T, int EPI>
-__device__ __forceinline__ void stage_slot(char* img, const Args& a, const T* xb, int mvalid,
-                                           int tn, int k0, int wl, int lane) {
-  const int rr = lane >> 2, c = lane & 3;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int p = wl + 4 * q;
-    if (q < 4) {
-      const int r = 16 * p + rr;
-      const int ch = c ^ swz64(r);
-      int wrow;
-      if constexpr (EPI == kSwiGLU) {
-        const int w = r & 63;
-        wrow = (w < 32 ? 0 : a.F) + tn * 128 + (r >> 6) * 32 + colperm(w & 31);
-      } else {
-        wrow = tn * BN + colperm(r);
-      }
-      const unsigned off =
-          (unsigned)(((long long)wrow * a.ldw + k0 + 8 * ch) * (long long)sizeof(T));
-      dma16(a.w, off, img + p * 16 * SROWB);
-    } else {
-      const int r = 16 * (p - 16) + rr;
-      const int ch = c ^ swz64(r);
-      const int m = min(r, mvalid - 1);
-      const unsigned off = (unsigned)(((long long)m * a.ldx + k0 + 8 * ch) * (long long)sizeof(T));
-      dma16(xb, off, img + p * 16 * SROWB);
-    }
-  }
-}
-
-// fragments of one k-step from its two slots (half-step s from slot s)
-template <typename T>
-__device__ __forceinline__ void read_frags_ring(const char* s0, const char* s1, int nrow0,
-                                                int mrow0, uint4 (&fa)[2][NI], uint4 (&fb)[2][MJ],
-                                                int lane) {
-  const int lr = lane & 15, lg = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const char* img = s ? s1 : s0;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int r = nrow0 + 16 * i + lr;
-      fa[s][i] = *reinterpret_cast<const uint4*>(img + r * SROWB + ((lg ^ swz64(r)) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      const int r = mrow0 + 16 * j + lr;
-      fb[s][j] = *reinterpret_cast<const uint4*>(img + SIMG + r * SROWB + ((lg ^ swz64(r)) << 4));
-    }
-  }
-}
-
-__device__ __forceinline__ int slot_next(int h) { return h == NSLOT - 1 ? 0 : h + 1; }
-
 // PROBE (cost split, plain store only; the output is garbage): bit 0 = no LDS-DMA after the
 // prologue, bit 1 = no fragment reads, bit 2 = no MFMAs.  LOOP: 0 plain two-stage loop, 1
-// ping-pong over two 64-deep stages, 2 ping-pong over the 5-slot ring
-// ---- quarter ring (LOOP 3): 10 slots of 128 rows x 128 B (16 KiB), the whole LDS ----------
-// stage k's quarters j = 0..3 are [x rows 0-127 | W rows 0-127 | W rows 128-255 | x rows 128-255]
-// in slots (4k + j) mod 10; a wave group's share of one quarter: its wave wl issues pieces
-// wl, wl + 4, wl + 8, wl + 12 (8 rows each)
-constexpr int QB = 128 * ROWB, NQ = 10;
-
-template <typename T, int EPI>
-__device__ __forceinline__ void stage_quarter(char* img, int j, const Args& a, const T* xb,
-                                              int mvalid, int tn, int k0, int wl, int lane) {
-  const int rr = lane >> 3, c = lane & 7;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int p = wl + 4 * q;
-    const int r = 8 * p + rr;  // row within the quarter
-    const int ch = c ^ swz(r);
-    unsigned off;
-    const void* base;
-    if (j == 1 || j == 2) {
-      const int rw = r + (j == 2 ? 128 : 0);  // W image row
-      int wrow;
-      if constexpr (EPI == kSwiGLU) {
-        const int w = rw & 63;
-        wrow = (w < 32 ? 0 : a.F) + tn * 128 + (rw >> 6) * 32 + colperm(w & 31);
-      } else {
-        wrow = tn * BN + colperm(rw);
-      }
-      off = (unsigned)(((long long)wrow * a.ldw + k0 + 8 * ch) * (long long)sizeof(T));
-      base = a.w;
-    } else {
-      const int m = min(r + (j == 3 ? 128 : 0), mvalid - 1);
-      off = (unsigned)(((long long)m * a.ldx + k0 + 8 * ch) * (long long)sizeof(T));
-      base = xb;
-    }
-    dma16(base, off, img + p * 8 * ROWB);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void read_frags_q(const char* xq, const char* wq, int wrow0,
-                                             uint4 (&fa)[2][NI], uint4 (&fb)[2][MJ], int lane) {
-  const int lr = lane & 15, lg = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int r = wrow0 + 16 * i + lr;
-      fa[s][i] = *reinterpret_cast<const uint4*>(wq + r * ROWB + (((4 * s + lg) ^ swz(r)) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      const int r = 16 * j + lr;
-      fb[s][j] = *reinterpret_cast<const uint4*>(xq + r * ROWB + (((4 * s + lg) ^ swz(r)) << 4));
-    }
-  }
-}
-
-__device__ __forceinline__ int qslot(int k, int j) { return (4 * k + j) % NQ; }
-
+// ping-pong over two 64-deep stages.  (Two LDS rings -- 5 half-step slots of 64-byte rows, and 10
+// quarter slots -- were measured 1.22-1.25x the library and removed: profiles/r6_mlp_gemm.)
 template <typename T, int EPI, int LOOP, int PROBE = 0>
 __global__ void __launch_bounds__(NT, 1) mlp_gemm_kernel(Args a) {
   constexpr bool PP = LOOP == 1;
-  __shared__ __attribute__((aligned(16))) char lds[LOOP == 2 ? NSLOT * SLOT_B
-                                                   : LOOP == 3 ? NQ * QB : NSTAGE * STAGE_B];
+  __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE_B];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // XCD-aware bijective remap: blocks are dealt round-robin over the 8 XCDs, so XCD x gets the
@@ -434,150 +313,7 @@ __global__ void __launch_bounds__(NT, 1) mlp_gemm_kernel(Args a) {
   const int kb = slice == 1 ? nk_all / 2 : 0;
   const int nk = slice < 0 ? nk_all : slice == 0 ? nk_all / 2 : nk_all - nk_all / 2;
   const int kofs = kb * BK;
-  if constexpr (LOOP == 3) {
-    // Ping-pong (as LOOP 1) over the quarter ring.  A quarter is refilled only after the
-    // barrier that follows every wave's reads of it: x0 (read by group 0 in interval 2k) and W0
-    // (read by both groups by the end of 2k + 1) ... Stage k + 2 goes into slots freed at:
-    // x0, W0 -> stage k - 1's W1 / x1 slots (free from interval 2k), W1 -> stage k's x0 slot
-    // (free from 2k + 1), x1 -> stage k's W0 slot (free from 2k + 2).  Issuers: group 0 issues
-    // x0 + W0 of stage k + 2 at the start of interval 2k; group 1 W1 at the start of 2k + 1 and
-    // x1 at the start of 2k + 2.  Each group's vmcnt(8) before a barrier retires its quarters
-    // issued one step earlier: 3-4 intervals of load latency cover instead of 1.5-2.
-    uint4 fa[2][NI], fb[2][MJ];
-    const bool g1 = wid >= 4;
-    const int wl = wid & 3;
-    const int wq_j = 1 + (wn >> 1), wrow0 = (wn & 1) * 64;  // this wave's W quarter and rows
-    const int xq_j = g1 ? 3 : 0;
-    // prologue: stages 0 and 1; group 0 x0 / W0, group 1 W1 / x1 of each
-    for (int st = 0; st < 2 && st < nk; ++st) {
-      for (int j = 0; j < 4; ++j)
-        if ((j < 2) != g1)
-          stage_quarter<T, EPI>(lds + qslot(st, j) * QB, j, a, xb, mvalid, tn, st * BK, wl, lane);
-    }
-    wait_vm<0>();
-    bar();
-    if (!g1) {
-      for (int k = 0; k < nk; ++k) {
-        // interval 2k: issue x0 / W0 of stage k + 2; load step k
-        const bool more = k + 2 < nk && !(PROBE & 1);
-        if (more) {
-          stage_quarter<T, EPI>(lds + qslot(k + 2, 0) * QB, 0, a, xb, mvalid, tn, (k + 2) * BK,
-                                wl, lane);
-          stage_quarter<T, EPI>(lds + qslot(k + 2, 1) * QB, 1, a, xb, mvalid, tn, (k + 2) * BK,
-                                wl, lane);
-        }
-        if (!(PROBE & 2))
-          read_frags_q<T>(lds + qslot(k, xq_j) * QB, lds + qslot(k, wq_j) * QB, wrow0, fa, fb,
-                          lane);
-        wait_lds();
-        bar();
-        // interval 2k + 1: compute step k; x0 / W0 of stage k + 1 have landed
-        if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
-        if (more) wait_vm<8>(); else wait_vm<0>();
-        bar();
-      }
-    } else {
-      // after the prologue (all retired) this group issues W1(s) in interval 2s - 3 and x1(s)
-      // in 2s - 2 (s >= 2); it retires x1(k) before the barrier ending interval 2k (it reads it
-      // in 2k + 1) and W1(k + 1) before the barrier ending 2k + 1 (group 0 reads it in 2k + 2)
-      for (int k = 0; k < nk; ++k) {
-        // interval 2k: issue x1 of stage k + 1 (its slot, stage k - 1's W0, is free now);
-        // compute step k - 1
-        const bool x1_next = k >= 1 && k + 1 < nk && !(PROBE & 1);
-        if (x1_next)
-          stage_quarter<T, EPI>(lds + qslot(k + 1, 3) * QB, 3, a, xb, mvalid, tn, (k + 1) * BK,
-                                wl, lane);
-        if (k > 0) {
-          if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
-        }
-        if (x1_next) wait_vm<8>(); else wait_vm<0>();  // x1(k) landed (younger: W1, x1 of k+1)
-        bar();
-        // interval 2k + 1: issue W1 of stage k + 2 (its slot, stage k's x0, is free now);
-        // load step k; retire W1(k + 1)
-        const bool w1_next = k + 2 < nk && !(PROBE & 1);
-        if (w1_next)
-          stage_quarter<T, EPI>(lds + qslot(k + 2, 2) * QB, 2, a, xb, mvalid, tn, (k + 2) * BK,
-                                wl, lane);
-        if (!(PROBE & 2))
-          read_frags_q<T>(lds + qslot(k, xq_j) * QB, lds + qslot(k, wq_j) * QB, wrow0, fa, fb,
-                          lane);
-        wait_lds();
-        // younger than W1(k + 1): x1(k + 1) (issued in 2k when k >= 1) and W1(k + 2)
-        if (w1_next) {
-          if (x1_next) wait_vm<8>(); else wait_vm<4>();
-        } else if (x1_next) {
-          wait_vm<4>();
-        } else {
-          wait_vm<0>();
-        }
-        bar();
-      }
-      if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
-    }
-  } else if constexpr (LOOP == 2) {
-    // Ping-pong as LOOP 1, over a ring of 5 half-step slots: step k reads slots 2k, 2k + 1
-    // (mod 5) in intervals 2k (group 0) and 2k + 1 (group 1).  Group 0 issues slot 2k + 4 at
-    // the start of interval 2k (that slot was last read in interval 2k - 1), group 1 slot
-    // 2k + 5 at the end of interval 2k + 1 after its own reads; each group waits (counted
-    // vmcnt: the slot it issued one step earlier) before the barrier that ends interval 2k + 1,
-    // so 1.5 steps of loads (96 KiB per CU) stay in flight instead of one.
-    uint4 fa[2][NI], fb[2][MJ];
-    const bool g1 = wid >= 4;
-    const int wl = wid & 3;
-    const int nh = 2 * nk;  // half-steps
-    // prologue: group 0 issues slots 0 and 2, group 1 slots 1 and 3; slots 0 and 1 land first
-    stage_slot<T, EPI>(lds + (g1 ? 1 : 0) * SLOT_B, a, xb, mvalid, tn, (g1 ? 1 : 0) * 32, wl, lane);
-    if ((g1 ? 3 : 2) < nh) {
-      stage_slot<T, EPI>(lds + (g1 ? 3 : 2) * SLOT_B, a, xb, mvalid, tn, (g1 ? 3 : 2) * 32, wl,
-                         lane);
-      wait_vm<8>();
-    } else {
-      wait_vm<0>();
-    }
-    bar();
-    int h0 = 0;  // slot of half-step 2k
-    if (!g1) {
-      for (int k = 0; k < nk; ++k) {
-        const int h1 = slot_next(h0), h2 = slot_next(h1), h3 = slot_next(h2), h4 = slot_next(h3);
-        // interval 2k: load step k; issue half-step 2k + 4
-        if (!(PROBE & 2))
-          read_frags_ring<T>(lds + h0 * SLOT_B, lds + h1 * SLOT_B, nrow0, mrow0, fa, fb, lane);
-        const bool more = 2 * k + 4 < nh;
-        if (more && !(PROBE & 1))
-          stage_slot<T, EPI>(lds + h4 * SLOT_B, a, xb, mvalid, tn, (2 * k + 4) * 32, wl, lane);
-        wait_lds();
-        bar();
-        // interval 2k + 1: compute step k; half-step 2k + 2 (this group's) must have landed
-        if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
-        if (more && !(PROBE & 1)) wait_vm<8>(); else wait_vm<0>();
-        bar();
-        h0 = h2;
-      }
-    } else {
-      for (int k = 0; k < nk; ++k) {
-        const int h1 = slot_next(h0), h2 = slot_next(h1);
-        // interval 2k: compute step k - 1
-        if (k > 0) {
-          if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
-        }
-        bar();
-        // interval 2k + 1: load step k; issue half-step 2k + 5 into slot h0 (= 2k + 5 mod 5)
-        if (!(PROBE & 2))
-          read_frags_ring<T>(lds + h0 * SLOT_B, lds + h1 * SLOT_B, nrow0, mrow0, fa, fb, lane);
-        wait_lds();
-        const bool more = 2 * k + 5 < nh;
-        if (more && !(PROBE & 1)) {
-          stage_slot<T, EPI>(lds + h0 * SLOT_B, a, xb, mvalid, tn, (2 * k + 5) * 32, wl, lane);
-          wait_vm<8>();  // half-step 2k + 3 landed
-        } else {
-          wait_vm<0>();
-        }
-        bar();
-        h0 = h2;
-      }
-      if (!(PROBE & 4)) mfma_step<T>(fa, fb, acc); else keep_live(fa, fb);
-    }
-  } else if constexpr (!PP) {
+  if constexpr (!PP) {
     stage<T, EPI>(lds, a, xb, mvalid, tn, 0, wid, lane);
     for (int kt = 0; kt < nk; ++kt) {
       wait_vm<0>();   // this wave's pieces of stage kt have landed
@@ -821,9 +557,9 @@ extern "C" hipError_t lumen_mlp_gemm(int dtype, int epi, const void* x, long lon
                                      int M, int N, int K, int F, int group_m, float* ws, int* cnt,
                                      int split, hipStream_t st) {
   using namespace lumen::mg;
-  // bit 4: the plain two-stage loop; bit 8: ping-pong over the quarter ring; bit 9: ping-pong
-  // over the half-step ring (A/B probes); default: ping-pong over two stages
-  const int loop = (epi & 16) ? 0 : (epi & 256) ? 3 : (epi & 512) ? 2 : 1;
+  // bit 4: the plain two-stage loop (A/B probe); default: ping-pong over two stages
+  if (epi & ~(15 | 16 | (7 << 5))) return hipErrorInvalidValue;
+  const int loop = (epi & 16) ? 0 : 1;
   const int probe_bits = epi & (7 << 5);  // bits 5-7: cost-split probe builds (plain store)
   epi &= 15;
   if (M < 1 || K < BK || K % BK || group_m < 1 || ldx < K || ldw < K || ldx % 8 || ldw % 8 ||
@@ -855,13 +591,9 @@ extern "C" hipError_t lumen_mlp_gemm(int dtype, int epi, const void* x, long lon
   Args a{x, w, c, act, gu, ldx, ldw, ldc, ldact, ldgu, M, N, K, F, tiles_m, tiles_n, group_m,
          tiles_m * tiles_n - split, split, ws, cnt};
   if (dtype == lumen::kBF16)
-    return loop == 3   ? launch<lumen::bf16, 3>(epi | probe_bits, a, st)
-           : loop == 2 ? launch<lumen::bf16, 2>(epi | probe_bits, a, st)
-           : loop == 1 ? launch<lumen::bf16, 1>(epi | probe_bits, a, st)
+    return loop == 1 ? launch<lumen::bf16, 1>(epi | probe_bits, a, st)
                        : launch<lumen::bf16, 0>(epi, a, st);
   if (dtype == lumen::kF16)
-    return loop == 3   ? launch<lumen::fp16, 3>(epi, a, st)
-           : loop == 2 ? launch<lumen::fp16, 2>(epi, a, st)
-           : loop == 1 ? launch<lumen::fp16, 1>(epi, a, st) : launch<lumen::fp16, 0>(epi, a, st);
+    return loop == 1 ? launch<lumen::fp16, 1>(epi, a, st) : launch<lumen::fp16, 0>(epi, a, st);
   return hipErrorInvalidValue;
 }
