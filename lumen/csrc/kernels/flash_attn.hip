@@ -748,7 +748,7 @@ __device__ __forceinline__ float xor32_sum(float v) {
   return a + b;
 }
 
-template <typename T, bool CAUSAL, bool MASK, int PR = 0>
+template <typename T, bool CAUSAL, bool MASK>
 __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, const Off32& off,
                                            const uint4 (&qf)[8], f32x16 (&acc)[4], float& m_i,
                                            float& l_i, int kv0, int L, int qrow, int hi,
@@ -784,17 +784,6 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
     vr[1][n] = tr32a<1>(vb, off, n);
     vr[2][n] = tr32a<2>(vb, off, n);
     vr[3][n] = tr32a<3>(vb, off, n);
-  }
-  if (PR == 5) {  // cost probe: no softmax
-    const uint4 pb[4] = {pack8<T>(st[0], 0), pack8<T>(st[0], 1), pack8<T>(st[1], 0),
-                         pack8<T>(st[1], 1)};
-#pragma unroll
-    for (int sl = 0; sl < 4; ++sl) {
-      lgkm_wait(vr[sl][0], vr[sl][1], vr[sl][2], vr[sl][3]);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) acc[n] = Mfma32<T>::run(as_u4(vr[sl][n]), pb[sl], acc[n]);
-    }
-    return;
   }
   float mx = -INFINITY;
 #pragma unroll
@@ -845,10 +834,9 @@ __device__ __forceinline__ void fwd32_tile(const char* kimg, const char* vimg, c
   }
 }
 
-// PROBE (cost split, LUMEN_FA_PROBE; never the default): 1 = key loop without the tile math
-// (loads, waits and barriers only), 2 = key loop without the K / V loads (math on stale LDS),
-// 3 = no key loop (Q load, first K / V tile, O / LSE stores), 5 = tile math without the softmax
-template <typename T, bool CAUSAL, bool PAGED = false, int PROBE = 0>
+// (Cost-split probe builds of this kernel -- key loop without the tile math, without the K / V
+// loads, no key loop, no softmax -- produced profiles/r5_fa and were removed afterwards.)
+template <typename T, bool CAUSAL, bool PAGED = false>
 __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   constexpr int BM = 128;
   // Two SEPARATE LDS objects for the ping-pong K|V buffers, with the loop unrolled by two so
@@ -918,26 +906,25 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   }
   // one K/V tile: prefetch the next into `nxt`, wait for `cur`, compute, release `cur`
   auto tile = [&](char* cur, char* nxt, int kv0) {
-    if (PROBE == 2) {
-    } else if (kv0 + BN < kv_end) {
+    if (kv0 + BN < kv_end) {
       stage(nxt, kv0 + BN);
       wait_vm_8();
     } else {
       wait_vm_all();
     }
     lds_fence_barrier();
-    if (PROBE != 1 && kv0 < w_end) {  // (causal: tiles entirely above this wave's rows are skipped)
+    if (kv0 < w_end) {  // (causal: tiles entirely above this wave's rows are skipped)
       const bool need_mask = (kv0 + BN > Lk) || (CAUSAL && kv0 + BN - 1 > wq0 + qoff);
       if (need_mask)
-        fwd32_tile<T, CAUSAL, true, PROBE>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos,
+        fwd32_tile<T, CAUSAL, true>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos,
                                            hi, a.scale_log2);
       else
-        fwd32_tile<T, CAUSAL, false, PROBE>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos,
+        fwd32_tile<T, CAUSAL, false>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, Lk, qpos,
                                             hi, a.scale_log2);
     }
     lds_fence_barrier();  // every wave is done with `cur` before it is refilled
   };
-  for (int kv0 = 0; kv0 < (PROBE == 3 ? 0 : kv_end); kv0 += 2 * BN) {
+  for (int kv0 = 0; kv0 < kv_end; kv0 += 2 * BN) {
     tile(bufA, bufB, kv0);
     if (kv0 + BN < kv_end) tile(bufB, bufA, kv0 + BN);
   }
@@ -994,154 +981,9 @@ __global__ void __launch_bounds__(256, CAUSAL ? 2 : 1) fwd32_kernel(Args a) {
   }
 }
 
-// stage64_async_s for a 512-thread workgroup: wave w fills image rows [8w, 8w + 8) in 2 DMA
-// instructions (saddr + voffset form, as stage64_async_s)
-template <typename T>
-__device__ __forceinline__ void stage64_async8_s(char* img, const T* base, long long ld, int r0,
-                                                 int rmax) {
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const char* tile = reinterpret_cast<const char*>(base + (long long)r0 * ld);
-  const int last = rmax - 1 - r0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wid * 2 + i) * 4 + (lane >> 4);
-    const int ch = (lane & 15) ^ swz(row);
-    const unsigned off = (unsigned)((row < last ? row : last) * (int)ld + ch * 8) * sizeof(T);
-    __builtin_amdgcn_global_load_lds(
-        (const void*)(tile + off),
-        (__attribute__((address_space(3))) void*)(img + (wid * 2 + i) * 1024), 16, 0, 0);
-  }
-}
-
-// ---- forward, 256-query tiles (LUMEN_FA_FWD256=1, mt 21) --------------------------------------
-// fwd32_kernel's per-wave tile math with 8 waves (32 queries each) per workgroup and ONE
-// workgroup per CU: every K / V tile staged into LDS serves 256 queries instead of 128, which
-// cuts the K / V bytes a causal sequence streams through the CUs by ~40 % (S = 512: 12 instead of
-// 20 tile loads per (sequence, head)); profiles/r5_fa measured the 128-row kernel bound by that
-// traffic (key loop without math 32.6 of 40.5 us).  Three [K | V] buffers: the Q block (64 KiB)
-// lands in B + C beside tile 0 in A; then a ring A -> B -> C with two tiles in flight.
-template <int N>
-__device__ __forceinline__ void wait_vm_n() { __builtin_amdgcn_s_waitcnt(0xF70 | N); }
-
-template <typename T, bool CAUSAL>
-__global__ void __launch_bounds__(512, 1) fwd256_kernel(Args a) {
-  constexpr int BM = 256;
-  __shared__ __attribute__((aligned(16))) char bufA[2 * IMG];  // [K | V]
-  __shared__ __attribute__((aligned(16))) char bufB[2 * IMG];
-  __shared__ __attribute__((aligned(16))) char bufC[2 * IMG];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int lq = lane & 31, hi = lane >> 5;
-  auto run = [&](const int seq, const int q0, const int head) {
-  const int kvh = head / (a.nh / a.nkv);
-  const int s0 = a.cu[seq], L = a.cu[seq + 1] - s0;
-  const T* Q = reinterpret_cast<const T*>(a.q) + (long long)s0 * a.ldq + head * D;
-  const T* K = reinterpret_cast<const T*>(a.k) + (long long)s0 * a.ldk + kvh * D;
-  const T* V = reinterpret_cast<const T*>(a.v) + (long long)s0 * a.ldv + kvh * D;
-  const int wq0 = q0 + wid * 32;
-  const int qrow = wq0 + lq;
-  Off32 off;
-  make_off32(off, lane);
-  f32x16 acc[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) acc[n] = zero16();
-  float m_i = -INFINITY, l_i = 0.f;
-  const int kv_end = CAUSAL ? min(L, q0 + BM) : L;
-  const int w_end = CAUSAL ? min(kv_end, wq0 + 32) : kv_end;
-  auto stage = [&](char* img, int r0) {  // 4 DMA instructions per wave
-    stage64_async8_s(img, K, a.ldk, r0, L);
-    stage64_async8_s(img + IMG, V, a.ldv, r0, L);
-  };
-  uint4 qf[8];
-  {
-    // Q rows [q0, q0 + 256) -> B (rows 0-127) and C (128-255), 2 DMA instructions per wave per
-    // 64-row image; rows >= L are clamped duplicates (never stored)
-    stage64_async8_s(bufB, Q, a.ldq, q0, L);
-    if (q0 + 64 < L) stage64_async8_s(bufB + IMG, Q, a.ldq, q0 + 64, L);
-    if (q0 + 128 < L) stage64_async8_s(bufC, Q, a.ldq, q0 + 128, L);
-    if (q0 + 192 < L) stage64_async8_s(bufC + IMG, Q, a.ldq, q0 + 192, L);
-    if (kv_end > 0) {
-      stage(bufA, 0);
-      wait_vm_n<4>();  // this wave's Q pieces landed (the newest 4 are tile 0)
-    } else {
-      wait_vm_all();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const int r = 32 * wid + lq;  // row of the 256-row Q block
-    const char* qi = (r < 128 ? bufB : bufC) + ((r >> 6) & 1) * IMG;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = row_read(qi, r & 63, 2 * ks + hi);
-    lds_fence_barrier();  // B and C are the next prefetch targets
-    if (BN < kv_end) stage(bufB, BN);
-  }
-  // tile at kv0 in `cur`; tile kv0 + 2 BN is prefetched into `pre` (the buffer tile kv0 - BN
-  // used, released by the barrier that closed it)
-  auto tile = [&](char* cur, char* pre, int kv0) {
-    if (kv0 + 2 * BN < kv_end) {
-      stage(pre, kv0 + 2 * BN);
-      wait_vm_n<8>();
-    } else if (kv0 + BN < kv_end) {
-      wait_vm_n<4>();
-    } else {
-      wait_vm_all();
-    }
-    lds_fence_barrier();
-    if (kv0 < w_end) {
-      const bool need_mask = (kv0 + BN > L) || (CAUSAL && kv0 + BN - 1 > wq0);
-      if (need_mask)
-        fwd32_tile<T, CAUSAL, true>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
-                                    a.scale_log2);
-      else
-        fwd32_tile<T, CAUSAL, false>(cur, cur + IMG, off, qf, acc, m_i, l_i, kv0, L, qrow, hi,
-                                     a.scale_log2);
-    }
-    lds_fence_barrier();
-  };
-  for (int kv0 = 0; kv0 < kv_end; kv0 += 3 * BN) {
-    tile(bufA, bufC, kv0);
-    if (kv0 + BN < kv_end) tile(bufB, bufA, kv0 + BN);
-    if (kv0 + 2 * BN < kv_end) tile(bufC, bufB, kv0 + 2 * BN);
-  }
-  // epilogue as fwd32_kernel: each wave's 32 x 128 tile through 8 KiB of LDS (waves 0-3 in A,
-  // 4-7 in B; both free after the loop's last barrier), out as whole 256-byte rows
-  {
-    int ln = threadIdx.x;
-    asm volatile("" : "+v"(ln));
-    const int lq2 = ln & 31, hi2 = (ln >> 5) & 1;
-    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
-    char* ot = (wid < 4 ? bufA : bufB) + (wid & 3) * 8192;
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        struct alignas(8) O4 { T v[4]; } o4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o4.v[i] = from_f32<T>(acc[n][4 * j + i] * inv);
-        *reinterpret_cast<O4*>(ot + img_off(lq2, 4 * n + j) + 8 * hi2) = o4;
-      }
-    if (hi == 0 && a.lse && qrow < L)
-      a.lse[(long long)head * a.T + s0 + qrow] = l_i > 0.f ? m_i + __log2f(l_i) : INFINITY;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    T* O = reinterpret_cast<T*>(a.o) + (long long)s0 * a.ldo + head * D;
-    const int ch = ln & 15;
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int r = 4 * it + ((ln >> 4) & 3);
-      const uint4 v = *reinterpret_cast<const uint4*>(ot + img_off(r, ch));
-      if (wq0 + r < L) *reinterpret_cast<uint4*>(O + (long long)(wq0 + r) * a.ldo + ch * 8) = v;
-    }
-  }
-  lds_fence_barrier();  // the next item refills A / B / C
-  };
-  // persistent: snake order over the heaviest-first item list (as fwd32_kernel)
-  const int G = gridDim.x, w = blockIdx.x;
-  for (int base = 0; base < a.nitems; base += G) {
-    const int it = (a.snake && ((base / G) & 1)) ? base + G - 1 - w : base + w;
-    if (it >= a.nitems) continue;
-    const int ti = it / a.nh;
-    run(a.tiles[2 * ti], a.tiles[2 * ti + 1], it - ti * a.nh);
-  }
-}
+// (A 256-query-tile forward -- 8 waves, one workgroup per CU, a 3-buffer K / V ring -- measured
+// 48.5 vs 39.9 us per call and 90.30 vs 90.20 ms per step, profiles/r5_fa, and was removed: with
+// one workgroup per CU the two waves of a SIMD run their MFMA and softmax phases in lockstep.)
 
 template <typename T, bool CAUSAL, bool MASK>
 __device__ __forceinline__ void dq32_tile(const char* kimg, const char* vimg, const Off32& off,
@@ -1400,21 +1242,11 @@ static int cu_count() {
 template <typename T>
 static hipError_t launch(int which, int causal, int mt, int ntiles, const Args& a, hipStream_t st) {
   dim3 block(256);
-  if (which == 0 && mt == 21) {  // forward, 256-row tiles (persistent only: a.nitems > 0)
-    if (a.nitems <= 0) return hipErrorInvalidValue;
-    dim3 grid(std::min(a.nitems, cu_count()), 1), block8(512);
-    if (causal) hipLaunchKernelGGL((fwd256_kernel<T, true>), grid, block8, 0, st, a);
-    else hipLaunchKernelGGL((fwd256_kernel<T, false>), grid, block8, 0, st, a);
-  } else if (which == 0) {  // forward: 32x32x16 kernel, 128-row tiles
+  if (which == 0) {  // forward: 32x32x16 kernel, 128-row tiles
     if (mt != 20) return hipErrorInvalidValue;
     dim3 grid(ntiles, a.tiles3 ? 1 : a.nh);
     if (a.nitems > 0) grid = dim3(std::min(a.nitems, (causal ? 2 : 1) * cu_count()), 1);
-    static const int probe = [] { const char* e = std::getenv("LUMEN_FA_PROBE"); return e ? std::atoi(e) : 0; }();
-    if (causal && probe == 1) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 1>), grid, block, 0, st, a);
-    else if (causal && probe == 2) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 2>), grid, block, 0, st, a);
-    else if (causal && probe == 3) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 3>), grid, block, 0, st, a);
-    else if (causal && probe == 5) hipLaunchKernelGGL((fwd32_kernel<T, true, false, 5>), grid, block, 0, st, a);
-    else if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
+    if (causal) hipLaunchKernelGGL((fwd32_kernel<T, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((fwd32_kernel<T, false>), grid, block, 0, st, a);
   } else if (which == 1) {
     dim3 grid((unsigned)((a.T + 3) / 4));
@@ -1497,10 +1329,6 @@ extern "C" hipError_t lumen_flash_attn(int dtype, int which, int causal, int mt,
   a.kv_lens = nullptr; a.block_tables = nullptr; a.bt_stride = 0; a.block_size = 0;
   a.ds = nullptr; a.ds_off = nullptr; a.ds_total = 0; a.tiles3 = tiles3;
   a.nitems = (which == 0 && mt == 20 && !tiles3 && (fa_persist() & 2)) ? ntiles * nh : 0;
-  if (which == 0 && mt == 21) {  // the 256-row forward is persistent-only, 1-D (seq, row) tiles
-    if (tiles3) return hipErrorInvalidValue;
-    a.nitems = ntiles * nh;
-  }
   a.snake = (fa_persist() >> 3) & 1;
   if (which == 6 || which == 7 || which == 8) return hipErrorInvalidValue;  // other entries
   if (dtype == lumen::kBF16) return lumen::fa::launch<lumen::bf16>(which, causal, mt, ntiles, a, st);

@@ -329,10 +329,7 @@ import os as _os
 # forward: the 32x32x16 MFMA kernel, 32 queries per wave, 128-row tiles (56 vs 71 us for the
 # 16x16x32 forms at B8 S512, profiles/r02_fa; those variants were removed)
 FA_FWD_MT, FA_FWD_ROWS = 20, 128
-# LUMEN_FA_FWD256=1: the 8-wave, 256-query-tile forward (mt 21, persistent, one workgroup per
-# CU): each staged K / V tile serves twice the queries (profiles/r5_fa)
-if _os.environ.get("LUMEN_FA_FWD256", "0") == "1":
-    FA_FWD_MT, FA_FWD_ROWS = 21, 256
+# (a 256-query-tile forward, mt 21, measured slower and was removed: profiles/r5_fa)
 # backward: 16x16x32 dK/dV (64-key tiles) + 32x32x16 dQ (128-query tiles), or -- while the buffer
 # fits -- the dS hand-off pair below
 # dS hand-off: the dK/dV kernel stores dS per 64x64 tile and the dQ kernel forms
