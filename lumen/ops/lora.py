@@ -178,6 +178,7 @@ def _zeros(*shape, device, train: bool = False):
 
 USE_V3 = _os.environ.get("LUMEN_LORA_V3", "1") != "0"
 DY_TW = int(_os.environ.get("LUMEN_LORA_DY_TW", "0"))  # dY rows per block of lora3_dy (0 = auto)
+DXA_TW = int(_os.environ.get("LUMEN_LORA_DXA_TW", "0"))  # x rows per block of lora3_dxa (0 = auto)
 # per-call A/B (scripts/probes/lora_kernels.py, us): the v3 UP write-back was on par with v2
 # without RoPE (o_proj 15.0 vs 14.3) and slower with it (q|k|v 55.7 vs 45.6), so v2 is the
 # forward UP; v3's DOWN (17.3 vs 21.9), fused dY pass (32.5 vs 53.3) and dx update win.  A
@@ -459,7 +460,7 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
         dx = torch.empty_like(x2d)
     if need_dA and dx is not None and DXA:
         # one pass over the [T, K] rows: dA from the staged x tiles, dx updated lane-locally
-        tw = 256 if math.ceil(K / 128) * math.ceil(T / 256) >= 512 else 128
+        tw = DXA_TW or (256 if math.ceil(K / 128) * math.ceil(T / 256) >= 512 else 128)
         slot = _DELTA_SLOT[0]
         delta = None
         if slot is not None and R == 16 and K % 128 == 0 and dx.shape == x2d.shape:
