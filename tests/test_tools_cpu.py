@@ -531,3 +531,34 @@ def test_bench_wall_budget_skips_sections_torchrun():
     assert {"comm_probe", "zero3_release", "zero3_hybrid"} <= skipped, x["budget"]
     assert x["comm"] is None and x["zero3_release"]["skipped"] == "wall budget"
     assert x["budget"]["ran"] == [] and x["budget"]["wall_budget_s"] == 1.0
+
+
+def test_box_hwmon_sampler_reads_fake_sysfs(tmp_path):
+    """extra.box's clock / power sampler (lumen/utils/boxcal.py) on a fake hwmon directory:
+    SCLK from freq1_input (Hz), power from power1_average (uW), summarised as mean / min / p50 /
+    max; a missing hwmon (CPU runs, containers without sysfs) yields an empty record, no thread."""
+    import time as _time
+
+    from lumen.utils.boxcal import HwmonSampler, gpu_hwmon, summarize
+
+    hw = tmp_path / "hwmon7"
+    hw.mkdir()
+    (hw / "freq1_input").write_text("1900000000\n")
+    (hw / "power1_average").write_text("1350000000\n")
+    smp = HwmonSampler(str(hw), period_s=0.002).start()
+    _time.sleep(0.05)
+    (hw / "freq1_input").write_text("2000000000\n")
+    _time.sleep(0.05)
+    rec = smp.stop()
+    assert rec["hwmon"] == str(hw) and rec["samples"] >= 4
+    assert rec["sclk_mhz_min"] == 1900.0 and rec["sclk_mhz_max"] == 2000.0
+    assert 1900.0 <= rec["sclk_mhz_mean"] <= 2000.0
+    assert rec["power_w_mean"] == 1350.0 and rec["power_w_max"] == 1350.0
+    # no hwmon: nothing sampled, no thread started
+    none = HwmonSampler(None).start()
+    assert none._t is None and none.stop() == {"hwmon": None, "samples": 0}
+    s = summarize([3.0, 1.0, 2.0], [], "x")
+    assert (s["sclk_mhz_min"], s["sclk_mhz_p50"], s["sclk_mhz_max"]) == (1.0, 2.0, 3.0)
+    assert "power_w_mean" not in s
+    # CPU: no device properties -> no hwmon path
+    assert gpu_hwmon() is None
