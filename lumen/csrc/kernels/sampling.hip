@@ -46,13 +46,38 @@ struct Row {
   int V;
   float invT;
   __device__ __forceinline__ float ld(int j) const { return to_f32(p[j]) * invT; }
-  // f(j, z) for every element this thread owns
+  // f(j, z) for every element this thread owns, 8 at a time: the 8 loads are issued before any
+  // f runs (f's LDS histogram atomics would otherwise order each load behind the previous
+  // element's atomic -- one LDS / L2 round trip per element, ~7 us per pass over V = 32000)
   template <typename F>
   __device__ __forceinline__ void each(F&& f) const {
-    if constexpr (NPT > 0) {
-      for (int j = threadIdx.x; j < V; j += kSampNT) f(j, zl[j]);
-    } else {
-      for (int j = threadIdx.x; j < V; j += kSampNT) f(j, ld(j));
+    constexpr int U = 8;
+    int j0 = threadIdx.x;
+    // full batches: no per-element bounds test (each one cost an exec-mask branch)
+    for (; j0 + (U - 1) * kSampNT < V; j0 += U * kSampNT) {
+      float zz[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (NPT > 0) zz[u] = zl[j0 + u * kSampNT];
+        else zz[u] = ld(j0 + u * kSampNT);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) f(j0 + u * kSampNT, zz[u]);
+    }
+    for (; j0 < V; j0 += U * kSampNT) {
+      float zz[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * kSampNT;
+        const int jc = j < V ? j : V - 1;  // clamped: unconditional loads
+        if constexpr (NPT > 0) zz[u] = zl[jc];
+        else zz[u] = ld(jc);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * kSampNT;
+        if (j < V) f(j, zz[u]);
+      }
     }
   }
 };
@@ -70,13 +95,23 @@ __device__ __forceinline__ void pick_digit(const C* hist, unsigned long long nee
     v[q] = hist[255 - 4 * lane - q];
     s += v[q];
   }
-  // inclusive prefix over lanes (lane 0 = the top bins)
+  // inclusive prefix over lanes (lane 0 = the top bins); counts fit 32 bits: one shuffle a step
   unsigned long long pre = s;
+  if constexpr (sizeof(C) == 4) {
+    unsigned p32 = static_cast<unsigned>(s);
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned lo = __shfl_up(static_cast<unsigned>(pre), o, 64);
-    const unsigned hi = __shfl_up(static_cast<unsigned>(pre >> 32), o, 64);
-    if (lane >= o) pre += (static_cast<unsigned long long>(hi) << 32) | lo;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned t = __shfl_up(p32, o, 64);
+      if (lane >= o) p32 += t;
+    }
+    pre = p32;
+  } else {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned lo = __shfl_up(static_cast<unsigned>(pre), o, 64);
+      const unsigned hi = __shfl_up(static_cast<unsigned>(pre >> 32), o, 64);
+      if (lane >= o) pre += (static_cast<unsigned long long>(hi) << 32) | lo;
+    }
   }
   const unsigned long long hit = __ballot(pre >= need);
   const int first = hit ? __builtin_ctzll(hit) : 63;
@@ -162,11 +197,34 @@ __global__ void __launch_bounds__(kSampNT) sample_kernel(
   row.invT = greedy ? 1.f : 1.f / temp;
   row.zl = zlds;
   if constexpr (NPT > 0) {
-    for (int j = threadIdx.x; j < V; j += kSampNT) zlds[j] = row.ld(j);
+    // 16-byte loads, 4 per thread in flight (one 2-byte load per element, a few in flight, left
+    // the row copy latency-bound: ~20 us of a greedy step), then the scalar tail
+    constexpr int E = 16 / static_cast<int>(sizeof(T));
+    const bool al = (reinterpret_cast<uintptr_t>(row.p) & 15) == 0;
+    const int nv = al ? V / E : 0;
+    for (int i0 = threadIdx.x; i0 < nv; i0 += 4 * kSampNT) {
+      uint4 u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = min(i0 + q * kSampNT, nv - 1);  // clamped: unconditional loads
+        u[q] = reinterpret_cast<const uint4*>(row.p)[i];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + q * kSampNT;
+        if (i < nv) {
+          const T* e = reinterpret_cast<const T*>(&u[q]);
+#pragma unroll
+          for (int t = 0; t < E; ++t) zlds[i * E + t] = to_f32(e[t]) * row.invT;
+        }
+      }
+    }
+    for (int j = nv * E + threadIdx.x; j < V; j += kSampNT) zlds[j] = row.ld(j);
     __syncthreads();
   }
   float m = -INFINITY;
   row.each([&](int, float z) { m = fmaxf(m, z); });
+  const float tmax = m;  // this thread's own maximum (every thread owns >= 1 element: V >= 512)
   m = block_max<kSampNT>(m, red);
   float s = 0.f;
   row.each([&](int, float z) { s += __expf(z - m); });
@@ -174,9 +232,15 @@ __global__ void __launch_bounds__(kSampNT) sample_kernel(
   uint32_t tau = 0;  // keep key >= tau (0: everything)
   if (!greedy) {
     const int k = top_k[row_i];
-    if (k > 0 && k < V)
-      tau = radix_select<T, NPT, false>(row, m, 0u, static_cast<unsigned long long>(k), hc, hm,
+    if (k > 0 && k < V) {
+      // lower bound for the k-th largest key: the smallest of the 512 per-thread maxima (512
+      // distinct elements are >= it, so for k <= 512 the k-th largest is too).  Only keys >= it
+      // enter the histograms: the first level's LDS atomics drop from V to the upper tail
+      uint32_t lo = 0;
+      if (k <= kSampNT && V >= kSampNT) lo = fkey(-block_max<kSampNT>(-tmax, red));
+      tau = radix_select<T, NPT, false>(row, m, lo, static_cast<unsigned long long>(k), hc, hm,
                                         &sel_b, &sel_need);
+    }
     const float p = top_p[row_i];
     if (p < 1.f) {
       // mass of the top-k-kept set, fixed point (exact integer sum)
