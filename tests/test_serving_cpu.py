@@ -812,3 +812,39 @@ def test_serve_cli_feature_flags_parse():
     assert a.num_speculative_tokens == 3 and a.ngram_prompt_lookup_max == 5
     d = build_parser().parse_args([])
     assert not d.enable_prefix_caching and d.num_speculative_tokens == 0
+
+
+def test_topk_topp_keep_vllm_semantics():
+    """The sort-based reference of vLLM 0.6.0's ``_apply_top_k_top_p`` that the GPU sampler is
+    tested against, pinned on hand-computed rows: top-k keeps ties of the k-th value; top-p works
+    on the top-k-RENORMALISED distribution and keeps the smallest head reaching p (>= 1 token);
+    the sampler draws only inside the kept set."""
+    import math
+
+    from lumen.serve.model_runner import sample_ref, topk_topp_keep
+
+    z = torch.tensor([3.0, 1.0, 2.0, 2.0, 0.0, -1.0])
+    # top-k 3: the 3rd largest value is 2.0, held twice -> 4 kept (ties)
+    assert topk_topp_keep(z, 3, 1.0).tolist() == [True, False, True, True, False, False]
+    # k >= V or k <= 0: no truncation
+    assert topk_topp_keep(z, 6, 1.0).all() and topk_topp_keep(z, 0, 1.0).all()
+    # top-p alone: softmax masses sorted 3.0 > 2.0 = 2.0 > 1.0 > ...; head mass before each token
+    e = [math.exp(v) for v in z.tolist()]
+    tot = sum(e)
+    p_top = e[0] / tot  # ~0.48
+    assert topk_topp_keep(z, 0, p_top * 0.5).tolist() == [True] + [False] * 5  # >= 1 token
+    keep = topk_topp_keep(z, 0, p_top + 1e-3)  # needs the next token too
+    assert int(keep.sum()) == 2 and bool(keep[0])
+    # top-p after top-k: renormalised over {3, 2, 2} (k = 2 keeps the tie): 3.0 alone has mass
+    # e^3 / (e^3 + 2 e^2) ~ 0.576, so p = 0.55 keeps just it, while over the full row it would not
+    kk = topk_topp_keep(z, 2, 0.55)
+    assert kk.tolist() == [True, False, False, False, False, False]
+    assert e[0] / tot < 0.55 < e[0] / (e[0] + 2 * e[2])
+    # the CPU sampler draws inside the kept set only
+    logits = z.repeat(64, 1)
+    t = torch.full((64,), 1.0)
+    tok, lp = sample_ref(logits, t, torch.full((64,), 0.9), torch.full((64,), 3, dtype=torch.int32),
+                         seed=7, offset=0)
+    kept = topk_topp_keep(z, 3, 0.9)
+    assert all(bool(kept[i]) for i in tok.tolist())
+    assert torch.allclose(lp, torch.log_softmax(z, -1)[tok])
