@@ -229,6 +229,10 @@ class LLMEngine:
             free, total = torch.cuda.mem_get_info(self.device)
             budget = free - (1 - self.cfg.gpu_memory_utilization) * total
             budget -= 4 << 30  # activations / graphs / workspace headroom
+            if os.environ.get("LUMEN_SHARED_GPU_REHEARSAL") == "1" and self.tp > 1:
+                # ranks sharing one device (rehearsal) each see the same free memory before any
+                # of them allocates: split it, or the last rank to allocate runs out
+                budget /= self.tp
         else:
             budget = 256 << 20
         nb = int(max(budget, per_block * 64) // per_block)
