@@ -498,13 +498,16 @@ void lora3_down(const at::Tensor& x, int64_t ldx, const at::Tensor& A, at::Tenso
   }
   float* sp = nullptr;
   if (slab && slab->defined()) {
-    // deterministic K-block sum: slab f32 >= ceil(T / 64) * ceil(K / 1024) * 64 * R, cnt zeroed
-    if (!cnt || !cnt->defined() || cnt->scalar_type() != at::kInt || !cnt->is_cuda() ||
-        cnt->numel() < (T + 63) / 64 || slab->scalar_type() != at::kFloat || !slab->is_cuda() ||
+    // deterministic K-block sum: slab f32 >= ceil(T / 64) * ceil(K / 1024) * 64 * R; with cnt
+    // (zeroed) the last-arriving K block sums in the kernel, without it a second launch does
+    const bool with_cnt = cnt && cnt->defined();
+    if ((with_cnt && (cnt->scalar_type() != at::kInt || !cnt->is_cuda() ||
+                      cnt->numel() < (T + 63) / 64)) ||
+        slab->scalar_type() != at::kFloat || !slab->is_cuda() ||
         slab->numel() < ((T + 63) / 64) * ((K + 1023) / 1024) * 64 * R)
       throw std::invalid_argument("lumen: lora3_down slab / cnt too small");
     sp = slab->data_ptr<float>();
-    cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+    cp = with_cnt ? reinterpret_cast<unsigned*>(cnt->data_ptr<int>()) : nullptr;
   }
   check(lumen_lora3_down(dcode(x), x.data_ptr(), ldx, A.data_ptr<float>(), A.stride(0),
                          Z.data_ptr<float>(), ldz, static_cast<int>(T), static_cast<int>(K),
@@ -563,8 +566,9 @@ void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r,
     if (segs[i].size() != 4) throw std::invalid_argument("lumen: lora3_dy segment = (n_off, r_off, b_off, n_len)");
     no[i] = segs[i][0]; ro[i] = segs[i][1]; bo[i] = segs[i][2]; nl[i] = static_cast<int>(segs[i][3]);
   }
-  // deterministic sums (ws f32, cnt int32 zeroed): dZ partials [nseg][gy][gx][tw][r], then dB
-  // partials [nseg][gx][gy][256][r]; counters: dZ [nseg][gy], then dB [nseg][gx]
+  // deterministic sums (ws f32): dZ partials [nseg][gy][gx][tw][r], then dB partials
+  // [nseg][gx][gy][256][r].  With cnt (int32, zeroed; dZ [nseg][gy], then dB [nseg][gx]) the
+  // last-arriving workgroups sum them inside the kernel; without it a second launch does
   float *sz = nullptr, *sb = nullptr;
   unsigned *cz = nullptr, *cb = nullptr;
   if (ws && ws->defined()) {
@@ -572,14 +576,17 @@ void lora3_dy(const at::Tensor& dy, int64_t ldy, const at::Tensor& B, int64_t r,
     for (int i = 0; i < nseg; ++i) maxl = std::max(maxl, nl[i]);
     const long long gx = (maxl + 255) / 256, gy = (T + tw - 1) / tw;
     const long long nz = nseg * gy * gx * tw * r, nb = nseg * gx * gy * 256 * r;
-    if (!cnt || !cnt->defined() || !ws->is_cuda() || ws->scalar_type() != at::kFloat ||
-        !cnt->is_cuda() || cnt->scalar_type() != at::kInt || ws->numel() < nz + nb ||
-        cnt->numel() < nseg * (gx + gy))
+    const bool with_cnt = cnt && cnt->defined();
+    if (!ws->is_cuda() || ws->scalar_type() != at::kFloat || ws->numel() < nz + nb ||
+        (with_cnt && (!cnt->is_cuda() || cnt->scalar_type() != at::kInt ||
+                      cnt->numel() < nseg * (gx + gy))))
       throw std::invalid_argument("lumen: lora3_dy deterministic workspace too small");
     sz = ws->data_ptr<float>();
     sb = sz + nz;
-    cz = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
-    cb = cz + nseg * gy;
+    if (with_cnt) {
+      cz = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+      cb = cz + nseg * gy;
+    }
   }
   check(lumen_lora3_dy(dcode(dy), dy.data_ptr(), ldy, B.data_ptr<float>(), static_cast<int>(r),
                        Z.data_ptr<float>(), ldz, dZ.data_ptr<float>(), lddz, dB.data_ptr<float>(),
@@ -671,14 +678,17 @@ void lora3_dxa(const at::Tensor& x, at::Tensor& dx, const at::Tensor& dZ, const 
     throw std::invalid_argument("lumen: lora3_dxa: x/dx [T, K] 16-bit, dZ [T, R] f32, A/dA [R, K] f32");
   float* sp = nullptr;
   unsigned* cp = nullptr;
-  if (ws && ws->defined()) {  // deterministic dA: partials [gx][gy][R][128], counters [gx]
+  // deterministic dA: partials [gx][gy][R][128]; with counters [gx] the last-arriving row
+  // block sums them in the kernel, without them a second launch does
+  if (ws && ws->defined()) {
     const long long gx = (x.size(1) + 127) / 128, gy = (x.size(0) + tw - 1) / tw;
-    if (!cnt || !cnt->defined() || !ws->is_cuda() || ws->scalar_type() != at::kFloat ||
-        !cnt->is_cuda() || cnt->scalar_type() != at::kInt ||
-        ws->numel() < gx * gy * 128 * dZ.size(1) || cnt->numel() < gx)
+    const bool with_cnt = cnt && cnt->defined();
+    if (!ws->is_cuda() || ws->scalar_type() != at::kFloat ||
+        ws->numel() < gx * gy * 128 * dZ.size(1) ||
+        (with_cnt && (!cnt->is_cuda() || cnt->scalar_type() != at::kInt || cnt->numel() < gx)))
       throw std::invalid_argument("lumen: lora3_dxa deterministic workspace too small");
     sp = ws->data_ptr<float>();
-    cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
+    if (with_cnt) cp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
   }
   check(lumen_lora3_dxa(dcode(x), x.data_ptr(), x.stride(0), dx.data_ptr(), dx.stride(0),
                         dZ.data_ptr<float>(), A.data_ptr<float>(), A.stride(0),

@@ -185,6 +185,7 @@ __global__ void __launch_bounds__(512) down3_kernel(DownArgs a) {
       const int o = (i / J) * JP + i % J;
       det::st_wt(mine + i, alpha * (red[0][o] + red[1][o] + red[2][o] + red[3][o]));
     }
+    if (a.cnt == nullptr) return;  // split form: down3_reduce_kernel sums the slabs
     __shared__ int lastf;
     if (!det::last_arriver(a.cnt + blockIdx.x, gridDim.y, &lastf)) return;
     // the row tile's sum in K-block order; Z written once, the fold tail straight from it
@@ -635,6 +636,8 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
             if (cb + cl < NL) det::st_wt(sb + (long long)cl * a.r + jt * 16 + L, dbacc[cc][m][jt][r]);
           }
     }
+    // split form (no counters): dy3_reduce_kernel sums the slabs in a second launch
+    if (a.cnt_z == nullptr) return;
     __shared__ int lastf;
     const int ncb = (NL + 128 * kDyCC - 1) / (128 * kDyCC);  // column blocks of this segment
     const int J = NJ * 16;
@@ -680,6 +683,95 @@ __global__ void __launch_bounds__(256) dy3_kernel(DyArgs a) {
         }
       }
   }
+}
+
+// The deterministic dZ / dB sums of dy3 as their own whole-chip launch (split form): one thread
+// per output pair, the partials of the column blocks (dZ) / row blocks (dB) added in block order
+// with 16 loads in flight.  In the in-kernel form one last-arriving workgroup pulled each 128-400
+// KB reduction through a single CU (latency-bound, profiles/r6_det).
+// grid (ceil(max(T, max n_len) * r / 2 / 256), nseg, 2): z = 0 dZ, z = 1 dB
+__device__ __forceinline__ float2 sum_pairs_plain(const float* base, long long stride, int n) {
+  float2 v = make_float2(0.f, 0.f);
+  for (int q0 = 0; q0 < n; q0 += 16) {
+    float2 u[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = q0 + k < n ? q0 + k : n - 1;
+      u[k] = *reinterpret_cast<const float2*>(base + q * stride);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (q0 + k < n) {
+        v.x += u[k].x;
+        v.y += u[k].y;
+      }
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(256) dy3_reduce_kernel(DyArgs a, int gx_n, int gy_n) {
+  const int seg = blockIdx.y;
+  const int NL = a.seg.n_len[seg];
+  const int hr = a.r / 2;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int j = (int)(i % hr) * 2;
+  if (blockIdx.z == 0) {
+    const long long t = i / hr;
+    if (t >= a.T) return;
+    const int gy = (int)(t / a.TW), tl = (int)(t % a.TW);
+    const int ncb = (NL + 128 * kDyCC - 1) / (128 * kDyCC);
+    const float* base = a.slab_z + (((long long)seg * gy_n + gy) * gx_n) * ((long long)a.TW * a.r) +
+                        (long long)tl * a.r + j;
+    const float2 v = sum_pairs_plain(base, (long long)a.TW * a.r, ncb);
+    float* o = a.dZ + a.seg.r_off[seg] + t * a.lddz + j;
+    o[0] = a.alpha * v.x;
+    o[1] = a.alpha * v.y;
+  } else {
+    const long long c = i / hr;
+    if (c >= NL) return;
+    const int gx = (int)(c / (128 * kDyCC)), cl = (int)(c % (128 * kDyCC));
+    const float* base = a.slab_b + (((long long)seg * gx_n + gx) * gy_n) * (256LL * a.r) +
+                        (long long)cl * a.r + j;
+    const float2 v = sum_pairs_plain(base, 256LL * a.r, gy_n);
+    float* o = a.dB + (a.seg.b_off[seg] + c) * a.r + j;
+    o[0] += a.alpha * v.x;
+    o[1] += a.alpha * v.y;
+  }
+}
+
+// dxa3's deterministic dA sums as their own launch (split form, as dy3_reduce_kernel): one
+// thread per (row j, column pair), the row blocks' partials [gx][gy][R][128] added in order.
+// grid (ceil(R * K / 2 / 256))
+__global__ void __launch_bounds__(256) dxa3_reduce_kernel(const float* __restrict__ slab,
+                                                          float* __restrict__ dA, long long ldda,
+                                                          int R, int K, int gy_n, float scale) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int hk = K / 2;
+  if (i >= (long long)R * hk) return;
+  const int j = (int)(i / hk), k = (int)(i % hk) * 2;
+  const int gx = k / 128, kl = k % 128;
+  const float2 v = sum_pairs_plain(slab + ((long long)gx * gy_n) * (128LL * R) +
+                                       (long long)j * 128 + kl,
+                                   128LL * R, gy_n);
+  float* o = dA + (long long)j * ldda + k;
+  o[0] += scale * v.x;
+  o[1] += scale * v.y;
+}
+
+// down3's deterministic Z sums as their own launch (split form): one thread per (row, column
+// pair), the K blocks' partials [tile][gy][64][J] added in order.  grid (ceil(T * J / 2 / 256))
+__global__ void __launch_bounds__(256) down3_reduce_kernel(const float* __restrict__ slab,
+                                                           float* __restrict__ Z, long long ldz,
+                                                           int T, int J, int gy_n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int hj = J / 2;
+  if (i >= (long long)T * hj) return;
+  const int t = (int)(i / hj), j = (int)(i % hj) * 2;
+  const int tile = t / 64, row = t % 64;
+  const float2 v = sum_pairs_plain(slab + ((long long)tile * gy_n) * (64LL * J) +
+                                       (long long)row * J + j,
+                                   64LL * J, gy_n);
+  *reinterpret_cast<float2*>(Z + (long long)t * ldz + j) = v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -942,6 +1034,7 @@ __global__ void __launch_bounds__(256) dxa3_kernel(DxaArgs a) {
           const int kl = wid * 32 + m * 16 + L, j = jt * 16 + g * 4 + r;
           if (c0 + kl < a.K && j < a.R) det::st_wt(sp + (long long)j * 128 + kl, da[m][jt][r]);
         }
+    if (a.cnt == nullptr) return;  // split form: dxa3_reduce_kernel sums the slabs
     __shared__ int lastf;
     if (!det::last_arriver(a.cnt + blockIdx.x, gridDim.y, &lastf)) return;
     const float* base = a.slab + (long long)blockIdx.x * gridDim.y * (128LL * a.R);
@@ -1073,7 +1166,9 @@ extern "C" hipError_t lumen_lora3_down(int dtype, const void* x, long long ldx, 
     return hipErrorInvalidValue;
   if (xe != nullptr && (cnt == nullptr || (KP & 7) || KP < R || (ldxe & 7) || (xk & 7)))
     return hipErrorInvalidValue;
-  if (slab != nullptr && (cnt == nullptr || (ldz & 1)))
+  // slab with cnt: in-kernel last-arriver sums; slab without cnt (and no fold tail): the split
+  // form, down3_reduce_kernel after
+  if (slab != nullptr && ((ldz & 1) || (cnt == nullptr && xe != nullptr)))
     return hipErrorInvalidValue;
   lv3::DownArgs a{x, ldx, A, lda, Z, ldz, T, K, alpha,
                   {static_cast<unsigned>(seed) ^ static_cast<unsigned>(seed >> 32), thresh, drop_scale,
@@ -1097,6 +1192,11 @@ extern "C" hipError_t lumen_lora3_down(int dtype, const void* x, long long ldx, 
   else return hipErrorInvalidValue;
 #undef LV3_DOWN_NJ
 #undef LV3_DOWN
+  if (slab != nullptr && cnt == nullptr) {
+    const long long n = (long long)T * (R / 2);
+    hipLaunchKernelGGL(lv3::down3_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, (const float*)slab, Z, ldz, T, R, (int)grid.y);
+  }
   return hipGetLastError();
 }
 
@@ -1163,7 +1263,9 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
   a.dy = dy; a.ldy = ldy; a.B = B; a.r = r; a.Z = Z; a.ldz = ldz; a.dZ = dZ; a.lddz = lddz;
   a.dB = dB; a.T = T; a.TW = tw; a.alpha = alpha;
   a.slab_z = slab_z; a.slab_b = slab_b; a.cnt_z = cnt_z; a.cnt_b = cnt_b;
-  if (slab_z != nullptr && (slab_b == nullptr || cnt_z == nullptr || cnt_b == nullptr ||
+  // deterministic sums: slabs with counters = in-kernel last-arriver sums; slabs without
+  // counters = the split form (dy3_reduce_kernel launched after dy3)
+  if (slab_z != nullptr && (slab_b == nullptr || (cnt_z == nullptr) != (cnt_b == nullptr) ||
                             (lddz & 1)))
     return hipErrorInvalidValue;
   a.seg.nseg = nseg;
@@ -1187,6 +1289,12 @@ extern "C" hipError_t lumen_lora3_dy(int dtype, const void* dy, long long ldy, c
   else if (dtype == kF16) { LV3_DY(fp16) }
   else return hipErrorInvalidValue;
 #undef LV3_DY
+  if (slab_z != nullptr && cnt_z == nullptr) {
+    const long long n = (long long)(T > maxl ? T : maxl) * (r / 2);
+    const dim3 rgrid((unsigned)((n + 255) / 256), nseg, 2);
+    hipLaunchKernelGGL(lv3::dy3_reduce_kernel, rgrid, dim3(256), 0, st, a, (int)grid.x,
+                       (int)grid.y);
+  }
   return hipGetLastError();
 }
 
@@ -1245,7 +1353,8 @@ extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, v
   a.x = x; a.ldx = ldx; a.dx = dx; a.lddx = lddx; a.dZ = dZ; a.A = A; a.lda = lda; a.dA = dA;
   a.ldda = ldda; a.T = T; a.K = K; a.R = R; a.TW = tw; a.delta = delta;
   a.slab = slab; a.cnt = cnt;
-  if (slab != nullptr && (cnt == nullptr || (ldda & 1))) return hipErrorInvalidValue;
+  // slab with cnt: in-kernel last-arriver sums; slab without cnt: dxa3_reduce_kernel after
+  if (slab != nullptr && (ldda & 1)) return hipErrorInvalidValue;
   const bool drop = thresh != 0;
   a.da_scale = drop ? drop_scale : 1.f;
   a.dx_scale = drop ? drop_scale : 1.f;
@@ -1274,11 +1383,14 @@ extern "C" hipError_t lumen_lora3_dxa(int dtype, const void* x, long long ldx, v
     else if (dtype == kF16) LV3_DXA_D(fp16);
     else return hipErrorInvalidValue;
 #undef LV3_DXA_D
-    return hipGetLastError();
-  }
-  if (dtype == kBF16) { LV3_DXA_NJ(bf16) }
+  } else if (dtype == kBF16) { LV3_DXA_NJ(bf16) }
   else if (dtype == kF16) { LV3_DXA_NJ(fp16) }
   else return hipErrorInvalidValue;
+  if (slab != nullptr && cnt == nullptr) {
+    const long long n = (long long)R * (K / 2);
+    hipLaunchKernelGGL(lv3::dxa3_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, (const float*)slab, dA, ldda, R, K, (int)grid.y, a.da_scale);
+  }
 #undef LV3_DXA_NJ
 #undef LV3_DXA
   return hipGetLastError();

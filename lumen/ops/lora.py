@@ -179,6 +179,9 @@ def _zeros(*shape, device, train: bool = False):
 USE_V3 = _os.environ.get("LUMEN_LORA_V3", "1") != "0"
 DY_TW = int(_os.environ.get("LUMEN_LORA_DY_TW", "0"))  # dY rows per block of lora3_dy (0 = auto)
 DXA_TW = int(_os.environ.get("LUMEN_LORA_DXA_TW", "0"))  # x rows per block of lora3_dxa (0 = auto)
+# deterministic mode: the forward Z, the dY pass's dZ / dB and the x pass's dA sums as second
+# whole-chip launches (1) or inside the kernels by the last-arriving workgroups (0)
+DET_SPLIT = _os.environ.get("LUMEN_DET_SPLIT", "1") != "0"
 # per-call A/B (scripts/probes/lora_kernels.py, us): the v3 UP write-back was on par with v2
 # without RoPE (o_proj 15.0 vs 14.3) and slower with it (q|k|v 55.7 vs 45.6), so v2 is the
 # forward UP; v3's DOWN (17.3 vs 21.9), fused dY pass (32.5 vs 53.3) and dx update win.  A
@@ -234,7 +237,7 @@ def _lora3_down(x2d, A, Z, p, seed):
                             math.ceil(T / 64))
     native().lora3_down(x2d, x2d.stride(0), A, Z, R, T, K, R, 1.0, int(seed) & 0x7FFFFFFFFFFFFFFF,
                         drop_threshold(p), 1.0 / (1.0 - p) if p > 0 else 1.0, K, 0,
-                        None, 0, 0, cnt, slab)
+                        None, 0, 0, None if (slab is not None and DET_SPLIT) else cnt, slab)
 
 
 def _lora3_fwd(x2d, y, A, B, Z, segs, r, scale, p, seed, rope):
@@ -433,7 +436,7 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
                                   ns * (gx + gy))
             nat.lora3_dy(dy, dy.stride(0), B, r, Z, R, dZ, R, dB, T, tw_, scale,
                          [(n_off, r_off, b_off, n_len) for (n_off, n_len, r_off, b_off) in ch],
-                         ws, cnt)
+                         ws, None if DET_SPLIT else cnt)
 
     if dx_fn is not None and BWD_OVERLAP and dy.is_cuda:
         # the dY pass (memory-bound, f32 atomics) beside the input-gradient GEMM (MFMA-bound):
@@ -470,7 +473,8 @@ def _lora3_bwd(dy, x2d, A, B, Z, dx, segs, r, scale, p, seed, need_dA, need_dB, 
             ws, cnt = _det_ws(dev, math.ceil(K / 128) * math.ceil(T / tw) * 128 * R,
                               math.ceil(K / 128))
         nat.lora3_dxa(x2d, dx, dZ, A, dA, tw, int(seed) & 0x7FFFFFFFFFFFFFFF, drop_threshold(p),
-                      1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, delta, ws, cnt)
+                      1.0 / (1.0 - p) if p > 0 else 1.0, K, 0, delta, ws,
+                      None if DET_SPLIT else cnt)
         if delta is not None:
             slot["delta"], slot["key"] = delta, (dx.data_ptr(), dx._version)
     else:

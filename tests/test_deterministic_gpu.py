@@ -33,14 +33,24 @@ def _grads(seed=5, T=1024):
     return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.requires_grad}
 
 
-def test_adapter_grads_bitwise_reproducible(monkeypatch):
+@pytest.mark.parametrize("split", [True, False])
+def test_adapter_grads_bitwise_reproducible(monkeypatch, split):
+    """split: the dY pass's dZ / dB sums in a second whole-chip launch (default) or inside the
+    kernel by the last-arriving workgroups; both bit-identical run to run and equal to each
+    other."""
     import lumen.ops.lora as L
 
     monkeypatch.setattr(L, "DETERMINISTIC", True)
+    monkeypatch.setattr(L, "DET_SPLIT", split)
     a, b = _grads(), _grads()
     assert a.keys() == b.keys() and len(a) > 0
     for k in a:
         assert torch.equal(a[k], b[k]), k
+    # both forms add the same partials in the same order
+    monkeypatch.setattr(L, "DET_SPLIT", not split)
+    d = _grads()
+    for k in a:
+        assert torch.equal(a[k], d[k]), k
     # the same sums as the atomic form, up to f32 summation order
     monkeypatch.setattr(L, "DETERMINISTIC", False)
     c = _grads()
